@@ -1,0 +1,181 @@
+/*
+ * pnp.h — C ABI of libpnp.so, the MI355X-native batched kinematics / DLS-IK / env-step engine
+ * for the panda_mujoco_gym shelf pick-and-place scene.
+ *
+ * The reference crosses one boundary for all of its hot-path arithmetic: the MuJoCo Python
+ * binding (mj_step / mj_forward / mj_kinematics / mj_jacSite / mju_mat2Quat, MjModel, MjData).
+ * Each entry point below replaces one of those call sites, batched over B independent envs
+ * (SURVEY.md §8b).  Conventions:
+ *   - every call returns int32 status: 0 ok, <0 error; pnp_last_error() gives a thread-local
+ *     message.  No C++ exception crosses the ABI.
+ *   - all batch buffers are CALLER-OWNED DEVICE pointers (e.g. torch.Tensor.data_ptr()),
+ *     structure-of-arrays, row-major [B, n], fp32 (the _f64 variants: fp64, for debugging and
+ *     bit-level parity against the CPU oracle).
+ *   - `stream` is a hipStream_t passed as void* (torch.cuda.current_stream().cuda_stream);
+ *     every call is asynchronous and stream-ordered; no host synchronisation inside.
+ *   - model descriptions are HOST pointers read once by pnp_model_create.
+ *   - quaternions are MuJoCo wxyz; matrices row-major 3x3.
+ */
+#ifndef PNP_H
+#define PNP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PNP_ABI_VERSION 1
+
+#define PNP_OK 0
+#define PNP_ERR_ARG -1
+#define PNP_ERR_HIP -2
+#define PNP_ERR_MODEL -3
+#define PNP_ERR_UNSUPPORTED -4
+
+/* Compiled model, MjModel field names (subset the scene needs).  Produced by the host MJCF
+ * compiler (mujoco-panda-pnp_amd/pnp_amd/mjcf.py) from assets/shelf_pnp.xml; replaces
+ * MjModel.from_xml_path (reference envs/panda_env.py:108).  All reals are float64. */
+typedef struct pnp_model_desc {
+  int32_t nq, nv, nu, nbody, njnt, ngeom, nsite, nmocap, neq, nmesh, nmeshvert;
+  /* <option> (assets/shelf_pnp.xml:4-6) */
+  double timestep;
+  double gravity[3];
+  int32_t noslip_iterations, iterations;
+  double tolerance;
+  int32_t cone_pyramidal, multiccd, warmstart, integrator_euler;
+  /* bodies [nbody] */
+  const int32_t* body_parentid;
+  const int32_t* body_rootid;
+  const int32_t* body_weldid;
+  const int32_t* body_mocapid;
+  const int32_t* body_jntadr;
+  const int32_t* body_jntnum;
+  const int32_t* body_dofadr;
+  const int32_t* body_dofnum;
+  const double* body_pos;     /* [nbody*3] */
+  const double* body_quat;    /* [nbody*4] */
+  const double* body_ipos;    /* [nbody*3] */
+  const double* body_iquat;   /* [nbody*4] */
+  const double* body_mass;    /* [nbody]   */
+  const double* body_inertia; /* [nbody*3] */
+  /* joints [njnt]: type 0 free, 1 ball, 2 slide, 3 hinge (mjtJoint) */
+  const int32_t* jnt_type;
+  const int32_t* jnt_qposadr;
+  const int32_t* jnt_dofadr;
+  const int32_t* jnt_bodyid;
+  const int32_t* jnt_limited;
+  const double* jnt_pos;      /* [njnt*3] */
+  const double* jnt_axis;     /* [njnt*3] */
+  const double* jnt_range;    /* [njnt*2] */
+  /* dofs [nv] */
+  const int32_t* dof_jntid;
+  const int32_t* dof_bodyid;
+  const double* dof_armature;
+  const double* dof_damping;
+  const double* qpos0;        /* [nq] */
+  /* geoms [ngeom]: type 0 plane, 2 sphere, 6 box, 7 mesh (mjtGeom) */
+  const int32_t* geom_type;
+  const int32_t* geom_bodyid;
+  const int32_t* geom_contype;
+  const int32_t* geom_conaffinity;
+  const int32_t* geom_condim;
+  const int32_t* geom_priority;
+  const int32_t* geom_dataid;  /* mesh id or -1 */
+  const double* geom_size;     /* [ngeom*3] */
+  const double* geom_pos;      /* [ngeom*3] */
+  const double* geom_quat;     /* [ngeom*4] */
+  const double* geom_friction; /* [ngeom*3] */
+  const double* geom_solref;   /* [ngeom*2] */
+  const double* geom_solimp;   /* [ngeom*5] */
+  const double* geom_margin;
+  const double* geom_gap;
+  /* convex-hull meshes */
+  const int32_t* mesh_vertadr; /* [nmesh] */
+  const int32_t* mesh_vertnum; /* [nmesh] */
+  const double* mesh_vert;     /* [nmeshvert*3], in the geom frame */
+  /* sites [nsite] */
+  const int32_t* site_bodyid;
+  const double* site_pos;      /* [nsite*3] */
+  const double* site_quat;     /* [nsite*4] */
+  /* actuators [nu]: general, joint transmission, affine bias */
+  const int32_t* actuator_trnid;
+  const int32_t* actuator_biastype;
+  const int32_t* actuator_ctrllimited;
+  const int32_t* actuator_forcelimited;
+  const double* actuator_gear;       /* [nu]   (gear[0]) */
+  const double* actuator_gainprm;    /* [nu*3] */
+  const double* actuator_biasprm;    /* [nu*3] */
+  const double* actuator_ctrlrange;  /* [nu*2] */
+  const double* actuator_forcerange; /* [nu*2] */
+  /* equality [neq]: type 1 = weld */
+  const int32_t* eq_type;
+  const int32_t* eq_obj1id;
+  const int32_t* eq_obj2id;
+  const double* eq_solref;     /* [neq*2]  */
+  const double* eq_solimp;     /* [neq*5]  */
+  const double* eq_data;       /* [neq*11] anchor(3) relpos(3) relquat(4) torquescale(1) */
+} pnp_model_desc;
+
+/* Parameters of JacobianIKController.solve (reference skills/ik_solver.py:35-37). */
+typedef struct pnp_ik_params {
+  int32_t max_iters;   /* default 100  */
+  double pos_thresh;   /* default 1e-3 */
+  double damping;      /* default 1e-2 (added as damping*I3, ik_solver.py:79) */
+  double step_limit;   /* default 0.1  */
+} pnp_ik_params;
+
+/* flags[b] bits written by pnp_ik_dls* (IKResult.converged / IKResult.success,
+ * reference skills/ik_solver.py:16-24, 88-92) */
+#define PNP_IK_CONVERGED 1u
+#define PNP_IK_SUCCESS 2u
+
+typedef struct pnp_model pnp_model;  /* opaque device-resident model */
+
+int32_t pnp_abi_version(void);
+/* sizeof(pnp_model_desc) as compiled into the library: lets bindings check their struct layout. */
+int32_t pnp_model_desc_size(void);
+const char* pnp_last_error(void);
+
+/* Replaces MjModel.from_xml_path + JacobianIKController.__init__ constants (reference
+ * envs/panda_env.py:108-109, skills/ik_solver.py:27-33): copies the model constants to the
+ * current HIP device (fp32 and fp64 images). */
+int32_t pnp_model_create(const pnp_model_desc* desc, pnp_model** out);
+int32_t pnp_model_destroy(pnp_model* model);
+
+/* Batched mj_kinematics restricted to what the hot path reads (site frames), reference
+ * skills/ik_solver.py:58-59, envs/panda_env.py:285-291,344-346, 337-342 (site_xpos / site_xmat).
+ *   qpos[B*nq], mocap_pos[B*nmocap*3] (may be NULL), mocap_quat[B*nmocap*4] (may be NULL)
+ *   -> site_xpos[B*nsite*3], site_xmat[B*nsite*9] (either may be NULL). */
+int32_t pnp_site_kinematics(pnp_model* model, const float* qpos, const float* mocap_pos,
+                            const float* mocap_quat, float* site_xpos, float* site_xmat,
+                            int32_t B, void* stream);
+int32_t pnp_site_kinematics_f64(pnp_model* model, const double* qpos, const double* mocap_pos,
+                                const double* mocap_quat, double* site_xpos, double* site_xmat,
+                                int32_t B, void* stream);
+
+/* Batched position Jacobian of a site (mj_jacSite jacp, reference skills/ik_solver.py:70-72):
+ *   qpos[B*nq] -> jacp[B*3*nv] (row-major 3 x nv per env). */
+int32_t pnp_jac_site(pnp_model* model, int32_t site_id, const float* qpos, float* jacp,
+                     int32_t B, void* stream);
+int32_t pnp_jac_site_f64(pnp_model* model, int32_t site_id, const double* qpos, double* jacp,
+                         int32_t B, void* stream);
+
+/* Batched JacobianIKController.solve (reference skills/ik_solver.py:35-101), one solve per env:
+ *   q_init[B*7], target[B*3] -> q_out[B*7], final_pos[B*3], pos_error[B], iterations[B],
+ *   flags[B] (PNP_IK_CONVERGED | PNP_IK_SUCCESS).
+ * The site must hang below the 7 arm hinges (ee_center_site); joints 0..6 are the ones solved,
+ * limits are jnt_range[0..6].  Other qpos entries do not affect the site and are not read. */
+int32_t pnp_ik_dls(pnp_model* model, int32_t site_id, pnp_ik_params params, const float* q_init,
+                   const float* target, float* q_out, float* final_pos, float* pos_error,
+                   int32_t* iterations, uint8_t* flags, int32_t B, void* stream);
+int32_t pnp_ik_dls_f64(pnp_model* model, int32_t site_id, pnp_ik_params params,
+                       const double* q_init, const double* target, double* q_out,
+                       double* final_pos, double* pos_error, int32_t* iterations, uint8_t* flags,
+                       int32_t B, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PNP_H */

@@ -1,0 +1,298 @@
+// ik_dls.hip — batched JacobianIKController.solve (reference skills/ik_solver.py:35-101).
+//
+// One thread per env, the whole solve (<= max_iters iterations) inside one launch, all per-env
+// state in VGPRs: the 7 joint angles, the chain frames, the 3x7 Jacobian and the 3x3 DLS
+// system never leave registers.  HBM traffic is the 92 B/solve of the batch arrays
+// (q_init 28 + target 12 in; q 28 + final_pos 12 + err 4 + iters 4 + flags 1 out).
+//
+// Kinematics: the 10-body root->ee_center_site path is folded on the host (pnp_capi.cpp) into
+// 7 hinge "segments" {fixed transform to the joint body, rotation about +-z} plus a fixed site
+// offset, so the FK loop is a fully unrolled chain of 3x3 products with static register
+// indices.  The numerics follow MuJoCo's mj_kinematics / mj_jacSite semantics (see oracle.c).
+//
+// Control flow is the reference's, line for line:
+//   for i < max_iters: p = FK(q); e = target - p; if |e| < thr: converged, iters = i+1, break
+//                      J = jacp; dq = J^T (J J^T + damping I)^-1 e   (LU, partial pivoting)
+//                      q = clip(q + clip(dq, +-step), lo, hi); iters = i+1
+//   final = FK(q); err = |final - target|; success = converged && err < 2 thr
+#include "pnp_internal.h"
+
+template <typename T>
+struct IKSeg {
+  T Rpre[7][9];   // fixed rotation from the previous joint frame to joint j's body frame
+  T ppre[7][3];   // fixed translation (in the previous joint frame)
+  T sgn[7];       // hinge axis = sgn * z
+  T psite[3];     // site position in the frame of the last joint body
+  T lo[7], hi[7];
+  T qpos0[7];
+};
+
+template <typename T>
+__device__ __forceinline__ void ik_fk(const IKSeg<T>& c, const T q[7], T site[3], T anchor[7][3],
+                                      T axis[7][3]) {
+  T R[9], p[3];
+#pragma unroll
+  for (int j = 0; j < 7; j++) {
+    if (j == 0) {
+#pragma unroll
+      for (int k = 0; k < 9; k++) R[k] = c.Rpre[0][k];
+      p[0] = c.ppre[0][0]; p[1] = c.ppre[0][1]; p[2] = c.ppre[0][2];
+    } else {
+      T d[3];
+      d_mulmatvec3(d, R, c.ppre[j]);
+      p[0] += d[0]; p[1] += d[1]; p[2] += d[2];
+      T N[9];
+#pragma unroll
+      for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int col = 0; col < 3; col++)
+          N[3 * r + col] = R[3 * r + 0] * c.Rpre[j][0 + col] + R[3 * r + 1] * c.Rpre[j][3 + col] +
+                           R[3 * r + 2] * c.Rpre[j][6 + col];
+#pragma unroll
+      for (int k = 0; k < 9; k++) R[k] = N[k];
+    }
+    // joint j: anchor at the body origin, world axis = sgn * (R e_z)
+    anchor[j][0] = p[0]; anchor[j][1] = p[1]; anchor[j][2] = p[2];
+    axis[j][0] = c.sgn[j] * R[2]; axis[j][1] = c.sgn[j] * R[5]; axis[j][2] = c.sgn[j] * R[8];
+    T s, co;
+    d_sincos(q[j] - c.qpos0[j], &s, &co);
+    s *= c.sgn[j];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      const T a = R[3 * r + 0], b = R[3 * r + 1];
+      R[3 * r + 0] = a * co + b * s;
+      R[3 * r + 1] = b * co - a * s;
+    }
+  }
+  T d[3];
+  d_mulmatvec3(d, R, c.psite);
+  site[0] = p[0] + d[0]; site[1] = p[1] + d[1]; site[2] = p[2] + d[2];
+}
+
+// 3x3 solve, LU with partial pivoting (LAPACK getrf/getrs order, as numpy.linalg.solve).
+template <typename T>
+__device__ __forceinline__ void solve3(T A[9], T b[3]) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    int p = k;
+    T mx = fabs(A[3 * k + k]);
+#pragma unroll
+    for (int i = k + 1; i < 3; i++) {
+      const T v = fabs(A[3 * i + k]);
+      if (v > mx) { mx = v; p = i; }
+    }
+    // branch-free row swap (p is data dependent: keep register indices static)
+#pragma unroll
+    for (int i = k + 1; i < 3; i++) {
+      const bool sw = (p == i);
+#pragma unroll
+      for (int col = 0; col < 3; col++) {
+        const T x = A[3 * k + col], y = A[3 * i + col];
+        A[3 * k + col] = sw ? y : x;
+        A[3 * i + col] = sw ? x : y;
+      }
+      const T x = b[k], y = b[i];
+      b[k] = sw ? y : x;
+      b[i] = sw ? x : y;
+    }
+    const T r = T(1) / A[3 * k + k];
+#pragma unroll
+    for (int i = k + 1; i < 3; i++) {
+      const T l = A[3 * i + k] * r;
+#pragma unroll
+      for (int col = k + 1; col < 3; col++) A[3 * i + col] -= l * A[3 * k + col];
+      b[i] -= l * b[k];
+    }
+  }
+#pragma unroll
+  for (int i = 2; i >= 0; i--) {
+    T s = b[i];
+#pragma unroll
+    for (int col = i + 1; col < 3; col++) s -= A[3 * i + col] * b[col];
+    b[i] = s / A[3 * i + i];
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(64) ik_dls_kernel(IKSeg<T> c, int max_iters, T thr, T damping,
+                                                    T step, const T* __restrict__ q_init,
+                                                    const T* __restrict__ target,
+                                                    T* __restrict__ q_out, T* __restrict__ final_pos,
+                                                    T* __restrict__ pos_error,
+                                                    int32_t* __restrict__ iterations,
+                                                    uint8_t* __restrict__ flags, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  T q[7], tg[3];
+#pragma unroll
+  for (int j = 0; j < 7; j++) q[j] = q_init[(size_t)b * 7 + j];
+  tg[0] = target[(size_t)b * 3]; tg[1] = target[(size_t)b * 3 + 1]; tg[2] = target[(size_t)b * 3 + 2];
+
+  T site[3], anchor[7][3], axis[7][3];
+  ik_fk(c, q, site, anchor, axis);
+  int converged = 0, iters = 0;
+  for (int i = 0; i < max_iters; i++) {
+    const T e0 = tg[0] - site[0], e1 = tg[1] - site[1], e2 = tg[2] - site[2];
+    const T n = sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+    if (n < thr) {
+      converged = 1;
+      iters = i + 1;
+      break;
+    }
+    // jacp columns: axis_j x (site - anchor_j)
+    T J[3][7];
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+      const T r0 = site[0] - anchor[j][0], r1 = site[1] - anchor[j][1], r2 = site[2] - anchor[j][2];
+      J[0][j] = axis[j][1] * r2 - axis[j][2] * r1;
+      J[1][j] = axis[j][2] * r0 - axis[j][0] * r2;
+      J[2][j] = axis[j][0] * r1 - axis[j][1] * r0;
+    }
+    T A[9];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+      for (int col = r; col < 3; col++) {
+        T acc = 0;
+#pragma unroll
+        for (int k = 0; k < 7; k++) acc += J[r][k] * J[col][k];
+        A[3 * r + col] = acc;
+        A[3 * col + r] = acc;
+      }
+    A[0] += damping; A[4] += damping; A[8] += damping;
+    T y[3] = {e0, e1, e2};
+    solve3(A, y);
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+      T dq = J[0][j] * y[0] + J[1][j] * y[1] + J[2][j] * y[2];
+      dq = fmin(fmax(dq, -step), step);
+      q[j] = fmin(fmax(q[j] + dq, c.lo[j]), c.hi[j]);
+    }
+    ik_fk(c, q, site, anchor, axis);
+    iters = i + 1;
+  }
+  const T d0 = site[0] - tg[0], d1 = site[1] - tg[1], d2 = site[2] - tg[2];
+  const T err = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+#pragma unroll
+  for (int j = 0; j < 7; j++) q_out[(size_t)b * 7 + j] = q[j];
+  final_pos[(size_t)b * 3] = site[0];
+  final_pos[(size_t)b * 3 + 1] = site[1];
+  final_pos[(size_t)b * 3 + 2] = site[2];
+  pos_error[b] = err;
+  iterations[b] = iters;
+  flags[b] = (uint8_t)((converged ? PNP_IK_CONVERGED : 0u) |
+                       ((converged && err < thr * T(2)) ? PNP_IK_SUCCESS : 0u));
+}
+
+// ---------------------------------------------------------------------------- host side
+static void mat_mul3(double r[9], const double a[9], const double b[9]) {
+  double t[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) t[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+  for (int k = 0; k < 9; k++) r[k] = t[k];
+}
+
+static void quat_to_mat(double m[9], const double q[4]) {
+  double q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
+  double q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
+  double q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
+  m[0] = q00 + q11 - q22 - q33; m[4] = q00 - q11 + q22 - q33; m[8] = q00 - q11 - q22 + q33;
+  m[1] = 2 * (q12 - q03); m[2] = 2 * (q13 + q02); m[3] = 2 * (q12 + q03);
+  m[5] = 2 * (q23 - q01); m[6] = 2 * (q13 - q02); m[7] = 2 * (q23 + q01);
+}
+
+// Fold the root -> site body path into 7 hinge segments.  Requirements (the Panda satisfies
+// them; anything else is PNP_ERR_UNSUPPORTED): no mocap/free/slide/ball joint on the path,
+// exactly the hinges 0..6 in order, each hinge through its body origin about +-z.
+static int32_t build_segments(const pnp_model* M, int site, IKSeg<double>* out) {
+  const DevModel<double>& m = M->h;
+  int path[PNP_MAXBODY], n = 0;
+  for (int b = m.site_bodyid[site]; b > 0; b = m.body_parentid[b]) {
+    if (n >= PNP_MAXBODY) return PNP_ERR_MODEL;
+    path[n++] = b;
+  }
+  double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, p[3] = {0, 0, 0};
+  int nj = 0;
+  for (int k = n - 1; k >= 0; k--) {
+    const int b = path[k];
+    if (m.body_mocapid[b] >= 0) return PNP_ERR_UNSUPPORTED;
+    double Rb[9], d[3];
+    quat_to_mat(Rb, m.body_quat[b]);
+    for (int r = 0; r < 3; r++) d[r] = R[3 * r] * m.body_pos[b][0] + R[3 * r + 1] * m.body_pos[b][1] + R[3 * r + 2] * m.body_pos[b][2];
+    p[0] += d[0]; p[1] += d[1]; p[2] += d[2];
+    mat_mul3(R, R, Rb);
+    for (int j = m.body_jntadr[b]; j >= 0 && j < m.body_jntadr[b] + m.body_jntnum[b]; j++) {
+      if (m.jnt_type[j] != 3 || j != nj || nj >= 7) return PNP_ERR_UNSUPPORTED;
+      if (m.jnt_pos[j][0] != 0 || m.jnt_pos[j][1] != 0 || m.jnt_pos[j][2] != 0) return PNP_ERR_UNSUPPORTED;
+      if (m.jnt_axis[j][0] != 0 || m.jnt_axis[j][1] != 0 || fabs(fabs(m.jnt_axis[j][2]) - 1) > 1e-12)
+        return PNP_ERR_UNSUPPORTED;
+      for (int t = 0; t < 9; t++) out->Rpre[nj][t] = R[t];
+      for (int t = 0; t < 3; t++) out->ppre[nj][t] = p[t];
+      out->sgn[nj] = m.jnt_axis[j][2] > 0 ? 1.0 : -1.0;
+      out->lo[nj] = M->jnt_range[j][0];
+      out->hi[nj] = M->jnt_range[j][1];
+      out->qpos0[nj] = m.qpos0[m.jnt_qposadr[j]];
+      nj++;
+      // the next segment starts in this joint's (unrotated) body frame
+      R[0] = 1; R[1] = 0; R[2] = 0; R[3] = 0; R[4] = 1; R[5] = 0; R[6] = 0; R[7] = 0; R[8] = 1;
+      p[0] = p[1] = p[2] = 0;
+    }
+  }
+  if (nj != 7) return PNP_ERR_UNSUPPORTED;
+  for (int r = 0; r < 3; r++)
+    out->psite[r] = p[r] + R[3 * r] * m.site_pos[site][0] + R[3 * r + 1] * m.site_pos[site][1] +
+                    R[3 * r + 2] * m.site_pos[site][2];
+  return PNP_OK;
+}
+
+template <typename T>
+static int32_t launch_ik(pnp_model* model, int32_t site, pnp_ik_params prm, const T* q_init,
+                         const T* target, T* q_out, T* final_pos, T* pos_error, int32_t* iterations,
+                         uint8_t* flags, int32_t B, void* stream) {
+  if (!model || B < 0 || site < 0 || site >= model->h.nsite || prm.max_iters < 0) {
+    pnp_set_error("pnp_ik_dls: bad argument (model=%p site=%d B=%d max_iters=%d)", (void*)model,
+                  site, B, prm.max_iters);
+    return PNP_ERR_ARG;
+  }
+  if (B == 0) return PNP_OK;
+  if (!q_init || !target || !q_out || !final_pos || !pos_error || !iterations || !flags) {
+    pnp_set_error("pnp_ik_dls: null buffer");
+    return PNP_ERR_ARG;
+  }
+  IKSeg<double> s64;
+  int32_t rc = build_segments(model, site, &s64);
+  if (rc) {
+    pnp_set_error("pnp_ik_dls: site %d is not below a 7-hinge +-z chain", site);
+    return rc;
+  }
+  IKSeg<T> s;
+  for (int j = 0; j < 7; j++) {
+    for (int t = 0; t < 9; t++) s.Rpre[j][t] = (T)s64.Rpre[j][t];
+    for (int t = 0; t < 3; t++) s.ppre[j][t] = (T)s64.ppre[j][t];
+    s.sgn[j] = (T)s64.sgn[j];
+    s.lo[j] = (T)s64.lo[j];
+    s.hi[j] = (T)s64.hi[j];
+    s.qpos0[j] = (T)s64.qpos0[j];
+  }
+  for (int t = 0; t < 3; t++) s.psite[t] = (T)s64.psite[t];
+  hipLaunchKernelGGL(ik_dls_kernel<T>, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, s,
+                     prm.max_iters, (T)prm.pos_thresh, (T)prm.damping, (T)prm.step_limit, q_init,
+                     target, q_out, final_pos, pos_error, iterations, flags, B);
+  return pnp_check_launch("ik_dls_kernel");
+}
+
+extern "C" int32_t pnp_ik_dls(pnp_model* model, int32_t site_id, pnp_ik_params params,
+                              const float* q_init, const float* target, float* q_out,
+                              float* final_pos, float* pos_error, int32_t* iterations,
+                              uint8_t* flags, int32_t B, void* stream) {
+  return launch_ik<float>(model, site_id, params, q_init, target, q_out, final_pos, pos_error,
+                          iterations, flags, B, stream);
+}
+
+extern "C" int32_t pnp_ik_dls_f64(pnp_model* model, int32_t site_id, pnp_ik_params params,
+                                  const double* q_init, const double* target, double* q_out,
+                                  double* final_pos, double* pos_error, int32_t* iterations,
+                                  uint8_t* flags, int32_t B, void* stream) {
+  return launch_ik<double>(model, site_id, params, q_init, target, q_out, final_pos, pos_error,
+                           iterations, flags, B, stream);
+}

@@ -1,0 +1,69 @@
+"""ctypes binding of libpnp.so (include/pnp.h).  Fails loudly if the HIP library is missing:
+there is no CPU fallback anywhere in the product path."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from .model import PnpIKParams, PnpModelDesc
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpnp.so")
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+ABI_VERSION = 1
+
+# every symbol include/pnp.h declares (tests check the library exports all of them)
+EXPORTS = [
+    "pnp_abi_version", "pnp_model_desc_size", "pnp_last_error", "pnp_model_create",
+    "pnp_model_destroy", "pnp_site_kinematics", "pnp_site_kinematics_f64", "pnp_jac_site",
+    "pnp_jac_site_f64", "pnp_ik_dls", "pnp_ik_dls_f64",
+]
+
+_lib = None
+
+
+class PnpError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libpnp.so (build it with `make -C mujoco-panda-pnp_amd/csrc`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PnpError(f"libpnp.so not found at {LIB_PATH}; build the HIP extension first "
+                       f"(make -C {CSRC} or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    P, I32 = C.c_void_p, C.c_int32
+    L.pnp_abi_version.restype = I32
+    L.pnp_model_desc_size.restype = I32
+    L.pnp_last_error.restype = C.c_char_p
+    L.pnp_model_create.argtypes = [C.POINTER(PnpModelDesc), C.POINTER(P)]
+    L.pnp_model_create.restype = I32
+    L.pnp_model_destroy.argtypes = [P]
+    L.pnp_model_destroy.restype = I32
+    for name in ("pnp_site_kinematics", "pnp_site_kinematics_f64"):
+        f = getattr(L, name)
+        f.argtypes = [P, P, P, P, P, P, I32, P]
+        f.restype = I32
+    for name in ("pnp_jac_site", "pnp_jac_site_f64"):
+        f = getattr(L, name)
+        f.argtypes = [P, I32, P, P, I32, P]
+        f.restype = I32
+    for name in ("pnp_ik_dls", "pnp_ik_dls_f64"):
+        f = getattr(L, name)
+        f.argtypes = [P, I32, PnpIKParams, P, P, P, P, P, P, P, I32, P]
+        f.restype = I32
+    if L.pnp_abi_version() != ABI_VERSION:
+        raise PnpError(f"libpnp ABI {L.pnp_abi_version()} != binding ABI {ABI_VERSION}")
+    if L.pnp_model_desc_size() != C.sizeof(PnpModelDesc):
+        raise PnpError(f"pnp_model_desc size mismatch: lib {L.pnp_model_desc_size()} vs "
+                       f"binding {C.sizeof(PnpModelDesc)}")
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().pnp_last_error().decode(errors="replace")
+        raise PnpError(f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,123 @@
+"""Device-resident engine: a pnp_model handle plus batched launches on torch tensors.
+
+All tensors are CUDA (HIP) tensors owned by the caller; launches go on
+``torch.cuda.current_stream()``.  fp32 tensors use the product kernels, fp64 tensors the
+debugging instantiation of the same kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+from .model import PandaModel, PnpIKParams, load_model
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _need(t, dtype, shape_tail, name):
+    if t is None:
+        raise ValueError(f"{name} is required")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor (got {t.device}); the engine has no CPU path")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if tuple(t.shape[1:]) != tuple(shape_tail):
+        raise ValueError(f"{name}: shape {tuple(t.shape)}, expected [B, {', '.join(map(str, shape_tail))}]")
+    return t
+
+
+class Engine:
+    """Owns one device image of the compiled model (pnp_model_create)."""
+
+    def __init__(self, model: PandaModel | None = None, device=None):
+        self.model = model or load_model()
+        self.lib = _lib.load()
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.pnp_model_create(C.byref(self.model.desc()), C.byref(h)), "pnp_model_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.lib.pnp_model_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ kinematics
+    def site_kinematics(self, qpos, mocap_pos=None, mocap_quat=None, want_xmat=True):
+        m = self.model
+        dt = qpos.dtype
+        _need(qpos, dt, (m.nq,), "qpos")
+        B = qpos.shape[0]
+        if mocap_pos is not None:
+            _need(mocap_pos, dt, (m.nmocap * 3,), "mocap_pos")
+        if mocap_quat is not None:
+            _need(mocap_quat, dt, (m.nmocap * 4,), "mocap_quat")
+        sx = torch.empty(B, m.nsite, 3, dtype=dt, device=qpos.device)
+        sm = torch.empty(B, m.nsite, 9, dtype=dt, device=qpos.device) if want_xmat else None
+        fn = self.lib.pnp_site_kinematics if dt == torch.float32 else self.lib.pnp_site_kinematics_f64
+        _lib.check(fn(self._h, _ptr(qpos), _ptr(mocap_pos), _ptr(mocap_quat), _ptr(sx), _ptr(sm), B,
+                      _stream()), "pnp_site_kinematics")
+        return sx, sm
+
+    def jac_site(self, qpos, site="ee_center_site"):
+        m = self.model
+        _need(qpos, qpos.dtype, (m.nq,), "qpos")
+        B = qpos.shape[0]
+        jac = torch.empty(B, 3, m.nv, dtype=qpos.dtype, device=qpos.device)
+        fn = self.lib.pnp_jac_site if qpos.dtype == torch.float32 else self.lib.pnp_jac_site_f64
+        sid = site if isinstance(site, int) else m.site_id(site)
+        _lib.check(fn(self._h, sid, _ptr(qpos), _ptr(jac), B, _stream()), "pnp_jac_site")
+        return jac
+
+    # ------------------------------------------------------------------ IK
+    def ik_dls_into(self, q_init, target, out, site="ee_center_site", max_iters=100, pos_thresh=1e-3,
+                    damping=1e-2, step_limit=0.1):
+        """Launch only (no allocation): ``out`` = dict(q, final_pos, pos_error, iterations, flags)."""
+        B = q_init.shape[0]
+        fn = self.lib.pnp_ik_dls if q_init.dtype == torch.float32 else self.lib.pnp_ik_dls_f64
+        sid = site if isinstance(site, int) else self.model.site_id(site)
+        prm = PnpIKParams(int(max_iters), float(pos_thresh), float(damping), float(step_limit))
+        _lib.check(fn(self._h, sid, prm, _ptr(q_init), _ptr(target), _ptr(out["q"]), _ptr(out["final_pos"]),
+                      _ptr(out["pos_error"]), _ptr(out["iterations"]), _ptr(out["flags"]), B, _stream()),
+                   "pnp_ik_dls")
+        return out
+
+    def ik_dls(self, q_init, target, site="ee_center_site", **params):
+        """Batched JacobianIKController.solve (reference skills/ik_solver.py:35-101)."""
+        dt = q_init.dtype
+        _need(q_init, dt, (7,), "q_init")
+        _need(target, dt, (3,), "target")
+        B, dev = q_init.shape[0], q_init.device
+        out = dict(q=torch.empty(B, 7, dtype=dt, device=dev), final_pos=torch.empty(B, 3, dtype=dt, device=dev),
+                   pos_error=torch.empty(B, dtype=dt, device=dev),
+                   iterations=torch.empty(B, dtype=torch.int32, device=dev),
+                   flags=torch.empty(B, dtype=torch.uint8, device=dev))
+        return self.ik_dls_into(q_init, target, out, site=site, **params)
+
+
+_ENGINES = {}
+
+
+def get_engine(device=None) -> Engine:
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    key = (dev.type, dev.index)
+    if key not in _ENGINES:
+        _ENGINES[key] = Engine(device=dev)
+    return _ENGINES[key]

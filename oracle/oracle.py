@@ -1,0 +1,110 @@
+"""ctypes binding of liboracle.so — the CPU fp64 restatement of the reference hot path.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by the product package (mujoco-panda-pnp_amd/pnp_amd).
+See oracle.c for the reference file:line each routine restates.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "mujoco-panda-pnp_amd"))
+from pnp_amd.model import PnpIKParams, load_model  # noqa: E402  (host-side model data only)
+
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        L.orc_ik_dls_batch.argtypes = [P, C.c_int, PnpIKParams, P, P, P, P, P, P, P, C.c_int, C.c_int]
+        L.orc_ik_dls_batch.restype = C.c_int
+        L.orc_site_kinematics_batch.argtypes = [P, P, P, P, P, P, C.c_int]
+        L.orc_site_kinematics_batch.restype = C.c_int
+        L.orc_jac_site_batch.argtypes = [P, C.c_int, P, P, C.c_int]
+        L.orc_jac_site_batch.restype = C.c_int
+        L.orc_mat2quat.argtypes = [P, P]
+        L.orc_mat2quat.restype = None
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def _desc_ptr(model):
+    return C.cast(C.pointer(model.desc()), C.c_void_p)
+
+
+def ik_params(max_iters=100, pos_thresh=1e-3, damping=1e-2, step_limit=0.1):
+    return PnpIKParams(int(max_iters), float(pos_thresh), float(damping), float(step_limit))
+
+
+def ik_dls(q_init, target, site="ee_center_site", nthreads=1, model=None, **params):
+    """Batched JacobianIKController.solve on the CPU (fp64)."""
+    m = model or load_model()
+    q_init = np.ascontiguousarray(q_init, np.float64).reshape(-1, 7)
+    target = np.ascontiguousarray(target, np.float64).reshape(-1, 3)
+    B = q_init.shape[0]
+    out = dict(q=np.zeros((B, 7)), final_pos=np.zeros((B, 3)), pos_error=np.zeros(B),
+               iterations=np.zeros(B, np.int32), flags=np.zeros(B, np.uint8))
+    rc = lib().orc_ik_dls_batch(_desc_ptr(m), m.site_id(site), ik_params(**params), _p(q_init),
+                                _p(target), _p(out["q"]), _p(out["final_pos"]), _p(out["pos_error"]),
+                                _p(out["iterations"]), _p(out["flags"]), B, int(nthreads))
+    if rc:
+        raise RuntimeError("orc_ik_dls_batch failed")
+    return out
+
+
+def site_kinematics(qpos, mocap_pos=None, mocap_quat=None, model=None):
+    m = model or load_model()
+    qpos = np.ascontiguousarray(qpos, np.float64).reshape(-1, m.nq)
+    B = qpos.shape[0]
+    if mocap_pos is not None:
+        mocap_pos = np.ascontiguousarray(mocap_pos, np.float64).reshape(B, -1)
+    if mocap_quat is not None:
+        mocap_quat = np.ascontiguousarray(mocap_quat, np.float64).reshape(B, -1)
+    sx = np.zeros((B, m.nsite, 3))
+    sm = np.zeros((B, m.nsite, 9))
+    rc = lib().orc_site_kinematics_batch(_desc_ptr(m), _p(qpos), _p(mocap_pos), _p(mocap_quat),
+                                         _p(sx), _p(sm), B)
+    if rc:
+        raise RuntimeError("orc_site_kinematics_batch failed")
+    return sx, sm
+
+
+def jac_site(qpos, site="ee_center_site", model=None):
+    m = model or load_model()
+    qpos = np.ascontiguousarray(qpos, np.float64).reshape(-1, m.nq)
+    B = qpos.shape[0]
+    jac = np.zeros((B, 3, m.nv))
+    rc = lib().orc_jac_site_batch(_desc_ptr(m), m.site_id(site), _p(qpos), _p(jac), B)
+    if rc:
+        raise RuntimeError("orc_jac_site_batch failed")
+    return jac
+
+
+def mat2quat(mat):
+    mat = np.ascontiguousarray(mat, np.float64).reshape(9)
+    q = np.zeros(4)
+    lib().orc_mat2quat(_p(q), _p(mat))
+    return q

@@ -1,0 +1,97 @@
+"""CPU tests of the host side: compiled model, RNG, workloads, and that libpnp.so loads and
+exports every symbol include/pnp.h declares (no compute calls: there is no GPU here)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "pnp.h")
+
+
+def test_model_census(model):
+    # SURVEY.md Appendix A
+    assert (model.nq, model.nv, model.nu, model.nbody, model.njnt, model.nsite, model.nmocap, model.neq) == \
+        (37, 33, 9, 20, 13, 7, 1, 1)
+    coll = (model.geom_contype != 0) | (model.geom_conaffinity != 0)
+    assert coll.sum() == 40
+    assert np.allclose(model.body_mass[model.body_id("cube1")], 0.064)
+    assert np.allclose(model.dof_armature[:9], 0.1) and np.allclose(model.dof_damping[:9], 1.0)
+    assert np.allclose(model.jnt_range[3], [-3.0718, -0.0698])
+    assert model.opt_timestep == 0.002 and model.opt_noslip_iterations == 3
+    assert list(model.names_jnt[:9]) == [f"joint{i}" for i in range(1, 8)] + ["finger_joint1", "finger_joint2"]
+    assert model.jnt_qposadr[model.joint_id("obj_joint")] == 30
+
+
+@pytest.mark.skipif(not os.path.exists("/root/reference/panda_mujoco_gym/assets/shelf_pnp.xml"),
+                    reason="reference MJCF only present in the build container")
+def test_committed_model_matches_fresh_compile(model):
+    from pnp_amd.mjcf import compile_xml
+    fresh = compile_xml()
+    for k, v in fresh.items():
+        a = np.asarray(v)
+        b = getattr(model, k) if not isinstance(getattr(model, k), np.ndarray) else getattr(model, k)
+        if a.dtype.kind in "fi":
+            np.testing.assert_allclose(np.asarray(b, a.dtype), a, err_msg=k)
+        else:
+            assert np.array_equal(np.asarray(b), a), k
+
+
+def test_philox_known_answers():
+    from pnp_amd import rng
+    z = rng.philox4x32(np.zeros((1, 4), np.uint32), (0, 0))[0]
+    assert [hex(x) for x in z] == ["0x6627e8d5", "0xe169c58d", "0xbc57ac4c", "0x9b00dbd8"]
+    f = rng.philox4x32(np.full((1, 4), 0xFFFFFFFF, np.uint32), (0xFFFFFFFF, 0xFFFFFFFF))[0]
+    assert [hex(x) for x in f] == ["0x408f276d", "0x41c83b0e", "0xa20bc7c6", "0x6d5451fd"]
+
+
+def test_workload_is_shard_invariant(model):
+    from pnp_amd import workloads
+    full_q, full_d = workloads.ik_inputs(model, np.arange(256))
+    for r in range(4):
+        q, d = workloads.ik_inputs(model, np.arange(r * 64, (r + 1) * 64))
+        assert np.array_equal(q, full_q[r * 64:(r + 1) * 64]) and np.array_equal(d, full_d[r * 64:(r + 1) * 64])
+    lo, hi = model.jnt_range[:7, 0], model.jnt_range[:7, 1]
+    span = hi - lo
+    assert np.all(full_q >= lo + 0.05 * span - 1e-12) and np.all(full_q <= hi - 0.05 * span + 1e-12)
+    assert np.all(np.abs(full_d) <= 0.02)
+
+
+def _header_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int32_t|const char\*)\s+(pnp_\w+)\s*\(", src, re.M)))
+
+
+def test_library_loads_and_exports_header_symbols():
+    from pnp_amd import _lib
+    L = _lib.load()
+    syms = _header_symbols()
+    assert len(syms) >= 11
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(_lib.EXPORTS)
+    assert L.pnp_abi_version() == 1
+    from pnp_amd.model import PnpModelDesc
+    assert L.pnp_model_desc_size() == C.sizeof(PnpModelDesc)
+
+
+def test_library_rejects_bad_arguments_without_gpu():
+    """Argument validation happens before any HIP call, so it is testable on the CPU."""
+    from pnp_amd import _lib
+    from pnp_amd.model import PnpIKParams
+    L = _lib.load()
+    rc = L.pnp_model_create(None, None)
+    assert rc == -1 and b"null" in L.pnp_last_error()
+    rc = L.pnp_ik_dls(None, 0, PnpIKParams(100, 1e-3, 1e-2, 0.1), None, None, None, None, None, None, None, 4, None)
+    assert rc == -1 and b"bad argument" in L.pnp_last_error()
+
+
+def test_product_package_never_imports_oracle():
+    pkg = os.path.join(ROOT, "mujoco-panda-pnp_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith((".py", ".hip", ".cpp", ".h")):
+                txt = open(os.path.join(dp, f)).read()
+                assert "import oracle" not in txt and "from oracle" not in txt and "liboracle" not in txt, f
