@@ -17,6 +17,8 @@
 //   final = FK(q); err = |final - target|; success = converged && err < 2 thr
 #include "pnp_internal.h"
 
+#include "gen/panda_chain.h"
+
 template <typename T>
 struct IKSeg {
   T Rpre[7][9];   // fixed rotation from the previous joint frame to joint j's body frame
@@ -27,7 +29,49 @@ struct IKSeg {
   T qpos0[7];
 };
 
-template <typename T>
+// Chain constants: compile-time (baked Panda chain, gen/panda_chain.h) or kernel-argument.
+// After full unrolling every index is static, so the baked values fold into the FMAs and the
+// 0 / +-1 entries of the +-90 deg body rotations disappear.
+#define IK_CONST(field, cfield, ...) \
+  (BAKED ? (T)panda_chain::field __VA_ARGS__ : c.cfield __VA_ARGS__)
+
+// ---------------------------------------------------------------------------- fp32 fast math
+// sin/cos for the arm's joint-angle range (|x| < 2^7): Cody-Waite reduction by pi/2 in three
+// parts + Cephes minimax polynomials on [-pi/4, pi/4] (<= 1 ulp there).  The library sincosf
+// carries a Payne-Hanek large-argument path that more than doubled the kernel's instruction
+// count; joint angles never need it.
+__device__ __forceinline__ void fast_sincos(float x, float* s, float* c) {
+  const float k = __builtin_rintf(x * 0.636619772367581343f);
+  float r = __builtin_fmaf(k, -1.5703125f, x);
+  r = __builtin_fmaf(k, -4.837512969970703125e-4f, r);
+  r = __builtin_fmaf(k, -7.549789954891882e-8f, r);
+  const float r2 = r * r;
+  float ps = __builtin_fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
+  ps = __builtin_fmaf(r2, ps, -1.6666654611e-1f);
+  const float sn = __builtin_fmaf(r * r2, ps, r);
+  float pc = __builtin_fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+  pc = __builtin_fmaf(r2, pc, 4.166664568298827e-2f);
+  const float cs = __builtin_fmaf(r2 * r2, pc, __builtin_fmaf(r2, -0.5f, 1.0f));
+  const int q = (int)k;
+  const float ss = (q & 1) ? cs : sn;
+  const float cc = (q & 1) ? sn : cs;
+  *s = (q & 2) ? -ss : ss;
+  *c = ((q + 1) & 2) ? -cc : cc;
+}
+
+template <typename T> struct KMath;
+template <> struct KMath<float> {
+  static __device__ __forceinline__ void sincos(float x, float* s, float* c) { fast_sincos(x, s, c); }
+  static __device__ __forceinline__ float sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+  static __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+};
+template <> struct KMath<double> {
+  static __device__ __forceinline__ void sincos(double x, double* s, double* c) { ::sincos(x, s, c); }
+  static __device__ __forceinline__ double sqrt(double x) { return ::sqrt(x); }
+  static __device__ __forceinline__ double rcp(double x) { return 1.0 / x; }
+};
+
+template <typename T, bool BAKED>
 __device__ __forceinline__ void ik_fk(const IKSeg<T>& c, const T q[7], T site[3], T anchor[7][3],
                                       T axis[7][3]) {
   T R[9], p[3];
@@ -35,28 +79,32 @@ __device__ __forceinline__ void ik_fk(const IKSeg<T>& c, const T q[7], T site[3]
   for (int j = 0; j < 7; j++) {
     if (j == 0) {
 #pragma unroll
-      for (int k = 0; k < 9; k++) R[k] = c.Rpre[0][k];
-      p[0] = c.ppre[0][0]; p[1] = c.ppre[0][1]; p[2] = c.ppre[0][2];
+      for (int k = 0; k < 9; k++) R[k] = IK_CONST(kRpre, Rpre, [0][k]);
+#pragma unroll
+      for (int k = 0; k < 3; k++) p[k] = IK_CONST(kPpre, ppre, [0][k]);
     } else {
-      T d[3];
-      d_mulmatvec3(d, R, c.ppre[j]);
-      p[0] += d[0]; p[1] += d[1]; p[2] += d[2];
+#pragma unroll
+      for (int r = 0; r < 3; r++)
+        p[r] += R[3 * r + 0] * IK_CONST(kPpre, ppre, [j][0]) + R[3 * r + 1] * IK_CONST(kPpre, ppre, [j][1]) +
+                R[3 * r + 2] * IK_CONST(kPpre, ppre, [j][2]);
       T N[9];
 #pragma unroll
       for (int r = 0; r < 3; r++)
 #pragma unroll
         for (int col = 0; col < 3; col++)
-          N[3 * r + col] = R[3 * r + 0] * c.Rpre[j][0 + col] + R[3 * r + 1] * c.Rpre[j][3 + col] +
-                           R[3 * r + 2] * c.Rpre[j][6 + col];
+          N[3 * r + col] = R[3 * r + 0] * IK_CONST(kRpre, Rpre, [j][0 + col]) +
+                           R[3 * r + 1] * IK_CONST(kRpre, Rpre, [j][3 + col]) +
+                           R[3 * r + 2] * IK_CONST(kRpre, Rpre, [j][6 + col]);
 #pragma unroll
       for (int k = 0; k < 9; k++) R[k] = N[k];
     }
     // joint j: anchor at the body origin, world axis = sgn * (R e_z)
+    const T sg = IK_CONST(kSgn, sgn, [j]);
     anchor[j][0] = p[0]; anchor[j][1] = p[1]; anchor[j][2] = p[2];
-    axis[j][0] = c.sgn[j] * R[2]; axis[j][1] = c.sgn[j] * R[5]; axis[j][2] = c.sgn[j] * R[8];
+    axis[j][0] = sg * R[2]; axis[j][1] = sg * R[5]; axis[j][2] = sg * R[8];
     T s, co;
-    d_sincos(q[j] - c.qpos0[j], &s, &co);
-    s *= c.sgn[j];
+    KMath<T>::sincos(q[j] - IK_CONST(kQpos0, qpos0, [j]), &s, &co);
+    s *= sg;
 #pragma unroll
     for (int r = 0; r < 3; r++) {
       const T a = R[3 * r + 0], b = R[3 * r + 1];
@@ -64,41 +112,41 @@ __device__ __forceinline__ void ik_fk(const IKSeg<T>& c, const T q[7], T site[3]
       R[3 * r + 1] = b * co - a * s;
     }
   }
-  T d[3];
-  d_mulmatvec3(d, R, c.psite);
-  site[0] = p[0] + d[0]; site[1] = p[1] + d[1]; site[2] = p[2] + d[2];
+#pragma unroll
+  for (int r = 0; r < 3; r++)
+    site[r] = p[r] + R[3 * r + 0] * IK_CONST(kPsite, psite, [0]) + R[3 * r + 1] * IK_CONST(kPsite, psite, [1]) +
+              R[3 * r + 2] * IK_CONST(kPsite, psite, [2]);
 }
 
-// 3x3 solve, LU with partial pivoting (LAPACK getrf/getrs order, as numpy.linalg.solve).
-template <typename T>
-__device__ __forceinline__ void solve3(T A[9], T b[3]) {
+// fp64: 3x3 LU with partial pivoting (LAPACK getrf/getrs order, as numpy.linalg.solve), so
+// the debugging instantiation tracks the reference's arithmetic.
+__device__ __forceinline__ void solve3(double A[9], double b[3]) {
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     int p = k;
-    T mx = fabs(A[3 * k + k]);
+    double mx = fabs(A[3 * k + k]);
 #pragma unroll
     for (int i = k + 1; i < 3; i++) {
-      const T v = fabs(A[3 * i + k]);
+      const double v = fabs(A[3 * i + k]);
       if (v > mx) { mx = v; p = i; }
     }
-    // branch-free row swap (p is data dependent: keep register indices static)
 #pragma unroll
-    for (int i = k + 1; i < 3; i++) {
+    for (int i = k + 1; i < 3; i++) {   // branch-free swap keeps register indices static
       const bool sw = (p == i);
 #pragma unroll
       for (int col = 0; col < 3; col++) {
-        const T x = A[3 * k + col], y = A[3 * i + col];
+        const double x = A[3 * k + col], y = A[3 * i + col];
         A[3 * k + col] = sw ? y : x;
         A[3 * i + col] = sw ? x : y;
       }
-      const T x = b[k], y = b[i];
+      const double x = b[k], y = b[i];
       b[k] = sw ? y : x;
       b[i] = sw ? x : y;
     }
-    const T r = T(1) / A[3 * k + k];
+    const double r = 1.0 / A[3 * k + k];
 #pragma unroll
     for (int i = k + 1; i < 3; i++) {
-      const T l = A[3 * i + k] * r;
+      const double l = A[3 * i + k] * r;
 #pragma unroll
       for (int col = k + 1; col < 3; col++) A[3 * i + col] -= l * A[3 * k + col];
       b[i] -= l * b[k];
@@ -106,14 +154,30 @@ __device__ __forceinline__ void solve3(T A[9], T b[3]) {
   }
 #pragma unroll
   for (int i = 2; i >= 0; i--) {
-    T s = b[i];
+    double s = b[i];
 #pragma unroll
     for (int col = i + 1; col < 3; col++) s -= A[3 * i + col] * b[col];
     b[i] = s / A[3 * i + i];
   }
 }
 
-template <typename T>
+// fp32: A = J J^T + damping I is symmetric positive definite (damping > 0), so an LDL^T
+// factorisation needs no pivoting: 3 reciprocals + ~20 FMAs, backward stable.
+__device__ __forceinline__ void solve3(float A[9], float b[3]) {
+  const float d0 = A[0], i0 = __builtin_amdgcn_rcpf(d0);
+  const float l10 = A[3] * i0, l20 = A[6] * i0;
+  const float d1 = __builtin_fmaf(-l10, A[3], A[4]), i1 = __builtin_amdgcn_rcpf(d1);
+  const float l21 = __builtin_fmaf(-l20, A[3], A[7]) * i1;
+  const float d2 = A[8] - l20 * A[6] - l21 * l21 * d1, i2 = __builtin_amdgcn_rcpf(d2);
+  const float z0 = b[0], z1 = __builtin_fmaf(-l10, z0, b[1]);
+  const float z2 = b[2] - l20 * z0 - l21 * z1;
+  const float x2 = z2 * i2;
+  const float x1 = __builtin_fmaf(-l21, x2, z1 * i1);
+  const float x0 = z0 * i0 - l10 * x1 - l20 * x2;
+  b[0] = x0; b[1] = x1; b[2] = x2;
+}
+
+template <typename T, bool BAKED>
 __global__ void __launch_bounds__(64) ik_dls_kernel(IKSeg<T> c, int max_iters, T thr, T damping,
                                                     T step, const T* __restrict__ q_init,
                                                     const T* __restrict__ target,
@@ -129,11 +193,11 @@ __global__ void __launch_bounds__(64) ik_dls_kernel(IKSeg<T> c, int max_iters, T
   tg[0] = target[(size_t)b * 3]; tg[1] = target[(size_t)b * 3 + 1]; tg[2] = target[(size_t)b * 3 + 2];
 
   T site[3], anchor[7][3], axis[7][3];
-  ik_fk(c, q, site, anchor, axis);
+  ik_fk<T, BAKED>(c, q, site, anchor, axis);
   int converged = 0, iters = 0;
   for (int i = 0; i < max_iters; i++) {
     const T e0 = tg[0] - site[0], e1 = tg[1] - site[1], e2 = tg[2] - site[2];
-    const T n = sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+    const T n = KMath<T>::sqrt(e0 * e0 + e1 * e1 + e2 * e2);
     if (n < thr) {
       converged = 1;
       iters = i + 1;
@@ -166,13 +230,13 @@ __global__ void __launch_bounds__(64) ik_dls_kernel(IKSeg<T> c, int max_iters, T
     for (int j = 0; j < 7; j++) {
       T dq = J[0][j] * y[0] + J[1][j] * y[1] + J[2][j] * y[2];
       dq = fmin(fmax(dq, -step), step);
-      q[j] = fmin(fmax(q[j] + dq, c.lo[j]), c.hi[j]);
+      q[j] = fmin(fmax(q[j] + dq, IK_CONST(kLo, lo, [j])), IK_CONST(kHi, hi, [j]));
     }
-    ik_fk(c, q, site, anchor, axis);
+    ik_fk<T, BAKED>(c, q, site, anchor, axis);
     iters = i + 1;
   }
   const T d0 = site[0] - tg[0], d1 = site[1] - tg[1], d2 = site[2] - tg[2];
-  const T err = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+  const T err = KMath<T>::sqrt(d0 * d0 + d1 * d1 + d2 * d2);
 #pragma unroll
   for (int j = 0; j < 7; j++) q_out[(size_t)b * 7 + j] = q[j];
   final_pos[(size_t)b * 3] = site[0];
@@ -245,6 +309,23 @@ static int32_t build_segments(const pnp_model* M, int site, IKSeg<double>* out) 
   return PNP_OK;
 }
 
+// The baked kernel is used only when the runtime chain is the generated one (same site body,
+// every constant within 1e-12); any other model/site runs the kernel-argument path.
+static bool matches_baked(const IKSeg<double>& s, int site_body) {
+  using namespace panda_chain;
+  if (site_body != kSiteBody) return false;
+  auto near = [](double a, double b) { return fabs(a - b) <= 1e-12; };
+  for (int j = 0; j < 7; j++) {
+    for (int t = 0; t < 9; t++) if (!near(s.Rpre[j][t], kRpre[j][t])) return false;
+    for (int t = 0; t < 3; t++) if (!near(s.ppre[j][t], kPpre[j][t])) return false;
+    if (!near(s.sgn[j], kSgn[j]) || !near(s.lo[j], kLo[j]) || !near(s.hi[j], kHi[j]) ||
+        !near(s.qpos0[j], kQpos0[j]))
+      return false;
+  }
+  for (int t = 0; t < 3; t++) if (!near(s.psite[t], kPsite[t])) return false;
+  return true;
+}
+
 template <typename T>
 static int32_t launch_ik(pnp_model* model, int32_t site, pnp_ik_params prm, const T* q_init,
                          const T* target, T* q_out, T* final_pos, T* pos_error, int32_t* iterations,
@@ -275,7 +356,9 @@ static int32_t launch_ik(pnp_model* model, int32_t site, pnp_ik_params prm, cons
     s.qpos0[j] = (T)s64.qpos0[j];
   }
   for (int t = 0; t < 3; t++) s.psite[t] = (T)s64.psite[t];
-  hipLaunchKernelGGL(ik_dls_kernel<T>, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, s,
+  const bool baked = matches_baked(s64, model->h.site_bodyid[site]);
+  auto kern = baked ? ik_dls_kernel<T, true> : ik_dls_kernel<T, false>;
+  hipLaunchKernelGGL(kern, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, s,
                      prm.max_iters, (T)prm.pos_thresh, (T)prm.damping, (T)prm.step_limit, q_init,
                      target, q_out, final_pos, pos_error, iterations, flags, B);
   return pnp_check_launch("ik_dls_kernel");
