@@ -11,7 +11,7 @@ synthetic (Philox, seed 20250808, counter = global env index, so rank r owns env
     torchrun --nproc-per-node N bench.py --gpus N ...    (one process per GPU)
 
 Rank 0 prints ONE JSON line.  `value` = all ranks' solves / max-over-ranks wall time.
-`roofline` prices the ik_dls kernel at its algorithmic 92 B/solve against HBM peak, with the
+`roofline` prices the ik_dls kernel at its algorithmic 89 B/solve against HBM peak, with the
 kernel's average duration from HIP events on the launch stream.  `cpu_baseline` (rank 0, N=1)
 times the CPU oracle (fp64 C restatement of the same solve, all allowed host threads) on a
 bounded sample of the same inputs.
@@ -35,7 +35,7 @@ from pnp_amd.engine import get_engine  # noqa: E402
 
 BASELINE_METRIC = "env-steps/sec @4096 envs/GPU, 1/2/4/8 MI355X; DLS-IK solves/sec"
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
-IK_BYTES_PER_SOLVE = 92         # q_init 28 + target 12 in; q 28 + final_pos 12 + err 4 + iters 4 + flags 4 out
+IK_BYTES_PER_SOLVE = 89         # q_init 28 + target 12 in; q 28 + final_pos 12 + err 4 + iters 4 + flags 1 out
 
 
 def host_threads():
@@ -159,7 +159,7 @@ def main():
         },
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                     "kernel": "ik_dls_kernel<float>", "kernel_avg_ms": kern_ms,
+                     "kernel": "ik_dls_kernel<float, true>", "kernel_avg_ms": kern_ms,
                      "algorithmic_bytes_per_launch": IK_BYTES_PER_SOLVE * B},
         "ik_stats": {"mean_iterations": float(iters.mean()), "max_iterations": int(iters.max()),
                      "converged_frac": float((fl & 1).astype(bool).mean()),
