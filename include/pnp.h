@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 1
+#define PNP_ABI_VERSION 2
 
 #define PNP_OK 0
 #define PNP_ERR_ARG -1
@@ -59,6 +59,9 @@ typedef struct pnp_model_desc {
   const double* body_iquat;   /* [nbody*4] */
   const double* body_mass;    /* [nbody]   */
   const double* body_inertia; /* [nbody*3] */
+  const double* body_invweight0;   /* [nbody*2] mj_setConst: mean diag of J M^-1 J^T (tran, rot) */
+  const double* body_subtreemass;  /* [nbody] */
+  const int32_t* body_treedepth;   /* [nbody] depth below the world (world = 0) */
   /* joints [njnt]: type 0 free, 1 ball, 2 slide, 3 hinge (mjtJoint) */
   const int32_t* jnt_type;
   const int32_t* jnt_qposadr;
@@ -68,11 +71,16 @@ typedef struct pnp_model_desc {
   const double* jnt_pos;      /* [njnt*3] */
   const double* jnt_axis;     /* [njnt*3] */
   const double* jnt_range;    /* [njnt*2] */
+  const double* jnt_solref;   /* [njnt*2] solreflimit */
+  const double* jnt_solimp;   /* [njnt*5] solimplimit */
+  const double* jnt_margin;   /* [njnt]   */
   /* dofs [nv] */
   const int32_t* dof_jntid;
   const int32_t* dof_bodyid;
   const double* dof_armature;
   const double* dof_damping;
+  const int32_t* dof_parentid;  /* [nv] parent dof in the tree, -1 at a tree root */
+  const double* dof_invweight0; /* [nv] mj_setConst: diag(M^-1) at qpos0 (free joints averaged) */
   const double* qpos0;        /* [nq] */
   /* geoms [ngeom]: type 0 plane, 2 sphere, 6 box, 7 mesh (mjtGeom) */
   const int32_t* geom_type;
@@ -90,6 +98,8 @@ typedef struct pnp_model_desc {
   const double* geom_solimp;   /* [ngeom*5] */
   const double* geom_margin;
   const double* geom_gap;
+  const double* geom_solmix;
+  const double* geom_rbound;   /* bounding-sphere radius (0 for planes) */
   /* convex-hull meshes */
   const int32_t* mesh_vertadr; /* [nmesh] */
   const int32_t* mesh_vertnum; /* [nmesh] */
@@ -173,6 +183,60 @@ int32_t pnp_ik_dls_f64(pnp_model* model, int32_t site_id, pnp_ik_params params,
                        const double* q_init, const double* target, double* q_out,
                        double* final_pos, double* pos_error, int32_t* iterations, uint8_t* flags,
                        int32_t B, void* stream);
+
+
+/* ------------------------------------------------------------------ physics step (mj_step) */
+/* Per-env simulation state, SoA device arrays [B, n] (MjData fields of the same names). */
+typedef struct pnp_state {
+  float* qpos;            /* [B*nq] */
+  float* qvel;            /* [B*nv] */
+  float* ctrl;            /* [B*nu] */
+  float* mocap_pos;       /* [B*nmocap*3] */
+  float* mocap_quat;      /* [B*nmocap*4] wxyz */
+  float* qacc_warmstart;  /* [B*nv] */
+  float* time;            /* [B] */
+  uint32_t* warn;         /* [B] PNP_WARN_* bits, sticky */
+} pnp_state;
+typedef struct pnp_state_f64 {
+  double* qpos; double* qvel; double* ctrl; double* mocap_pos; double* mocap_quat;
+  double* qacc_warmstart; double* time; uint32_t* warn;
+} pnp_state_f64;
+
+/* warn bits (mjtWarning subset); bad state triggers mj_resetData semantics for that env */
+#define PNP_WARN_BADQPOS 1u
+#define PNP_WARN_BADQVEL 2u
+#define PNP_WARN_BADQACC 4u
+#define PNP_WARN_CONTACTFULL 8u
+#define PNP_WARN_CNSTRFULL 16u
+
+/* nsub x mj_step on every env, in place (reference envs/panda_env.py:355-358 calls this with
+ * nsub = 25, ten times; skills/base.py:43 and scripts/execute_pnp.py:103 with nsub = 1).
+ * ctrl and mocap are held constant over the nsub sub-steps, as in the reference. */
+int32_t pnp_step(pnp_model* model, const pnp_state* state, int32_t B, int32_t nsub, void* stream);
+int32_t pnp_step_f64(pnp_model* model, const pnp_state_f64* state, int32_t B, int32_t nsub, void* stream);
+
+/* Debug/parity: one mj_forward per env (state not advanced), dumping intermediates into
+ * dbg[B * PNP_DBG_SIZE] (float64, device) at the offsets below. */
+#define PNP_DBG_QM 0            /* nv*nv dense joint-space inertia (incl. armature) */
+#define PNP_DBG_BIAS 1296       /* qfrc_bias[nv] */
+#define PNP_DBG_ACT 1332        /* qfrc_actuator[nv] */
+#define PNP_DBG_QACC_SMOOTH 1368
+#define PNP_DBG_QACC 1404
+#define PNP_DBG_COUNTS 1440     /* ncon, nefc, solver iterations, warn */
+#define PNP_DBG_CON 1444        /* ncon x 16: pos3 frame9 dist geom1 geom2 dim */
+#define PNP_DBG_CON_STRIDE 16
+#define PNP_DBG_EFC_FORCE 1892  /* nefc (<= 128) */
+#define PNP_DBG_EFC_POS 2020
+#define PNP_DBG_EFC_D 2148
+#define PNP_DBG_EFC_AREF 2276
+#define PNP_DBG_EFC_TYPE 2404
+#define PNP_DBG_EFC_J 2532      /* nefc x nv dense */
+#define PNP_DBG_SIZE 7168
+int32_t pnp_forward_debug(pnp_model* model, const pnp_state* state, int32_t B, double* dbg, void* stream);
+int32_t pnp_forward_debug_f64(pnp_model* model, const pnp_state_f64* state, int32_t B, double* dbg,
+                              void* stream);
+/* LDS bytes one env occupies in the step kernel (fp64 != 0: the debug instantiation). */
+int32_t pnp_step_lds_bytes(int32_t fp64);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,291 @@
+// collide_dev.h — narrowphase colliders of the step kernel (included by step.hip).
+// Same algorithms, same contact conventions as oracle/collision.c (normal from geom1 to geom2,
+// contact point midway between the surfaces, MuJoCo mj_contactParam mixing):
+//   plane-sphere, plane-box (corners below the plane, <= 4), plane-mesh (<= 4 deepest hull
+//   vertices), sphere-sphere, sphere-box, box-box (SAT over 15 axes + reference/incident face
+//   clipping, edge-edge).  Convex mesh vs non-plane: not yet (as in the oracle: no contact).
+// One lane runs one candidate pair; results stay in the lane's registers/scratch until the
+// wave-wide scan places them.
+#pragma once
+
+template <typename T>
+__device__ __forceinline__ void c_set_normal(Con<T>& c, const T n[3]) {
+  for (int k = 0; k < 9; k++) c.frame[k] = 0;
+  c.frame[0] = n[0]; c.frame[1] = n[1]; c.frame[2] = n[2];
+}
+
+template <typename T>
+__device__ int c_plane_sphere(const T* p1, const T* R1, const T* p2, T r, T margin, Con<T>* c) {
+  const T n[3] = {R1[2], R1[5], R1[8]}, v[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  const T dist = t_dot3(v, n) - r;
+  if (dist > margin) return 0;
+  c[0].dist = dist;
+  c_set_normal(c[0], n);
+  for (int k = 0; k < 3; k++) c[0].pos[k] = p2[k] - n[k] * (r + dist * T(0.5));
+  return 1;
+}
+
+template <typename T>
+__device__ int c_plane_box(const T* p1, const T* R1, const T* p2, const T* R2, const T* s, T margin, Con<T>* c) {
+  const T n[3] = {R1[2], R1[5], R1[8]}, v[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  const T dist = t_dot3(v, n);
+  int cnt = 0;
+  for (int i = 0; i < 8; i++) {
+    const T cr[3] = {(i & 1) ? s[0] : -s[0], (i & 2) ? s[1] : -s[1], (i & 4) ? s[2] : -s[2]};
+    T w[3];
+    d_mulmatvec3(w, R2, cr);
+    const T ld = t_dot3(n, w);
+    if (dist + ld > margin || ld > 0) continue;
+    c[cnt].dist = dist + ld;
+    c_set_normal(c[cnt], n);
+    for (int k = 0; k < 3; k++) c[cnt].pos[k] = w[k] + p2[k] - n[k] * c[cnt].dist * T(0.5);
+    if (++cnt >= 4) return 4;
+  }
+  return cnt;
+}
+
+template <typename T>
+__device__ int c_plane_mesh(const DevPhys<T>& m, const T* p1, const T* R1, const T* p2, const T* R2, int mesh, T margin,
+                            Con<T>* c) {
+  const T n[3] = {R1[2], R1[5], R1[8]};
+  const int a = m.mesh_vertadr[mesh], nv = m.mesh_vertnum[mesh];
+  T best[4];
+  int bi[4], cnt = 0;
+  for (int i = 0; i < nv; i++) {
+    T w[3];
+    d_mulmatvec3(w, R2, m.mesh_vert[a + i]);
+    const T dd = (w[0] + p2[0] - p1[0]) * n[0] + (w[1] + p2[1] - p1[1]) * n[1] + (w[2] + p2[2] - p1[2]) * n[2];
+    if (dd > margin) continue;
+    int pos = cnt < 4 ? cnt : 4;
+    while (pos > 0 && best[pos - 1] > dd) pos--;
+    if (pos >= 4) continue;
+    for (int k = (cnt < 4 ? cnt : 3); k > pos; k--) { best[k] = best[k - 1]; bi[k] = bi[k - 1]; }
+    best[pos] = dd;
+    bi[pos] = i;
+    if (cnt < 4) cnt++;
+  }
+  for (int k = 0; k < cnt; k++) {
+    T w[3];
+    d_mulmatvec3(w, R2, m.mesh_vert[a + bi[k]]);
+    c[k].dist = best[k];
+    c_set_normal(c[k], n);
+    for (int t = 0; t < 3; t++) c[k].pos[t] = w[t] + p2[t] - n[t] * best[k] * T(0.5);
+  }
+  return cnt;
+}
+
+template <typename T>
+__device__ int c_sphere_sphere(const T* p1, T r1, const T* p2, T r2, T margin, Con<T>* c) {
+  T n[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  const T len = PM<T>::sqrt_(t_dot3(n, n));
+  const T dist = len - r1 - r2;
+  if (dist > margin) return 0;
+  if (len < T(1e-15)) { n[0] = 1; n[1] = 0; n[2] = 0; }
+  else { n[0] /= len; n[1] /= len; n[2] /= len; }
+  c[0].dist = dist;
+  c_set_normal(c[0], n);
+  for (int k = 0; k < 3; k++) c[0].pos[k] = p1[k] + n[k] * (r1 + dist * T(0.5));
+  return 1;
+}
+
+template <typename T>
+__device__ int c_sphere_box(const T* p1, T r, const T* p2, const T* R2, const T* s, T margin, Con<T>* c) {
+  const T v[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+  T lc[3], cl[3], nl[3], n[3];
+  t_mulmattvec3(lc, R2, v);
+  bool inside = true;
+  for (int k = 0; k < 3; k++) {
+    cl[k] = fmin(fmax(lc[k], -s[k]), s[k]);
+    if (cl[k] != lc[k]) inside = false;
+  }
+  T dist;
+  if (!inside) {
+    for (int k = 0; k < 3; k++) nl[k] = cl[k] - lc[k];
+    const T dd = PM<T>::sqrt_(t_dot3(nl, nl));
+    dist = dd - r;
+    if (dist > margin) return 0;
+    for (int k = 0; k < 3; k++) nl[k] /= dd;
+  } else {
+    int kk = 0;
+    T pen = s[0] - fabs(lc[0]);
+    for (int k = 1; k < 3; k++)
+      if (s[k] - fabs(lc[k]) < pen) { pen = s[k] - fabs(lc[k]); kk = k; }
+    nl[0] = nl[1] = nl[2] = 0;
+    nl[kk] = lc[kk] >= 0 ? T(-1) : T(1);
+    dist = -(pen + r);
+  }
+  d_mulmatvec3(n, R2, nl);
+  c[0].dist = dist;
+  c_set_normal(c[0], n);
+  for (int k = 0; k < 3; k++) c[0].pos[k] = p1[k] + n[k] * (r + dist * T(0.5));
+  return 1;
+}
+
+template <typename T>
+__device__ int c_clip(T (*poly)[3], int np, int axis, T sgn, T lim, T (*out)[3]) {
+  int no = 0;
+  for (int i = 0; i < np; i++) {
+    const T* a = poly[i];
+    const T* b = poly[(i + 1) % np];
+    const T da = sgn * a[axis] - lim, db = sgn * b[axis] - lim;
+    if (da <= 0) { out[no][0] = a[0]; out[no][1] = a[1]; out[no][2] = a[2]; no++; }
+    if ((da < 0 && db > 0) || (da > 0 && db < 0)) {
+      const T t = da / (da - db);
+      for (int k = 0; k < 3; k++) out[no][k] = a[k] + t * (b[k] - a[k]);
+      no++;
+    }
+  }
+  return no;
+}
+
+template <typename T>
+__device__ int c_box_face(const T* pr, const T* Rr, const T* sr, int ia, const T* nr, const T* pi, const T* Ri,
+                          const T* si, const T* nframe, T margin, Con<T>* c) {
+  const int iu = (ia + 1) % 3, iv = (ia + 2) % 3;
+  const T u[3] = {Rr[iu], Rr[3 + iu], Rr[6 + iu]}, v[3] = {Rr[iv], Rr[3 + iv], Rr[6 + iv]};
+  T cref[3];
+  for (int k = 0; k < 3; k++) cref[k] = pr[k] + nr[k] * sr[ia];
+  int ja = 0;
+  T best = -1;
+  for (int j = 0; j < 3; j++) {
+    const T a = fabs(Ri[j] * nr[0] + Ri[3 + j] * nr[1] + Ri[6 + j] * nr[2]);
+    if (a > best) { best = a; ja = j; }
+  }
+  const T bj[3] = {Ri[ja], Ri[3 + ja], Ri[6 + ja]};
+  const T sg = t_dot3(bj, nr) > 0 ? T(-1) : T(1);
+  const int ju = (ja + 1) % 3, jv = (ja + 2) % 3;
+  const T bu[3] = {Ri[ju], Ri[3 + ju], Ri[6 + ju]}, bv[3] = {Ri[jv], Ri[3 + jv], Ri[6 + jv]};
+  T poly[8][3], tmp[8][3];
+  const T su[4] = {1, -1, -1, 1}, sv[4] = {1, 1, -1, -1};
+  for (int q = 0; q < 4; q++) {
+    T w[3];
+    for (int k = 0; k < 3; k++) w[k] = pi[k] + sg * bj[k] * si[ja] + su[q] * bu[k] * si[ju] + sv[q] * bv[k] * si[jv] - cref[k];
+    poly[q][0] = t_dot3(w, u); poly[q][1] = t_dot3(w, v); poly[q][2] = t_dot3(w, nr);
+  }
+  int np = 4;
+  np = c_clip(poly, np, 0, T(1), sr[iu], tmp);
+  np = c_clip(tmp, np, 0, T(-1), sr[iu], poly);
+  np = c_clip(poly, np, 1, T(1), sr[iv], tmp);
+  np = c_clip(tmp, np, 1, T(-1), sr[iv], poly);
+  int cnt = 0;
+  for (int q = 0; q < np && cnt < 8; q++) {
+    const T dist = poly[q][2];
+    if (dist > margin) continue;
+    c[cnt].dist = dist;
+    c_set_normal(c[cnt], nframe);
+    for (int k = 0; k < 3; k++) c[cnt].pos[k] = cref[k] + u[k] * poly[q][0] + v[k] * poly[q][1] + nr[k] * poly[q][2] * T(0.5);
+    cnt++;
+  }
+  return cnt;
+}
+
+template <typename T>
+__device__ int c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, const T* R2, const T* s2, T margin, Con<T>* c) {
+  const T Tv[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  T A[3][3], Bm[3][3], AB[3][3];
+  for (int i = 0; i < 3; i++)
+    for (int k = 0; k < 3; k++) { A[i][k] = R1[3 * k + i]; Bm[i][k] = R2[3 * k + i]; }
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) AB[i][j] = t_dot3(A[i], Bm[j]);
+  T best = T(-1e30), bestn[3] = {0, 0, 0};
+  int btype = -1, bi = 0, bj = 0;
+  for (int i = 0; i < 3; i++) {
+    const T tl = t_dot3(Tv, A[i]);
+    const T rb = s2[0] * fabs(AB[i][0]) + s2[1] * fabs(AB[i][1]) + s2[2] * fabs(AB[i][2]);
+    const T sep = fabs(tl) - s1[i] - rb;
+    if (sep > margin) return 0;
+    if (sep > best) { best = sep; btype = 0; bi = i; for (int k = 0; k < 3; k++) bestn[k] = tl >= 0 ? A[i][k] : -A[i][k]; }
+  }
+  for (int j = 0; j < 3; j++) {
+    const T tl = t_dot3(Tv, Bm[j]);
+    const T ra = s1[0] * fabs(AB[0][j]) + s1[1] * fabs(AB[1][j]) + s1[2] * fabs(AB[2][j]);
+    const T sep = fabs(tl) - ra - s2[j];
+    if (sep > margin) return 0;
+    if (sep > best) { best = sep; btype = 1; bj = j; for (int k = 0; k < 3; k++) bestn[k] = tl >= 0 ? Bm[j][k] : -Bm[j][k]; }
+  }
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) {
+      T L[3];
+      t_cross(L, A[i], Bm[j]);
+      const T len = PM<T>::sqrt_(t_dot3(L, L));
+      if (len < T(1e-6)) continue;
+      for (int k = 0; k < 3; k++) L[k] /= len;
+      const T tl = t_dot3(Tv, L);
+      const T ra = s1[0] * fabs(t_dot3(A[0], L)) + s1[1] * fabs(t_dot3(A[1], L)) + s1[2] * fabs(t_dot3(A[2], L));
+      const T rb = s2[0] * fabs(t_dot3(Bm[0], L)) + s2[1] * fabs(t_dot3(Bm[1], L)) + s2[2] * fabs(t_dot3(Bm[2], L));
+      const T sep = fabs(tl) - ra - rb;
+      if (sep > margin) return 0;
+      if (T(1.05) * sep > best + T(1e-12)) {
+        best = sep; btype = 2; bi = i; bj = j;
+        for (int k = 0; k < 3; k++) bestn[k] = tl >= 0 ? L[k] : -L[k];
+      }
+    }
+  if (btype == 0) return c_box_face(p1, R1, s1, bi, bestn, p2, R2, s2, bestn, margin, c);
+  if (btype == 1) {
+    const T nr[3] = {-bestn[0], -bestn[1], -bestn[2]};
+    return c_box_face(p2, R2, s2, bj, nr, p1, R1, s1, bestn, margin, c);
+  }
+  T pa[3] = {p1[0], p1[1], p1[2]}, pb[3] = {p2[0], p2[1], p2[2]};
+  for (int t = 0; t < 3; t++) {
+    if (t != bi) {
+      const T sg = t_dot3(A[t], bestn) > 0 ? T(1) : T(-1);
+      for (int k = 0; k < 3; k++) pa[k] += sg * s1[t] * A[t][k];
+    }
+    if (t != bj) {
+      const T sg = t_dot3(Bm[t], bestn) > 0 ? T(-1) : T(1);
+      for (int k = 0; k < 3; k++) pb[k] += sg * s2[t] * Bm[t][k];
+    }
+  }
+  const T ua[3] = {A[bi][0], A[bi][1], A[bi][2]}, ub[3] = {Bm[bj][0], Bm[bj][1], Bm[bj][2]};
+  const T w[3] = {pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]};
+  const T a = t_dot3(ua, ub), dd = t_dot3(ua, w), e = t_dot3(ub, w), den = 1 - a * a;
+  T ta = 0, tb = 0;
+  if (den > T(1e-12)) { ta = (a * e - dd) / den; tb = (e - a * dd) / den; }
+  for (int k = 0; k < 3; k++) { pa[k] += ta * ua[k]; pb[k] += tb * ub[k]; }
+  c[0].dist = best;
+  c_set_normal(c[0], bestn);
+  for (int k = 0; k < 3; k++) c[0].pos[k] = T(0.5) * (pa[k] + pb[k]);
+  return 1;
+}
+
+template <typename T>
+__device__ void c_params(const DevPhys<T>& m, Con<T>& c, int g1, int g2) {
+  c.g1 = g1;
+  c.g2 = g2;
+  c.dim = max(m.geom_condim[g1], m.geom_condim[g2]);
+  if (m.geom_priority[g1] != m.geom_priority[g2]) c.dim = m.geom_priority[g1] > m.geom_priority[g2] ? m.geom_condim[g1] : m.geom_condim[g2];
+  T f[3];
+  for (int k = 0; k < 3; k++) f[k] = fmax(m.geom_friction[g1][k], m.geom_friction[g2][k]);
+  c.friction[0] = c.friction[1] = f[0];
+  c.friction[2] = f[1];
+  c.friction[3] = c.friction[4] = f[2];
+  const T s1 = m.geom_solmix[g1], s2 = m.geom_solmix[g2];
+  T mix;
+  if (s1 >= T(1e-15) && s2 >= T(1e-15)) mix = s1 / (s1 + s2);
+  else if (s1 < T(1e-15) && s2 < T(1e-15)) mix = T(0.5);
+  else mix = s1 < T(1e-15) ? T(0) : T(1);
+  if (m.geom_solref[g1][0] > 0 && m.geom_solref[g2][0] > 0)
+    for (int k = 0; k < 2; k++) c.solref[k] = mix * m.geom_solref[g1][k] + (1 - mix) * m.geom_solref[g2][k];
+  else
+    for (int k = 0; k < 2; k++) c.solref[k] = fmin(m.geom_solref[g1][k], m.geom_solref[g2][k]);
+  for (int k = 0; k < 5; k++) c.solimp[k] = mix * m.geom_solimp[g1][k] + (1 - mix) * m.geom_solimp[g2][k];
+  c.includemargin = fmax(m.geom_margin[g1], m.geom_margin[g2]) - fmax(m.geom_gap[g1], m.geom_gap[g2]);
+}
+
+template <typename T>
+__device__ int collide_pair(const DevPhys<T>& m, const Env<T>& s, int pair, Con<T>* out) {
+  const int g1 = m.pair_g1[pair], g2 = m.pair_g2[pair];
+  const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+  const T *p1 = s.gpos[g1], *R1 = s.gmat[g1], *s1 = m.geom_size[g1];
+  const T *p2 = s.gpos[g2], *R2 = s.gmat[g2], *s2 = m.geom_size[g2];
+  const T margin = fmax(m.geom_margin[g1], m.geom_margin[g2]);
+  int n = 0;
+  if (t1 == 0 && t2 == 2) n = c_plane_sphere(p1, R1, p2, s2[0], margin, out);
+  else if (t1 == 0 && t2 == 6) n = c_plane_box(p1, R1, p2, R2, s2, margin, out);
+  else if (t1 == 0 && t2 == 7) n = c_plane_mesh(m, p1, R1, p2, R2, m.geom_dataid[g2], margin, out);
+  else if (t1 == 2 && t2 == 2) n = c_sphere_sphere(p1, s1[0], p2, s2[0], margin, out);
+  else if (t1 == 2 && t2 == 6) n = c_sphere_box(p1, s1[0], p2, R2, s2, margin, out);
+  else if (t1 == 6 && t2 == 6) n = c_box_box(p1, R1, s1, p2, R2, s2, margin, out);
+  for (int k = 0; k < n; k++) c_params(m, out[k], g1, g2);
+  return n;
+}

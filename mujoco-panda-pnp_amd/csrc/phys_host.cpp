@@ -1,0 +1,250 @@
+// phys_host.cpp — builds the DevPhys<T> device image (phys_model.h) from pnp_model_desc.
+//
+// Host-side model compilation for the step kernel (the part of MuJoCo's compiler/mj_setConst
+// the kernel relies on, plus the lane-parallel index tables).  Collision pair filtering follows
+// MuJoCo 2.3.3 mj_collision: contype/conaffinity bitmask, same weld body (incl. static-static),
+// weld parent/child when both are non-world (filterparent).  Pairs are kept in (g1 < g2) model
+// order with g1 the lower geom type, the order the CPU oracle visits them.
+#include <cstdio>
+#include <cstring>
+
+#include "phys_model.h"
+#include "pnp_internal.h"
+
+template <typename T>
+int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
+  memset(d, 0, sizeof(*d));
+  if (s->nbody > PH_MAXB || s->njnt > PH_MAXJ || s->nv > PH_MAXV || s->nq > PH_MAXQ || s->nu > PH_MAXU ||
+      s->neq > 4 || s->nmocap > 2 || s->nbody > 32 || s->nv > 64 || s->nmesh > PH_MAXMESH ||
+      s->nmeshvert > PH_MAXMESHV) {
+    snprintf(err, errlen, "model exceeds the step kernel's compiled capacity");
+    return -1;
+  }
+  d->nq = s->nq; d->nv = s->nv; d->nu = s->nu; d->nbody = s->nbody; d->njnt = s->njnt;
+  d->nmocap = s->nmocap; d->neq = s->neq;
+  d->timestep = (T)s->timestep;
+  for (int k = 0; k < 3; k++) d->gravity[k] = (T)s->gravity[k];
+  d->noslip_iterations = s->noslip_iterations;
+  d->iterations = s->iterations;
+  // ---- bodies
+  for (int b = 0; b < s->nbody; b++) {
+    d->body_parentid[b] = s->body_parentid[b];
+    d->body_rootid[b] = s->body_rootid[b];
+    d->body_weldid[b] = s->body_weldid[b];
+    d->body_mocapid[b] = s->body_mocapid[b];
+    d->body_jntadr[b] = s->body_jntadr[b];
+    d->body_jntnum[b] = s->body_jntnum[b];
+    d->body_dofadr[b] = s->body_dofadr[b];
+    d->body_dofnum[b] = s->body_dofnum[b];
+    for (int k = 0; k < 3; k++) {
+      d->body_pos[b][k] = (T)s->body_pos[3 * b + k];
+      d->body_ipos[b][k] = (T)s->body_ipos[3 * b + k];
+      d->body_inertia[b][k] = (T)s->body_inertia[3 * b + k];
+    }
+    for (int k = 0; k < 4; k++) {
+      d->body_quat[b][k] = (T)s->body_quat[4 * b + k];
+      d->body_iquat[b][k] = (T)s->body_iquat[4 * b + k];
+    }
+    d->body_mass[b] = (T)s->body_mass[b];
+    d->body_invweight0[b][0] = (T)s->body_invweight0[2 * b];
+    d->body_invweight0[b][1] = (T)s->body_invweight0[2 * b + 1];
+    d->body_subtreemass[b] = (T)s->body_subtreemass[b];
+    // root -> body path (world excluded)
+    int path[PH_MAXDEPTH + 1], n = 0;
+    for (int c = b; c > 0; c = s->body_parentid[c]) {
+      if (n >= PH_MAXDEPTH) { snprintf(err, errlen, "tree deeper than %d", PH_MAXDEPTH); return -1; }
+      path[n++] = c;
+    }
+    d->body_pathlen[b] = n;
+    for (int k = 0; k < n; k++) d->body_path[b][k] = path[n - 1 - k];
+    uint64_t dm = 0;
+    for (int k = 0; k < n; k++) {
+      int c = path[k];
+      for (int q = 0; q < s->body_dofnum[c]; q++) dm |= 1ull << (s->body_dofadr[c] + q);
+    }
+    d->body_dofmask[b] = dm;
+  }
+  for (int b = 0; b < s->nbody; b++) {
+    uint32_t st = 0;
+    for (int c = 0; c < s->nbody; c++) {
+      int x = c;
+      while (x > 0 && x != b) x = s->body_parentid[x];
+      if (x == b && (b > 0 || c == 0)) st |= 1u << c;
+    }
+    d->body_subtree[b] = st;
+  }
+  // ---- trees: root bodies (children of the world) whose subtree has dofs; dofs contiguous
+  int ntree = 0;
+  for (int b = 0; b < s->nbody; b++) d->body_tree[b] = -1;
+  for (int r = 1; r < s->nbody; r++) {
+    if (s->body_parentid[r] != 0) continue;
+    int lo = 1 << 30, hi = -1;
+    for (int c = 0; c < s->nbody; c++)
+      if (d->body_subtree[r] >> c & 1)
+        for (int q = 0; q < s->body_dofnum[c]; q++) {
+          int dof = s->body_dofadr[c] + q;
+          if (dof < lo) lo = dof;
+          if (dof > hi) hi = dof;
+        }
+    if (hi < 0) continue;
+    if (ntree >= PH_MAXT || hi - lo + 1 > PH_MAXTDOF) { snprintf(err, errlen, "too many trees / tree dofs"); return -1; }
+    d->tree_dofadr[ntree] = lo;
+    d->tree_dofnum[ntree] = hi - lo + 1;
+    for (int c = 0; c < s->nbody; c++)
+      if (d->body_subtree[r] >> c & 1) d->body_tree[c] = ntree;
+    ntree++;
+  }
+  d->ntree = ntree;
+  int moff = 0;
+  for (int t = 0; t < ntree; t++) {
+    d->tree_moff[t] = moff;
+    moff += d->tree_dofnum[t] * d->tree_dofnum[t];
+  }
+  if (moff > PH_MAXMBLK) { snprintf(err, errlen, "tree mass-matrix blocks exceed capacity"); return -1; }
+  d->nmblock = moff;
+  // ---- joints
+  for (int j = 0; j < s->njnt; j++) {
+    d->jnt_type[j] = s->jnt_type[j];
+    d->jnt_qposadr[j] = s->jnt_qposadr[j];
+    d->jnt_dofadr[j] = s->jnt_dofadr[j];
+    d->jnt_bodyid[j] = s->jnt_bodyid[j];
+    d->jnt_limited[j] = s->jnt_limited[j];
+    for (int k = 0; k < 3; k++) {
+      d->jnt_pos[j][k] = (T)s->jnt_pos[3 * j + k];
+      d->jnt_axis[j][k] = (T)s->jnt_axis[3 * j + k];
+    }
+    for (int k = 0; k < 2; k++) {
+      d->jnt_range[j][k] = (T)s->jnt_range[2 * j + k];
+      d->jnt_solref[j][k] = (T)s->jnt_solref[2 * j + k];
+    }
+    for (int k = 0; k < 5; k++) d->jnt_solimp[j][k] = (T)s->jnt_solimp[5 * j + k];
+    d->jnt_margin[j] = (T)s->jnt_margin[j];
+    if (s->jnt_type[j] == 1) { snprintf(err, errlen, "ball joints not supported by the step kernel"); return -1; }
+  }
+  // ---- dofs
+  for (int i = 0; i < s->nv; i++) {
+    d->dof_bodyid[i] = s->dof_bodyid[i];
+    d->dof_jntid[i] = s->dof_jntid[i];
+    d->dof_parentid[i] = s->dof_parentid[i];
+    d->dof_tree[i] = d->body_tree[s->dof_bodyid[i]];
+    d->dof_armature[i] = (T)s->dof_armature[i];
+    d->dof_damping[i] = (T)s->dof_damping[i];
+    d->dof_invweight0[i] = (T)s->dof_invweight0[i];
+    // cvel used for cdof_dot: all strict ancestors; for the rotational dofs of a free joint the
+    // ancestors of the joint plus its translational dofs (MuJoCo mj_comVel free/ball case)
+    uint64_t vm = 0;
+    int j = s->dof_jntid[i], first = s->jnt_dofadr[j];
+    if (s->jnt_type[j] == 0 && i >= first + 3) {
+      for (int a = s->dof_parentid[first]; a >= 0; a = s->dof_parentid[a]) vm |= 1ull << a;
+      for (int q = 0; q < 3; q++) vm |= 1ull << (first + q);
+    } else {
+      for (int a = s->dof_parentid[i]; a >= 0; a = s->dof_parentid[a]) vm |= 1ull << a;
+    }
+    d->dof_velmask[i] = vm;
+  }
+  for (int i = 0; i < s->nq; i++) d->qpos0[i] = (T)s->qpos0[i];
+  int ne = 0;
+  for (int i = 0; i < s->nv; i++)
+    for (int j = i; j >= 0; j = s->dof_parentid[j]) {
+      if (ne >= PH_MAXMENTRY) { snprintf(err, errlen, "too many M entries"); return -1; }
+      d->mentry_i[ne] = i;
+      d->mentry_j[ne] = j;
+      ne++;
+    }
+  d->nmentry = ne;
+  T mi = 0;
+  d->meaninertia = mi;
+  // ---- collidable geoms + pairs
+  int ng = 0, map[512];
+  for (int g = 0; g < s->ngeom && g < 512; g++) {
+    map[g] = -1;
+    if (!s->geom_contype[g] && !s->geom_conaffinity[g]) continue;
+    if (ng >= PH_MAXG) { snprintf(err, errlen, "too many collidable geoms"); return -1; }
+    map[g] = ng;
+    d->geom_id[ng] = g;
+    d->geom_type[ng] = s->geom_type[g];
+    d->geom_bodyid[ng] = s->geom_bodyid[g];
+    d->geom_dataid[ng] = s->geom_dataid[g];
+    d->geom_condim[ng] = s->geom_condim[g];
+    d->geom_priority[ng] = s->geom_priority[g];
+    for (int k = 0; k < 3; k++) {
+      d->geom_size[ng][k] = (T)s->geom_size[3 * g + k];
+      d->geom_pos[ng][k] = (T)s->geom_pos[3 * g + k];
+      d->geom_friction[ng][k] = (T)s->geom_friction[3 * g + k];
+    }
+    for (int k = 0; k < 4; k++) d->geom_quat[ng][k] = (T)s->geom_quat[4 * g + k];
+    for (int k = 0; k < 2; k++) d->geom_solref[ng][k] = (T)s->geom_solref[2 * g + k];
+    for (int k = 0; k < 5; k++) d->geom_solimp[ng][k] = (T)s->geom_solimp[5 * g + k];
+    d->geom_margin[ng] = (T)s->geom_margin[g];
+    d->geom_gap[ng] = (T)s->geom_gap[g];
+    d->geom_solmix[ng] = (T)s->geom_solmix[g];
+    d->geom_rbound[ng] = (T)s->geom_rbound[g];
+    if (s->geom_type[g] != 0 && s->geom_type[g] != 2 && s->geom_type[g] != 6 && s->geom_type[g] != 7) {
+      snprintf(err, errlen, "geom type %d not supported by the step kernel", s->geom_type[g]);
+      return -1;
+    }
+    ng++;
+  }
+  d->ngeom = ng;
+  int np = 0;
+  for (int g1 = 0; g1 < s->ngeom; g1++) {
+    if (map[g1] < 0) continue;
+    for (int g2 = g1 + 1; g2 < s->ngeom; g2++) {
+      if (map[g2] < 0) continue;
+      int ct1 = s->geom_contype[g1], ca1 = s->geom_conaffinity[g1];
+      int ct2 = s->geom_contype[g2], ca2 = s->geom_conaffinity[g2];
+      if (!(ct1 & ca2) && !(ct2 & ca1)) continue;
+      int w1 = s->body_weldid[s->geom_bodyid[g1]], w2 = s->body_weldid[s->geom_bodyid[g2]];
+      if (w1 == w2) continue;
+      int p1 = s->body_weldid[s->body_parentid[w1]], p2 = s->body_weldid[s->body_parentid[w2]];
+      if (w1 != 0 && w2 != 0 && (w1 == p2 || w2 == p1)) continue;
+      if (np >= PH_MAXPAIR) { snprintf(err, errlen, "too many collision pairs"); return -1; }
+      int a = g1, b = g2;
+      if (s->geom_type[a] > s->geom_type[b]) { int t = a; a = b; b = t; }
+      d->pair_g1[np] = map[a];
+      d->pair_g2[np] = map[b];
+      np++;
+    }
+  }
+  d->npair = np;
+  for (int k = 0; k < s->nmesh; k++) {
+    d->mesh_vertadr[k] = s->mesh_vertadr[k];
+    d->mesh_vertnum[k] = s->mesh_vertnum[k];
+  }
+  for (int v = 0; v < s->nmeshvert; v++)
+    for (int k = 0; k < 3; k++) d->mesh_vert[v][k] = (T)s->mesh_vert[3 * v + k];
+  // ---- actuators
+  for (int i = 0; i < s->nu; i++) {
+    int j = s->actuator_trnid[i];
+    d->act_trnid[i] = j;
+    d->act_dof[i] = s->jnt_dofadr[j];
+    d->act_qadr[i] = s->jnt_qposadr[j];
+    d->act_biastype[i] = s->actuator_biastype[i];
+    d->act_ctrllimited[i] = s->actuator_ctrllimited[i];
+    d->act_forcelimited[i] = s->actuator_forcelimited[i];
+    d->act_gear[i] = (T)s->actuator_gear[i];
+    for (int k = 0; k < 3; k++) {
+      d->act_gainprm[i][k] = (T)s->actuator_gainprm[3 * i + k];
+      d->act_biasprm[i][k] = (T)s->actuator_biasprm[3 * i + k];
+    }
+    for (int k = 0; k < 2; k++) {
+      d->act_ctrlrange[i][k] = (T)s->actuator_ctrlrange[2 * i + k];
+      d->act_forcerange[i][k] = (T)s->actuator_forcerange[2 * i + k];
+    }
+  }
+  // ---- equality
+  for (int e = 0; e < s->neq; e++) {
+    d->eq_type[e] = s->eq_type[e];
+    d->eq_obj1id[e] = s->eq_obj1id[e];
+    d->eq_obj2id[e] = s->eq_obj2id[e];
+    for (int k = 0; k < 2; k++) d->eq_solref[e][k] = (T)s->eq_solref[2 * e + k];
+    for (int k = 0; k < 5; k++) d->eq_solimp[e][k] = (T)s->eq_solimp[5 * e + k];
+    for (int k = 0; k < 11; k++) d->eq_data[e][k] = (T)s->eq_data[11 * e + k];
+  }
+  for (int b = 0; b < s->nbody; b++)
+    if (s->body_mocapid[b] >= 0) d->mocap_body[s->body_mocapid[b]] = b;
+  return 0;
+}
+
+template int build_phys<float>(const pnp_model_desc*, DevPhys<float>*, char*, int);
+template int build_phys<double>(const pnp_model_desc*, DevPhys<double>*, char*, int);

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <new>
 
+#include "phys_model.h"
 #include "pnp_internal.h"
 
 static thread_local char g_err[512] = "";
@@ -110,6 +111,28 @@ extern "C" int32_t pnp_model_create(const pnp_model_desc* desc, pnp_model** out)
     delete m;
     return PNP_ERR_HIP;
   }
+  // physics images for the step kernel; a model outside the kernel's capacity keeps IK and
+  // kinematics working and reports the reason from pnp_step
+  m->p_f32 = nullptr;
+  m->p_f64 = nullptr;
+  m->phys_err[0] = 0;
+  DevPhys<float>* pf = new (std::nothrow) DevPhys<float>();
+  DevPhys<double>* pd = new (std::nothrow) DevPhys<double>();
+  if (pf && pd && build_phys(desc, pf, m->phys_err, sizeof(m->phys_err)) == 0 &&
+      build_phys(desc, pd, m->phys_err, sizeof(m->phys_err)) == 0) {
+    if (hipMalloc(&m->p_f32, sizeof(*pf)) == hipSuccess && hipMalloc(&m->p_f64, sizeof(*pd)) == hipSuccess &&
+        hipMemcpy(m->p_f32, pf, sizeof(*pf), hipMemcpyHostToDevice) == hipSuccess &&
+        hipMemcpy(m->p_f64, pd, sizeof(*pd), hipMemcpyHostToDevice) == hipSuccess) {
+    } else {
+      snprintf(m->phys_err, sizeof(m->phys_err), "device allocation of the physics image failed");
+      if (m->p_f32) (void)hipFree(m->p_f32);
+      if (m->p_f64) (void)hipFree(m->p_f64);
+      m->p_f32 = nullptr;
+      m->p_f64 = nullptr;
+    }
+  }
+  delete pf;
+  delete pd;
   *out = m;
   return PNP_OK;
 }
@@ -118,6 +141,8 @@ extern "C" int32_t pnp_model_destroy(pnp_model* model) {
   if (!model) return PNP_OK;
   (void)hipFree(model->d_f32);
   (void)hipFree(model->d_f64);
+  if (model->p_f32) (void)hipFree(model->p_f32);
+  if (model->p_f64) (void)hipFree(model->p_f64);
   delete model;
   return PNP_OK;
 }

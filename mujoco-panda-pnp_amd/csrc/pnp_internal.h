@@ -55,13 +55,27 @@ struct IKChain {
   T qpos0[7];
 };
 
+template <typename T> struct DevPhys;
+
 struct pnp_model {
   int device;
   DevModel<float>* d_f32;   // device images
   DevModel<double>* d_f64;
   DevModel<double> h;       // host copy (fp64) used to build chains
   double jnt_range[PNP_MAXJNT][2];
+  DevPhys<float>* p_f32;    // step-kernel images (null if the model is outside its capacity)
+  DevPhys<double>* p_f64;
+  char phys_err[160];
 };
+
+template <typename T> struct pnp_state_t {  // same layout as pnp_state / pnp_state_f64
+  T* qpos; T* qvel; T* ctrl; T* mocap_pos; T* mocap_quat; T* qacc_warmstart; T* time; uint32_t* warn;
+};
+
+template <typename T> const DevPhys<T>* phys_image(const pnp_model* m);
+template <> inline const DevPhys<float>* phys_image<float>(const pnp_model* m) { return m->p_f32; }
+template <> inline const DevPhys<double>* phys_image<double>(const pnp_model* m) { return m->p_f64; }
+template <typename T> int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen);
 
 // ---------------------------------------------------------------------------- error plumbing
 void pnp_set_error(const char* fmt, ...);

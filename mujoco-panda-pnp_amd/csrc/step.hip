@@ -1,0 +1,1354 @@
+// step.hip — batched mj_step for the shelf_pnp scene: one 64-lane wave per env, K sub-steps
+// fused per launch with the whole per-env state resident in LDS.
+//
+// Reference: envs/panda_env.py:355-358 (_mujoco_step: 10 x mj_step(nstep=25)),
+// skills/base.py:39-46 (_step_sim), scripts/execute_pnp.py:102-107; MuJoCo 2.3.3 mj_step with
+// the options of assets/shelf_pnp.xml:4-6 (Euler, dt 0.002, noslip 3, pyramidal, warmstart).
+// Stage for stage the same algorithms as oracle/physics.c (which documents them):
+//   kinematics -> comPos -> CRBA(+armature) -> per-tree Cholesky of M -> collision ->
+//   constraints (weld, joint limits, pyramidal contacts; impedance) -> comVel -> passive ->
+//   RNE -> reference accel -> actuation -> qacc_smooth -> Newton (primal, exact line search) ->
+//   noslip (pyramidal pairs) -> checkAcc -> Euler (implicit damping, quaternion integration).
+//
+// Lane mapping (no tree-level barriers anywhere):
+//   bodies  : lane b composes its own root->b chain (body_path); cvel/cacc/crb/forces by masks
+//   dofs    : lane d (cdof, cdof_dot, bias projection, gradients)
+//   trees   : lane t factorises / solves its dense tree block of M (arm 9x9, cubes 6x6)
+//   islands : lane i factorises its island block of the Newton Hessian (trees joined by rows)
+//   pairs   : lane p runs broadphase + narrowphase of one candidate geom pair
+//   rows    : lane r (impedance, reference acceleration, J.x); rows are stored sparsely over
+//             the dofs of the <= 2 trees they touch (PH_ROWW slots)
+#include "phys_model.h"
+#include "pnp_internal.h"
+
+#define NT 64
+
+template <typename T> struct PM;
+template <> struct PM<float> {
+  static __device__ __forceinline__ float sqrt_(float x) { return __builtin_sqrtf(x); }
+  static __device__ __forceinline__ float eps() { return 1.1920929e-07f; }
+};
+template <> struct PM<double> {
+  static __device__ __forceinline__ double sqrt_(double x) { return __builtin_sqrt(x); }
+  static __device__ __forceinline__ double eps() { return 2.220446049250313e-16; }
+};
+
+template <typename T>
+struct Con {
+  T pos[3], frame[9], dist, includemargin, friction[5], solref[2], solimp[5];
+  int dim, g1, g2;
+};
+
+template <typename T>
+struct Env {
+  // ---- state
+  T qpos[PH_MAXQ], qvel[PH_MAXV], ctrl[PH_MAXU], mocap_pos[6], mocap_quat[8], qacc_ws[PH_MAXV];
+  T time;
+  uint32_t warn;
+  int ncon, nefc, ne, nlive, nisland, solver_iter;
+  // ---- position stage
+  T xpos[PH_MAXB][3], xquat[PH_MAXB][4], xmat[PH_MAXB][9], xipos[PH_MAXB][3], ximat[PH_MAXB][9];
+  T xanchor[PH_MAXJ][3], xaxis[PH_MAXJ][3];
+  T gpos[PH_MAXG][3], gmat[PH_MAXG][9];
+  T subcom[PH_MAXB][3];
+  T cinert[PH_MAXB][10], crb[PH_MAXB][10], cdof[PH_MAXV][6], cvel[PH_MAXB][6], cdofdot[PH_MAXV][6];
+  T scr6[PH_MAXB > PH_MAXV ? PH_MAXB : PH_MAXV][6];   // per-body / per-dof 6-vector scratch
+  T scr6b[PH_MAXB][6];
+  T M[PH_MAXMBLK];    // per-tree dense blocks
+  T L[PH_MAXMBLK];    // Cholesky factors of the blocks
+  // ---- vectors
+  T qfrc_bias[PH_MAXV], qfrc_passive[PH_MAXV], qfrc_act[PH_MAXV], qfrc_smooth[PH_MAXV];
+  T qacc_smooth[PH_MAXV], qacc[PH_MAXV], x[PH_MAXV], grad[PH_MAXV], p[PH_MAXV], v1[PH_MAXV], v2[PH_MAXV];
+  // ---- collision
+  int live[PH_MAXPAIR];
+  int pcount[NT];
+  Con<T> con[PH_MAXCON];
+  // ---- constraints (sparse rows)
+  int efc_t0[PH_MAXEFC], efc_t1[PH_MAXEFC], efc_type[PH_MAXEFC], efc_id[PH_MAXEFC];
+  T efc_J[PH_MAXEFC][PH_ROWW];
+  T efc_W[PH_MAXEFC][PH_ROWW];
+  T efc_pos[PH_MAXEFC], efc_margin[PH_MAXEFC], efc_diag[PH_MAXEFC], efc_D[PH_MAXEFC];
+  T efc_k[PH_MAXEFC], efc_bk[PH_MAXEFC], efc_imp[PH_MAXEFC], efc_aref[PH_MAXEFC], efc_bb[PH_MAXEFC];
+  T efc_force[PH_MAXEFC], efc_jar[PH_MAXEFC], efc_Jp[PH_MAXEFC];
+  int efc_act[PH_MAXEFC];
+  int lim_count[PH_MAXJ];
+  // ---- Newton
+  T H[PH_MAXV][PH_MAXV];
+  int tree_island[PH_MAXT], isl_n[PH_MAXT], isl_dof[PH_MAXT][PH_MAXV];
+  T red[8];
+};
+
+// ============================================================================ small helpers
+__device__ __forceinline__ int lane_id() { return threadIdx.x; }
+__device__ __forceinline__ void wsync() { __syncthreads(); }
+
+template <typename T>
+__device__ __forceinline__ T wsum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void t_normalize4(T q[4]) {
+  T n = PM<T>::sqrt_(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < T(1e-15)) { q[0] = 1; q[1] = q[2] = q[3] = 0; }
+  else if (fabs(n - T(1)) > T(1e-15)) { T s = T(1) / n; q[0] *= s; q[1] *= s; q[2] *= s; q[3] *= s; }
+}
+template <typename T>
+__device__ __forceinline__ T t_normalize3(T v[3]) {
+  T n = PM<T>::sqrt_(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+  if (n < T(1e-15)) { v[0] = 1; v[1] = v[2] = 0; return 0; }
+  T s = T(1) / n;
+  v[0] *= s; v[1] *= s; v[2] *= s;
+  return n;
+}
+template <typename T>
+__device__ __forceinline__ void t_cross(T r[3], const T a[3], const T b[3]) {
+  T t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+template <typename T>
+__device__ __forceinline__ T t_dot3(const T a[3], const T b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+template <typename T>
+__device__ __forceinline__ void t_mulmattvec3(T r[3], const T m[9], const T v[3]) {
+  T t0 = m[0] * v[0] + m[3] * v[1] + m[6] * v[2];
+  T t1 = m[1] * v[0] + m[4] * v[1] + m[7] * v[2];
+  T t2 = m[2] * v[0] + m[5] * v[1] + m[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+template <typename T>
+__device__ __forceinline__ void t_mulinertvec(T r[6], const T* i, const T v[6]) {
+  r[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
+  r[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
+  r[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
+  r[3] = i[8] * v[1] - i[7] * v[2] + i[9] * v[3];
+  r[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
+  r[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
+}
+template <typename T>
+__device__ __forceinline__ void t_crossmotion(T r[6], const T vel[6], const T v[6]) {
+  r[0] = -vel[2] * v[1] + vel[1] * v[2];
+  r[1] = vel[2] * v[0] - vel[0] * v[2];
+  r[2] = -vel[1] * v[0] + vel[0] * v[1];
+  r[3] = -vel[2] * v[4] + vel[1] * v[5];
+  r[4] = vel[2] * v[3] - vel[0] * v[5];
+  r[5] = -vel[1] * v[3] + vel[0] * v[4];
+  r[3] += -vel[5] * v[1] + vel[4] * v[2];
+  r[4] += vel[5] * v[0] - vel[3] * v[2];
+  r[5] += -vel[4] * v[0] + vel[3] * v[1];
+}
+template <typename T>
+__device__ __forceinline__ void t_crossforce(T r[6], const T vel[6], const T f[6]) {
+  r[0] = -vel[2] * f[1] + vel[1] * f[2];
+  r[1] = vel[2] * f[0] - vel[0] * f[2];
+  r[2] = -vel[1] * f[0] + vel[0] * f[1];
+  r[3] = -vel[2] * f[4] + vel[1] * f[5];
+  r[4] = vel[2] * f[3] - vel[0] * f[5];
+  r[5] = -vel[1] * f[3] + vel[0] * f[4];
+  r[0] += -vel[5] * f[4] + vel[4] * f[5];
+  r[1] += vel[5] * f[3] - vel[3] * f[5];
+  r[2] += -vel[4] * f[3] + vel[3] * f[4];
+}
+template <typename T>
+__device__ __forceinline__ void t_rotvecquat_mj(T r[3], const T v[3], const T q[4]) {
+  // MuJoCo shortcut semantics (zero vector / identity quaternion)
+  if (v[0] == 0 && v[1] == 0 && v[2] == 0) { r[0] = r[1] = r[2] = 0; return; }
+  if (q[0] == 1 && q[1] == 0 && q[2] == 0 && q[3] == 0) { r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; return; }
+  d_rotvecquat(r, v, q);
+}
+
+// slot s of a sparse row -> dof index
+template <typename T>
+__device__ __forceinline__ int slot_dof(const DevPhys<T>& m, int t0, int t1, int s) {
+  if (t0 < 0) return -1;
+  int n0 = m.tree_dofnum[t0];
+  if (s < n0) return m.tree_dofadr[t0] + s;
+  if (t1 < 0) return -1;
+  s -= n0;
+  return s < m.tree_dofnum[t1] ? m.tree_dofadr[t1] + s : -1;
+}
+template <typename T>
+__device__ __forceinline__ int row_width(const DevPhys<T>& m, int t0, int t1) {
+  return (t0 >= 0 ? m.tree_dofnum[t0] : 0) + (t1 >= 0 ? m.tree_dofnum[t1] : 0);
+}
+template <typename T>
+__device__ __forceinline__ int mblk(const DevPhys<T>& m, int i, int j) {
+  // i, j in the same tree
+  int t = m.dof_tree[i];
+  int a = m.tree_dofadr[t], n = m.tree_dofnum[t];
+  return m.tree_moff[t] + (i - a) * n + (j - a);
+}
+
+// ============================================================================ position stage
+template <typename T>
+__device__ void st_kinematics(const DevPhys<T>& m, Env<T>& s) {
+  const int b = lane_id();
+  if (b < m.nbody) {
+    T p[3] = {0, 0, 0}, q[4] = {1, 0, 0, 0}, R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    const int n = b ? m.body_pathlen[b] : 0;
+    for (int k = 0; k < n; k++) {
+      const int c = m.body_path[b][k];
+      const int ja = m.body_jntadr[c], jn = m.body_jntnum[c];
+      if (jn == 1 && m.jnt_type[ja] == 0) {
+        const T* qp = s.qpos + m.jnt_qposadr[ja];
+        p[0] = qp[0]; p[1] = qp[1]; p[2] = qp[2];
+        q[0] = qp[3]; q[1] = qp[4]; q[2] = qp[5]; q[3] = qp[6];
+        t_normalize4(q);
+        if (c == b) {
+          for (int t = 0; t < 3; t++) { s.xanchor[ja][t] = p[t]; s.xaxis[ja][t] = m.jnt_axis[ja][t]; }
+        }
+      } else {
+        T bp[3], bq[4];
+        const int mid = m.body_mocapid[c];
+        if (mid >= 0) {
+          for (int t = 0; t < 3; t++) bp[t] = s.mocap_pos[3 * mid + t];
+          for (int t = 0; t < 4; t++) bq[t] = s.mocap_quat[4 * mid + t];
+          t_normalize4(bq);
+        } else {
+          for (int t = 0; t < 3; t++) bp[t] = m.body_pos[c][t];
+          for (int t = 0; t < 4; t++) bq[t] = m.body_quat[c][t];
+        }
+        if (k > 0) {
+          T d[3];
+          d_mulmatvec3(d, R, bp);
+          p[0] += d[0]; p[1] += d[1]; p[2] += d[2];
+          d_mulquat(q, q, bq);
+        } else {
+          p[0] = bp[0]; p[1] = bp[1]; p[2] = bp[2];
+          q[0] = bq[0]; q[1] = bq[1]; q[2] = bq[2]; q[3] = bq[3];
+        }
+        for (int j = 0; j < jn; j++) {
+          const int jid = ja + j, qa = m.jnt_qposadr[jid], ty = m.jnt_type[jid];
+          T ax[3], an[3];
+          t_rotvecquat_mj(ax, m.jnt_axis[jid], q);
+          t_rotvecquat_mj(an, m.jnt_pos[jid], q);
+          an[0] += p[0]; an[1] += p[1]; an[2] += p[2];
+          if (ty == 2) {
+            const T dd = s.qpos[qa] - m.qpos0[qa];
+            p[0] += ax[0] * dd; p[1] += ax[1] * dd; p[2] += ax[2] * dd;
+          } else if (ty == 3) {
+            const T ang = s.qpos[qa] - m.qpos0[qa];
+            T ql[4] = {1, 0, 0, 0}, v[3];
+            if (ang != T(0)) {
+              T sn, cs;
+              d_sincos(ang * T(0.5), &sn, &cs);
+              ql[0] = cs; ql[1] = m.jnt_axis[jid][0] * sn; ql[2] = m.jnt_axis[jid][1] * sn; ql[3] = m.jnt_axis[jid][2] * sn;
+            }
+            d_mulquat(q, q, ql);
+            t_rotvecquat_mj(v, m.jnt_pos[jid], q);
+            p[0] = an[0] - v[0]; p[1] = an[1] - v[1]; p[2] = an[2] - v[2];
+          }
+          if (c == b) {
+            for (int t = 0; t < 3; t++) { s.xanchor[jid][t] = an[t]; s.xaxis[jid][t] = ax[t]; }
+          }
+        }
+      }
+      t_normalize4(q);
+      d_quat2mat(R, q);
+    }
+    for (int t = 0; t < 3; t++) s.xpos[b][t] = p[t];
+    for (int t = 0; t < 4; t++) s.xquat[b][t] = q[t];
+    for (int t = 0; t < 9; t++) s.xmat[b][t] = R[t];
+  }
+  wsync();
+  // inertial frames (bodies) and geom frames (collidable geoms)
+  for (int i = lane_id(); i < m.nbody + m.ngeom; i += NT) {
+    if (i < m.nbody) {
+      T v[3], q[4], R[9];
+      d_mulmatvec3(v, s.xmat[i], m.body_ipos[i]);
+      d_mulquat(q, s.xquat[i], m.body_iquat[i]);
+      d_quat2mat(R, q);
+      for (int t = 0; t < 3; t++) s.xipos[i][t] = s.xpos[i][t] + v[t];
+      for (int t = 0; t < 9; t++) s.ximat[i][t] = R[t];
+    } else {
+      const int g = i - m.nbody, b = m.geom_bodyid[g];
+      T v[3], q[4], R[9];
+      d_mulmatvec3(v, s.xmat[b], m.geom_pos[g]);
+      d_mulquat(q, s.xquat[b], m.geom_quat[g]);
+      d_quat2mat(R, q);
+      for (int t = 0; t < 3; t++) s.gpos[g][t] = s.xpos[b][t] + v[t];
+      for (int t = 0; t < 9; t++) s.gmat[g][t] = R[t];
+    }
+  }
+  wsync();
+}
+
+template <typename T>
+__device__ void st_compos_crb(const DevPhys<T>& m, Env<T>& s) {
+  const int l = lane_id();
+  // subtree COM of each root body (only roots are read: cinert and cdof are rooted there)
+  if (l > 0 && l < m.nbody && m.body_rootid[l] == l) {
+    T acc[3] = {0, 0, 0};
+    for (int i = 1; i < m.nbody; i++)
+      if (m.body_rootid[i] == l)
+        for (int t = 0; t < 3; t++) acc[t] += s.xipos[i][t] * m.body_mass[i];
+    if (m.body_subtreemass[l] < T(1e-15)) for (int t = 0; t < 3; t++) s.subcom[l][t] = s.xipos[l][t];
+    else for (int t = 0; t < 3; t++) s.subcom[l][t] = acc[t] / m.body_subtreemass[l];
+  }
+  wsync();
+  // cinert (bodies), cdof (joints)
+  if (l < m.nbody) {
+    if (l == 0) {
+      for (int t = 0; t < 10; t++) s.cinert[0][t] = 0;
+    } else {
+      const T* c = s.subcom[m.body_rootid[l]];
+      T dif[3] = {s.xipos[l][0] - c[0], s.xipos[l][1] - c[1], s.xipos[l][2] - c[2]};
+      const T* I = m.body_inertia[l];
+      const T* R = s.ximat[l];
+      const T ms = m.body_mass[l];
+      T tmp[9];
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+          tmp[3 * i + j] = R[3 * i] * I[0] * R[3 * j] + R[3 * i + 1] * I[1] * R[3 * j + 1] + R[3 * i + 2] * I[2] * R[3 * j + 2];
+      T* o = s.cinert[l];
+      o[0] = tmp[0] + ms * (dif[1] * dif[1] + dif[2] * dif[2]);
+      o[1] = tmp[4] + ms * (dif[0] * dif[0] + dif[2] * dif[2]);
+      o[2] = tmp[8] + ms * (dif[0] * dif[0] + dif[1] * dif[1]);
+      o[3] = tmp[1] - ms * dif[0] * dif[1];
+      o[4] = tmp[2] - ms * dif[0] * dif[2];
+      o[5] = tmp[5] - ms * dif[1] * dif[2];
+      o[6] = ms * dif[0]; o[7] = ms * dif[1]; o[8] = ms * dif[2];
+      o[9] = ms;
+    }
+  }
+  if (l < m.njnt) {
+    const int da = m.jnt_dofadr[l], bi = m.jnt_bodyid[l];
+    const T* c = s.subcom[m.body_rootid[bi]];
+    T off[3] = {c[0] - s.xanchor[l][0], c[1] - s.xanchor[l][1], c[2] - s.xanchor[l][2]};
+    switch (m.jnt_type[l]) {
+      case 0:
+        for (int i = 0; i < 3; i++) {
+          for (int t = 0; t < 6; t++) s.cdof[da + i][t] = 0;
+          s.cdof[da + i][3 + i] = 1;
+        }
+        for (int i = 0; i < 3; i++) {
+          T ax[3] = {s.xmat[bi][i], s.xmat[bi][i + 3], s.xmat[bi][i + 6]};
+          T* cd = s.cdof[da + 3 + i];
+          cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
+          t_cross(cd + 3, ax, off);
+        }
+        break;
+      case 2: {
+        T* cd = s.cdof[da];
+        cd[0] = cd[1] = cd[2] = 0;
+        cd[3] = s.xaxis[l][0]; cd[4] = s.xaxis[l][1]; cd[5] = s.xaxis[l][2];
+        break;
+      }
+      case 3: {
+        T* cd = s.cdof[da];
+        T ax[3] = {s.xaxis[l][0], s.xaxis[l][1], s.xaxis[l][2]};
+        cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
+        t_cross(cd + 3, ax, off);
+        break;
+      }
+      default:
+        break;
+    }
+  }
+  wsync();
+  // composite inertia: crb[b] = sum of cinert over the subtree of b
+  if (l > 0 && l < m.nbody) {
+    T acc[10];
+    for (int t = 0; t < 10; t++) acc[t] = 0;
+    uint32_t st = m.body_subtree[l];
+    while (st) {
+      const int c = __builtin_ctz(st);
+      st &= st - 1;
+      for (int t = 0; t < 10; t++) acc[t] += s.cinert[c][t];
+    }
+    for (int t = 0; t < 10; t++) s.crb[l][t] = acc[t];
+  }
+  wsync();
+  // buf_i = crb[body(i)] * cdof_i
+  if (l < m.nv) {
+    T r[6];
+    t_mulinertvec(r, s.crb[m.dof_bodyid[l]], s.cdof[l]);
+    for (int t = 0; t < 6; t++) s.scr6[l][t] = r[t];
+  }
+  for (int i = l; i < m.nmblock; i += NT) s.M[i] = 0;
+  wsync();
+  for (int e = l; e < m.nmentry; e += NT) {
+    const int i = m.mentry_i[e], j = m.mentry_j[e];
+    T v = 0;
+    for (int t = 0; t < 6; t++) v += s.cdof[j][t] * s.scr6[i][t];
+    if (i == j) v += m.dof_armature[i];
+    s.M[mblk(m, i, j)] = v;
+    s.M[mblk(m, j, i)] = v;
+  }
+  wsync();
+}
+
+// dense Cholesky of an n x n block (row stride ld) into Lb (lower); one lane
+template <typename T>
+__device__ void chol_block(const T* A, T* Lb, int n, int ld) {
+  for (int j = 0; j < n; j++) {
+    T sjj = A[j * ld + j];
+    for (int k = 0; k < j; k++) sjj -= Lb[j * ld + k] * Lb[j * ld + k];
+    sjj = PM<T>::sqrt_(sjj > T(0) ? sjj : T(1e-30));
+    Lb[j * ld + j] = sjj;
+    const T inv = T(1) / sjj;
+    for (int i = j + 1; i < n; i++) {
+      T t = A[i * ld + j];
+      for (int k = 0; k < j; k++) t -= Lb[i * ld + k] * Lb[j * ld + k];
+      Lb[i * ld + j] = t * inv;
+    }
+  }
+}
+
+// x = (L L^T)^-1 b on one block; x, b are indexed through dof lists (idx) of a global vector
+template <typename T>
+__device__ void chol_solve_block(const T* Lb, int n, int ld, const int* idx, int adr, T* x, const T* b) {
+  T y[PH_MAXV];
+  for (int i = 0; i < n; i++) {
+    T v = b[idx ? idx[i] : adr + i];
+    for (int k = 0; k < i; k++) v -= Lb[i * ld + k] * y[k];
+    y[i] = v / Lb[i * ld + i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    T v = y[i];
+    for (int k = i + 1; k < n; k++) v -= Lb[k * ld + i] * x[idx ? idx[k] : adr + k];
+    x[idx ? idx[i] : adr + i] = v / Lb[i * ld + i];
+  }
+}
+
+template <typename T>
+__device__ void st_factor_M(const DevPhys<T>& m, Env<T>& s) {
+  const int t = lane_id();
+  if (t < m.ntree) {
+    const int n = m.tree_dofnum[t], o = m.tree_moff[t];
+    chol_block(s.M + o, s.L + o, n, n);
+  }
+  wsync();
+}
+
+// x = M^-1 b (tree blocks, lane per tree); x and b may alias
+template <typename T>
+__device__ void solve_M(const DevPhys<T>& m, Env<T>& s, T* x, const T* b) {
+  const int t = lane_id();
+  if (t < m.ntree) {
+    const int n = m.tree_dofnum[t], o = m.tree_moff[t];
+    chol_solve_block(s.L + o, n, n, (const int*)nullptr, m.tree_dofadr[t], x, b);
+  }
+  wsync();
+}
+
+// r = M v (tree blocks, lane per dof)
+template <typename T>
+__device__ T mulM_row(const DevPhys<T>& m, const Env<T>& s, int i, const T* v) {
+  const int t = m.dof_tree[i];
+  const int a = m.tree_dofadr[t], n = m.tree_dofnum[t], o = m.tree_moff[t] + (i - a) * n;
+  T r = 0;
+  for (int k = 0; k < n; k++) r += s.M[o + k] * v[a + k];
+  return r;
+}
+
+// ============================================================================ collision
+#include "collide_dev.h"
+
+template <typename T>
+__device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
+  const int l = lane_id();
+  // broadphase: bounding spheres; survivors compacted in pair order
+  if (l == 0) s.nlive = 0;
+  wsync();
+  for (int base = 0; base < m.npair; base += NT) {
+    const int pi = base + l;
+    bool keep = false;
+    if (pi < m.npair) {
+      const int g1 = m.pair_g1[pi], g2 = m.pair_g2[pi];
+      const T r1 = m.geom_rbound[g1], r2 = m.geom_rbound[g2];
+      const T mg = fmax(m.geom_margin[g1], m.geom_margin[g2]);
+      keep = true;
+      if (r1 > 0 && r2 > 0) {
+        T v[3] = {s.gpos[g1][0] - s.gpos[g2][0], s.gpos[g1][1] - s.gpos[g2][1], s.gpos[g1][2] - s.gpos[g2][2]};
+        keep = PM<T>::sqrt_(t_dot3(v, v)) <= r1 + r2 + mg;
+      }
+    }
+    const uint64_t bal = __ballot(keep);
+    const int before = __popcll(bal & ((1ull << l) - 1));
+    if (keep) s.live[s.nlive + before] = pi;
+    wsync();
+    if (l == 0) s.nlive += __popcll(bal);
+    wsync();
+  }
+  // narrowphase: count pass, exclusive scan, write pass (same order as the oracle)
+  if (l == 0) s.ncon = 0;
+  wsync();
+  for (int base = 0; base < s.nlive; base += NT) {
+    const int k = base + l;
+    Con<T> tmp[8];
+    int n = 0;
+    if (k < s.nlive) n = collide_pair(m, s, s.live[k], tmp);
+    // inclusive scan of counts over the wave
+    int incl = n;
+    for (int o = 1; o < 64; o <<= 1) {
+      int y = __shfl_up(incl, o);
+      if (l >= o) incl += y;
+    }
+    const int total = __shfl(incl, 63);
+    const int off = s.ncon + incl - n;
+    for (int c = 0; c < n; c++)
+      if (off + c < PH_MAXCON) s.con[off + c] = tmp[c];
+    wsync();
+    if (l == 0) {
+      if (s.ncon + total > PH_MAXCON) s.warn |= 8u;
+      s.ncon = min(s.ncon + total, PH_MAXCON);
+    }
+    wsync();
+  }
+}
+
+// ============================================================================ constraints
+template <typename T>
+__device__ T impedance_(const T* si, T x) {
+  const T dmin = fmin(fmax(si[0], T(0.0001)), T(0.9999)), dmax = fmin(fmax(si[1], T(0.0001)), T(0.9999));
+  const T width = si[2], mid = si[3], power = si[4];
+  x = fabs(x);
+  if (width <= T(1e-15) || x >= width) return dmax;
+  T y = x / width;
+  if (power != T(1)) {
+    if (y <= mid) y = pow(y, power) / pow(mid, power - 1);
+    else y = T(1) - pow(T(1) - y, power) / pow(T(1) - mid, power - 1);
+  }
+  return dmin + y * (dmax - dmin);
+}
+
+template <typename T>
+__device__ void row_imp(const DevPhys<T>& m, Env<T>& s, int r, const T* solref, const T* solimp) {
+  const T dmax = fmin(fmax(solimp[1], T(0.0001)), T(0.9999));
+  T k, b;
+  if (solref[0] > 0) {
+    const T tc = fmax(solref[0], 2 * m.timestep), dr = solref[1];
+    k = T(1) / (dmax * dmax * tc * tc * dr * dr);
+    b = T(2) / (dmax * tc);
+  } else {
+    k = -solref[0] / (dmax * dmax);
+    b = -solref[1] / dmax;
+  }
+  const T imp = impedance_(solimp, s.efc_pos[r] - s.efc_margin[r]);
+  s.efc_k[r] = k;
+  s.efc_bk[r] = b;
+  s.efc_imp[r] = imp;
+  const T R = fmax(T(1e-15), (1 - imp) * s.efc_diag[r] / imp);
+  s.efc_D[r] = T(1) / R;
+}
+
+// translational Jacobian column of world point pt on body b at dof d (0 if d does not move b)
+template <typename T>
+__device__ __forceinline__ void jac_col(const DevPhys<T>& m, const Env<T>& s, int b, int d, const T pt[3], T jp[3], T jr[3]) {
+  if (d < 0 || !(m.body_dofmask[b] >> d & 1)) {
+    jp[0] = jp[1] = jp[2] = 0;
+    jr[0] = jr[1] = jr[2] = 0;
+    return;
+  }
+  const T* c = s.subcom[m.body_rootid[b]];
+  const T off[3] = {pt[0] - c[0], pt[1] - c[1], pt[2] - c[2]};
+  const T* cd = s.cdof[d];
+  T t[3];
+  t_cross(t, cd, off);
+  for (int k = 0; k < 3; k++) { jp[k] = cd[3 + k] + t[k]; jr[k] = cd[k]; }
+}
+
+template <typename T>
+__device__ void st_constraints(const DevPhys<T>& m, Env<T>& s) {
+  const int l = lane_id();
+  // ---- weld rows (one equality in this scene; loop kept general)
+  int nrow = 0;
+  for (int e = 0; e < m.neq; e++) {
+    if (m.eq_type[e] != 1) continue;
+    const T* data = m.eq_data[e];
+    const int id0 = m.eq_obj1id[e], id1 = m.eq_obj2id[e];
+    T pos0[3], pos1[3], q[4], q1[4], q2[4];
+    d_mulmatvec3(pos0, s.xmat[id0], data + 3);
+    d_mulmatvec3(pos1, s.xmat[id1], data);
+    for (int k = 0; k < 3; k++) { pos0[k] += s.xpos[id0][k]; pos1[k] += s.xpos[id1][k]; }
+    const T ts = data[10];
+    d_mulquat(q, s.xquat[id0], data + 6);
+    q1[0] = s.xquat[id1][0]; q1[1] = -s.xquat[id1][1]; q1[2] = -s.xquat[id1][2]; q1[3] = -s.xquat[id1][3];
+    d_mulquat(q2, q1, q);
+    int t0 = m.body_tree[id0] >= 0 && m.body_dofmask[id0] ? m.body_tree[id0] : -1;
+    int t1 = m.body_tree[id1] >= 0 && m.body_dofmask[id1] ? m.body_tree[id1] : -1;
+    if (t0 < 0) { t0 = t1; t1 = -1; }
+    if (t0 == t1) t1 = -1;
+    const T tran = m.body_invweight0[id0][0] + m.body_invweight0[id1][0];
+    const T rot = m.body_invweight0[id0][1] + m.body_invweight0[id1][1];
+    const int r0 = nrow;
+    const int w = row_width(m, t0, t1);
+    if (l < w) {
+      const int d = slot_dof(m, t0, t1, l);
+      T jp0[3], jr0[3], jp1[3], jr1[3];
+      jac_col(m, s, id0, d, pos0, jp0, jr0);
+      jac_col(m, s, id1, d, pos1, jp1, jr1);
+      T ax[3] = {jr0[0] - jr1[0], jr0[1] - jr1[1], jr0[2] - jr1[2]};
+      T tq[4], t3[4];
+      tq[0] = -q1[1] * ax[0] - q1[2] * ax[1] - q1[3] * ax[2];
+      tq[1] = q1[0] * ax[0] + q1[2] * ax[2] - q1[3] * ax[1];
+      tq[2] = q1[0] * ax[1] + q1[3] * ax[0] - q1[1] * ax[2];
+      tq[3] = q1[0] * ax[2] + q1[1] * ax[1] - q1[2] * ax[0];
+      d_mulquat(t3, tq, q);
+      for (int k = 0; k < 3; k++) {
+        s.efc_J[r0 + k][l] = jp0[k] - jp1[k];
+        s.efc_J[r0 + 3 + k][l] = T(0.5) * t3[1 + k] * ts;
+      }
+    }
+    if (l < 6) {
+      const int r = r0 + l;
+      s.efc_t0[r] = t0; s.efc_t1[r] = t1;
+      s.efc_type[r] = 0; s.efc_id[r] = e;
+      s.efc_pos[r] = l < 3 ? pos0[l] - pos1[l] : q2[1 + (l - 3)] * ts;
+      s.efc_margin[r] = 0;
+      s.efc_diag[r] = l < 3 ? tran : rot;
+    }
+    nrow += 6;
+  }
+  wsync();
+  if (l < 6 * m.neq) row_imp(m, s, l, m.eq_solref[l / 6], m.eq_solimp[l / 6]);
+  const int ne = nrow;
+  // ---- joint limits: count per joint, scan, emit
+  int nl = 0;
+  if (l < m.njnt && m.jnt_limited[l] && (m.jnt_type[l] == 2 || m.jnt_type[l] == 3)) {
+    const T v = s.qpos[m.jnt_qposadr[l]], mg = m.jnt_margin[l];
+    nl = (v - m.jnt_range[l][0] < mg) + (m.jnt_range[l][1] - v < mg);
+  }
+  int incl = nl;
+  for (int o = 1; o < 64; o <<= 1) {
+    int y = __shfl_up(incl, o);
+    if (l >= o) incl += y;
+  }
+  const int nlim = __shfl(incl, 63);
+  if (nl) {
+    int r = ne + incl - nl;
+    const T v = s.qpos[m.jnt_qposadr[l]], mg = m.jnt_margin[l];
+    const int d = m.jnt_dofadr[l], t = m.dof_tree[d];
+    for (int side = -1; side <= 1; side += 2) {
+      const T dist = side * (m.jnt_range[l][(side + 1) / 2] - v);
+      if (dist < mg && r < PH_MAXEFC) {
+        s.efc_t0[r] = t; s.efc_t1[r] = -1;
+        s.efc_type[r] = 3; s.efc_id[r] = l;
+        for (int k = 0; k < PH_ROWW; k++) s.efc_J[r][k] = 0;
+        s.efc_J[r][d - m.tree_dofadr[t]] = T(-side);
+        s.efc_pos[r] = dist;
+        s.efc_margin[r] = mg;
+        s.efc_diag[r] = m.dof_invweight0[d];
+        row_imp(m, s, r, m.jnt_solref[l], m.jnt_solimp[l]);
+        r++;
+      }
+    }
+  }
+  nrow = ne + nlim;
+  wsync();
+  // ---- contacts (pyramidal): 2*(dim-1) rows each
+  int crow = nrow;
+  for (int c = 0; c < s.ncon; c++) {
+    const Con<T>& con = s.con[c];
+    const int nr = 2 * (con.dim - 1);
+    if (crow + nr > PH_MAXEFC) { if (l == 0) s.warn |= 16u; break; }
+    const int b1 = m.geom_bodyid[con.g1], b2 = m.geom_bodyid[con.g2];
+    int t0 = m.body_dofmask[b1] ? m.body_tree[b1] : -1;
+    int t1 = m.body_dofmask[b2] ? m.body_tree[b2] : -1;
+    if (t0 < 0) { t0 = t1; t1 = -1; }
+    if (t0 == t1) t1 = -1;
+    const int w = row_width(m, t0, t1);
+    if (l < w) {
+      const int d = slot_dof(m, t0, t1, l);
+      T jp1[3], jr1[3], jp2[3], jr2[3];
+      jac_col(m, s, b1, d, con.pos, jp1, jr1);
+      jac_col(m, s, b2, d, con.pos, jp2, jr2);
+      T jd[3] = {jp2[0] - jp1[0], jp2[1] - jp1[1], jp2[2] - jp1[2]};
+      T cj[3];
+      for (int k = 0; k < 3; k++) cj[k] = con.frame[3 * k] * jd[0] + con.frame[3 * k + 1] * jd[1] + con.frame[3 * k + 2] * jd[2];
+      for (int k = 1; k < con.dim && k < 3; k++) {
+        const T fri = con.friction[k - 1];
+        s.efc_J[crow + 2 * (k - 1)][l] = cj[0] + fri * cj[k];
+        s.efc_J[crow + 2 * (k - 1) + 1][l] = cj[0] - fri * cj[k];
+      }
+    } else if (l < PH_ROWW) {
+      for (int k = 0; k < nr; k++) s.efc_J[crow + k][l] = 0;
+    }
+    if (l < nr) {
+      const int r = crow + l, k = l / 2 + 1;
+      const T tran = m.body_invweight0[b1][0] + m.body_invweight0[b2][0];
+      const T rot = m.body_invweight0[b1][1] + m.body_invweight0[b2][1];
+      const T fri = con.friction[k - 1];
+      s.efc_t0[r] = t0; s.efc_t1[r] = t1;
+      s.efc_type[r] = 6; s.efc_id[r] = c;
+      s.efc_pos[r] = con.dist;
+      s.efc_margin[r] = con.includemargin;
+      s.efc_diag[r] = tran + fri * fri * (k < 3 ? tran : rot);
+      row_imp(m, s, r, con.solref, con.solimp);
+    }
+    crow += nr;
+  }
+  // zero the unused tail slots of every row (widths vary)
+  wsync();
+  for (int i = l; i < crow * PH_ROWW; i += NT) {
+    const int r = i / PH_ROWW, k = i % PH_ROWW;
+    if (k >= row_width(m, s.efc_t0[r], s.efc_t1[r])) s.efc_J[r][k] = 0;
+  }
+  if (l == 0) { s.nefc = crow; s.ne = ne; }
+  wsync();
+}
+
+// ============================================================================ velocity stage
+template <typename T>
+__device__ void st_velocity(const DevPhys<T>& m, Env<T>& s) {
+  const int l = lane_id();
+  // cvel of bodies
+  if (l < m.nbody) {
+    T cv[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t dm = l ? m.body_dofmask[l] : 0;
+    while (dm) {
+      const int d = __builtin_ctzll(dm);
+      dm &= dm - 1;
+      for (int t = 0; t < 6; t++) cv[t] += s.cdof[d][t] * s.qvel[d];
+    }
+    for (int t = 0; t < 6; t++) s.cvel[l][t] = cv[t];
+  }
+  // cdof_dot
+  if (l < m.nv) {
+    const int j = m.dof_jntid[l];
+    if (m.jnt_type[j] == 0 && l < m.jnt_dofadr[j] + 3) {
+      for (int t = 0; t < 6; t++) s.cdofdot[l][t] = 0;
+    } else {
+      T cv[6] = {0, 0, 0, 0, 0, 0};
+      uint64_t vm = m.dof_velmask[l];
+      while (vm) {
+        const int d = __builtin_ctzll(vm);
+        vm &= vm - 1;
+        for (int t = 0; t < 6; t++) cv[t] += s.cdof[d][t] * s.qvel[d];
+      }
+      T r[6];
+      t_crossmotion(r, cv, s.cdof[l]);
+      for (int t = 0; t < 6; t++) s.cdofdot[l][t] = r[t];
+    }
+    s.qfrc_passive[l] = -m.dof_damping[l] * s.qvel[l];
+  }
+  wsync();
+  // RNE: cacc, cfrc_body
+  if (l > 0 && l < m.nbody) {
+    T ca[6] = {0, 0, 0, -m.gravity[0], -m.gravity[1], -m.gravity[2]};
+    uint64_t dm = m.body_dofmask[l];
+    while (dm) {
+      const int d = __builtin_ctzll(dm);
+      dm &= dm - 1;
+      for (int t = 0; t < 6; t++) ca[t] += s.cdofdot[d][t] * s.qvel[d];
+    }
+    T f[6], tmp[6], tmp1[6];
+    t_mulinertvec(f, s.cinert[l], ca);
+    t_mulinertvec(tmp, s.cinert[l], s.cvel[l]);
+    t_crossforce(tmp1, s.cvel[l], tmp);
+    for (int t = 0; t < 6; t++) s.scr6b[l][t] = f[t] + tmp1[t];
+  }
+  wsync();
+  if (l > 0 && l < m.nbody) {
+    T acc[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t st = m.body_subtree[l];
+    while (st) {
+      const int c = __builtin_ctz(st);
+      st &= st - 1;
+      for (int t = 0; t < 6; t++) acc[t] += s.scr6b[c][t];
+    }
+    for (int t = 0; t < 6; t++) s.scr6[l][t] = acc[t];
+  }
+  wsync();
+  if (l < m.nv) {
+    T v = 0;
+    for (int t = 0; t < 6; t++) v += s.cdof[l][t] * s.scr6[m.dof_bodyid[l]][t];
+    s.qfrc_bias[l] = v;
+  }
+  // reference acceleration of the rows
+  for (int r = l; r < s.nefc; r += NT) {
+    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
+    T v = 0;
+    for (int k = 0; k < w; k++) v += s.efc_J[r][k] * s.qvel[slot_dof(m, t0, t1, k)];
+    s.efc_aref[r] = -s.efc_bk[r] * v - s.efc_k[r] * s.efc_imp[r] * (s.efc_pos[r] - s.efc_margin[r]);
+  }
+  wsync();
+}
+
+// ============================================================================ acceleration
+template <typename T>
+__device__ void st_actuation_smooth(const DevPhys<T>& m, Env<T>& s) {
+  const int l = lane_id();
+  if (l < m.nv) {
+    T f = 0;
+    for (int i = 0; i < m.nu; i++) {
+      if (m.act_dof[i] != l) continue;
+      T ctrl = s.ctrl[i];
+      if (m.act_ctrllimited[i]) ctrl = fmin(fmax(ctrl, m.act_ctrlrange[i][0]), m.act_ctrlrange[i][1]);
+      const T gear = m.act_gear[i];
+      const T len = gear * s.qpos[m.act_qadr[i]], vel = gear * s.qvel[l];
+      T force = m.act_gainprm[i][0] * ctrl;
+      if (m.act_biastype[i]) force += m.act_biasprm[i][0] + m.act_biasprm[i][1] * len + m.act_biasprm[i][2] * vel;
+      if (m.act_forcelimited[i]) force = fmin(fmax(force, m.act_forcerange[i][0]), m.act_forcerange[i][1]);
+      f += gear * force;
+    }
+    s.qfrc_act[l] = f;
+    s.qfrc_smooth[l] = s.qfrc_passive[l] - s.qfrc_bias[l] + f;
+  }
+  wsync();
+  solve_M(m, s, s.qacc_smooth, s.qfrc_smooth);
+  for (int r = l; r < s.nefc; r += NT) {
+    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
+    T v = -s.efc_aref[r];
+    for (int k = 0; k < w; k++) v += s.efc_J[r][k] * s.qacc_smooth[slot_dof(m, t0, t1, k)];
+    s.efc_bb[r] = v;
+  }
+  wsync();
+}
+
+// ============================================================================ Newton solver
+// jar = J x - aref, active set, cost (returned on every lane)
+template <typename T>
+__device__ T eval_cost(const DevPhys<T>& m, Env<T>& s, const T* x, bool store) {
+  const int l = lane_id();
+  T c = 0;
+  if (l < m.nv) {
+    s.v1[l] = x[l] - s.qacc_smooth[l];
+  }
+  wsync();
+  if (l < m.nv) c += T(0.5) * s.v1[l] * mulM_row(m, s, l, s.v1);
+  for (int r = l; r < s.nefc; r += NT) {
+    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
+    T v = -s.efc_aref[r];
+    for (int k = 0; k < w; k++) v += s.efc_J[r][k] * x[slot_dof(m, t0, t1, k)];
+    const int a = r < s.ne || v < 0;
+    if (store) { s.efc_jar[r] = v; s.efc_act[r] = a; }
+    if (a) c += T(0.5) * s.efc_D[r] * v * v;
+  }
+  c = wsum(c);
+  wsync();
+  return c;
+}
+
+template <typename T>
+__device__ void build_islands(const DevPhys<T>& m, Env<T>& s) {
+  if (lane_id() == 0) {
+    int par[PH_MAXT];
+    for (int t = 0; t < m.ntree; t++) par[t] = t;
+    for (int r = 0; r < s.nefc; r++) {
+      int a = s.efc_t0[r], b = s.efc_t1[r];
+      if (a < 0 || b < 0) continue;
+      while (par[a] != a) a = par[a];
+      while (par[b] != b) b = par[b];
+      if (a != b) par[a > b ? a : b] = a < b ? a : b;
+    }
+    int nis = 0, id[PH_MAXT];
+    for (int t = 0; t < m.ntree; t++) {
+      int r = t;
+      while (par[r] != r) r = par[r];
+      if (r == t) { id[t] = nis; s.isl_n[nis] = 0; nis++; }
+    }
+    for (int t = 0; t < m.ntree; t++) {
+      int r = t;
+      while (par[r] != r) r = par[r];
+      s.tree_island[t] = id[r];
+    }
+    for (int i = 0; i < m.nv; i++) {
+      const int isl = s.tree_island[m.dof_tree[i]];
+      s.isl_dof[isl][s.isl_n[isl]++] = i;
+    }
+    s.nisland = nis;
+  }
+  wsync();
+}
+
+// exact minimiser of the convex piecewise quadratic phi(a) = cost(x + a p) (semi-smooth Newton
+// on phi', bracketed)
+template <typename T>
+__device__ T line_search(const DevPhys<T>& m, Env<T>& s) {
+  const int l = lane_id();
+  if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
+  for (int r = l; r < s.nefc; r += NT) {
+    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
+    T v = 0;
+    for (int k = 0; k < w; k++) v += s.efc_J[r][k] * s.p[slot_dof(m, t0, t1, k)];
+    s.efc_Jp[r] = v;
+  }
+  wsync();
+  T A0 = 0, B0 = 0;
+  if (l < m.nv) {
+    const T mp = mulM_row(m, s, l, s.p);
+    A0 = s.p[l] * 0 + mp * s.p[l];
+    B0 = mp * s.v1[l];
+  }
+  A0 = wsum(A0);
+  B0 = wsum(B0);
+  T lo = 0, hi = T(-1), a = 1;
+  for (int it = 0; it < 60; it++) {
+    T d1 = 0, d2 = 0;
+    for (int r = l; r < s.nefc; r += NT) {
+      const T jp = s.efc_Jp[r], v = s.efc_jar[r] + a * jp;
+      if (r < s.ne || v < 0) { d1 += s.efc_D[r] * v * jp; d2 += s.efc_D[r] * jp * jp; }
+    }
+    d1 = wsum(d1) + A0 * a + B0;
+    d2 = wsum(d2) + A0;
+    if (d1 == T(0)) break;
+    if (d1 > 0) hi = a; else lo = a;
+    T an = a - d1 / d2;
+    if (!(an > lo) || (hi >= T(0) && !(an < hi))) an = hi >= T(0) ? T(0.5) * (lo + hi) : T(2) * a;
+    if (an == a || (hi >= T(0) && hi - lo <= PM<T>::eps() * hi)) { a = an; break; }
+    a = an;
+  }
+  return a;
+}
+
+template <typename T>
+__device__ void st_newton(const DevPhys<T>& m, Env<T>& s) {
+  const int l = lane_id();
+  if (s.nefc == 0) {
+    if (l < m.nv) s.qacc[l] = s.qacc_smooth[l];
+    if (l == 0) s.solver_iter = 0;
+    wsync();
+    return;
+  }
+  build_islands(m, s);
+  const T cws = eval_cost(m, s, s.qacc_ws, false);
+  const T csm = eval_cost(m, s, s.qacc_smooth, false);
+  if (l < m.nv) s.x[l] = cws < csm ? s.qacc_ws[l] : s.qacc_smooth[l];
+  wsync();
+  T cost = eval_cost(m, s, s.x, true);
+  int it = 0;
+  for (; it < m.iterations; it++) {
+    // gradient
+    if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
+    wsync();
+    T g2 = 0;
+    if (l < m.nv) {
+      T g = mulM_row(m, s, l, s.v1);
+      const int t = m.dof_tree[l];
+      for (int r = 0; r < s.nefc; r++) {
+        if (!s.efc_act[r]) continue;
+        const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
+        int k = -1;
+        if (t0 == t) k = l - m.tree_dofadr[t0];
+        else if (t1 == t) k = m.tree_dofnum[t0] + l - m.tree_dofadr[t1];
+        if (k >= 0) g += s.efc_J[r][k] * s.efc_D[r] * s.efc_jar[r];
+      }
+      s.grad[l] = g;
+      g2 = g * g;
+    }
+    g2 = wsum(g2);
+    if (!(g2 > 0)) break;
+    // Hessian island blocks: M (same tree) + sum_active D J J^T
+    for (int e = l; e < m.nv * m.nv; e += NT) {
+      const int i = e / m.nv, j = e % m.nv;
+      const int ti = m.dof_tree[i], tj = m.dof_tree[j];
+      if (s.tree_island[ti] != s.tree_island[tj] || j > i) continue;
+      T h = ti == tj ? s.M[mblk(m, i, j)] : T(0);
+      for (int r = 0; r < s.nefc; r++) {
+        if (!s.efc_act[r]) continue;
+        const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
+        int ki = -1, kj = -1;
+        if (t0 == ti) ki = i - m.tree_dofadr[t0]; else if (t1 == ti) ki = m.tree_dofnum[t0] + i - m.tree_dofadr[t1];
+        if (ki < 0) continue;
+        if (t0 == tj) kj = j - m.tree_dofadr[t0]; else if (t1 == tj) kj = m.tree_dofnum[t0] + j - m.tree_dofadr[t1];
+        if (kj < 0) continue;
+        h += s.efc_J[r][ki] * s.efc_D[r] * s.efc_J[r][kj];
+      }
+      s.H[i][j] = h;
+      s.H[j][i] = h;
+    }
+    wsync();
+    // factor + solve per island (lane per island): p = -H^-1 grad
+    if (l < s.nisland) {
+      const int n = s.isl_n[l];
+      const int* idx = s.isl_dof[l];
+      // gather the island block into a compact dense matrix in place of its rows of H
+      T Hb[PH_MAXV * 0 + 1];
+      (void)Hb;
+      // Cholesky on the scattered block: index through idx
+      for (int jj = 0; jj < n; jj++) {
+        const int j = idx[jj];
+        T sjj = s.H[j][j];
+        for (int kk = 0; kk < jj; kk++) sjj -= s.H[j][idx[kk]] * s.H[j][idx[kk]];
+        sjj = PM<T>::sqrt_(sjj > T(0) ? sjj : T(1e-30));
+        s.H[j][j] = sjj;
+        const T inv = T(1) / sjj;
+        for (int ii = jj + 1; ii < n; ii++) {
+          const int i = idx[ii];
+          T t = s.H[i][j];
+          for (int kk = 0; kk < jj; kk++) t -= s.H[i][idx[kk]] * s.H[j][idx[kk]];
+          s.H[i][j] = t * inv;
+        }
+      }
+      T y[PH_MAXV];
+      for (int ii = 0; ii < n; ii++) {
+        const int i = idx[ii];
+        T v = s.grad[i];
+        for (int kk = 0; kk < ii; kk++) v -= s.H[i][idx[kk]] * y[kk];
+        y[ii] = v / s.H[i][i];
+      }
+      for (int ii = n - 1; ii >= 0; ii--) {
+        const int i = idx[ii];
+        T v = y[ii];
+        for (int kk = ii + 1; kk < n; kk++) v -= s.H[idx[kk]][i] * s.p[idx[kk]];
+        s.p[i] = v / s.H[i][i];
+      }
+    }
+    wsync();
+    if (l < m.nv) s.p[l] = -s.p[l];
+    wsync();
+    const T alpha = line_search(m, s);
+    if (!(alpha > 0)) break;
+    if (l < m.nv) s.x[l] += alpha * s.p[l];
+    wsync();
+    const T nc = eval_cost(m, s, s.x, true);
+    const T impr = cost - nc;
+    cost = nc;
+    if (!(impr > PM<T>::eps() * fabs(cost)) && it > 0) { it++; break; }
+  }
+  if (l == 0) s.solver_iter = it;
+  for (int r = l; r < s.nefc; r += NT) s.efc_force[r] = s.efc_act[r] ? -s.efc_D[r] * s.efc_jar[r] : T(0);
+  if (l < m.nv) s.qacc[l] = s.x[l];
+  wsync();
+}
+
+// ============================================================================ no-slip
+template <typename T>
+__device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
+  const int l = lane_id();
+  if (m.noslip_iterations <= 0 || s.nefc == 0) return;
+  // W_r = M^-1 J_r^T for contact rows (block-diagonal M: solve per tree of the row)
+  for (int r = l; r < s.nefc; r += NT) {
+    if (s.efc_type[r] != 6) continue;
+    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
+    int base = 0;
+    for (int h = 0; h < 2; h++) {
+      const int t = h ? t1 : t0;
+      if (t < 0) continue;
+      const int n = m.tree_dofnum[t], o = m.tree_moff[t];
+      T y[PH_MAXTDOF];
+      for (int i = 0; i < n; i++) {
+        T v = s.efc_J[r][base + i];
+        for (int k = 0; k < i; k++) v -= s.L[o + i * n + k] * y[k];
+        y[i] = v / s.L[o + i * n + i];
+      }
+      for (int i = n - 1; i >= 0; i--) {
+        T v = y[i];
+        for (int k = i + 1; k < n; k++) v -= s.L[o + k * n + i] * s.efc_W[r][base + k];
+        s.efc_W[r][base + i] = v / s.L[o + i * n + i];
+      }
+      base += n;
+    }
+    for (int k = base; k < PH_ROWW; k++) s.efc_W[r][k] = 0;
+  }
+  // v = M^-1 J^T f (all rows)
+  if (l < m.nv) {
+    const int t = m.dof_tree[l];
+    T g = 0;
+    for (int r = 0; r < s.nefc; r++) {
+      const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
+      int k = -1;
+      if (t0 == t) k = l - m.tree_dofadr[t0];
+      else if (t1 == t) k = m.tree_dofnum[t0] + l - m.tree_dofadr[t1];
+      if (k >= 0) g += s.efc_J[r][k] * s.efc_force[r];
+    }
+    s.v2[l] = g;
+  }
+  wsync();
+  solve_M(m, s, s.v2, s.v2);
+  for (int iter = 0; iter < m.noslip_iterations; iter++) {
+    for (int i = s.ne; i < s.nefc; i++) {
+      if (s.efc_type[i] != 6) continue;
+      const int dim = s.con[s.efc_id[i]].dim;
+      for (int j = i; j < i + 2 * (dim - 1); j += 2) {
+        const int t0 = s.efc_t0[j], t1 = s.efc_t1[j], w = row_width(m, t0, t1);
+        T r0 = 0, r1 = 0, a00 = 0, a01 = 0, a10 = 0, a11 = 0;
+        if (l < w) {
+          const int d = slot_dof(m, t0, t1, l);
+          const T J0 = s.efc_J[j][l], J1 = s.efc_J[j + 1][l];
+          const T W0 = s.efc_W[j][l], W1 = s.efc_W[j + 1][l];
+          r0 = J0 * s.v2[d]; r1 = J1 * s.v2[d];
+          a00 = J0 * W0; a01 = J0 * W1; a10 = J1 * W0; a11 = J1 * W1;
+        }
+        r0 = wsum(r0); r1 = wsum(r1); a00 = wsum(a00); a01 = wsum(a01); a10 = wsum(a10); a11 = wsum(a11);
+        r0 += s.efc_bb[j];
+        r1 += s.efc_bb[j + 1];
+        const T f0 = s.efc_force[j], f1 = s.efc_force[j + 1];
+        const T bc0 = r0 - (a00 * f0 + a01 * f1), bc1 = r1 - (a10 * f0 + a11 * f1);
+        const T mid = T(0.5) * (f0 + f1);
+        const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;
+        T n0, n1;
+        if (K1 < T(1e-15)) { n0 = n1 = mid; }
+        else {
+          T y = -K0 / K1;
+          if (y < -mid) y = -mid; else if (y > mid) y = mid;
+          n0 = mid + y; n1 = mid - y;
+        }
+        const T df0 = n0 - f0, df1 = n1 - f1;
+        if (l < w) {
+          const int d = slot_dof(m, t0, t1, l);
+          s.v2[d] += s.efc_W[j][l] * df0 + s.efc_W[j + 1][l] * df1;
+        }
+        wsync();
+        if (l == 0) { s.efc_force[j] = n0; s.efc_force[j + 1] = n1; }
+        wsync();
+      }
+      i += 2 * (dim - 1) - 1;
+    }
+  }
+}
+
+template <typename T>
+__device__ void st_finish_accel(const DevPhys<T>& m, Env<T>& s) {
+  const int l = lane_id();
+  if (s.nefc == 0) return;
+  if (l < m.nv) {
+    const int t = m.dof_tree[l];
+    T g = 0;
+    for (int r = 0; r < s.nefc; r++) {
+      const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
+      int k = -1;
+      if (t0 == t) k = l - m.tree_dofadr[t0];
+      else if (t1 == t) k = m.tree_dofnum[t0] + l - m.tree_dofadr[t1];
+      if (k >= 0) g += s.efc_J[r][k] * s.efc_force[r];
+    }
+    s.v2[l] = s.qfrc_smooth[l] + g;
+  }
+  wsync();
+  if (m.noslip_iterations > 0) solve_M(m, s, s.qacc, s.v2);
+}
+
+// ============================================================================ reset / Euler
+template <typename T>
+__device__ void reset_state(const DevPhys<T>& m, Env<T>& s) {
+  const int l = lane_id();
+  if (l < m.nq) s.qpos[l] = m.qpos0[l];
+  if (l < m.nv) { s.qvel[l] = 0; s.qacc_ws[l] = 0; }
+  if (l < m.nu) s.ctrl[l] = 0;
+  if (l < m.nmocap) {
+    const int b = m.mocap_body[l];
+    for (int t = 0; t < 3; t++) s.mocap_pos[3 * l + t] = m.body_pos[b][t];
+    for (int t = 0; t < 4; t++) s.mocap_quat[4 * l + t] = m.body_quat[b][t];
+  }
+  if (l == 0) s.time = 0;
+  wsync();
+}
+
+template <typename T>
+__device__ __forceinline__ bool is_bad(T x) { return !(fabs(x) <= T(1e10)); }
+
+template <typename T>
+__device__ void st_euler(const DevPhys<T>& m, Env<T>& s) {
+  const int l = lane_id();
+  const T h = m.timestep;
+  // qfrc = M qacc ; (M + h D) qacc_e = qfrc  (implicit joint damping)
+  if (l < m.nv) s.v1[l] = mulM_row(m, s, l, s.qacc);
+  wsync();
+  if (l < m.ntree) {
+    const int n = m.tree_dofnum[l], o = m.tree_moff[l], a = m.tree_dofadr[l];
+    T* A = s.H[0];   // scratch: n x n
+    for (int i = 0; i < n; i++)
+      for (int j = 0; j < n; j++) A[o + i * n + j] = s.M[o + i * n + j] + (i == j ? h * m.dof_damping[a + i] : T(0));
+    chol_block(A + o, A + o, n, n);
+    chol_solve_block(A + o, n, n, (const int*)nullptr, a, s.v2, s.v1);
+  }
+  wsync();
+  if (l < m.nv) s.qvel[l] += h * s.v2[l];
+  wsync();
+  if (l < m.njnt) {
+    const int qa = m.jnt_qposadr[l], da = m.jnt_dofadr[l];
+    if (m.jnt_type[l] == 0) {
+      for (int k = 0; k < 3; k++) s.qpos[qa + k] += h * s.qvel[da + k];
+      T ax[3] = {s.qvel[da + 3], s.qvel[da + 4], s.qvel[da + 5]}, qr[4] = {1, 0, 0, 0};
+      const T ang = h * t_normalize3(ax);
+      if (ang != T(0)) {
+        T sn, cs;
+        d_sincos(ang * T(0.5), &sn, &cs);
+        qr[0] = cs; qr[1] = ax[0] * sn; qr[2] = ax[1] * sn; qr[3] = ax[2] * sn;
+      }
+      T q[4] = {s.qpos[qa + 3], s.qpos[qa + 4], s.qpos[qa + 5], s.qpos[qa + 6]};
+      t_normalize4(q);
+      d_mulquat(q, q, qr);
+      for (int k = 0; k < 4; k++) s.qpos[qa + 3 + k] = q[k];
+    } else {
+      s.qpos[qa] += h * s.qvel[da];
+    }
+  }
+  if (l < m.nv) s.qacc_ws[l] = s.qacc[l];
+  if (l == 0) s.time += h;
+  wsync();
+}
+
+// ============================================================================ forward / kernel
+template <typename T>
+__device__ void forward(const DevPhys<T>& m, Env<T>& s) {
+  st_kinematics(m, s);
+  st_compos_crb(m, s);
+  st_factor_M(m, s);
+  st_collision(m, s);
+  st_constraints(m, s);
+  st_velocity(m, s);
+  st_actuation_smooth(m, s);
+  st_newton(m, s);
+  st_noslip(m, s);
+  st_finish_accel(m, s);
+}
+
+template <typename T>
+__device__ void check_state(const DevPhys<T>& m, Env<T>& s) {
+  const int l = lane_id();
+  const bool bq = l < m.nq && is_bad(s.qpos[l]);
+  const bool bv = l < m.nv && is_bad(s.qvel[l]);
+  const uint64_t mq = __ballot(bq), mv = __ballot(bv);
+  if (mq || mv) {
+    if (l == 0) s.warn |= (mq ? 1u : 0u) | (mv ? 2u : 0u);
+    wsync();
+    reset_state(m, s);
+  }
+}
+
+template <typename T>
+__device__ void mj_step_dev(const DevPhys<T>& m, Env<T>& s) {
+  check_state(m, s);
+  forward(m, s);
+  const int l = lane_id();
+  const uint64_t bad = __ballot(l < m.nv && is_bad(s.qacc[l]));
+  if (bad) {
+    if (l == 0) s.warn |= 4u;
+    wsync();
+    reset_state(m, s);
+    forward(m, s);
+  }
+  st_euler(m, s);
+}
+
+template <typename T>
+__device__ void load_env(const DevPhys<T>& m, Env<T>& s, const pnp_state_t<T>& st, int b) {
+  const int l = lane_id();
+  if (l < m.nq) s.qpos[l] = st.qpos[(size_t)b * m.nq + l];
+  if (l < m.nv) { s.qvel[l] = st.qvel[(size_t)b * m.nv + l]; s.qacc_ws[l] = st.qacc_warmstart[(size_t)b * m.nv + l]; }
+  if (l < m.nu) s.ctrl[l] = st.ctrl[(size_t)b * m.nu + l];
+  if (l < 3 * m.nmocap) s.mocap_pos[l] = st.mocap_pos[(size_t)b * 3 * m.nmocap + l];
+  if (l < 4 * m.nmocap) s.mocap_quat[l] = st.mocap_quat[(size_t)b * 4 * m.nmocap + l];
+  if (l == 0) { s.time = st.time[b]; s.warn = st.warn[b]; }
+  wsync();
+}
+
+template <typename T>
+__device__ void store_env(const DevPhys<T>& m, const Env<T>& s, const pnp_state_t<T>& st, int b) {
+  const int l = lane_id();
+  if (l < m.nq) st.qpos[(size_t)b * m.nq + l] = s.qpos[l];
+  if (l < m.nv) { st.qvel[(size_t)b * m.nv + l] = s.qvel[l]; st.qacc_warmstart[(size_t)b * m.nv + l] = s.qacc_ws[l]; }
+  if (l < m.nu) st.ctrl[(size_t)b * m.nu + l] = s.ctrl[l];
+  if (l < 3 * m.nmocap) st.mocap_pos[(size_t)b * 3 * m.nmocap + l] = s.mocap_pos[l];
+  if (l < 4 * m.nmocap) st.mocap_quat[(size_t)b * 4 * m.nmocap + l] = s.mocap_quat[l];
+  if (l == 0) { st.time[b] = s.time; st.warn[b] = s.warn; }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(NT) step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st, int B, int nsub) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
+  const DevPhys<T>& m = *mp;
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  load_env(m, s, st, b);
+  for (int k = 0; k < nsub; k++) mj_step_dev(m, s);
+  store_env(m, s, st, b);
+}
+
+// debug: one forward, dump intermediates (layout PNP_DBG_* in include/pnp.h)
+template <typename T>
+__global__ void __launch_bounds__(NT) forward_debug_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st, int B,
+                                                          double* __restrict__ dbg) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
+  const DevPhys<T>& m = *mp;
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  load_env(m, s, st, b);
+  forward(m, s);
+  double* o = dbg + (size_t)b * PNP_DBG_SIZE;
+  const int l = lane_id();
+  const int nv = m.nv;
+  for (int e = l; e < nv * nv; e += NT) {
+    const int i = e / nv, j = e % nv;
+    o[PNP_DBG_QM + e] = m.dof_tree[i] == m.dof_tree[j] ? (double)s.M[mblk(m, i, j)] : 0.0;
+  }
+  if (l < nv) {
+    o[PNP_DBG_BIAS + l] = s.qfrc_bias[l];
+    o[PNP_DBG_ACT + l] = s.qfrc_act[l];
+    o[PNP_DBG_QACC_SMOOTH + l] = s.qacc_smooth[l];
+    o[PNP_DBG_QACC + l] = s.qacc[l];
+  }
+  if (l == 0) {
+    o[PNP_DBG_COUNTS + 0] = s.ncon;
+    o[PNP_DBG_COUNTS + 1] = s.nefc;
+    o[PNP_DBG_COUNTS + 2] = s.solver_iter;
+    o[PNP_DBG_COUNTS + 3] = s.warn;
+  }
+  for (int c = l; c < s.ncon; c += NT) {
+    double* q = o + PNP_DBG_CON + c * PNP_DBG_CON_STRIDE;
+    for (int t = 0; t < 3; t++) q[t] = s.con[c].pos[t];
+    for (int t = 0; t < 9; t++) q[3 + t] = s.con[c].frame[t];
+    q[12] = s.con[c].dist;
+    q[13] = m.geom_id[s.con[c].g1];
+    q[14] = m.geom_id[s.con[c].g2];
+    q[15] = s.con[c].dim;
+  }
+  for (int r = l; r < s.nefc; r += NT) {
+    o[PNP_DBG_EFC_FORCE + r] = s.efc_force[r];
+    o[PNP_DBG_EFC_POS + r] = s.efc_pos[r];
+    o[PNP_DBG_EFC_D + r] = s.efc_D[r];
+    o[PNP_DBG_EFC_AREF + r] = s.efc_aref[r];
+    o[PNP_DBG_EFC_TYPE + r] = s.efc_type[r];
+    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
+    double* Jr = o + PNP_DBG_EFC_J + r * nv;
+    for (int k = 0; k < nv; k++) Jr[k] = 0;
+    for (int k = 0; k < w; k++) Jr[slot_dof(m, t0, t1, k)] = s.efc_J[r][k];
+  }
+}
+
+// ============================================================================ host launchers
+template <typename T>
+static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B, int32_t nsub, void* stream,
+                           double* dbg) {
+  if (!model || !st || B < 0 || nsub < 0) { pnp_set_error("pnp_step: bad argument"); return PNP_ERR_ARG; }
+  if (B == 0 || (nsub == 0 && !dbg)) return PNP_OK;
+  if (!st->qpos || !st->qvel || !st->ctrl || !st->mocap_pos || !st->mocap_quat || !st->qacc_warmstart ||
+      !st->time || !st->warn) {
+    pnp_set_error("pnp_step: null state buffer");
+    return PNP_ERR_ARG;
+  }
+  const DevPhys<T>* dm = phys_image<T>(model);
+  if (!dm) { pnp_set_error("pnp_step: model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  const size_t lds = sizeof(Env<T>);
+  if (dbg) {
+    auto k = forward_debug_kernel<T>;
+    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+      pnp_set_error("pnp_forward_debug: LDS %zu B not available", lds);
+      return PNP_ERR_HIP;
+    }
+    hipLaunchKernelGGL(k, dim3(B), dim3(NT), lds, (hipStream_t)stream, dm, *st, B, dbg);
+    return pnp_check_launch("forward_debug_kernel");
+  }
+  auto k = step_kernel<T>;
+  if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    pnp_set_error("pnp_step: LDS %zu B not available", lds);
+    return PNP_ERR_HIP;
+  }
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), lds, (hipStream_t)stream, dm, *st, B, nsub);
+  return pnp_check_launch("step_kernel");
+}
+
+extern "C" int32_t pnp_step(pnp_model* model, const pnp_state* st, int32_t B, int32_t nsub, void* stream) {
+  return launch_step<float>(model, reinterpret_cast<const pnp_state_t<float>*>(st), B, nsub, stream, nullptr);
+}
+extern "C" int32_t pnp_step_f64(pnp_model* model, const pnp_state_f64* st, int32_t B, int32_t nsub, void* stream) {
+  return launch_step<double>(model, reinterpret_cast<const pnp_state_t<double>*>(st), B, nsub, stream, nullptr);
+}
+extern "C" int32_t pnp_forward_debug(pnp_model* model, const pnp_state* st, int32_t B, double* dbg, void* stream) {
+  if (!dbg) { pnp_set_error("pnp_forward_debug: null dbg"); return PNP_ERR_ARG; }
+  return launch_step<float>(model, reinterpret_cast<const pnp_state_t<float>*>(st), B, 0, stream, dbg);
+}
+extern "C" int32_t pnp_forward_debug_f64(pnp_model* model, const pnp_state_f64* st, int32_t B, double* dbg,
+                                         void* stream) {
+  if (!dbg) { pnp_set_error("pnp_forward_debug: null dbg"); return PNP_ERR_ARG; }
+  return launch_step<double>(model, reinterpret_cast<const pnp_state_t<double>*>(st), B, 0, stream, dbg);
+}
+extern "C" int32_t pnp_step_lds_bytes(int32_t fp64) {
+  return fp64 ? (int32_t)sizeof(Env<double>) : (int32_t)sizeof(Env<float>);
+}

@@ -86,6 +86,47 @@ class Engine:
         _lib.check(fn(self._h, sid, _ptr(qpos), _ptr(jac), B, _stream()), "pnp_jac_site")
         return jac
 
+    # ------------------------------------------------------------------ physics
+    def new_state(self, B, dtype=torch.float32):
+        """Model-default state (mj_resetData) for B envs: dict of device tensors (SoA)."""
+        m, dev = self.model, self.device
+        mb = int((m.body_mocapid >= 0).nonzero()[0][0])
+        t = lambda a: torch.as_tensor(a, dtype=dtype, device=dev).contiguous()
+        import numpy as np
+        return dict(qpos=t(np.tile(m.qpos0, (B, 1))), qvel=t(np.zeros((B, m.nv))), ctrl=t(np.zeros((B, m.nu))),
+                    mocap_pos=t(np.tile(m.body_pos[mb], (B, 1))), mocap_quat=t(np.tile(m.body_quat[mb], (B, 1))),
+                    qacc_warmstart=t(np.zeros((B, m.nv))), time=t(np.zeros(B)),
+                    warn=torch.zeros(B, dtype=torch.int32, device=dev))
+
+    def _state_struct(self, st):
+        m = self.model
+        dt = st["qpos"].dtype
+        B = st["qpos"].shape[0]
+        shapes = dict(qpos=(m.nq,), qvel=(m.nv,), ctrl=(m.nu,), mocap_pos=(3 * m.nmocap,),
+                      mocap_quat=(4 * m.nmocap,), qacc_warmstart=(m.nv,), time=(), warn=())
+        for k, tail in shapes.items():
+            t = st[k]
+            want = torch.int32 if k == "warn" else dt
+            if t.dtype != want or not t.is_cuda or not t.is_contiguous() or tuple(t.shape) != (B,) + tail:
+                raise ValueError(f"state[{k}]: need contiguous {want} device tensor of shape {(B,) + tail}, "
+                                 f"got {t.dtype} {tuple(t.shape)} on {t.device}")
+        return _lib.PnpState(*[t.data_ptr() for t in (st[k] for k in _lib.STATE_FIELDS)]), B, dt
+
+    def step(self, st, nsub=1):
+        """nsub x mj_step in place on every env (fp32: product kernel; fp64: debug instantiation)."""
+        S, B, dt = self._state_struct(st)
+        fn = self.lib.pnp_step if dt == torch.float32 else self.lib.pnp_step_f64
+        _lib.check(fn(self._h, C.byref(S), B, int(nsub), _stream()), "pnp_step")
+        return st
+
+    def forward_debug(self, st):
+        """One mj_forward per env; returns the PNP_DBG_* record [B, PNP_DBG_SIZE] (float64)."""
+        S, B, dt = self._state_struct(st)
+        dbg = torch.zeros(B, _lib.DBG["SIZE"], dtype=torch.float64, device=self.device)
+        fn = self.lib.pnp_forward_debug if dt == torch.float32 else self.lib.pnp_forward_debug_f64
+        _lib.check(fn(self._h, C.byref(S), B, _ptr(dbg), _stream()), "pnp_forward_debug")
+        return dbg
+
     # ------------------------------------------------------------------ IK
     def ik_dls_into(self, q_init, target, out, site="ee_center_site", max_iters=100, pos_thresh=1e-3,
                     damping=1e-2, step_limit=0.1):

@@ -331,6 +331,9 @@ class _ModelBuilder:
         jnt_axis = np.zeros((nj, 3))
         jnt_range = np.zeros((nj, 2))
         jnt_limited = np.zeros(nj, np.int32)
+        jnt_solref = np.tile([0.02, 1.0], (nj, 1))          # solreflimit default
+        jnt_solimp = np.tile([0.9, 0.95, 0.001, 0.5, 2.0], (nj, 1))   # solimplimit default
+        jnt_margin = np.zeros(nj)
         dof_armature, dof_damping, dof_jntid, dof_bodyid = [], [], [], []
         qpos0 = []
         nq = nv = 0
@@ -343,6 +346,12 @@ class _ModelBuilder:
             jnt_pos[j] = _vec(a.get("pos", "0 0 0"))
             ax = _vec(a.get("axis", "0 0 1"))
             jnt_axis[j] = ax / np.linalg.norm(ax)
+            if "solreflimit" in a:
+                jnt_solref[j] = _vec(a["solreflimit"])
+            if "solimplimit" in a:
+                si = _vec(a["solimplimit"])
+                jnt_solimp[j] = np.concatenate([si, jnt_solimp[j][si.size:]])
+            jnt_margin[j] = float(a.get("margin", 0))
             if t != JNT_FREE and "range" in a:
                 jnt_range[j] = _vec(a["range"])
                 lim = a.get("limited", "auto")
@@ -464,6 +473,8 @@ class _ModelBuilder:
         geom_margin = np.zeros(ng)
         geom_gap = np.zeros(ng)
         geom_dataid = -np.ones(ng, np.int32)
+        geom_solmix = np.ones(ng)
+        geom_rbound = np.zeros(ng)
         mesh_names, mesh_vert, mesh_vertadr, mesh_vertnum = [], [], [], []
         for k, g in enumerate(geoms):
             t = _GEOM_TYPES[g.get("type", "sphere")]
@@ -485,6 +496,7 @@ class _ModelBuilder:
             geom_solimp[k] = np.concatenate([si, _vec("0.9 0.95 0.001 0.5 2")[si.size:]])
             geom_margin[k] = float(g.get("margin", 0))
             geom_gap[k] = float(g.get("gap", 0))
+            geom_solmix[k] = float(g.get("solmix", 1))
             collidable = geom_contype[k] != 0 or geom_conaffinity[k] != 0
             if t == GEOM_MESH and collidable:
                 mname = g["mesh"]
@@ -495,6 +507,11 @@ class _ModelBuilder:
                     mesh_vert.append(hv)
                     mesh_names.append(mname)
                 geom_dataid[k] = mesh_names.index(mname)
+                geom_rbound[k] = np.linalg.norm(mesh_vert[geom_dataid[k]], axis=1).max()
+            elif t == GEOM_BOX:
+                geom_rbound[k] = np.linalg.norm(geom_size[k])
+            elif t == GEOM_SPHERE:
+                geom_rbound[k] = geom_size[k][0]
         # ---- sites
         ns = len(sites)
         site_bodyid = np.array([s["body"] for s in sites], np.int32)
@@ -559,6 +576,7 @@ class _ModelBuilder:
             body_ipos=body_ipos, body_iquat=body_iquat, body_mass=body_mass, body_inertia=body_inertia,
             jnt_type=jnt_type, jnt_qposadr=jnt_qposadr, jnt_dofadr=jnt_dofadr, jnt_bodyid=jnt_bodyid,
             jnt_pos=jnt_pos, jnt_axis=jnt_axis, jnt_range=jnt_range, jnt_limited=jnt_limited,
+            jnt_solref=jnt_solref, jnt_solimp=jnt_solimp, jnt_margin=jnt_margin,
             dof_armature=np.array(dof_armature), dof_damping=np.array(dof_damping),
             dof_jntid=np.array(dof_jntid, np.int32), dof_bodyid=np.array(dof_bodyid, np.int32),
             qpos0=np.array(qpos0, np.float64),
@@ -566,7 +584,7 @@ class _ModelBuilder:
             geom_conaffinity=geom_conaffinity, geom_condim=geom_condim, geom_priority=geom_priority,
             geom_size=geom_size, geom_pos=geom_pos, geom_quat=geom_quat, geom_friction=geom_friction,
             geom_solref=geom_solref, geom_solimp=geom_solimp, geom_margin=geom_margin, geom_gap=geom_gap,
-            geom_dataid=geom_dataid,
+            geom_dataid=geom_dataid, geom_solmix=geom_solmix, geom_rbound=geom_rbound,
             mesh_vertadr=np.array(mesh_vertadr, np.int32), mesh_vertnum=np.array(mesh_vertnum, np.int32),
             mesh_vert=(np.concatenate(mesh_vert) if mesh_vert else np.zeros((0, 3))),
             site_bodyid=site_bodyid, site_pos=site_pos, site_quat=site_quat,
@@ -580,6 +598,8 @@ class _ModelBuilder:
             names_site=np.array(snames), names_mesh=np.array(mesh_names, dtype="U32"),
             names_actuator=np.array([a.get("name", "") for a in self.actuators]),
         ))
+        from . import setconst
+        out.update(setconst.compute(out))
         return out
 
 

@@ -28,15 +28,19 @@ _DESC_FIELDS = [
     ("body_parentid", "I"), ("body_rootid", "I"), ("body_weldid", "I"), ("body_mocapid", "I"),
     ("body_jntadr", "I"), ("body_jntnum", "I"), ("body_dofadr", "I"), ("body_dofnum", "I"),
     ("body_pos", "D"), ("body_quat", "D"), ("body_ipos", "D"), ("body_iquat", "D"),
-    ("body_mass", "D"), ("body_inertia", "D"),
+    ("body_mass", "D"), ("body_inertia", "D"), ("body_invweight0", "D"), ("body_subtreemass", "D"),
+    ("body_treedepth", "I"),
     ("jnt_type", "I"), ("jnt_qposadr", "I"), ("jnt_dofadr", "I"), ("jnt_bodyid", "I"),
     ("jnt_limited", "I"), ("jnt_pos", "D"), ("jnt_axis", "D"), ("jnt_range", "D"),
+    ("jnt_solref", "D"), ("jnt_solimp", "D"), ("jnt_margin", "D"),
     ("dof_jntid", "I"), ("dof_bodyid", "I"), ("dof_armature", "D"), ("dof_damping", "D"),
+    ("dof_parentid", "I"), ("dof_invweight0", "D"),
     ("qpos0", "D"),
     ("geom_type", "I"), ("geom_bodyid", "I"), ("geom_contype", "I"), ("geom_conaffinity", "I"),
     ("geom_condim", "I"), ("geom_priority", "I"), ("geom_dataid", "I"), ("geom_size", "D"),
     ("geom_pos", "D"), ("geom_quat", "D"), ("geom_friction", "D"), ("geom_solref", "D"),
-    ("geom_solimp", "D"), ("geom_margin", "D"), ("geom_gap", "D"),
+    ("geom_solimp", "D"), ("geom_margin", "D"), ("geom_gap", "D"), ("geom_solmix", "D"),
+    ("geom_rbound", "D"),
     ("mesh_vertadr", "I"), ("mesh_vertnum", "I"), ("mesh_vert", "D"),
     ("site_bodyid", "I"), ("site_pos", "D"), ("site_quat", "D"),
     ("actuator_trnid", "I"), ("actuator_biastype", "I"), ("actuator_ctrllimited", "I"),

@@ -108,3 +108,70 @@ def mat2quat(mat):
     q = np.zeros(4)
     lib().orc_mat2quat(_p(q), _p(mat))
     return q
+
+
+# ------------------------------------------------------------------ physics (physics.c)
+STATE_KEYS = ("qpos", "qvel", "ctrl", "mocap_pos", "mocap_quat", "qacc_warmstart", "time", "warn")
+
+
+def _phys_lib():
+    L = lib()
+    if not getattr(L, "_phys_ready", False):
+        P = C.c_void_p
+        L.orc_step_batch.argtypes = [P, P, P, P, P, P, P, P, P, C.c_int, C.c_int, C.c_int]
+        L.orc_step_batch.restype = C.c_int
+        L.orc_data_new.restype = P
+        L.orc_data_free.argtypes = [P]
+        L.orc_set_state.argtypes = [P, P, P, P, P, P, P, P]
+        L.orc_forward.argtypes = [P, P]
+        L.orc_step.argtypes = [P, P]
+        L.orc_field.argtypes = [P, P, C.c_char_p, P, C.c_int]
+        L.orc_field.restype = C.c_int
+        L._phys_ready = True
+    return L
+
+
+def new_state(B, model=None):
+    """Model-default state (mj_resetData) for B envs, float64 SoA."""
+    m = model or load_model()
+    mocap_body = int(np.nonzero(m.body_mocapid >= 0)[0][0])
+    return dict(qpos=np.tile(m.qpos0, (B, 1)), qvel=np.zeros((B, m.nv)), ctrl=np.zeros((B, m.nu)),
+                mocap_pos=np.tile(m.body_pos[mocap_body], (B, 1)),
+                mocap_quat=np.tile(m.body_quat[mocap_body], (B, 1)),
+                qacc_warmstart=np.zeros((B, m.nv)), time=np.zeros(B), warn=np.zeros(B, np.uint32))
+
+
+def step(state, nsub=1, nthreads=1, model=None):
+    """In-place: nsub mj_step's per env (fp64 oracle)."""
+    m = model or load_model()
+    L = _phys_lib()
+    for k in STATE_KEYS:
+        dt = np.uint32 if k == "warn" else np.float64
+        if not (state[k].flags.c_contiguous and state[k].dtype == dt):
+            state[k] = np.ascontiguousarray(state[k], dt)
+    B = state["qpos"].shape[0]
+    rc = L.orc_step_batch(_desc_ptr(m), *[_p(state[k]) for k in STATE_KEYS], B, int(nsub), int(nthreads))
+    if rc:
+        raise RuntimeError("orc_step_batch failed")
+    return state
+
+
+def forward_fields(state_row, fields, model=None, do_step=False):
+    """One mj_forward (or mj_step) of one env; returns {field: array}."""
+    m = model or load_model()
+    L = _phys_lib()
+    d = L.orc_data_new()
+    try:
+        arrs = [np.ascontiguousarray(state_row[k], np.float64) for k in STATE_KEYS[:6]]
+        L.orc_set_state(_desc_ptr(m), d, *[_p(a) for a in arrs])
+        (L.orc_step if do_step else L.orc_forward)(_desc_ptr(m), d)
+        out = {}
+        buf = np.zeros(200000)
+        for f in fields:
+            n = L.orc_field(_desc_ptr(m), d, f.encode(), _p(buf), buf.size)
+            if n < 0:
+                raise KeyError(f)
+            out[f] = buf[:n].copy()
+        return out
+    finally:
+        L.orc_data_free(d)

@@ -1,0 +1,872 @@
+/*
+ * physics.c — fp64 CPU restatement of MuJoCo 2.3.3 mj_step for the shelf_pnp scene.
+ * TEST INFRASTRUCTURE ONLY: loaded by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg as the checker / the CPU baseline; never linked into libpnp.so.
+ *
+ * Reference call sites (the physics the reference executes through the MuJoCo binding):
+ *   envs/panda_env.py:355-358 (_mujoco_step: 10 x mj_step(nstep=25)), skills/base.py:39-46
+ *   (_step_sim), scripts/execute_pnp.py:102-107; options from assets/shelf_pnp.xml:4-6
+ *   (Euler, dt 0.002, noslip_iterations 3, pyramidal cone, multiccd, warmstart).
+ * MuJoCo 2.3.3 (requirements.txt:1) is NOT vendored and not installed; each stage below restates
+ * its published algorithm (engine_forward.c, engine_core_smooth.c, engine_core_constraint.c,
+ * engine_solver.c, engine_passive.c, engine_collision_*.c):
+ *   mj_kinematics, mj_comPos, mj_crb (+armature), mj_factorM, mj_collision (collision.c),
+ *   mj_makeConstraint (weld, joint limits, pyramidal contacts; diagApprox from body/dof
+ *   invweight0; solref/solimp impedance), mj_comVel, mj_passive (joint damping), mj_rne,
+ *   mj_fwdActuation (affine servos, ctrl/force clamps), mj_fwdAcceleration, Newton solver on the
+ *   primal soft-constraint problem, mj_solNoSlip (pyramidal pairs), mj_checkPos/Vel/Acc with
+ *   auto-reset, mj_Euler with implicit joint damping and quaternion integration.
+ * Parity with real MuJoCo is UNPINNED for dynamics and contacts (no reference test pins them,
+ * SURVEY §8c); the solver here converges to the exact optimum of the same convex problem.
+ */
+#include "physics.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "spatial.h"
+
+typedef const pnp_model_desc Mdl;
+
+int orc_collision(Mdl* m, orc_data* d);  /* collision.c */
+
+/* ------------------------------------------------------------------ mj_kinematics */
+static void kinematics(Mdl* m, orc_data* d) {
+  d->xpos[0] = d->xpos[1] = d->xpos[2] = 0;
+  d->xquat[0] = 1; d->xquat[1] = d->xquat[2] = d->xquat[3] = 0;
+  sp_quat2mat(d->xmat, d->xquat);
+  memcpy(d->xipos, d->xpos, 3 * sizeof(double));
+  memcpy(d->ximat, d->xmat, 9 * sizeof(double));
+  for (int i = 1; i < m->nbody; i++) {
+    double p[3], q[4];
+    int ja = m->body_jntadr[i], jn = m->body_jntnum[i];
+    if (jn == 1 && m->jnt_type[ja] == 0) {
+      const double* qp = d->qpos + m->jnt_qposadr[ja];
+      memcpy(p, qp, 3 * sizeof(double));
+      memcpy(q, qp + 3, 4 * sizeof(double));
+      sp_normalize4(q);
+      memcpy(d->xanchor + 3 * ja, p, sizeof(p));
+      memcpy(d->xaxis + 3 * ja, m->jnt_axis + 3 * ja, 3 * sizeof(double));
+    } else {
+      int pid = m->body_parentid[i];
+      const double *bp, *bq;
+      double mq[4];
+      if (m->body_mocapid[i] >= 0) {
+        int k = m->body_mocapid[i];
+        bp = d->mocap_pos + 3 * k;
+        memcpy(mq, d->mocap_quat + 4 * k, sizeof(mq));
+        sp_normalize4(mq);
+        bq = mq;
+      } else {
+        bp = m->body_pos + 3 * i;
+        bq = m->body_quat + 4 * i;
+      }
+      if (pid) {
+        mulmatvec3(p, d->xmat + 9 * pid, bp);
+        p[0] += d->xpos[3 * pid]; p[1] += d->xpos[3 * pid + 1]; p[2] += d->xpos[3 * pid + 2];
+        sp_mulquat(q, d->xquat + 4 * pid, bq);
+      } else {
+        memcpy(p, bp, sizeof(p));
+        memcpy(q, bq, sizeof(q));
+      }
+      for (int j = 0; j < jn; j++) {
+        int jid = ja + j, qa = m->jnt_qposadr[jid], t = m->jnt_type[jid];
+        double ax[3], an[3];
+        sp_rotvecquat(ax, m->jnt_axis + 3 * jid, q);
+        sp_rotvecquat(an, m->jnt_pos + 3 * jid, q);
+        an[0] += p[0]; an[1] += p[1]; an[2] += p[2];
+        if (t == 2) {
+          double dd = d->qpos[qa] - m->qpos0[qa];
+          p[0] += ax[0] * dd; p[1] += ax[1] * dd; p[2] += ax[2] * dd;
+        } else if (t == 3) {
+          double ql[4], v[3];
+          sp_axisangle2quat(ql, m->jnt_axis + 3 * jid, d->qpos[qa] - m->qpos0[qa]);
+          sp_mulquat(q, q, ql);
+          sp_rotvecquat(v, m->jnt_pos + 3 * jid, q);
+          p[0] = an[0] - v[0]; p[1] = an[1] - v[1]; p[2] = an[2] - v[2];
+        }
+        memcpy(d->xanchor + 3 * jid, an, sizeof(an));
+        memcpy(d->xaxis + 3 * jid, ax, sizeof(ax));
+      }
+    }
+    sp_normalize4(q);
+    memcpy(d->xquat + 4 * i, q, sizeof(q));
+    memcpy(d->xpos + 3 * i, p, sizeof(p));
+    sp_quat2mat(d->xmat + 9 * i, q);
+  }
+  /* mj_local2Global for inertial frames, geoms, sites */
+  for (int i = 1; i < m->nbody; i++) {
+    double v[3], q[4];
+    mulmatvec3(v, d->xmat + 9 * i, m->body_ipos + 3 * i);
+    for (int k = 0; k < 3; k++) d->xipos[3 * i + k] = d->xpos[3 * i + k] + v[k];
+    sp_mulquat(q, d->xquat + 4 * i, m->body_iquat + 4 * i);
+    sp_quat2mat(d->ximat + 9 * i, q);
+  }
+  for (int g = 0; g < m->ngeom; g++) {
+    int b = m->geom_bodyid[g];
+    double v[3], q[4];
+    mulmatvec3(v, d->xmat + 9 * b, m->geom_pos + 3 * g);
+    for (int k = 0; k < 3; k++) d->geom_xpos[3 * g + k] = d->xpos[3 * b + k] + v[k];
+    sp_mulquat(q, d->xquat + 4 * b, m->geom_quat + 4 * g);
+    sp_quat2mat(d->geom_xmat + 9 * g, q);
+  }
+  for (int s = 0; s < m->nsite; s++) {
+    int b = m->site_bodyid[s];
+    double v[3], q[4];
+    mulmatvec3(v, d->xmat + 9 * b, m->site_pos + 3 * s);
+    for (int k = 0; k < 3; k++) d->site_xpos[3 * s + k] = d->xpos[3 * b + k] + v[k];
+    sp_mulquat(q, d->xquat + 4 * b, m->site_quat + 4 * s);
+    sp_quat2mat(d->site_xmat + 9 * s, q);
+  }
+}
+
+/* ------------------------------------------------------------------ mj_comPos */
+static void com_pos(Mdl* m, orc_data* d) {
+  for (int i = 0; i < m->nbody; i++)
+    for (int k = 0; k < 3; k++) d->subtree_com[3 * i + k] = d->xipos[3 * i + k] * m->body_mass[i];
+  for (int i = m->nbody - 1; i > 0; i--)
+    for (int k = 0; k < 3; k++) d->subtree_com[3 * m->body_parentid[i] + k] += d->subtree_com[3 * i + k];
+  for (int i = 0; i < m->nbody; i++) {
+    if (m->body_subtreemass[i] < ORC_MINVAL) memcpy(d->subtree_com + 3 * i, d->xipos + 3 * i, 3 * sizeof(double));
+    else for (int k = 0; k < 3; k++) d->subtree_com[3 * i + k] /= m->body_subtreemass[i];
+  }
+  memset(d->cinert, 0, 10 * sizeof(double));
+  for (int i = 1; i < m->nbody; i++) {
+    double off[3];
+    const double* c = d->subtree_com + 3 * m->body_rootid[i];
+    for (int k = 0; k < 3; k++) off[k] = d->xipos[3 * i + k] - c[k];
+    sp_inertcom(d->cinert + 10 * i, m->body_inertia + 3 * i, d->ximat + 9 * i, off, m->body_mass[i]);
+  }
+  for (int j = 0; j < m->njnt; j++) {
+    int da = m->jnt_dofadr[j], bi = m->jnt_bodyid[j];
+    double off[3], axis[3];
+    const double* c = d->subtree_com + 3 * m->body_rootid[bi];
+    for (int k = 0; k < 3; k++) off[k] = c[k] - d->xanchor[3 * j + k];
+    double* cd = d->cdof + 6 * da;
+    switch (m->jnt_type[j]) {
+      case 0:
+        memset(cd, 0, 18 * sizeof(double));
+        for (int i = 0; i < 3; i++) cd[3 + 7 * i] = 1;
+        for (int i = 0; i < 3; i++) {
+          axis[0] = d->xmat[9 * bi + i]; axis[1] = d->xmat[9 * bi + i + 3]; axis[2] = d->xmat[9 * bi + i + 6];
+          sp_dofcom(cd + 18 + 6 * i, axis, off);
+        }
+        break;
+      case 2:
+        cd[0] = cd[1] = cd[2] = 0;
+        memcpy(cd + 3, d->xaxis + 3 * j, 3 * sizeof(double));
+        break;
+      case 3:
+        sp_dofcom(cd, d->xaxis + 3 * j, off);
+        break;
+      default:
+        break;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ mj_crb + armature, factor */
+static void crb(Mdl* m, orc_data* d) {
+  int nv = m->nv;
+  memcpy(d->crb, d->cinert, 10 * m->nbody * sizeof(double));
+  for (int i = m->nbody - 1; i > 0; i--)
+    if (m->body_parentid[i] > 0)
+      for (int k = 0; k < 10; k++) d->crb[10 * m->body_parentid[i] + k] += d->crb[10 * i + k];
+  memset(d->qM, 0, nv * nv * sizeof(double));
+  for (int i = 0; i < nv; i++) {
+    double buf[6];
+    sp_mulinertvec(buf, d->crb + 10 * m->dof_bodyid[i], d->cdof + 6 * i);
+    for (int j = i; j >= 0; j = m->dof_parentid[j]) {
+      double v = 0;
+      for (int k = 0; k < 6; k++) v += d->cdof[6 * j + k] * buf[k];
+      d->qM[i * nv + j] = v;
+      d->qM[j * nv + i] = v;
+    }
+    d->qM[i * nv + i] += m->dof_armature[i];
+  }
+}
+
+/* dense Cholesky M = L L^T (lower) */
+static int chol(double* L, const double* A, int n) {
+  memcpy(L, A, n * n * sizeof(double));
+  for (int j = 0; j < n; j++) {
+    double s = L[j * n + j];
+    for (int k = 0; k < j; k++) s -= L[j * n + k] * L[j * n + k];
+    if (s <= 0) return -1;
+    s = sqrt(s);
+    L[j * n + j] = s;
+    for (int i = j + 1; i < n; i++) {
+      double t = L[i * n + j];
+      for (int k = 0; k < j; k++) t -= L[i * n + k] * L[j * n + k];
+      L[i * n + j] = t / s;
+    }
+    for (int k = j + 1; k < n; k++) L[j * n + k] = 0;
+  }
+  return 0;
+}
+
+static void chol_solve(double* x, const double* L, const double* b, int n) {
+  double y[ORC_MAXV];
+  for (int i = 0; i < n; i++) {
+    double s = b[i];
+    for (int k = 0; k < i; k++) s -= L[i * n + k] * y[k];
+    y[i] = s / L[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    double s = y[i];
+    for (int k = i + 1; k < n; k++) s -= L[k * n + i] * x[k];
+    x[i] = s / L[i * n + i];
+  }
+}
+
+static void mulM(Mdl* m, const orc_data* d, double* r, const double* v) {
+  int nv = m->nv;
+  for (int i = 0; i < nv; i++) {
+    double s = 0;
+    for (int k = 0; k < nv; k++) s += d->qM[i * nv + k] * v[k];
+    r[i] = s;
+  }
+}
+
+/* ------------------------------------------------------------------ Jacobians (mj_jac) */
+static void jac(Mdl* m, const orc_data* d, double* jp, double* jr, const double* pt, int body) {
+  int nv = m->nv;
+  if (jp) memset(jp, 0, 3 * nv * sizeof(double));
+  if (jr) memset(jr, 0, 3 * nv * sizeof(double));
+  while (body && !m->body_dofnum[body]) body = m->body_parentid[body];
+  if (!body) return;
+  double off[3];
+  const double* c = d->subtree_com + 3 * m->body_rootid[body];
+  for (int k = 0; k < 3; k++) off[k] = pt[k] - c[k];
+  for (int i = m->body_dofadr[body] + m->body_dofnum[body] - 1; i >= 0; i = m->dof_parentid[i]) {
+    const double* cd = d->cdof + 6 * i;
+    double t[3];
+    cross3(t, cd, off);
+    for (int k = 0; k < 3; k++) {
+      if (jr) jr[k * nv + i] = cd[k];
+      if (jp) jp[k * nv + i] = cd[3 + k] + t[k];
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ constraints */
+static int add_row(Mdl* m, orc_data* d, const double* J, double pos, double margin, int type, int id,
+                   double diagA) {
+  if (d->nefc >= ORC_MAXEFC) { d->warn |= ORC_WARN_CNSTRFULL; return -1; }
+  int r = d->nefc++;
+  memcpy(d->efc_J + r * m->nv, J, m->nv * sizeof(double));
+  d->efc_pos[r] = pos;
+  d->efc_margin[r] = margin;
+  d->efc_type[r] = type;
+  d->efc_id[r] = id;
+  d->efc_diagApprox[r] = diagA;
+  return r;
+}
+
+static double impedance(const double* si, double x) {
+  double dmin = fmin(fmax(si[0], 0.0001), 0.9999), dmax = fmin(fmax(si[1], 0.0001), 0.9999);
+  double width = si[2], mid = si[3], power = si[4];
+  x = fabs(x);
+  if (width <= ORC_MINVAL || x >= width) return dmax;
+  double y = x / width;
+  if (power != 1) {
+    if (y <= mid) y = pow(y, power) / pow(mid, power - 1);
+    else y = 1 - pow(1 - y, power) / pow(1 - mid, power - 1);
+  }
+  return dmin + y * (dmax - dmin);
+}
+
+/* per-row impedance, R, D and the k, b of the reference acceleration (mj_makeImpedance) */
+static void row_impedance(Mdl* m, orc_data* d, int r, const double* solref, const double* solimp) {
+  double dmax = fmin(fmax(solimp[1], 0.0001), 0.9999);
+  double k, b;
+  if (solref[0] > 0) {
+    double tc = fmax(solref[0], 2 * m->timestep), dr = solref[1];
+    k = 1.0 / (dmax * dmax * tc * tc * dr * dr);
+    b = 2.0 / (dmax * tc);
+  } else {
+    k = -solref[0] / (dmax * dmax);
+    b = -solref[1] / dmax;
+  }
+  double imp = impedance(solimp, d->efc_pos[r] - d->efc_margin[r]);
+  d->efc_KBIP[4 * r] = k;
+  d->efc_KBIP[4 * r + 1] = b;
+  d->efc_KBIP[4 * r + 2] = imp;
+  d->efc_R[r] = fmax(ORC_MINVAL, (1 - imp) * d->efc_diagApprox[r] / imp);
+  d->efc_D[r] = 1.0 / d->efc_R[r];
+}
+
+static void make_constraint(Mdl* m, orc_data* d) {
+  int nv = m->nv;
+  double J[ORC_MAXV];
+  double jp0[3 * ORC_MAXV], jr0[3 * ORC_MAXV], jp1[3 * ORC_MAXV], jr1[3 * ORC_MAXV];
+  d->nefc = 0;
+  /* equality: weld (mjEQ_WELD, anchor = data[0:3] on body2, relpose = data[3:10]) */
+  for (int e = 0; e < m->neq; e++) {
+    if (m->eq_type[e] != 1) continue;
+    const double* data = m->eq_data + 11 * e;
+    int id0 = m->eq_obj1id[e], id1 = m->eq_obj2id[e];
+    double pos0[3], pos1[3], cpos[6], q[4], q1[4], q2[4];
+    mulmatvec3(pos0, d->xmat + 9 * id0, data + 3);
+    mulmatvec3(pos1, d->xmat + 9 * id1, data);
+    for (int k = 0; k < 3; k++) { pos0[k] += d->xpos[3 * id0 + k]; pos1[k] += d->xpos[3 * id1 + k]; }
+    for (int k = 0; k < 3; k++) cpos[k] = pos0[k] - pos1[k];
+    jac(m, d, jp0, jr0, pos0, id0);
+    jac(m, d, jp1, jr1, pos1, id1);
+    double torquescale = data[10];
+    sp_mulquat(q, d->xquat + 4 * id0, data + 6);
+    sp_negquat(q1, d->xquat + 4 * id1);
+    sp_mulquat(q2, q1, q);
+    for (int k = 0; k < 3; k++) cpos[3 + k] = q2[1 + k] * torquescale;
+    double tran = m->body_invweight0[2 * id0] + m->body_invweight0[2 * id1];
+    double rot = m->body_invweight0[2 * id0 + 1] + m->body_invweight0[2 * id1 + 1];
+    double Jw[6 * ORC_MAXV];
+    for (int k = 0; k < 3; k++)
+      for (int c = 0; c < nv; c++) Jw[k * nv + c] = jp0[k * nv + c] - jp1[k * nv + c];
+    for (int c = 0; c < nv; c++) {
+      double ax[3] = {jr0[c] - jr1[c], jr0[nv + c] - jr1[nv + c], jr0[2 * nv + c] - jr1[2 * nv + c]};
+      double t[4], t3[4];
+      sp_mulquataxis(t, q1, ax);
+      sp_mulquat(t3, t, q);
+      for (int k = 0; k < 3; k++) Jw[(3 + k) * nv + c] = 0.5 * t3[1 + k] * torquescale;
+    }
+    for (int k = 0; k < 6; k++) {
+      int r = add_row(m, d, Jw + k * nv, cpos[k], 0, ORC_CNSTR_EQUALITY, e, k < 3 ? tran : rot);
+      if (r >= 0) row_impedance(m, d, r, m->eq_solref + 2 * e, m->eq_solimp + 5 * e);
+    }
+  }
+  d->ne = d->nefc;
+  /* joint limits (hinge / slide) */
+  for (int j = 0; j < m->njnt; j++) {
+    if (!m->jnt_limited[j] || (m->jnt_type[j] != 2 && m->jnt_type[j] != 3)) continue;
+    double v = d->qpos[m->jnt_qposadr[j]], margin = m->jnt_margin[j];
+    for (int side = -1; side <= 1; side += 2) {
+      double dist = side * (m->jnt_range[2 * j + (side + 1) / 2] - v);
+      if (dist < margin) {
+        memset(J, 0, nv * sizeof(double));
+        J[m->jnt_dofadr[j]] = -side;
+        int r = add_row(m, d, J, dist, margin, ORC_CNSTR_LIMIT_JOINT, j, m->dof_invweight0[m->jnt_dofadr[j]]);
+        if (r >= 0) row_impedance(m, d, r, m->jnt_solref + 2 * j, m->jnt_solimp + 5 * j);
+      }
+    }
+  }
+  /* contacts, pyramidal cone: rows J_n +- mu_k J_tk (mj_instantiateContact) */
+  for (int c = 0; c < d->ncon; c++) {
+    orc_contact* con = d->contact + c;
+    int b1 = m->geom_bodyid[con->geom1], b2 = m->geom_bodyid[con->geom2];
+    jac(m, d, jp0, jr0, con->pos, b1);
+    jac(m, d, jp1, jr1, con->pos, b2);
+    double cj[3 * ORC_MAXV];
+    for (int k = 0; k < 3; k++)
+      for (int v = 0; v < nv; v++) {
+        double s = 0;
+        for (int t = 0; t < 3; t++) s += con->frame[3 * k + t] * (jp1[t * nv + v] - jp0[t * nv + v]);
+        cj[k * nv + v] = s;
+      }
+    double tran = m->body_invweight0[2 * b1] + m->body_invweight0[2 * b2];
+    double rot = m->body_invweight0[2 * b1 + 1] + m->body_invweight0[2 * b2 + 1];
+    con->efc_address = d->nefc;
+    for (int k = 1; k < con->dim; k++) {
+      double fri = con->friction[k - 1];
+      double dA = tran + fri * fri * (k < 3 ? tran : rot);
+      for (int sgn = 1; sgn >= -1; sgn -= 2) {
+        for (int v = 0; v < nv; v++) J[v] = cj[v] + sgn * fri * cj[k * nv + v];
+        int r = add_row(m, d, J, con->dist, con->includemargin, ORC_CNSTR_CONTACT_PYRAMIDAL, c, dA);
+        if (r >= 0) row_impedance(m, d, r, con->solref, con->solimp);
+      }
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ velocity stage */
+static void com_vel(Mdl* m, orc_data* d) {
+  memset(d->cvel, 0, 6 * sizeof(double));
+  for (int i = 1; i < m->nbody; i++) {
+    double cv[6];
+    memcpy(cv, d->cvel + 6 * m->body_parentid[i], sizeof(cv));
+    int bda = m->body_dofadr[i];
+    for (int j = 0; j < m->body_dofnum[i]; j++) {
+      int dof = bda + j;
+      int t = m->jnt_type[m->dof_jntid[dof]];
+      if (t == 0) {
+        memset(d->cdof_dot + 6 * dof, 0, 18 * sizeof(double));
+        for (int k = 0; k < 3; k++)
+          for (int c = 0; c < 6; c++) cv[c] += d->cdof[6 * (dof + k) + c] * d->qvel[dof + k];
+        for (int k = 0; k < 3; k++) sp_crossmotion(d->cdof_dot + 6 * (dof + 3 + k), cv, d->cdof + 6 * (dof + 3 + k));
+        for (int k = 0; k < 3; k++)
+          for (int c = 0; c < 6; c++) cv[c] += d->cdof[6 * (dof + 3 + k) + c] * d->qvel[dof + 3 + k];
+        j += 5;
+      } else {
+        sp_crossmotion(d->cdof_dot + 6 * dof, cv, d->cdof + 6 * dof);
+        for (int c = 0; c < 6; c++) cv[c] += d->cdof[6 * dof + c] * d->qvel[dof];
+      }
+    }
+    memcpy(d->cvel + 6 * i, cv, sizeof(cv));
+  }
+}
+
+static void passive(Mdl* m, orc_data* d) {
+  for (int i = 0; i < m->nv; i++) d->qfrc_passive[i] = -m->dof_damping[i] * d->qvel[i];
+}
+
+static void rne(Mdl* m, orc_data* d) {
+  double cacc[ORC_MAXB * 6], cfrc[ORC_MAXB * 6];
+  memset(cacc, 0, 6 * sizeof(double));
+  for (int k = 0; k < 3; k++) cacc[3 + k] = -m->gravity[k];
+  memset(cfrc, 0, 6 * sizeof(double));
+  for (int i = 1; i < m->nbody; i++) {
+    double tmp[6], tmp1[6];
+    int bda = m->body_dofadr[i];
+    memcpy(cacc + 6 * i, cacc + 6 * m->body_parentid[i], 6 * sizeof(double));
+    for (int j = 0; j < m->body_dofnum[i]; j++)
+      for (int c = 0; c < 6; c++) cacc[6 * i + c] += d->cdof_dot[6 * (bda + j) + c] * d->qvel[bda + j];
+    sp_mulinertvec(cfrc + 6 * i, d->cinert + 10 * i, cacc + 6 * i);
+    sp_mulinertvec(tmp, d->cinert + 10 * i, d->cvel + 6 * i);
+    sp_crossforce(tmp1, d->cvel + 6 * i, tmp);
+    for (int c = 0; c < 6; c++) cfrc[6 * i + c] += tmp1[c];
+  }
+  for (int i = m->nbody - 1; i > 0; i--)
+    if (m->body_parentid[i])
+      for (int c = 0; c < 6; c++) cfrc[6 * m->body_parentid[i] + c] += cfrc[6 * i + c];
+  for (int i = 0; i < m->nv; i++) {
+    double s = 0;
+    for (int c = 0; c < 6; c++) s += d->cdof[6 * i + c] * cfrc[6 * m->dof_bodyid[i] + c];
+    d->qfrc_bias[i] = s;
+  }
+}
+
+static void reference_constraint(Mdl* m, orc_data* d) {
+  int nv = m->nv;
+  for (int r = 0; r < d->nefc; r++) {
+    double v = 0;
+    for (int c = 0; c < nv; c++) v += d->efc_J[r * nv + c] * d->qvel[c];
+    d->efc_vel[r] = v;
+    d->efc_aref[r] = -d->efc_KBIP[4 * r + 1] * v - d->efc_KBIP[4 * r] * d->efc_KBIP[4 * r + 2] * (d->efc_pos[r] - d->efc_margin[r]);
+  }
+}
+
+/* ------------------------------------------------------------------ actuation, smooth accel */
+static void actuation(Mdl* m, orc_data* d) {
+  memset(d->qfrc_actuator, 0, m->nv * sizeof(double));
+  for (int i = 0; i < m->nu; i++) {
+    double ctrl = d->ctrl[i];
+    if (m->actuator_ctrllimited[i])
+      ctrl = fmin(fmax(ctrl, m->actuator_ctrlrange[2 * i]), m->actuator_ctrlrange[2 * i + 1]);
+    int j = m->actuator_trnid[i];
+    double gear = m->actuator_gear[i];
+    double len = gear * d->qpos[m->jnt_qposadr[j]];
+    double vel = gear * d->qvel[m->jnt_dofadr[j]];
+    const double* gp = m->actuator_gainprm + 3 * i;
+    const double* bp = m->actuator_biasprm + 3 * i;
+    double f = gp[0] * ctrl;
+    if (m->actuator_biastype[i]) f += bp[0] + bp[1] * len + bp[2] * vel;
+    if (m->actuator_forcelimited[i])
+      f = fmin(fmax(f, m->actuator_forcerange[2 * i]), m->actuator_forcerange[2 * i + 1]);
+    d->actuator_force[i] = f;
+    d->qfrc_actuator[m->jnt_dofadr[j]] += gear * f;
+  }
+}
+
+/* ------------------------------------------------------------------ Newton solver (primal) */
+static double cost_eval(Mdl* m, orc_data* d, const double* x, double* jar, int* active) {
+  int nv = m->nv, ne = d->ne;
+  double dx[ORC_MAXV], Mdx[ORC_MAXV];
+  for (int i = 0; i < nv; i++) dx[i] = x[i] - d->qacc_smooth[i];
+  mulM(m, d, Mdx, dx);
+  double c = 0;
+  for (int i = 0; i < nv; i++) c += 0.5 * dx[i] * Mdx[i];
+  for (int r = 0; r < d->nefc; r++) {
+    double v = -d->efc_aref[r];
+    for (int k = 0; k < nv; k++) v += d->efc_J[r * nv + k] * x[k];
+    if (jar) jar[r] = v;
+    int a = r < ne || v < 0;
+    if (active) active[r] = a;
+    if (a) c += 0.5 * d->efc_D[r] * v * v;
+  }
+  return c;
+}
+
+/* exact minimiser of the convex piecewise-quadratic phi(alpha) = cost(x + alpha p) */
+static double line_search(Mdl* m, orc_data* d, const double* x, const double* p, const double* jar) {
+  int nv = m->nv, ne = d->ne, n = d->nefc;
+  double Mp[ORC_MAXV], dx[ORC_MAXV], Jp[ORC_MAXEFC];
+  for (int i = 0; i < nv; i++) dx[i] = x[i] - d->qacc_smooth[i];
+  mulM(m, d, Mp, p);
+  double A = 0, B = 0;
+  for (int i = 0; i < nv; i++) { A += p[i] * Mp[i]; B += Mp[i] * dx[i]; }
+  int act[ORC_MAXEFC];
+  double brk[ORC_MAXEFC];
+  int order[ORC_MAXEFC], nb = 0;
+  for (int r = 0; r < n; r++) {
+    double v = 0;
+    for (int k = 0; k < nv; k++) v += d->efc_J[r * nv + k] * p[k];
+    Jp[r] = v;
+    if (r < ne) { act[r] = 1; }
+    else {
+      act[r] = jar[r] < 0 || (jar[r] == 0 && v < 0);
+      if (v != 0) {
+        double a = -jar[r] / v;
+        if (a > 0) { brk[r] = a; order[nb++] = r; }
+      }
+    }
+    if (act[r]) { A += d->efc_D[r] * v * v; B += d->efc_D[r] * jar[r] * v; }
+  }
+  /* sort breakpoints (insertion sort; n is small) */
+  for (int i = 1; i < nb; i++) {
+    int t = order[i], j = i - 1;
+    while (j >= 0 && brk[order[j]] > brk[t]) { order[j + 1] = order[j]; j--; }
+    order[j + 1] = t;
+  }
+  if (B >= 0) return 0;
+  for (int i = 0; i < nb; i++) {
+    int r = order[i];
+    double a = brk[r];
+    if (A * a + B >= 0) return -B / A;
+    /* crossing the breakpoint toggles the row */
+    double v = Jp[r];
+    if (act[r]) { A -= d->efc_D[r] * v * v; B -= d->efc_D[r] * jar[r] * v; act[r] = 0; }
+    else { A += d->efc_D[r] * v * v; B += d->efc_D[r] * jar[r] * v; act[r] = 1; }
+  }
+  return A > 0 ? -B / A : 0;
+}
+
+static void solve_newton(Mdl* m, orc_data* d) {
+  int nv = m->nv, n = d->nefc;
+  double x[ORC_MAXV], grad[ORC_MAXV], pdir[ORC_MAXV], H[ORC_MAXV * ORC_MAXV], L[ORC_MAXV * ORC_MAXV];
+  double jar[ORC_MAXEFC];
+  int act[ORC_MAXEFC];
+  double c_ws = cost_eval(m, d, d->qacc_warmstart, NULL, NULL);
+  double c_sm = cost_eval(m, d, d->qacc_smooth, NULL, NULL);
+  memcpy(x, c_ws < c_sm ? d->qacc_warmstart : d->qacc_smooth, nv * sizeof(double));
+  double cost = cost_eval(m, d, x, jar, act);
+  double meaninertia = 0;
+  for (int i = 0; i < nv; i++) meaninertia += d->qM[i * nv + i];
+  meaninertia /= nv;
+  double scale = 1.0 / (meaninertia * (nv > 1 ? nv : 1));
+  int it = 0;
+  double gnorm = 0, improvement = 0;
+  for (; it < 200; it++) {
+    double Mdx[ORC_MAXV], dx[ORC_MAXV];
+    for (int i = 0; i < nv; i++) dx[i] = x[i] - d->qacc_smooth[i];
+    mulM(m, d, Mdx, dx);
+    memcpy(grad, Mdx, nv * sizeof(double));
+    memcpy(H, d->qM, nv * nv * sizeof(double));
+    for (int r = 0; r < n; r++) {
+      if (!act[r]) continue;
+      const double* Jr = d->efc_J + r * nv;
+      double Dr = d->efc_D[r];
+      for (int i = 0; i < nv; i++) {
+        if (Jr[i] == 0) continue;
+        grad[i] += Jr[i] * Dr * jar[r];
+        for (int k = 0; k < nv; k++) H[i * nv + k] += Jr[i] * Dr * Jr[k];
+      }
+    }
+    gnorm = 0;
+    for (int i = 0; i < nv; i++) gnorm += grad[i] * grad[i];
+    gnorm = sqrt(gnorm) * scale;
+    if (gnorm < 1e-14) break;
+    if (chol(L, H, nv)) break;
+    chol_solve(pdir, L, grad, nv);
+    for (int i = 0; i < nv; i++) pdir[i] = -pdir[i];
+    double alpha = line_search(m, d, x, pdir, jar);
+    if (alpha <= 0) break;
+    for (int i = 0; i < nv; i++) x[i] += alpha * pdir[i];
+    double nc = cost_eval(m, d, x, jar, act);
+    improvement = (cost - nc) * scale;
+    cost = nc;
+    if (improvement < 1e-18 && it > 0) { it++; break; }
+  }
+  d->solver_iter = it;
+  d->solver_gradient = gnorm;
+  d->solver_improvement = improvement;
+  /* forces, constraint force, acceleration */
+  for (int r = 0; r < n; r++) d->efc_force[r] = act[r] ? -d->efc_D[r] * jar[r] : 0;
+  memcpy(d->qacc, x, nv * sizeof(double));
+}
+
+/* ------------------------------------------------------------------ no-slip (pyramidal) */
+static void solve_noslip(Mdl* m, orc_data* d, int maxiter) {
+  int nv = m->nv, n = d->nefc;
+  if (maxiter <= 0 || n == 0) return;
+  /* A = J M^-1 J^T */
+  double* MinvJt = (double*)malloc(sizeof(double) * n * nv);
+  double* A = (double*)malloc(sizeof(double) * n * n);
+  if (!MinvJt || !A) { free(MinvJt); free(A); return; }
+  for (int r = 0; r < n; r++) chol_solve(MinvJt + r * nv, d->qLD, d->efc_J + r * nv, nv);
+  for (int r = 0; r < n; r++)
+    for (int c = 0; c < n; c++) {
+      double s = 0;
+      for (int k = 0; k < nv; k++) s += d->efc_J[r * nv + k] * MinvJt[c * nv + k];
+      A[r * n + c] = s;
+    }
+  double* f = d->efc_force;
+  for (int iter = 0; iter < maxiter; iter++) {
+    for (int i = d->ne; i < n; i++) {
+      if (d->efc_type[i] != ORC_CNSTR_CONTACT_PYRAMIDAL) continue;
+      int dim = d->contact[d->efc_id[i]].dim;
+      for (int j = i; j < i + 2 * (dim - 1); j += 2) {
+        double res[2], Ac[4], bc[2], old[2] = {f[j], f[j + 1]};
+        for (int t = 0; t < 2; t++) {
+          double s = d->efc_b[j + t];
+          for (int c = 0; c < n; c++) s += A[(j + t) * n + c] * f[c];
+          res[t] = s;
+        }
+        Ac[0] = A[j * n + j]; Ac[1] = A[j * n + j + 1]; Ac[2] = A[(j + 1) * n + j]; Ac[3] = A[(j + 1) * n + j + 1];
+        bc[0] = res[0] - (Ac[0] * old[0] + Ac[1] * old[1]);
+        bc[1] = res[1] - (Ac[2] * old[0] + Ac[3] * old[1]);
+        double mid = 0.5 * (f[j] + f[j + 1]);
+        double K1 = Ac[0] + Ac[3] - Ac[1] - Ac[2];
+        double K0 = mid * (Ac[0] - Ac[3]) + bc[0] - bc[1];
+        if (K1 < ORC_MINVAL) {
+          f[j] = f[j + 1] = mid;
+        } else {
+          double y = -K0 / K1;
+          if (y < -mid) y = -mid;
+          else if (y > mid) y = mid;
+          f[j] = mid + y;
+          f[j + 1] = mid - y;
+        }
+      }
+      i += 2 * (dim - 1) - 1;
+    }
+  }
+  free(MinvJt);
+  free(A);
+}
+
+/* ------------------------------------------------------------------ forward / step */
+static int is_bad(double x) { return !(fabs(x) <= 1e10); }
+
+static void reset_data(Mdl* m, orc_data* d) {
+  memcpy(d->qpos, m->qpos0, m->nq * sizeof(double));
+  memset(d->qvel, 0, m->nv * sizeof(double));
+  memset(d->ctrl, 0, m->nu * sizeof(double));
+  memset(d->qacc_warmstart, 0, m->nv * sizeof(double));
+  for (int b = 0; b < m->nbody; b++) {
+    int k = m->body_mocapid[b];
+    if (k < 0) continue;
+    memcpy(d->mocap_pos + 3 * k, m->body_pos + 3 * b, 3 * sizeof(double));
+    memcpy(d->mocap_quat + 4 * k, m->body_quat + 4 * b, 4 * sizeof(double));
+  }
+  d->time = 0;
+}
+
+void orc_forward(Mdl* m, orc_data* d) {
+  int nv = m->nv;
+  kinematics(m, d);
+  com_pos(m, d);
+  crb(m, d);
+  chol(d->qLD, d->qM, nv);
+  orc_collision(m, d);
+  make_constraint(m, d);
+  com_vel(m, d);
+  passive(m, d);
+  rne(m, d);
+  reference_constraint(m, d);
+  actuation(m, d);
+  for (int i = 0; i < nv; i++) d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i] + d->qfrc_actuator[i];
+  chol_solve(d->qacc_smooth, d->qLD, d->qfrc_smooth, nv);
+  for (int r = 0; r < d->nefc; r++) {
+    double s = -d->efc_aref[r];
+    for (int k = 0; k < nv; k++) s += d->efc_J[r * nv + k] * d->qacc_smooth[k];
+    d->efc_b[r] = s;
+  }
+  if (d->nefc == 0) {
+    memcpy(d->qacc, d->qacc_smooth, nv * sizeof(double));
+    memset(d->qfrc_constraint, 0, nv * sizeof(double));
+    d->solver_iter = 0;
+    return;
+  }
+  solve_newton(m, d);
+  solve_noslip(m, d, m->noslip_iterations);
+  for (int i = 0; i < nv; i++) {
+    double s = 0;
+    for (int r = 0; r < d->nefc; r++) s += d->efc_J[r * nv + i] * d->efc_force[r];
+    d->qfrc_constraint[i] = s;
+  }
+  if (m->noslip_iterations > 0) {
+    double q[ORC_MAXV];
+    for (int i = 0; i < nv; i++) q[i] = d->qfrc_smooth[i] + d->qfrc_constraint[i];
+    chol_solve(d->qacc, d->qLD, q, nv);
+  }
+}
+
+static void euler(Mdl* m, orc_data* d) {
+  int nv = m->nv;
+  double qacc[ORC_MAXV];
+  int damp = 0;
+  for (int i = 0; i < nv; i++) damp |= m->dof_damping[i] > 0;
+  if (!damp) {
+    memcpy(qacc, d->qacc, nv * sizeof(double));
+  } else {
+    double qfrc[ORC_MAXV], H[ORC_MAXV * ORC_MAXV], L[ORC_MAXV * ORC_MAXV];
+    mulM(m, d, qfrc, d->qacc);
+    memcpy(H, d->qM, nv * nv * sizeof(double));
+    for (int i = 0; i < nv; i++) H[i * nv + i] += m->timestep * m->dof_damping[i];
+    chol(L, H, nv);
+    chol_solve(qacc, L, qfrc, nv);
+  }
+  double h = m->timestep;
+  for (int i = 0; i < nv; i++) d->qvel[i] += h * qacc[i];
+  for (int j = 0; j < m->njnt; j++) {
+    int qa = m->jnt_qposadr[j], da = m->jnt_dofadr[j];
+    switch (m->jnt_type[j]) {
+      case 0:
+        for (int k = 0; k < 3; k++) d->qpos[qa + k] += h * d->qvel[da + k];
+        sp_quatintegrate(d->qpos + qa + 3, d->qvel + da + 3, h);
+        break;
+      case 1:
+        sp_quatintegrate(d->qpos + qa, d->qvel + da, h);
+        break;
+      default:
+        d->qpos[qa] += h * d->qvel[da];
+    }
+  }
+  d->time += h;
+  memcpy(d->qacc_warmstart, d->qacc, nv * sizeof(double));
+}
+
+void orc_step(Mdl* m, orc_data* d) {
+  for (int i = 0; i < m->nq; i++)
+    if (is_bad(d->qpos[i])) { d->warn |= ORC_WARN_BADQPOS; reset_data(m, d); break; }
+  for (int i = 0; i < m->nv; i++)
+    if (is_bad(d->qvel[i])) { d->warn |= ORC_WARN_BADQVEL; reset_data(m, d); break; }
+  orc_forward(m, d);
+  for (int i = 0; i < m->nv; i++)
+    if (is_bad(d->qacc[i])) {
+      d->warn |= ORC_WARN_BADQACC;
+      reset_data(m, d);
+      orc_forward(m, d);
+      break;
+    }
+  euler(m, d);
+}
+
+/* ------------------------------------------------------------------ batch API (ctypes) */
+typedef struct {
+  Mdl* m; double *qpos, *qvel, *ctrl, *mocap_pos, *mocap_quat, *qacc_ws, *time;
+  uint32_t* warn; int b0, b1, nsub;
+} step_job;
+
+static void load_state(Mdl* m, orc_data* d, const step_job* j, int b) {
+  memcpy(d->qpos, j->qpos + (size_t)b * m->nq, m->nq * sizeof(double));
+  memcpy(d->qvel, j->qvel + (size_t)b * m->nv, m->nv * sizeof(double));
+  memcpy(d->ctrl, j->ctrl + (size_t)b * m->nu, m->nu * sizeof(double));
+  memcpy(d->mocap_pos, j->mocap_pos + (size_t)b * 3 * m->nmocap, 3 * m->nmocap * sizeof(double));
+  memcpy(d->mocap_quat, j->mocap_quat + (size_t)b * 4 * m->nmocap, 4 * m->nmocap * sizeof(double));
+  memcpy(d->qacc_warmstart, j->qacc_ws + (size_t)b * m->nv, m->nv * sizeof(double));
+  d->time = j->time[b];
+  d->warn = j->warn[b];
+}
+
+static void store_state(Mdl* m, const orc_data* d, const step_job* j, int b) {
+  memcpy(j->qpos + (size_t)b * m->nq, d->qpos, m->nq * sizeof(double));
+  memcpy(j->qvel + (size_t)b * m->nv, d->qvel, m->nv * sizeof(double));
+  memcpy(j->ctrl + (size_t)b * m->nu, d->ctrl, m->nu * sizeof(double));
+  memcpy(j->mocap_pos + (size_t)b * 3 * m->nmocap, d->mocap_pos, 3 * m->nmocap * sizeof(double));
+  memcpy(j->mocap_quat + (size_t)b * 4 * m->nmocap, d->mocap_quat, 4 * m->nmocap * sizeof(double));
+  memcpy(j->qacc_ws + (size_t)b * m->nv, d->qacc_warmstart, m->nv * sizeof(double));
+  j->time[b] = d->time;
+  j->warn[b] = d->warn;
+}
+
+static void* step_worker(void* arg) {
+  step_job* j = (step_job*)arg;
+  orc_data* d = (orc_data*)calloc(1, sizeof(orc_data));
+  if (!d) return NULL;
+  for (int b = j->b0; b < j->b1; b++) {
+    load_state(j->m, d, j, b);
+    for (int s = 0; s < j->nsub; s++) orc_step(j->m, d);
+    store_state(j->m, d, j, b);
+  }
+  free(d);
+  return NULL;
+}
+
+/* In-place: nsub mj_step's of each of B envs over nthreads host threads. */
+int orc_step_batch(Mdl* m, double* qpos, double* qvel, double* ctrl, double* mocap_pos,
+                   double* mocap_quat, double* qacc_ws, double* time, uint32_t* warn, int B,
+                   int nsub, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > B) nthreads = B > 0 ? B : 1;
+  step_job* jobs = (step_job*)calloc((size_t)nthreads, sizeof(step_job));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  if (!jobs || !th) { free(jobs); free(th); return -1; }
+  for (int t = 0; t < nthreads; t++) {
+    step_job j = {m, qpos, qvel, ctrl, mocap_pos, mocap_quat, qacc_ws, time, warn,
+                  (int)((long)B * t / nthreads), (int)((long)B * (t + 1) / nthreads), nsub};
+    jobs[t] = j;
+    if (nthreads == 1) step_worker(&jobs[t]);
+    else pthread_create(&th[t], NULL, step_worker, &jobs[t]);
+  }
+  if (nthreads > 1)
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  free(jobs); free(th);
+  return 0;
+}
+
+/* Debug: one mj_forward from a given state into a caller-owned orc_data (fields via orc_field). */
+orc_data* orc_data_new(void) { return (orc_data*)calloc(1, sizeof(orc_data)); }
+void orc_data_free(orc_data* d) { free(d); }
+int orc_data_size(void) { return (int)sizeof(orc_data); }
+
+void orc_set_state(Mdl* m, orc_data* d, const double* qpos, const double* qvel, const double* ctrl,
+                   const double* mocap_pos, const double* mocap_quat, const double* qacc_ws) {
+  memcpy(d->qpos, qpos, m->nq * sizeof(double));
+  memcpy(d->qvel, qvel, m->nv * sizeof(double));
+  memcpy(d->ctrl, ctrl, m->nu * sizeof(double));
+  memcpy(d->mocap_pos, mocap_pos, 3 * m->nmocap * sizeof(double));
+  memcpy(d->mocap_quat, mocap_quat, 4 * m->nmocap * sizeof(double));
+  memcpy(d->qacc_warmstart, qacc_ws, m->nv * sizeof(double));
+}
+
+/* copy a named field out; returns its element count (or -1). */
+int orc_field(Mdl* m, const orc_data* d, const char* name, double* out, int cap) {
+  int nv = m->nv, n = -1;
+  const double* src = NULL;
+  double tmp[ORC_MAXEFC * 4];
+#define F(nm, ptr, cnt) else if (!strcmp(name, nm)) { src = (ptr); n = (cnt); }
+  if (0) {}
+  F("qpos", d->qpos, m->nq) F("qvel", d->qvel, nv) F("qacc", d->qacc, nv)
+  F("qacc_smooth", d->qacc_smooth, nv) F("qacc_warmstart", d->qacc_warmstart, nv)
+  F("xpos", d->xpos, 3 * m->nbody) F("xquat", d->xquat, 4 * m->nbody) F("xmat", d->xmat, 9 * m->nbody)
+  F("xipos", d->xipos, 3 * m->nbody) F("ximat", d->ximat, 9 * m->nbody)
+  F("geom_xpos", d->geom_xpos, 3 * m->ngeom) F("geom_xmat", d->geom_xmat, 9 * m->ngeom)
+  F("site_xpos", d->site_xpos, 3 * m->nsite) F("site_xmat", d->site_xmat, 9 * m->nsite)
+  F("subtree_com", d->subtree_com, 3 * m->nbody) F("cinert", d->cinert, 10 * m->nbody)
+  F("cdof", d->cdof, 6 * nv) F("cvel", d->cvel, 6 * m->nbody) F("cdof_dot", d->cdof_dot, 6 * nv)
+  F("qM", d->qM, nv * nv) F("qfrc_bias", d->qfrc_bias, nv) F("qfrc_passive", d->qfrc_passive, nv)
+  F("qfrc_actuator", d->qfrc_actuator, nv) F("actuator_force", d->actuator_force, m->nu)
+  F("qfrc_smooth", d->qfrc_smooth, nv) F("qfrc_constraint", d->qfrc_constraint, nv)
+  F("efc_J", d->efc_J, d->nefc * nv) F("efc_pos", d->efc_pos, d->nefc) F("efc_R", d->efc_R, d->nefc)
+  F("efc_D", d->efc_D, d->nefc) F("efc_aref", d->efc_aref, d->nefc) F("efc_vel", d->efc_vel, d->nefc)
+  F("efc_force", d->efc_force, d->nefc) F("efc_diagApprox", d->efc_diagApprox, d->nefc)
+  F("efc_b", d->efc_b, d->nefc)
+#undef F
+  else if (!strcmp(name, "efc_type")) { for (int r = 0; r < d->nefc; r++) tmp[r] = d->efc_type[r]; src = tmp; n = d->nefc; }
+  else if (!strcmp(name, "efc_id")) { for (int r = 0; r < d->nefc; r++) tmp[r] = d->efc_id[r]; src = tmp; n = d->nefc; }
+  else if (!strcmp(name, "ncon")) { tmp[0] = d->ncon; src = tmp; n = 1; }
+  else if (!strcmp(name, "nefc")) { tmp[0] = d->nefc; src = tmp; n = 1; }
+  else if (!strcmp(name, "solver_iter")) { tmp[0] = d->solver_iter; src = tmp; n = 1; }
+  else if (!strcmp(name, "warn")) { tmp[0] = d->warn; src = tmp; n = 1; }
+  else if (!strcmp(name, "contact")) {
+    /* per contact: pos3 frame9 dist includemargin friction5 solref2 solimp5 dim geom1 geom2 = 30 */
+    n = 30 * d->ncon;
+    if (n > cap) return -1;
+    for (int c = 0; c < d->ncon; c++) {
+      const orc_contact* k = d->contact + c;
+      double* o = out + 30 * c;
+      memcpy(o, k->pos, 3 * sizeof(double)); memcpy(o + 3, k->frame, 9 * sizeof(double));
+      o[12] = k->dist; o[13] = k->includemargin; memcpy(o + 14, k->friction, 5 * sizeof(double));
+      memcpy(o + 19, k->solref, 2 * sizeof(double)); memcpy(o + 21, k->solimp, 5 * sizeof(double));
+      o[26] = k->dim; o[27] = k->geom1; o[28] = k->geom2; o[29] = k->efc_address;
+    }
+    return n;
+  }
+  if (n < 0 || n > cap) return -1;
+  memcpy(out, src, n * sizeof(double));
+  return n;
+}

@@ -1,0 +1,93 @@
+"""Exploratory GPU-vs-oracle comparison of mj_step stages (prints a report; tests/ hold the
+asserted versions).  usage: python tools/step_parity.py [B]"""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mujoco-panda-pnp_amd"), os.path.join(ROOT, "tests")]
+from oracle import oracle as O  # noqa: E402
+from pnp_amd import _lib  # noqa: E402
+from pnp_amd.engine import get_engine  # noqa: E402
+import physics_states as PS  # noqa: E402
+
+D = _lib.DBG
+
+
+def to_dev(st, dt):
+    out = {}
+    for k, v in st.items():
+        if k == "warn":
+            out[k] = torch.as_tensor(v.astype(np.int32), device="cuda")
+        else:
+            out[k] = torch.as_tensor(v, dtype=dt, device="cuda").contiguous()
+    return out
+
+
+def oracle_forward(st, b, fields):
+    return O.forward_fields({k: st[k][b] for k in O.STATE_KEYS}, fields)
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+    t0 = time.time()
+    st = PS.settled_states(B, seed=0, nsettle=50)
+    PS.random_ctrl(st)
+    st["qvel"] += np.random.default_rng(3).normal(size=st["qvel"].shape) * 0.05
+    print(f"states ready in {time.time() - t0:.1f}s", flush=True)
+    eng = get_engine()
+    m = eng.model
+    nv = m.nv
+    for dt in (torch.float64, torch.float32):
+        dbg = eng.forward_debug(to_dev(st, dt)).cpu().numpy()
+        torch.cuda.synchronize()
+        errs = {k: 0.0 for k in ("qM", "bias", "act", "qacc_smooth", "qacc", "efc_force", "efc_pos")}
+        cnt_mis = 0
+        for b in range(B):
+            f = oracle_forward(st, b, ["qM", "qfrc_bias", "qfrc_actuator", "qacc_smooth", "qacc", "ncon", "nefc",
+                                       "efc_force", "efc_pos", "solver_iter"])
+            g = dbg[b]
+            ncon, nefc, it = int(g[D["COUNTS"]]), int(g[D["COUNTS"] + 1]), int(g[D["COUNTS"] + 2])
+            if ncon != int(f["ncon"][0]) or nefc != int(f["nefc"][0]):
+                cnt_mis += 1
+                print(f"  env {b}: ncon {ncon} vs {int(f['ncon'][0])}, nefc {nefc} vs {int(f['nefc'][0])}")
+                continue
+            rel = lambda a, r: np.abs(a - r).max() / max(1.0, np.abs(r).max())
+            errs["qM"] = max(errs["qM"], rel(g[D["QM"]:D["QM"] + nv * nv], f["qM"]))
+            errs["bias"] = max(errs["bias"], rel(g[D["BIAS"]:D["BIAS"] + nv], f["qfrc_bias"]))
+            errs["act"] = max(errs["act"], rel(g[D["ACT"]:D["ACT"] + nv], f["qfrc_actuator"]))
+            errs["qacc_smooth"] = max(errs["qacc_smooth"], rel(g[D["QACC_SMOOTH"]:D["QACC_SMOOTH"] + nv], f["qacc_smooth"]))
+            errs["qacc"] = max(errs["qacc"], rel(g[D["QACC"]:D["QACC"] + nv], f["qacc"]))
+            errs["efc_force"] = max(errs["efc_force"], rel(g[D["EFC_FORCE"]:D["EFC_FORCE"] + nefc], f["efc_force"]))
+            errs["efc_pos"] = max(errs["efc_pos"], rel(g[D["EFC_POS"]:D["EFC_POS"] + nefc], f["efc_pos"]))
+        print(dt, "count mismatches", cnt_mis, {k: f"{v:.2e}" for k, v in errs.items()},
+              "gpu iters", dbg[:, D["COUNTS"] + 2].mean(), flush=True)
+    # one and ten steps
+    for nsub in (1, 10):
+        ref = PS.copy_state(st)
+        O.step(ref, nsub=nsub, nthreads=8)
+        for dt in (torch.float64, torch.float32):
+            g = to_dev(st, dt)
+            eng.step(g, nsub)
+            torch.cuda.synchronize()
+            dq = np.abs(g["qpos"].double().cpu().numpy() - ref["qpos"]).max()
+            dv = np.abs(g["qvel"].double().cpu().numpy() - ref["qvel"]).max() / max(1, np.abs(ref["qvel"]).max())
+            print(f"nsub {nsub} {dt}: max|dqpos| {dq:.2e}  rel dqvel {dv:.2e}  warn {g['warn'].cpu().numpy().max()}",
+                  flush=True)
+    # timing of the fp32 kernel
+    for B2, nsub in ((4096, 10),):
+        big = {k: torch.cat([v] * (B2 // B)) for k, v in to_dev(st, torch.float32).items()}
+        eng.step(big, 1)
+        torch.cuda.synchronize()
+        t = time.time()
+        eng.step(big, nsub)
+        torch.cuda.synchronize()
+        t = time.time() - t
+        print(f"B={B2} nsub={nsub}: {t * 1e3:.1f} ms -> {B2 * nsub / t / 1e6:.3f} M env-steps/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
