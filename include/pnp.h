@@ -231,10 +231,18 @@ int32_t pnp_step_f64(pnp_model* model, const pnp_state_f64* state, int32_t B, in
 #define PNP_DBG_EFC_AREF 2276
 #define PNP_DBG_EFC_TYPE 2404
 #define PNP_DBG_EFC_J 2532      /* nefc x nv dense */
-#define PNP_DBG_SIZE 7168
+#define PNP_DBG_QACC_NEWTON 7140 /* Newton result before no-slip */
+#define PNP_DBG_SIZE 7184
 int32_t pnp_forward_debug(pnp_model* model, const pnp_state* state, int32_t B, double* dbg, void* stream);
 int32_t pnp_forward_debug_f64(pnp_model* model, const pnp_state_f64* state, int32_t B, double* dbg,
                               void* stream);
+/* Diagnostic: pnp_step with per-stage shader-clock cycles accumulated into
+ * stage_cycles[B * PNP_NSTAGE] (uint64, device, caller zeroes).  Stages: check, kinematics,
+ * comPos+CRB, factor M, collision, constraints, velocity+RNE, actuation+smooth, Newton, noslip,
+ * finish accel, Euler.  Separate instantiation: the product kernel carries no timers. */
+#define PNP_NSTAGE 12
+int32_t pnp_step_profile(pnp_model* model, const pnp_state* state, int32_t B, int32_t nsub,
+                         unsigned long long* stage_cycles, void* stream);
 /* LDS bytes one env occupies in the step kernel (fp64 != 0: the debug instantiation). */
 int32_t pnp_step_lds_bytes(int32_t fp64);
 

@@ -8,25 +8,42 @@
 // wave-wide scan places them.
 #pragma once
 
+// Colliders emit contacts into a sink: CountSink only counts (phase 1 of the wave-wide ordered
+// placement), LdsSink writes straight into the env's LDS contact list (phase 2).  No per-lane
+// contact arrays, so nothing spills to scratch.
 template <typename T>
-__device__ __forceinline__ void c_set_normal(Con<T>& c, const T n[3]) {
-  for (int k = 0; k < 9; k++) c.frame[k] = 0;
-  c.frame[0] = n[0]; c.frame[1] = n[1]; c.frame[2] = n[2];
-}
+struct CountSink {
+  int n = 0;
+  __device__ __forceinline__ void emit(T, const T*, const T*) { n++; }
+};
+template <typename T>
+struct LdsSink {
+  Con<T>* base;
+  int cap, n = 0;
+  __device__ __forceinline__ void emit(T dist, const T pos[3], const T nrm[3]) {
+    if (n < cap) {
+      Con<T>& c = base[n];
+      c.dist = dist;
+      for (int k = 0; k < 3; k++) c.pos[k] = pos[k];
+      for (int k = 0; k < 9; k++) c.frame[k] = 0;
+      c.frame[0] = nrm[0]; c.frame[1] = nrm[1]; c.frame[2] = nrm[2];
+    }
+    n++;
+  }
+};
 
-template <typename T>
-__device__ int c_plane_sphere(const T* p1, const T* R1, const T* p2, T r, T margin, Con<T>* c) {
+template <typename T, class S>
+__device__ void c_plane_sphere(const T* p1, const T* R1, const T* p2, T r, T margin, S& out) {
   const T n[3] = {R1[2], R1[5], R1[8]}, v[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
   const T dist = t_dot3(v, n) - r;
-  if (dist > margin) return 0;
-  c[0].dist = dist;
-  c_set_normal(c[0], n);
-  for (int k = 0; k < 3; k++) c[0].pos[k] = p2[k] - n[k] * (r + dist * T(0.5));
-  return 1;
+  if (dist > margin) return;
+  T pos[3];
+  for (int k = 0; k < 3; k++) pos[k] = p2[k] - n[k] * (r + dist * T(0.5));
+  out.emit(dist, pos, n);
 }
 
-template <typename T>
-__device__ int c_plane_box(const T* p1, const T* R1, const T* p2, const T* R2, const T* s, T margin, Con<T>* c) {
+template <typename T, class S>
+__device__ void c_plane_box(const T* p1, const T* R1, const T* p2, const T* R2, const T* s, T margin, S& out) {
   const T n[3] = {R1[2], R1[5], R1[8]}, v[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
   const T dist = t_dot3(v, n);
   int cnt = 0;
@@ -36,17 +53,17 @@ __device__ int c_plane_box(const T* p1, const T* R1, const T* p2, const T* R2, c
     d_mulmatvec3(w, R2, cr);
     const T ld = t_dot3(n, w);
     if (dist + ld > margin || ld > 0) continue;
-    c[cnt].dist = dist + ld;
-    c_set_normal(c[cnt], n);
-    for (int k = 0; k < 3; k++) c[cnt].pos[k] = w[k] + p2[k] - n[k] * c[cnt].dist * T(0.5);
-    if (++cnt >= 4) return 4;
+    const T dd = dist + ld;
+    T pos[3];
+    for (int k = 0; k < 3; k++) pos[k] = w[k] + p2[k] - n[k] * dd * T(0.5);
+    out.emit(dd, pos, n);
+    if (++cnt >= 4) return;
   }
-  return cnt;
 }
 
-template <typename T>
-__device__ int c_plane_mesh(const DevPhys<T>& m, const T* p1, const T* R1, const T* p2, const T* R2, int mesh, T margin,
-                            Con<T>* c) {
+template <typename T, class S>
+__device__ void c_plane_mesh(const DevPhys<T>& m, const T* p1, const T* R1, const T* p2, const T* R2, int mesh, T margin,
+                             S& out) {
   const T n[3] = {R1[2], R1[5], R1[8]};
   const int a = m.mesh_vertadr[mesh], nv = m.mesh_vertnum[mesh];
   T best[4];
@@ -65,31 +82,28 @@ __device__ int c_plane_mesh(const DevPhys<T>& m, const T* p1, const T* R1, const
     if (cnt < 4) cnt++;
   }
   for (int k = 0; k < cnt; k++) {
-    T w[3];
+    T w[3], pos[3];
     d_mulmatvec3(w, R2, m.mesh_vert[a + bi[k]]);
-    c[k].dist = best[k];
-    c_set_normal(c[k], n);
-    for (int t = 0; t < 3; t++) c[k].pos[t] = w[t] + p2[t] - n[t] * best[k] * T(0.5);
+    for (int t = 0; t < 3; t++) pos[t] = w[t] + p2[t] - n[t] * best[k] * T(0.5);
+    out.emit(best[k], pos, n);
   }
-  return cnt;
 }
 
-template <typename T>
-__device__ int c_sphere_sphere(const T* p1, T r1, const T* p2, T r2, T margin, Con<T>* c) {
+template <typename T, class S>
+__device__ void c_sphere_sphere(const T* p1, T r1, const T* p2, T r2, T margin, S& out) {
   T n[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
   const T len = PM<T>::sqrt_(t_dot3(n, n));
   const T dist = len - r1 - r2;
-  if (dist > margin) return 0;
+  if (dist > margin) return;
   if (len < T(1e-15)) { n[0] = 1; n[1] = 0; n[2] = 0; }
   else { n[0] /= len; n[1] /= len; n[2] /= len; }
-  c[0].dist = dist;
-  c_set_normal(c[0], n);
-  for (int k = 0; k < 3; k++) c[0].pos[k] = p1[k] + n[k] * (r1 + dist * T(0.5));
-  return 1;
+  T pos[3];
+  for (int k = 0; k < 3; k++) pos[k] = p1[k] + n[k] * (r1 + dist * T(0.5));
+  out.emit(dist, pos, n);
 }
 
-template <typename T>
-__device__ int c_sphere_box(const T* p1, T r, const T* p2, const T* R2, const T* s, T margin, Con<T>* c) {
+template <typename T, class S>
+__device__ void c_sphere_box(const T* p1, T r, const T* p2, const T* R2, const T* s, T margin, S& out) {
   const T v[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
   T lc[3], cl[3], nl[3], n[3];
   t_mulmattvec3(lc, R2, v);
@@ -103,7 +117,7 @@ __device__ int c_sphere_box(const T* p1, T r, const T* p2, const T* R2, const T*
     for (int k = 0; k < 3; k++) nl[k] = cl[k] - lc[k];
     const T dd = PM<T>::sqrt_(t_dot3(nl, nl));
     dist = dd - r;
-    if (dist > margin) return 0;
+    if (dist > margin) return;
     for (int k = 0; k < 3; k++) nl[k] /= dd;
   } else {
     int kk = 0;
@@ -115,10 +129,9 @@ __device__ int c_sphere_box(const T* p1, T r, const T* p2, const T* R2, const T*
     dist = -(pen + r);
   }
   d_mulmatvec3(n, R2, nl);
-  c[0].dist = dist;
-  c_set_normal(c[0], n);
-  for (int k = 0; k < 3; k++) c[0].pos[k] = p1[k] + n[k] * (r + dist * T(0.5));
-  return 1;
+  T pos[3];
+  for (int k = 0; k < 3; k++) pos[k] = p1[k] + n[k] * (r + dist * T(0.5));
+  out.emit(dist, pos, n);
 }
 
 template <typename T>
@@ -138,9 +151,9 @@ __device__ int c_clip(T (*poly)[3], int np, int axis, T sgn, T lim, T (*out)[3])
   return no;
 }
 
-template <typename T>
-__device__ int c_box_face(const T* pr, const T* Rr, const T* sr, int ia, const T* nr, const T* pi, const T* Ri,
-                          const T* si, const T* nframe, T margin, Con<T>* c) {
+template <typename T, class S>
+__device__ void c_box_face(const T* pr, const T* Rr, const T* sr, int ia, const T* nr, const T* pi, const T* Ri,
+                           const T* si, const T* nframe, T margin, S& out) {
   const int iu = (ia + 1) % 3, iv = (ia + 2) % 3;
   const T u[3] = {Rr[iu], Rr[3 + iu], Rr[6 + iu]}, v[3] = {Rr[iv], Rr[3 + iv], Rr[6 + iv]};
   T cref[3];
@@ -171,16 +184,15 @@ __device__ int c_box_face(const T* pr, const T* Rr, const T* sr, int ia, const T
   for (int q = 0; q < np && cnt < 8; q++) {
     const T dist = poly[q][2];
     if (dist > margin) continue;
-    c[cnt].dist = dist;
-    c_set_normal(c[cnt], nframe);
-    for (int k = 0; k < 3; k++) c[cnt].pos[k] = cref[k] + u[k] * poly[q][0] + v[k] * poly[q][1] + nr[k] * poly[q][2] * T(0.5);
+    T pos[3];
+    for (int k = 0; k < 3; k++) pos[k] = cref[k] + u[k] * poly[q][0] + v[k] * poly[q][1] + nr[k] * poly[q][2] * T(0.5);
+    out.emit(dist, pos, nframe);
     cnt++;
   }
-  return cnt;
 }
 
-template <typename T>
-__device__ int c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, const T* R2, const T* s2, T margin, Con<T>* c) {
+template <typename T, class S>
+__device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, const T* R2, const T* s2, T margin, S& out) {
   const T Tv[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
   T A[3][3], Bm[3][3], AB[3][3];
   for (int i = 0; i < 3; i++)
@@ -193,14 +205,14 @@ __device__ int c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, con
     const T tl = t_dot3(Tv, A[i]);
     const T rb = s2[0] * fabs(AB[i][0]) + s2[1] * fabs(AB[i][1]) + s2[2] * fabs(AB[i][2]);
     const T sep = fabs(tl) - s1[i] - rb;
-    if (sep > margin) return 0;
+    if (sep > margin) return;
     if (sep > best) { best = sep; btype = 0; bi = i; for (int k = 0; k < 3; k++) bestn[k] = tl >= 0 ? A[i][k] : -A[i][k]; }
   }
   for (int j = 0; j < 3; j++) {
     const T tl = t_dot3(Tv, Bm[j]);
     const T ra = s1[0] * fabs(AB[0][j]) + s1[1] * fabs(AB[1][j]) + s1[2] * fabs(AB[2][j]);
     const T sep = fabs(tl) - ra - s2[j];
-    if (sep > margin) return 0;
+    if (sep > margin) return;
     if (sep > best) { best = sep; btype = 1; bj = j; for (int k = 0; k < 3; k++) bestn[k] = tl >= 0 ? Bm[j][k] : -Bm[j][k]; }
   }
   for (int i = 0; i < 3; i++)
@@ -214,16 +226,17 @@ __device__ int c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, con
       const T ra = s1[0] * fabs(t_dot3(A[0], L)) + s1[1] * fabs(t_dot3(A[1], L)) + s1[2] * fabs(t_dot3(A[2], L));
       const T rb = s2[0] * fabs(t_dot3(Bm[0], L)) + s2[1] * fabs(t_dot3(Bm[1], L)) + s2[2] * fabs(t_dot3(Bm[2], L));
       const T sep = fabs(tl) - ra - rb;
-      if (sep > margin) return 0;
+      if (sep > margin) return;
       if (T(1.05) * sep > best + T(1e-12)) {
         best = sep; btype = 2; bi = i; bj = j;
         for (int k = 0; k < 3; k++) bestn[k] = tl >= 0 ? L[k] : -L[k];
       }
     }
-  if (btype == 0) return c_box_face(p1, R1, s1, bi, bestn, p2, R2, s2, bestn, margin, c);
+  if (btype == 0) { c_box_face(p1, R1, s1, bi, bestn, p2, R2, s2, bestn, margin, out); return; }
   if (btype == 1) {
     const T nr[3] = {-bestn[0], -bestn[1], -bestn[2]};
-    return c_box_face(p2, R2, s2, bj, nr, p1, R1, s1, bestn, margin, c);
+    c_box_face(p2, R2, s2, bj, nr, p1, R1, s1, bestn, margin, out);
+    return;
   }
   T pa[3] = {p1[0], p1[1], p1[2]}, pb[3] = {p2[0], p2[1], p2[2]};
   for (int t = 0; t < 3; t++) {
@@ -242,14 +255,28 @@ __device__ int c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, con
   T ta = 0, tb = 0;
   if (den > T(1e-12)) { ta = (a * e - dd) / den; tb = (e - a * dd) / den; }
   for (int k = 0; k < 3; k++) { pa[k] += ta * ua[k]; pb[k] += tb * ub[k]; }
-  c[0].dist = best;
-  c_set_normal(c[0], bestn);
-  for (int k = 0; k < 3; k++) c[0].pos[k] = T(0.5) * (pa[k] + pb[k]);
-  return 1;
+  T pos[3];
+  for (int k = 0; k < 3; k++) pos[k] = T(0.5) * (pa[k] + pb[k]);
+  out.emit(best, pos, bestn);
+}
+
+// mju_makeFrame: complete the contact frame from its normal (colliders set the normal only)
+template <typename T>
+__device__ void t_makeframe(T f[9]) {
+  t_normalize3(f);
+  if (PM<T>::sqrt_(f[3] * f[3] + f[4] * f[4] + f[5] * f[5]) < T(0.5)) {
+    if (fabs(f[1]) < T(0.5)) { f[3] = 0; f[4] = 1; f[5] = 0; }
+    else { f[3] = 0; f[4] = 0; f[5] = 1; }
+  }
+  const T d = f[0] * f[3] + f[1] * f[4] + f[2] * f[5];
+  f[3] -= f[0] * d; f[4] -= f[1] * d; f[5] -= f[2] * d;
+  t_normalize3(f + 3);
+  t_cross(f + 6, f, f + 3);
 }
 
 template <typename T>
 __device__ void c_params(const DevPhys<T>& m, Con<T>& c, int g1, int g2) {
+  t_makeframe(c.frame);
   c.g1 = g1;
   c.g2 = g2;
   c.dim = max(m.geom_condim[g1], m.geom_condim[g2]);
@@ -272,20 +299,17 @@ __device__ void c_params(const DevPhys<T>& m, Con<T>& c, int g1, int g2) {
   c.includemargin = fmax(m.geom_margin[g1], m.geom_margin[g2]) - fmax(m.geom_gap[g1], m.geom_gap[g2]);
 }
 
-template <typename T>
-__device__ int collide_pair(const DevPhys<T>& m, const Env<T>& s, int pair, Con<T>* out) {
+template <typename T, class S>
+__device__ void collide_pair(const DevPhys<T>& m, const Env<T>& s, int pair, S& out) {
   const int g1 = m.pair_g1[pair], g2 = m.pair_g2[pair];
   const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
   const T *p1 = s.gpos[g1], *R1 = s.gmat[g1], *s1 = m.geom_size[g1];
   const T *p2 = s.gpos[g2], *R2 = s.gmat[g2], *s2 = m.geom_size[g2];
   const T margin = fmax(m.geom_margin[g1], m.geom_margin[g2]);
-  int n = 0;
-  if (t1 == 0 && t2 == 2) n = c_plane_sphere(p1, R1, p2, s2[0], margin, out);
-  else if (t1 == 0 && t2 == 6) n = c_plane_box(p1, R1, p2, R2, s2, margin, out);
-  else if (t1 == 0 && t2 == 7) n = c_plane_mesh(m, p1, R1, p2, R2, m.geom_dataid[g2], margin, out);
-  else if (t1 == 2 && t2 == 2) n = c_sphere_sphere(p1, s1[0], p2, s2[0], margin, out);
-  else if (t1 == 2 && t2 == 6) n = c_sphere_box(p1, s1[0], p2, R2, s2, margin, out);
-  else if (t1 == 6 && t2 == 6) n = c_box_box(p1, R1, s1, p2, R2, s2, margin, out);
-  for (int k = 0; k < n; k++) c_params(m, out[k], g1, g2);
-  return n;
+  if (t1 == 0 && t2 == 2) c_plane_sphere(p1, R1, p2, s2[0], margin, out);
+  else if (t1 == 0 && t2 == 6) c_plane_box(p1, R1, p2, R2, s2, margin, out);
+  else if (t1 == 0 && t2 == 7) c_plane_mesh(m, p1, R1, p2, R2, m.geom_dataid[g2], margin, out);
+  else if (t1 == 2 && t2 == 2) c_sphere_sphere(p1, s1[0], p2, s2[0], margin, out);
+  else if (t1 == 2 && t2 == 6) c_sphere_box(p1, s1[0], p2, R2, s2, margin, out);
+  else if (t1 == 6 && t2 == 6) c_box_box(p1, R1, s1, p2, R2, s2, margin, out);
 }

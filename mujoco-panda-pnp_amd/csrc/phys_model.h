@@ -28,10 +28,12 @@
 #define PH_MAXMESHV 1400
 #define PH_MAXMESH 16
 #define PH_MAXCON 28
+#define PH_MAXLIVE 192    // broadphase survivors per sub-step
 #define PH_MAXEFC 128
+#define PH_MAXJSLOT 1280  // packed constraint-Jacobian slots (sum of row widths)
 #define PH_ROWW 16        // sparse row width: dofs of <= 2 trees (arm 9 + cube 6)
 #define PH_MAXMENTRY 160  // (i, j in ancestors(i)) entries of M
-#define PH_MAXMBLK 400    // sum over trees of tree_dofnum^2
+#define PH_MAXMBLK 256    // sum over trees of tree_dofnum^2
 
 template <typename T>
 struct DevPhys {

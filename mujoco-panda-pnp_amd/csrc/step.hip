@@ -22,6 +22,8 @@
 #include "pnp_internal.h"
 
 #define NT 64
+#define EJ(r, k) s.efc_Jv[s.efc_off[r] + (k)]
+#define EW(r, k) s.efc_Wv[s.efc_off[r] + (k)]
 
 template <typename T> struct PM;
 template <> struct PM<float> {
@@ -41,13 +43,16 @@ struct Con {
 
 template <typename T>
 struct Env {
+  // ---- small model tables read in every inner loop (copied from the global model image once
+  // per launch; global loads there would be latency-bound)
+  int c_tree_dofadr[PH_MAXT], c_tree_dofnum[PH_MAXT], c_tree_moff[PH_MAXT], c_dof_tree[PH_MAXV];
   // ---- state
   T qpos[PH_MAXQ], qvel[PH_MAXV], ctrl[PH_MAXU], mocap_pos[6], mocap_quat[8], qacc_ws[PH_MAXV];
   T time;
   uint32_t warn;
   int ncon, nefc, ne, nlive, nisland, solver_iter;
   // ---- position stage
-  T xpos[PH_MAXB][3], xquat[PH_MAXB][4], xmat[PH_MAXB][9], xipos[PH_MAXB][3], ximat[PH_MAXB][9];
+  T xpos[PH_MAXB][3], xquat[PH_MAXB][4], xmat[PH_MAXB][9], xipos[PH_MAXB][3];
   T xanchor[PH_MAXJ][3], xaxis[PH_MAXJ][3];
   T gpos[PH_MAXG][3], gmat[PH_MAXG][9];
   T subcom[PH_MAXB][3];
@@ -60,21 +65,27 @@ struct Env {
   T qfrc_bias[PH_MAXV], qfrc_passive[PH_MAXV], qfrc_act[PH_MAXV], qfrc_smooth[PH_MAXV];
   T qacc_smooth[PH_MAXV], qacc[PH_MAXV], x[PH_MAXV], grad[PH_MAXV], p[PH_MAXV], v1[PH_MAXV], v2[PH_MAXV];
   // ---- collision
-  int live[PH_MAXPAIR];
-  int pcount[NT];
   Con<T> con[PH_MAXCON];
   // ---- constraints (sparse rows)
   int efc_t0[PH_MAXEFC], efc_t1[PH_MAXEFC], efc_type[PH_MAXEFC], efc_id[PH_MAXEFC];
-  T efc_J[PH_MAXEFC][PH_ROWW];
-  T efc_W[PH_MAXEFC][PH_ROWW];
-  T efc_pos[PH_MAXEFC], efc_margin[PH_MAXEFC], efc_diag[PH_MAXEFC], efc_D[PH_MAXEFC];
-  T efc_k[PH_MAXEFC], efc_bk[PH_MAXEFC], efc_imp[PH_MAXEFC], efc_aref[PH_MAXEFC], efc_bb[PH_MAXEFC];
+  int efc_off[PH_MAXEFC + 1];   // packed rows: slots [efc_off[r], efc_off[r+1])
+  T efc_Jv[PH_MAXJSLOT];
+  T efc_pos[PH_MAXEFC], efc_D[PH_MAXEFC], efc_aref[PH_MAXEFC], efc_bb[PH_MAXEFC];
   T efc_force[PH_MAXEFC], efc_jar[PH_MAXEFC], efc_Jp[PH_MAXEFC];
   int efc_act[PH_MAXEFC];
   int lim_count[PH_MAXJ];
-  // ---- Newton
-  T H[PH_MAXV][PH_MAXV];
+  int con_rbase[PH_MAXCON], con_sbase[PH_MAXCON], con_t[PH_MAXCON][2];
+  // ---- Newton Hessian; its storage is reused by the broadphase survivor list (collision stage)
+  // and by W = M^-1 J^T (no-slip stage): the three lifetimes do not overlap
+  union {
+    T H[PH_MAXV][PH_MAXV];
+    T efc_Wv[PH_MAXJSLOT];
+    int live[PH_MAXLIVE];
+  };
   int tree_island[PH_MAXT], isl_n[PH_MAXT], isl_dof[PH_MAXT][PH_MAXV];
+  int isl_eoff[PH_MAXT + 1], isl_roff[PH_MAXT + 1];
+  short isl_row[PH_MAXEFC];
+  T isl_alpha[PH_MAXT];        // per-island line-search step (also the warm-start choice)
   T red[8];
 };
 
@@ -82,11 +93,44 @@ struct Env {
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 
+// ---- wave reductions on the DPP crossbar (no LDS round trips): butterfly inside each row of
+// 16 lanes (quad_perm 1032, quad_perm 2301, row_half_mirror, row_mirror), then the four row
+// sums are read with v_readlane.  gfx9 DPP controls: quad_perm 0x00-0xFF, row_mirror 0x140,
+// row_half_mirror 0x141.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffff), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ float rdlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ double rdlane(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// sum over each row of 16 lanes, result in every lane of the row
+template <typename T>
+__device__ __forceinline__ T rowsum16(T v) {
+  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);   // row_half_mirror
+  v += dpp_f<0x140>(v);   // row_mirror
+  return v;
+}
+// sum over the wave, result (wave-uniform) in every lane
 template <typename T>
 __device__ __forceinline__ T wsum(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v = rowsum16(v);
+  return (rdlane(v, 0) + rdlane(v, 16)) + (rdlane(v, 32) + rdlane(v, 48));
 }
 
 template <typename T>
@@ -159,26 +203,30 @@ __device__ __forceinline__ void t_rotvecquat_mj(T r[3], const T v[3], const T q[
 }
 
 // slot s of a sparse row -> dof index
+// tree tables come from the env's LDS copy (Env::c_*); the DevPhys argument is kept for
+// signature symmetry with the model-side helpers
 template <typename T>
-__device__ __forceinline__ int slot_dof(const DevPhys<T>& m, int t0, int t1, int s) {
+__device__ __forceinline__ int slot_dof_(const Env<T>& s, int t0, int t1, int k) {
   if (t0 < 0) return -1;
-  int n0 = m.tree_dofnum[t0];
-  if (s < n0) return m.tree_dofadr[t0] + s;
+  const int n0 = s.c_tree_dofnum[t0];
+  if (k < n0) return s.c_tree_dofadr[t0] + k;
   if (t1 < 0) return -1;
-  s -= n0;
-  return s < m.tree_dofnum[t1] ? m.tree_dofadr[t1] + s : -1;
+  k -= n0;
+  return k < s.c_tree_dofnum[t1] ? s.c_tree_dofadr[t1] + k : -1;
 }
 template <typename T>
-__device__ __forceinline__ int row_width(const DevPhys<T>& m, int t0, int t1) {
-  return (t0 >= 0 ? m.tree_dofnum[t0] : 0) + (t1 >= 0 ? m.tree_dofnum[t1] : 0);
+__device__ __forceinline__ int row_width_(const Env<T>& s, int t0, int t1) {
+  return (t0 >= 0 ? s.c_tree_dofnum[t0] : 0) + (t1 >= 0 ? s.c_tree_dofnum[t1] : 0);
 }
 template <typename T>
-__device__ __forceinline__ int mblk(const DevPhys<T>& m, int i, int j) {
-  // i, j in the same tree
-  int t = m.dof_tree[i];
-  int a = m.tree_dofadr[t], n = m.tree_dofnum[t];
-  return m.tree_moff[t] + (i - a) * n + (j - a);
+__device__ __forceinline__ int mblk_(const Env<T>& s, int i, int j) {
+  const int t = s.c_dof_tree[i];
+  const int a = s.c_tree_dofadr[t], n = s.c_tree_dofnum[t];
+  return s.c_tree_moff[t] + (i - a) * n + (j - a);
 }
+#define slot_dof(m, t0, t1, k) slot_dof_(s, t0, t1, k)
+#define row_width(m, t0, t1) row_width_(s, t0, t1)
+#define mblk(m, i, j) mblk_(s, i, j)
 
 // ============================================================================ position stage
 template <typename T>
@@ -255,12 +303,9 @@ __device__ void st_kinematics(const DevPhys<T>& m, Env<T>& s) {
   // inertial frames (bodies) and geom frames (collidable geoms)
   for (int i = lane_id(); i < m.nbody + m.ngeom; i += NT) {
     if (i < m.nbody) {
-      T v[3], q[4], R[9];
+      T v[3];
       d_mulmatvec3(v, s.xmat[i], m.body_ipos[i]);
-      d_mulquat(q, s.xquat[i], m.body_iquat[i]);
-      d_quat2mat(R, q);
       for (int t = 0; t < 3; t++) s.xipos[i][t] = s.xpos[i][t] + v[t];
-      for (int t = 0; t < 9; t++) s.ximat[i][t] = R[t];
     } else {
       const int g = i - m.nbody, b = m.geom_bodyid[g];
       T v[3], q[4], R[9];
@@ -295,7 +340,9 @@ __device__ void st_compos_crb(const DevPhys<T>& m, Env<T>& s) {
       const T* c = s.subcom[m.body_rootid[l]];
       T dif[3] = {s.xipos[l][0] - c[0], s.xipos[l][1] - c[1], s.xipos[l][2] - c[2]};
       const T* I = m.body_inertia[l];
-      const T* R = s.ximat[l];
+      T R[9], iq[4];
+      d_mulquat(iq, s.xquat[l], m.body_iquat[l]);
+      d_quat2mat(R, iq);
       const T ms = m.body_mass[l];
       T tmp[9];
       for (int i = 0; i < 3; i++)
@@ -436,8 +483,8 @@ __device__ void solve_M(const DevPhys<T>& m, Env<T>& s, T* x, const T* b) {
 // r = M v (tree blocks, lane per dof)
 template <typename T>
 __device__ T mulM_row(const DevPhys<T>& m, const Env<T>& s, int i, const T* v) {
-  const int t = m.dof_tree[i];
-  const int a = m.tree_dofadr[t], n = m.tree_dofnum[t], o = m.tree_moff[t] + (i - a) * n;
+  const int t = s.c_dof_tree[i];
+  const int a = s.c_tree_dofadr[t], n = s.c_tree_dofnum[t], o = s.c_tree_moff[t] + (i - a) * n;
   T r = 0;
   for (int k = 0; k < n; k++) r += s.M[o + k] * v[a + k];
   return r;
@@ -450,8 +497,7 @@ template <typename T>
 __device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
   const int l = lane_id();
   // broadphase: bounding spheres; survivors compacted in pair order
-  if (l == 0) s.nlive = 0;
-  wsync();
+  int nlive = 0;
   for (int base = 0; base < m.npair; base += NT) {
     const int pi = base + l;
     bool keep = false;
@@ -462,41 +508,44 @@ __device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
       keep = true;
       if (r1 > 0 && r2 > 0) {
         T v[3] = {s.gpos[g1][0] - s.gpos[g2][0], s.gpos[g1][1] - s.gpos[g2][1], s.gpos[g1][2] - s.gpos[g2][2]};
-        keep = PM<T>::sqrt_(t_dot3(v, v)) <= r1 + r2 + mg;
+        keep = t_dot3(v, v) <= (r1 + r2 + mg) * (r1 + r2 + mg);
       }
     }
     const uint64_t bal = __ballot(keep);
-    const int before = __popcll(bal & ((1ull << l) - 1));
-    if (keep) s.live[s.nlive + before] = pi;
-    wsync();
-    if (l == 0) s.nlive += __popcll(bal);
-    wsync();
+    const int pos = nlive + __popcll(bal & ((1ull << l) - 1));
+    if (keep && pos < PH_MAXLIVE) s.live[pos] = pi;
+    nlive += __popcll(bal);
   }
-  // narrowphase: count pass, exclusive scan, write pass (same order as the oracle)
-  if (l == 0) s.ncon = 0;
+  if (nlive > PH_MAXLIVE) { if (l == 0) s.warn |= 8u; nlive = PH_MAXLIVE; }
   wsync();
-  for (int base = 0; base < s.nlive; base += NT) {
+  // narrowphase in two passes (count, then write at the scanned offset): contact order = pair order
+  int ncon = 0;
+  for (int base = 0; base < nlive; base += NT) {
     const int k = base + l;
-    Con<T> tmp[8];
-    int n = 0;
-    if (k < s.nlive) n = collide_pair(m, s, s.live[k], tmp);
-    // inclusive scan of counts over the wave
-    int incl = n;
+    CountSink<T> cs;
+    if (k < nlive) collide_pair(m, s, s.live[k], cs);
+    int incl = cs.n;
     for (int o = 1; o < 64; o <<= 1) {
-      int y = __shfl_up(incl, o);
+      const int y = __shfl_up(incl, o);
       if (l >= o) incl += y;
     }
     const int total = __shfl(incl, 63);
-    const int off = s.ncon + incl - n;
-    for (int c = 0; c < n; c++)
-      if (off + c < PH_MAXCON) s.con[off + c] = tmp[c];
-    wsync();
-    if (l == 0) {
-      if (s.ncon + total > PH_MAXCON) s.warn |= 8u;
-      s.ncon = min(s.ncon + total, PH_MAXCON);
+    const int off = ncon + incl - cs.n;
+    if (cs.n) {
+      LdsSink<T> ls{s.con + off, PH_MAXCON - off};
+      if (ls.cap > 0) {
+        collide_pair(m, s, s.live[k], ls);
+        const int g1 = m.pair_g1[s.live[k]], g2 = m.pair_g2[s.live[k]];
+        for (int c = 0; c < cs.n && c < ls.cap; c++) c_params(m, s.con[off + c], g1, g2);
+      }
     }
-    wsync();
+    ncon += total;
   }
+  if (l == 0) {
+    if (ncon > PH_MAXCON) s.warn |= 8u;
+    s.ncon = min(ncon, PH_MAXCON);
+  }
+  wsync();
 }
 
 // ============================================================================ constraints
@@ -507,15 +556,22 @@ __device__ T impedance_(const T* si, T x) {
   x = fabs(x);
   if (width <= T(1e-15) || x >= width) return dmax;
   T y = x / width;
-  if (power != T(1)) {
+  if (power == T(2)) {
+    if (y <= mid) y = y * y / mid;
+    else y = T(1) - (T(1) - y) * (T(1) - y) / (T(1) - mid);
+  } else if (power != T(1)) {
     if (y <= mid) y = pow(y, power) / pow(mid, power - 1);
     else y = T(1) - pow(T(1) - y, power) / pow(T(1) - mid, power - 1);
   }
   return dmin + y * (dmax - dmin);
 }
 
+// impedance of row r from its pos / margin / diagApprox (mj_makeImpedance): stores D and the
+// position part of the reference acceleration; the velocity part (-b J qvel) is added by
+// finish_rows once the row's Jacobian is complete (b parked in efc_Jp meanwhile)
 template <typename T>
-__device__ void row_imp(const DevPhys<T>& m, Env<T>& s, int r, const T* solref, const T* solimp) {
+__device__ void row_imp(const DevPhys<T>& m, Env<T>& s, int r, T pos, T margin, T diag, const T* solref,
+                        const T* solimp) {
   const T dmax = fmin(fmax(solimp[1], T(0.0001)), T(0.9999));
   T k, b;
   if (solref[0] > 0) {
@@ -526,12 +582,11 @@ __device__ void row_imp(const DevPhys<T>& m, Env<T>& s, int r, const T* solref, 
     k = -solref[0] / (dmax * dmax);
     b = -solref[1] / dmax;
   }
-  const T imp = impedance_(solimp, s.efc_pos[r] - s.efc_margin[r]);
-  s.efc_k[r] = k;
-  s.efc_bk[r] = b;
-  s.efc_imp[r] = imp;
-  const T R = fmax(T(1e-15), (1 - imp) * s.efc_diag[r] / imp);
-  s.efc_D[r] = T(1) / R;
+  const T imp = impedance_(solimp, pos - margin);
+  s.efc_pos[r] = pos;
+  s.efc_D[r] = T(1) / fmax(T(1e-15), (1 - imp) * diag / imp);
+  s.efc_aref[r] = -k * imp * (pos - margin);
+  s.efc_Jp[r] = b;
 }
 
 // translational Jacobian column of world point pt on body b at dof d (0 if d does not move b)
@@ -551,14 +606,41 @@ __device__ __forceinline__ void jac_col(const DevPhys<T>& m, const Env<T>& s, in
 }
 
 template <typename T>
+__device__ __forceinline__ void body_trees(const DevPhys<T>& m, int b1, int b2, int& t0, int& t1) {
+  t0 = m.body_dofmask[b1] ? m.body_tree[b1] : -1;
+  t1 = m.body_dofmask[b2] ? m.body_tree[b2] : -1;
+  if (t0 < 0) { t0 = t1; t1 = -1; }
+  if (t0 == t1) t1 = -1;
+}
+
+// exclusive wave scan of a per-lane count; returns the offset, total in *tot
+__device__ __forceinline__ int wscan(int n, int* tot) {
+  const int l = threadIdx.x;
+  int incl = n;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (l >= o) incl += y;
+  }
+  *tot = __shfl(incl, 63);
+  return incl - n;
+}
+
+// Constraint rows in MuJoCo order: weld (6 per equality), joint limits, contacts (2(dim-1) per
+// contact, pyramidal edges J_n +- mu_k J_tk).  Every row is stored packed over the dofs of the
+// <= 2 trees it touches (weld: arm 9; limits: 1 slot; cube-shelf: 6).
+template <typename T>
 __device__ void st_constraints(const DevPhys<T>& m, Env<T>& s) {
   const int l = lane_id();
-  // ---- weld rows (one equality in this scene; loop kept general)
-  int nrow = 0;
+  int nrow = 0, nslot = 0;
+  // ---- weld
   for (int e = 0; e < m.neq; e++) {
     if (m.eq_type[e] != 1) continue;
     const T* data = m.eq_data[e];
     const int id0 = m.eq_obj1id[e], id1 = m.eq_obj2id[e];
+    int t0, t1;
+    body_trees(m, id0, id1, t0, t1);
+    const int w = row_width(m, t0, t1);
+    if (nrow + 6 > PH_MAXEFC || nslot + 6 * w > PH_MAXJSLOT) { if (l == 0) s.warn |= 16u; break; }
     T pos0[3], pos1[3], q[4], q1[4], q2[4];
     d_mulmatvec3(pos0, s.xmat[id0], data + 3);
     d_mulmatvec3(pos1, s.xmat[id1], data);
@@ -567,14 +649,16 @@ __device__ void st_constraints(const DevPhys<T>& m, Env<T>& s) {
     d_mulquat(q, s.xquat[id0], data + 6);
     q1[0] = s.xquat[id1][0]; q1[1] = -s.xquat[id1][1]; q1[2] = -s.xquat[id1][2]; q1[3] = -s.xquat[id1][3];
     d_mulquat(q2, q1, q);
-    int t0 = m.body_tree[id0] >= 0 && m.body_dofmask[id0] ? m.body_tree[id0] : -1;
-    int t1 = m.body_tree[id1] >= 0 && m.body_dofmask[id1] ? m.body_tree[id1] : -1;
-    if (t0 < 0) { t0 = t1; t1 = -1; }
-    if (t0 == t1) t1 = -1;
-    const T tran = m.body_invweight0[id0][0] + m.body_invweight0[id1][0];
-    const T rot = m.body_invweight0[id0][1] + m.body_invweight0[id1][1];
-    const int r0 = nrow;
-    const int w = row_width(m, t0, t1);
+    if (l < 6) {
+      const int r = nrow + l;
+      s.efc_off[r] = nslot + l * w;
+      s.efc_t0[r] = t0; s.efc_t1[r] = t1;
+      s.efc_type[r] = 0; s.efc_id[r] = e;
+      row_imp(m, s, r, l < 3 ? pos0[l] - pos1[l] : q2[1 + (l - 3)] * ts, T(0),
+              l < 3 ? m.body_invweight0[id0][0] + m.body_invweight0[id1][0]
+                    : m.body_invweight0[id0][1] + m.body_invweight0[id1][1],
+              m.eq_solref[e], m.eq_solimp[e]);
+    }
     if (l < w) {
       const int d = slot_dof(m, t0, t1, l);
       T jp0[3], jr0[3], jp1[3], jr1[3];
@@ -588,105 +672,122 @@ __device__ void st_constraints(const DevPhys<T>& m, Env<T>& s) {
       tq[3] = q1[0] * ax[2] + q1[1] * ax[1] - q1[2] * ax[0];
       d_mulquat(t3, tq, q);
       for (int k = 0; k < 3; k++) {
-        s.efc_J[r0 + k][l] = jp0[k] - jp1[k];
-        s.efc_J[r0 + 3 + k][l] = T(0.5) * t3[1 + k] * ts;
+        s.efc_Jv[nslot + k * w + l] = jp0[k] - jp1[k];
+        s.efc_Jv[nslot + (3 + k) * w + l] = T(0.5) * t3[1 + k] * ts;
       }
     }
-    if (l < 6) {
-      const int r = r0 + l;
-      s.efc_t0[r] = t0; s.efc_t1[r] = t1;
-      s.efc_type[r] = 0; s.efc_id[r] = e;
-      s.efc_pos[r] = l < 3 ? pos0[l] - pos1[l] : q2[1 + (l - 3)] * ts;
-      s.efc_margin[r] = 0;
-      s.efc_diag[r] = l < 3 ? tran : rot;
-    }
     nrow += 6;
+    nslot += 6 * w;
   }
-  wsync();
-  if (l < 6 * m.neq) row_imp(m, s, l, m.eq_solref[l / 6], m.eq_solimp[l / 6]);
   const int ne = nrow;
-  // ---- joint limits: count per joint, scan, emit
-  int nl = 0;
+  // ---- joint limits: count per joint, scan rows and slots, emit (rows span the joint's tree)
+  int nl = 0, wl = 0;
   if (l < m.njnt && m.jnt_limited[l] && (m.jnt_type[l] == 2 || m.jnt_type[l] == 3)) {
     const T v = s.qpos[m.jnt_qposadr[l]], mg = m.jnt_margin[l];
     nl = (v - m.jnt_range[l][0] < mg) + (m.jnt_range[l][1] - v < mg);
+    wl = m.tree_dofnum[m.dof_tree[m.jnt_dofadr[l]]];
   }
-  int incl = nl;
-  for (int o = 1; o < 64; o <<= 1) {
-    int y = __shfl_up(incl, o);
-    if (l >= o) incl += y;
-  }
-  const int nlim = __shfl(incl, 63);
+  int nlim, nlslot;
+  const int lo = wscan(nl, &nlim);
+  const int so = wscan(nl * wl, &nlslot);
   if (nl) {
-    int r = ne + incl - nl;
+    int r = nrow + lo, sl = nslot + so;
     const T v = s.qpos[m.jnt_qposadr[l]], mg = m.jnt_margin[l];
     const int d = m.jnt_dofadr[l], t = m.dof_tree[d];
     for (int side = -1; side <= 1; side += 2) {
       const T dist = side * (m.jnt_range[l][(side + 1) / 2] - v);
-      if (dist < mg && r < PH_MAXEFC) {
+      if (dist < mg && r < PH_MAXEFC && sl + wl <= PH_MAXJSLOT) {
+        s.efc_off[r] = sl;
         s.efc_t0[r] = t; s.efc_t1[r] = -1;
         s.efc_type[r] = 3; s.efc_id[r] = l;
-        for (int k = 0; k < PH_ROWW; k++) s.efc_J[r][k] = 0;
-        s.efc_J[r][d - m.tree_dofadr[t]] = T(-side);
-        s.efc_pos[r] = dist;
-        s.efc_margin[r] = mg;
-        s.efc_diag[r] = m.dof_invweight0[d];
-        row_imp(m, s, r, m.jnt_solref[l], m.jnt_solimp[l]);
+        for (int k = 0; k < wl; k++) s.efc_Jv[sl + k] = 0;
+        s.efc_Jv[sl + d - m.tree_dofadr[t]] = T(-side);
+        row_imp(m, s, r, dist, mg, m.dof_invweight0[d], m.jnt_solref[l], m.jnt_solimp[l]);
         r++;
+        sl += wl;
       }
     }
   }
-  nrow = ne + nlim;
+  if (nrow + nlim > PH_MAXEFC || nslot + nlslot > PH_MAXJSLOT) {
+    if (l == 0) s.warn |= 16u;
+    nlim = 0;   // (rows past capacity were not written; drop the limits block entirely)
+    nlslot = 0;
+  }
+  nrow += nlim;
+  nslot += nlslot;
   wsync();
-  // ---- contacts (pyramidal): 2*(dim-1) rows each
-  int crow = nrow;
-  for (int c = 0; c < s.ncon; c++) {
+  // ---- contacts: per-contact row/slot bases by scan, then lanes over (contact, slot)
+  const int nc = s.ncon;
+  int my_rows = 0, my_slots = 0, t0c = -1, t1c = -1;
+  if (l < nc) {
+    const Con<T>& con = s.con[l];
+    body_trees(m, m.geom_bodyid[con.g1], m.geom_bodyid[con.g2], t0c, t1c);
+    my_rows = 2 * (con.dim - 1);
+    my_slots = my_rows * row_width(m, t0c, t1c);
+  }
+  int trows, tslots;
+  const int rbase = nrow + wscan(my_rows, &trows);
+  const int sbase = nslot + wscan(my_slots, &tslots);
+  const bool fits = l < nc && rbase + my_rows <= PH_MAXEFC && sbase + my_slots <= PH_MAXJSLOT;
+  if (l < nc) {
+    s.con_rbase[l] = fits ? rbase : -1;
+    s.con_sbase[l] = sbase;
+    s.con_t[l][0] = t0c;
+    s.con_t[l][1] = t1c;
+  }
+  if (__ballot(l < nc && !fits) && l == 0) s.warn |= 16u;
+  wsync();
+  int kept_rows = nrow;
+  {
+    // last contact that fits bounds the row count (contacts are added in order)
+    int lastrow = (l < nc && fits) ? rbase + my_rows : 0;
+    for (int o = 32; o > 0; o >>= 1) lastrow = max(lastrow, __shfl_xor(lastrow, o));
+    kept_rows = max(nrow, lastrow);
+  }
+  // jacobian slots
+  for (int base = 0; base < nc * PH_ROWW; base += NT) {
+    const int idx = base + l;
+    const int c = idx / PH_ROWW, k = idx % PH_ROWW;
+    if (c >= nc || s.con_rbase[c] < 0) continue;
+    const int t0 = s.con_t[c][0], t1 = s.con_t[c][1], w = row_width(m, t0, t1);
+    if (k >= w) continue;
     const Con<T>& con = s.con[c];
-    const int nr = 2 * (con.dim - 1);
-    if (crow + nr > PH_MAXEFC) { if (l == 0) s.warn |= 16u; break; }
+    const int d = slot_dof(m, t0, t1, k);
+    T jp1[3], jr1[3], jp2[3], jr2[3];
+    jac_col(m, s, m.geom_bodyid[con.g1], d, con.pos, jp1, jr1);
+    jac_col(m, s, m.geom_bodyid[con.g2], d, con.pos, jp2, jr2);
+    const T jd[3] = {jp2[0] - jp1[0], jp2[1] - jp1[1], jp2[2] - jp1[2]};
+    T cj[3];
+    for (int a = 0; a < 3; a++) cj[a] = con.frame[3 * a] * jd[0] + con.frame[3 * a + 1] * jd[1] + con.frame[3 * a + 2] * jd[2];
+    const int sb = s.con_sbase[c];
+    for (int a = 1; a < con.dim && a < 3; a++) {
+      const T fri = con.friction[a - 1];
+      s.efc_Jv[sb + (2 * (a - 1)) * w + k] = cj[0] + fri * cj[a];
+      s.efc_Jv[sb + (2 * (a - 1) + 1) * w + k] = cj[0] - fri * cj[a];
+    }
+  }
+  // row scalars and impedance (lanes over rows)
+  for (int base = 0; base < nc * 4; base += NT) {
+    const int idx = base + l;
+    const int c = idx / 4, q = idx % 4;
+    if (c >= nc || s.con_rbase[c] < 0) continue;
+    const Con<T>& con = s.con[c];
+    if (q >= 2 * (con.dim - 1)) continue;
+    const int r = s.con_rbase[c] + q, k = q / 2 + 1;
+    const int t0 = s.con_t[c][0], t1 = s.con_t[c][1], w = row_width(m, t0, t1);
     const int b1 = m.geom_bodyid[con.g1], b2 = m.geom_bodyid[con.g2];
-    int t0 = m.body_dofmask[b1] ? m.body_tree[b1] : -1;
-    int t1 = m.body_dofmask[b2] ? m.body_tree[b2] : -1;
-    if (t0 < 0) { t0 = t1; t1 = -1; }
-    if (t0 == t1) t1 = -1;
-    const int w = row_width(m, t0, t1);
-    if (l < w) {
-      const int d = slot_dof(m, t0, t1, l);
-      T jp1[3], jr1[3], jp2[3], jr2[3];
-      jac_col(m, s, b1, d, con.pos, jp1, jr1);
-      jac_col(m, s, b2, d, con.pos, jp2, jr2);
-      T jd[3] = {jp2[0] - jp1[0], jp2[1] - jp1[1], jp2[2] - jp1[2]};
-      T cj[3];
-      for (int k = 0; k < 3; k++) cj[k] = con.frame[3 * k] * jd[0] + con.frame[3 * k + 1] * jd[1] + con.frame[3 * k + 2] * jd[2];
-      for (int k = 1; k < con.dim && k < 3; k++) {
-        const T fri = con.friction[k - 1];
-        s.efc_J[crow + 2 * (k - 1)][l] = cj[0] + fri * cj[k];
-        s.efc_J[crow + 2 * (k - 1) + 1][l] = cj[0] - fri * cj[k];
-      }
-    } else if (l < PH_ROWW) {
-      for (int k = 0; k < nr; k++) s.efc_J[crow + k][l] = 0;
-    }
-    if (l < nr) {
-      const int r = crow + l, k = l / 2 + 1;
-      const T tran = m.body_invweight0[b1][0] + m.body_invweight0[b2][0];
-      const T rot = m.body_invweight0[b1][1] + m.body_invweight0[b2][1];
-      const T fri = con.friction[k - 1];
-      s.efc_t0[r] = t0; s.efc_t1[r] = t1;
-      s.efc_type[r] = 6; s.efc_id[r] = c;
-      s.efc_pos[r] = con.dist;
-      s.efc_margin[r] = con.includemargin;
-      s.efc_diag[r] = tran + fri * fri * (k < 3 ? tran : rot);
-      row_imp(m, s, r, con.solref, con.solimp);
-    }
-    crow += nr;
+    const T tran = m.body_invweight0[b1][0] + m.body_invweight0[b2][0];
+    const T rot = m.body_invweight0[b1][1] + m.body_invweight0[b2][1];
+    const T fri = con.friction[k - 1];
+    s.efc_off[r] = s.con_sbase[c] + q * w;
+    s.efc_t0[r] = t0; s.efc_t1[r] = t1;
+    s.efc_type[r] = 6; s.efc_id[r] = c;
+    row_imp(m, s, r, con.dist, con.includemargin, tran + fri * fri * (k < 3 ? tran : rot), con.solref, con.solimp);
   }
-  // zero the unused tail slots of every row (widths vary)
-  wsync();
-  for (int i = l; i < crow * PH_ROWW; i += NT) {
-    const int r = i / PH_ROWW, k = i % PH_ROWW;
-    if (k >= row_width(m, s.efc_t0[r], s.efc_t1[r])) s.efc_J[r][k] = 0;
+  if (l == 0) {
+    s.nefc = kept_rows;
+    s.ne = ne;
   }
-  if (l == 0) { s.nefc = crow; s.ne = ne; }
   wsync();
 }
 
@@ -757,12 +858,12 @@ __device__ void st_velocity(const DevPhys<T>& m, Env<T>& s) {
     for (int t = 0; t < 6; t++) v += s.cdof[l][t] * s.scr6[m.dof_bodyid[l]][t];
     s.qfrc_bias[l] = v;
   }
-  // reference acceleration of the rows
+  // reference acceleration of the rows: aref = -b (J qvel) - k imp (pos - margin)
   for (int r = l; r < s.nefc; r += NT) {
     const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
     T v = 0;
-    for (int k = 0; k < w; k++) v += s.efc_J[r][k] * s.qvel[slot_dof(m, t0, t1, k)];
-    s.efc_aref[r] = -s.efc_bk[r] * v - s.efc_k[r] * s.efc_imp[r] * (s.efc_pos[r] - s.efc_margin[r]);
+    for (int k = 0; k < w; k++) v += EJ(r, k) * s.qvel[slot_dof(m, t0, t1, k)];
+    s.efc_aref[r] -= s.efc_Jp[r] * v;
   }
   wsync();
 }
@@ -792,39 +893,73 @@ __device__ void st_actuation_smooth(const DevPhys<T>& m, Env<T>& s) {
   for (int r = l; r < s.nefc; r += NT) {
     const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
     T v = -s.efc_aref[r];
-    for (int k = 0; k < w; k++) v += s.efc_J[r][k] * s.qacc_smooth[slot_dof(m, t0, t1, k)];
+    for (int k = 0; k < w; k++) v += EJ(r, k) * s.qacc_smooth[slot_dof(m, t0, t1, k)];
     s.efc_bb[r] = v;
   }
   wsync();
 }
 
 // ============================================================================ Newton solver
-// jar = J x - aref, active set, cost (returned on every lane)
+static_assert(PH_MAXEFC <= 2 * NT, "two constraint rows per lane");
+
+// Island-segmented wave sum: lane I (< nis) receives the sum over islands-I items of the three
+// per-lane items (one dof, two rows; island -1 = no item).  The cost separates over islands
+// (block-diagonal M, every row inside one island), so the solver runs per island: a single
+// global cost would hide the 1e-10 improvements of the 4 mg dummy island under the arm's cost in
+// fp32, and a single global step length would tie every island to the arm's line search.
+template <typename T>
+__device__ __forceinline__ T isl_wsum(T v0, int i0, T v1, int i1, T v2, int i2, int nis) {
+  T out = 0;
+  for (int I = 0; I < nis; I++) {
+    const T t = wsum((i0 == I ? v0 : T(0)) + (i1 == I ? v1 : T(0)) + (i2 == I ? v2 : T(0)));
+    if (lane_id() == I) out = t;
+  }
+  return out;
+}
+
+// jar = J x - aref, active set; returns island l's cost on lane l (< nisland)
 template <typename T>
 __device__ T eval_cost(const DevPhys<T>& m, Env<T>& s, const T* x, bool store) {
   const int l = lane_id();
-  T c = 0;
-  if (l < m.nv) {
-    s.v1[l] = x[l] - s.qacc_smooth[l];
-  }
+  if (l < m.nv) s.v1[l] = x[l] - s.qacc_smooth[l];
   wsync();
-  if (l < m.nv) c += T(0.5) * s.v1[l] * mulM_row(m, s, l, s.v1);
-  for (int r = l; r < s.nefc; r += NT) {
+  T cd = 0, cr[2] = {T(0), T(0)};
+  int di = -1, ri[2] = {-1, -1};
+  if (l < m.nv) {
+    cd = T(0.5) * s.v1[l] * mulM_row(m, s, l, s.v1);
+    di = s.tree_island[m.dof_tree[l]];
+  }
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int r = l + k * NT;
+    if (r >= s.nefc) continue;
     const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
     T v = -s.efc_aref[r];
-    for (int k = 0; k < w; k++) v += s.efc_J[r][k] * x[slot_dof(m, t0, t1, k)];
+    for (int q = 0; q < w; q++) v += EJ(r, q) * x[slot_dof(m, t0, t1, q)];
     const int a = r < s.ne || v < 0;
     if (store) { s.efc_jar[r] = v; s.efc_act[r] = a; }
-    if (a) c += T(0.5) * s.efc_D[r] * v * v;
+    if (a) cr[k] = T(0.5) * s.efc_D[r] * v * v;
+    ri[k] = s.tree_island[t0];
   }
-  c = wsum(c);
+  const T c = isl_wsum(cd, di, cr[0], ri[0], cr[1], ri[1], s.nisland);
   wsync();
   return c;
 }
 
 template <typename T>
+__device__ __forceinline__ int row_slot_(const Env<T>& s, int t0, int t1, int tree, int dof) {
+  if (t0 == tree) return dof - s.c_tree_dofadr[t0];
+  if (t1 == tree) return s.c_tree_dofnum[t0] + dof - s.c_tree_dofadr[t1];
+  return -1;
+}
+#define row_slot(m, t0, t1, tree, dof) row_slot_(s, t0, t1, tree, dof)
+
+// Islands = trees joined by constraint rows (union-find over <= 8 trees, one lane), their dof
+// lists, the rows of each island (CSR, wave ballots) and the island Hessian entry offsets.
+template <typename T>
 __device__ void build_islands(const DevPhys<T>& m, Env<T>& s) {
-  if (lane_id() == 0) {
+  const int l = lane_id();
+  if (l == 0) {
     int par[PH_MAXT];
     for (int t = 0; t < m.ntree; t++) par[t] = t;
     for (int r = 0; r < s.nefc; r++) {
@@ -849,49 +984,183 @@ __device__ void build_islands(const DevPhys<T>& m, Env<T>& s) {
       const int isl = s.tree_island[m.dof_tree[i]];
       s.isl_dof[isl][s.isl_n[isl]++] = i;
     }
+    int eo = 0;
+    for (int I = 0; I < nis; I++) {
+      s.isl_eoff[I] = eo;
+      eo += s.isl_n[I] * (s.isl_n[I] + 1) / 2;
+    }
+    s.isl_eoff[nis] = eo;
     s.nisland = nis;
   }
   wsync();
+  // rows grouped by island (stable, row order kept inside an island)
+  int off = 0;
+  for (int I = 0; I < s.nisland; I++) {
+    if (l == 0) s.isl_roff[I] = off;
+    for (int base = 0; base < s.nefc; base += NT) {
+      const int r = base + l;
+      const bool in = r < s.nefc && s.tree_island[s.efc_t0[r]] == I;
+      const uint64_t bal = __ballot(in);
+      if (in) s.isl_row[off + __popcll(bal & ((1ull << l) - 1))] = (short)r;
+      off += __popcll(bal);
+    }
+  }
+  if (l == 0) s.isl_roff[s.nisland] = off;
+  wsync();
 }
 
-// exact minimiser of the convex piecewise quadratic phi(a) = cost(x + a p) (semi-smooth Newton
-// on phi', bracketed)
-template <typename T>
-__device__ T line_search(const DevPhys<T>& m, Env<T>& s) {
-  const int l = lane_id();
-  if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
-  for (int r = l; r < s.nefc; r += NT) {
-    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
-    T v = 0;
-    for (int k = 0; k < w; k++) v += s.efc_J[r][k] * s.p[slot_dof(m, t0, t1, k)];
-    s.efc_Jp[r] = v;
+// Cholesky + solve of one island's Hessian block held in registers (n <= N), lane-private.
+// out = -(H^-1) g on the island's dofs.  The block is Jacobi-scaled first (H' = S H S with
+// S = diag(H)^-1/2): islands mix a 1e-12 kg m^2 rotational inertia (the r = 1 mm dummy sphere)
+// with 1e-5 constraint terms, and unscaled fp32 Cholesky would lose most digits there.
+template <typename T, int N>
+__device__ void island_newton_dir_reg(Env<T>& s, int I, int n) {
+  const int* idx = s.isl_dof[I];
+  int id[N];
+#pragma unroll
+  for (int a = 0; a < N; a++) id[a] = a < n ? idx[a] : 0;
+  T sc[N];
+#pragma unroll
+  for (int a = 0; a < N; a++) {
+    const T h = a < n ? s.H[id[a]][id[a]] : T(1);
+    sc[a] = h > T(0) ? T(1) / PM<T>::sqrt_(h) : T(1);
   }
-  wsync();
+  T L[N * (N + 1) / 2];
+#pragma unroll
+  for (int a = 0; a < N; a++)
+#pragma unroll
+    for (int b = 0; b <= a; b++) L[a * (a + 1) / 2 + b] = a < n ? s.H[id[a]][id[b]] * sc[a] * sc[b] : T(a == b);
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    T d = L[j * (j + 1) / 2 + j];
+#pragma unroll
+    for (int k = 0; k < j; k++) d -= L[j * (j + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+    d = PM<T>::sqrt_(d > T(0) ? d : T(1e-30));
+    L[j * (j + 1) / 2 + j] = d;
+    const T inv = T(1) / d;
+#pragma unroll
+    for (int i = j + 1; i < N; i++) {
+      T t = L[i * (i + 1) / 2 + j];
+#pragma unroll
+      for (int k = 0; k < j; k++) t -= L[i * (i + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+      L[i * (i + 1) / 2 + j] = t * inv;
+    }
+  }
+  T y[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    T v = i < n ? s.grad[id[i]] * sc[i] : T(0);
+#pragma unroll
+    for (int k = 0; k < i; k++) v -= L[i * (i + 1) / 2 + k] * y[k];
+    y[i] = v / L[i * (i + 1) / 2 + i];
+  }
+#pragma unroll
+  for (int i = N - 1; i >= 0; i--) {
+    T v = y[i];
+#pragma unroll
+    for (int k = i + 1; k < N; k++) v -= L[k * (k + 1) / 2 + i] * y[k];
+    y[i] = v / L[i * (i + 1) / 2 + i];
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++)
+    if (i < n) s.p[id[i]] = -y[i] * sc[i];
+}
+
+// generic (merged islands of any size): in-place Cholesky through the dof list, LDS resident
+template <typename T>
+__device__ void island_newton_dir_lds(Env<T>& s, int I, int n) {
+  const int* idx = s.isl_dof[I];
+  for (int jj = 0; jj < n; jj++) {
+    const int j = idx[jj];
+    T sjj = s.H[j][j];
+    for (int kk = 0; kk < jj; kk++) sjj -= s.H[j][idx[kk]] * s.H[j][idx[kk]];
+    sjj = PM<T>::sqrt_(sjj > T(0) ? sjj : T(1e-30));
+    s.H[j][j] = sjj;
+    const T inv = T(1) / sjj;
+    for (int ii = jj + 1; ii < n; ii++) {
+      const int i = idx[ii];
+      T t = s.H[i][j];
+      for (int kk = 0; kk < jj; kk++) t -= s.H[i][idx[kk]] * s.H[j][idx[kk]];
+      s.H[i][j] = t * inv;
+    }
+  }
+  for (int ii = 0; ii < n; ii++) {
+    const int i = idx[ii];
+    T v = s.grad[i];
+    for (int kk = 0; kk < ii; kk++) v -= s.H[i][idx[kk]] * s.p[idx[kk]];
+    s.p[i] = v / s.H[i][i];
+  }
+  for (int ii = n - 1; ii >= 0; ii--) {
+    const int i = idx[ii];
+    T v = s.p[i];
+    for (int kk = ii + 1; kk < n; kk++) v -= s.H[idx[kk]][i] * s.p[idx[kk]];
+    s.p[i] = v / s.H[i][i];
+  }
+  for (int ii = 0; ii < n; ii++) s.p[idx[ii]] = -s.p[idx[ii]];
+}
+
+// Exact minimiser of each island's convex piecewise quadratic phi_I(a) = cost_I(x + a p)
+// (semi-smooth Newton on phi', bracketed); lane I owns island I's bracket.  Islands with
+// done != 0 keep a = 0.  Leaves the step lengths in s.isl_alpha.
+template <typename T>
+__device__ void line_search(const DevPhys<T>& m, Env<T>& s, bool done) {
+  const int l = lane_id();
+  const int nis = s.nisland;
+  int di = -1, ri[2] = {-1, -1};
   T A0 = 0, B0 = 0;
   if (l < m.nv) {
+    s.v1[l] = s.x[l] - s.qacc_smooth[l];
+    di = s.tree_island[m.dof_tree[l]];
+  }
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int r = l + k * NT;
+    if (r >= s.nefc) continue;
+    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
+    T v = 0;
+    for (int q = 0; q < w; q++) v += EJ(r, q) * s.p[slot_dof(m, t0, t1, q)];
+    s.efc_Jp[r] = v;
+    ri[k] = s.tree_island[t0];
+  }
+  wsync();
+  if (l < m.nv) {
     const T mp = mulM_row(m, s, l, s.p);
-    A0 = s.p[l] * 0 + mp * s.p[l];
+    A0 = mp * s.p[l];
     B0 = mp * s.v1[l];
   }
-  A0 = wsum(A0);
-  B0 = wsum(B0);
-  T lo = 0, hi = T(-1), a = 1;
+  A0 = isl_wsum(A0, di, T(0), -1, T(0), -1, nis);
+  B0 = isl_wsum(B0, di, T(0), -1, T(0), -1, nis);
+  bool fin = l >= nis || done;
+  T lo = 0, hi = T(-1), a = fin ? T(0) : T(1);
+  if (l < nis) s.isl_alpha[l] = a;
   for (int it = 0; it < 60; it++) {
-    T d1 = 0, d2 = 0;
-    for (int r = l; r < s.nefc; r += NT) {
-      const T jp = s.efc_Jp[r], v = s.efc_jar[r] + a * jp;
-      if (r < s.ne || v < 0) { d1 += s.efc_D[r] * v * jp; d2 += s.efc_D[r] * jp * jp; }
+    wsync();
+    T d1r[2] = {T(0), T(0)}, d2r[2] = {T(0), T(0)};
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int r = l + k * NT;
+      if (r >= s.nefc) continue;
+      const T jp = s.efc_Jp[r], v = s.efc_jar[r] + s.isl_alpha[ri[k]] * jp;
+      if (r < s.ne || v < 0) { d1r[k] = s.efc_D[r] * v * jp; d2r[k] = s.efc_D[r] * jp * jp; }
     }
-    d1 = wsum(d1) + A0 * a + B0;
-    d2 = wsum(d2) + A0;
-    if (d1 == T(0)) break;
-    if (d1 > 0) hi = a; else lo = a;
-    T an = a - d1 / d2;
-    if (!(an > lo) || (hi >= T(0) && !(an < hi))) an = hi >= T(0) ? T(0.5) * (lo + hi) : T(2) * a;
-    if (an == a || (hi >= T(0) && hi - lo <= PM<T>::eps() * hi)) { a = an; break; }
-    a = an;
+    T d1 = isl_wsum(T(0), -1, d1r[0], ri[0], d1r[1], ri[1], nis) + A0 * a + B0;
+    T d2 = isl_wsum(T(0), -1, d2r[0], ri[0], d2r[1], ri[1], nis) + A0;
+    if (!fin) {
+      if (!(d2 > T(0))) { a = 0; fin = true; }
+      else if (d1 == T(0)) fin = true;
+      else {
+        if (d1 > 0) hi = a; else lo = a;
+        T an = a - d1 / d2;
+        if (!(an > lo) || (hi >= T(0) && !(an < hi))) an = hi >= T(0) ? T(0.5) * (lo + hi) : T(2) * a;
+        if (an == a || (hi >= T(0) && hi - lo <= PM<T>::eps() * hi)) fin = true;
+        a = an;
+      }
+    }
+    wsync();
+    if (l < nis) s.isl_alpha[l] = a;
+    if (!__ballot(!fin)) break;
   }
-  return a;
+  wsync();
 }
 
 template <typename T>
@@ -904,100 +1173,90 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s) {
     return;
   }
   build_islands(m, s);
+  // warm start per island: the better of qacc_warmstart and qacc_smooth
   const T cws = eval_cost(m, s, s.qacc_ws, false);
   const T csm = eval_cost(m, s, s.qacc_smooth, false);
-  if (l < m.nv) s.x[l] = cws < csm ? s.qacc_ws[l] : s.qacc_smooth[l];
+  if (l < s.nisland) s.isl_alpha[l] = cws < csm ? T(1) : T(0);
   wsync();
-  T cost = eval_cost(m, s, s.x, true);
+  if (l < m.nv) s.x[l] = s.isl_alpha[s.tree_island[m.dof_tree[l]]] != T(0) ? s.qacc_ws[l] : s.qacc_smooth[l];
+  wsync();
+  T cost = eval_cost(m, s, s.x, true);   // island l's cost on lane l
+  bool done = l >= s.nisland;
   int it = 0;
+  const int nent = s.isl_eoff[s.nisland];
   for (; it < m.iterations; it++) {
-    // gradient
+    // gradient g = M (x - x_smooth) + J^T (D jar) over the dof's island rows
     if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
     wsync();
-    T g2 = 0;
     if (l < m.nv) {
       T g = mulM_row(m, s, l, s.v1);
-      const int t = m.dof_tree[l];
-      for (int r = 0; r < s.nefc; r++) {
+      const int t = m.dof_tree[l], I = s.tree_island[t];
+      for (int rr = s.isl_roff[I]; rr < s.isl_roff[I + 1]; rr++) {
+        const int r = s.isl_row[rr];
         if (!s.efc_act[r]) continue;
-        const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
-        int k = -1;
-        if (t0 == t) k = l - m.tree_dofadr[t0];
-        else if (t1 == t) k = m.tree_dofnum[t0] + l - m.tree_dofadr[t1];
-        if (k >= 0) g += s.efc_J[r][k] * s.efc_D[r] * s.efc_jar[r];
+        const int k = row_slot(m, s.efc_t0[r], s.efc_t1[r], t, l);
+        if (k >= 0) g += EJ(r, k) * s.efc_D[r] * s.efc_jar[r];
       }
       s.grad[l] = g;
-      g2 = g * g;
     }
-    g2 = wsum(g2);
-    if (!(g2 > 0)) break;
-    // Hessian island blocks: M (same tree) + sum_active D J J^T
-    for (int e = l; e < m.nv * m.nv; e += NT) {
-      const int i = e / m.nv, j = e % m.nv;
+    // Hessian island blocks (lower triangle entries, lane per entry): M + sum_active D J J^T
+    for (int e = l; e < nent; e += NT) {
+      int I = 0;
+      while (e >= s.isl_eoff[I + 1]) I++;
+      const int le = e - s.isl_eoff[I];
+      int a = (int)((PM<float>::sqrt_(8.0f * le + 1.0f) - 1.0f) * 0.5f);
+      while (a * (a + 1) / 2 > le) a--;
+      while ((a + 1) * (a + 2) / 2 <= le) a++;
+      const int b = le - a * (a + 1) / 2;
+      const int i = s.isl_dof[I][a], j = s.isl_dof[I][b];
       const int ti = m.dof_tree[i], tj = m.dof_tree[j];
-      if (s.tree_island[ti] != s.tree_island[tj] || j > i) continue;
       T h = ti == tj ? s.M[mblk(m, i, j)] : T(0);
-      for (int r = 0; r < s.nefc; r++) {
+      for (int rr = s.isl_roff[I]; rr < s.isl_roff[I + 1]; rr++) {
+        const int r = s.isl_row[rr];
         if (!s.efc_act[r]) continue;
         const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
-        int ki = -1, kj = -1;
-        if (t0 == ti) ki = i - m.tree_dofadr[t0]; else if (t1 == ti) ki = m.tree_dofnum[t0] + i - m.tree_dofadr[t1];
-        if (ki < 0) continue;
-        if (t0 == tj) kj = j - m.tree_dofadr[t0]; else if (t1 == tj) kj = m.tree_dofnum[t0] + j - m.tree_dofadr[t1];
-        if (kj < 0) continue;
-        h += s.efc_J[r][ki] * s.efc_D[r] * s.efc_J[r][kj];
+        const int ki = row_slot(m, t0, t1, ti, i);
+        const int kj = row_slot(m, t0, t1, tj, j);
+        if (ki >= 0 && kj >= 0) h += EJ(r, ki) * s.efc_D[r] * EJ(r, kj);
       }
       s.H[i][j] = h;
       s.H[j][i] = h;
     }
     wsync();
-    // factor + solve per island (lane per island): p = -H^-1 grad
-    if (l < s.nisland) {
+    // Newton direction per island (lane per island)
+    if (l < s.nisland && !done) {
       const int n = s.isl_n[l];
-      const int* idx = s.isl_dof[l];
-      // gather the island block into a compact dense matrix in place of its rows of H
-      T Hb[PH_MAXV * 0 + 1];
-      (void)Hb;
-      // Cholesky on the scattered block: index through idx
-      for (int jj = 0; jj < n; jj++) {
-        const int j = idx[jj];
-        T sjj = s.H[j][j];
-        for (int kk = 0; kk < jj; kk++) sjj -= s.H[j][idx[kk]] * s.H[j][idx[kk]];
-        sjj = PM<T>::sqrt_(sjj > T(0) ? sjj : T(1e-30));
-        s.H[j][j] = sjj;
-        const T inv = T(1) / sjj;
-        for (int ii = jj + 1; ii < n; ii++) {
-          const int i = idx[ii];
-          T t = s.H[i][j];
-          for (int kk = 0; kk < jj; kk++) t -= s.H[i][idx[kk]] * s.H[j][idx[kk]];
-          s.H[i][j] = t * inv;
-        }
-      }
-      T y[PH_MAXV];
-      for (int ii = 0; ii < n; ii++) {
-        const int i = idx[ii];
-        T v = s.grad[i];
-        for (int kk = 0; kk < ii; kk++) v -= s.H[i][idx[kk]] * y[kk];
-        y[ii] = v / s.H[i][i];
-      }
-      for (int ii = n - 1; ii >= 0; ii--) {
-        const int i = idx[ii];
-        T v = y[ii];
-        for (int kk = ii + 1; kk < n; kk++) v -= s.H[idx[kk]][i] * s.p[idx[kk]];
-        s.p[i] = v / s.H[i][i];
-      }
+      if (n <= 6) island_newton_dir_reg<T, 6>(s, l, n);
+      else if (n <= 9) island_newton_dir_reg<T, 9>(s, l, n);
+      else island_newton_dir_lds(s, l, n);
     }
     wsync();
-    if (l < m.nv) s.p[l] = -s.p[l];
-    wsync();
-    const T alpha = line_search(m, s);
-    if (!(alpha > 0)) break;
-    if (l < m.nv) s.x[l] += alpha * s.p[l];
+    line_search(m, s, done);
+    if (l < m.nv) s.x[l] += s.isl_alpha[s.tree_island[m.dof_tree[l]]] * s.p[l];
+    // remember the active set the step was computed with
+    for (int r = l; r < s.nefc; r += NT) s.efc_Jp[r] = (T)s.efc_act[r];
     wsync();
     const T nc = eval_cost(m, s, s.x, true);
-    const T impr = cost - nc;
-    cost = nc;
-    if (!(impr > PM<T>::eps() * fabs(cost)) && it > 0) { it++; break; }
+    // island converged: its step did not change its active set (then its piecewise quadratic
+    // was a single quadratic along the step and x is that quadratic's exact minimiser), or its
+    // cost stopped decreasing
+    int ci[2] = {-1, -1};
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int r = l + k * NT;
+      if (r < s.nefc && (T)s.efc_act[r] != s.efc_Jp[r]) ci[k] = s.tree_island[s.efc_t0[r]];
+    }
+    bool changed = false;
+    for (int I = 0; I < s.nisland; I++) {
+      const bool any = __ballot(ci[0] == I || ci[1] == I) != 0;
+      if (l == I) changed = any;
+    }
+    if (!done) {
+      const T impr = cost - nc;
+      if (!changed || !(impr > 0) || !(s.isl_alpha[l] > T(0))) done = true;
+      cost = nc;
+    }
+    if (!__ballot(!done)) { it++; break; }
   }
   if (l == 0) s.solver_iter = it;
   for (int r = l; r < s.nefc; r += NT) s.efc_force[r] = s.efc_act[r] ? -s.efc_D[r] * s.efc_jar[r] : T(0);
@@ -1021,18 +1280,17 @@ __device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
       const int n = m.tree_dofnum[t], o = m.tree_moff[t];
       T y[PH_MAXTDOF];
       for (int i = 0; i < n; i++) {
-        T v = s.efc_J[r][base + i];
+        T v = EJ(r, base + i);
         for (int k = 0; k < i; k++) v -= s.L[o + i * n + k] * y[k];
         y[i] = v / s.L[o + i * n + i];
       }
       for (int i = n - 1; i >= 0; i--) {
         T v = y[i];
-        for (int k = i + 1; k < n; k++) v -= s.L[o + k * n + i] * s.efc_W[r][base + k];
-        s.efc_W[r][base + i] = v / s.L[o + i * n + i];
+        for (int k = i + 1; k < n; k++) v -= s.L[o + k * n + i] * EW(r, base + k);
+        EW(r, base + i) = v / s.L[o + i * n + i];
       }
       base += n;
     }
-    for (int k = base; k < PH_ROWW; k++) s.efc_W[r][k] = 0;
   }
   // v = M^-1 J^T f (all rows)
   if (l < m.nv) {
@@ -1043,7 +1301,7 @@ __device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
       int k = -1;
       if (t0 == t) k = l - m.tree_dofadr[t0];
       else if (t1 == t) k = m.tree_dofnum[t0] + l - m.tree_dofadr[t1];
-      if (k >= 0) g += s.efc_J[r][k] * s.efc_force[r];
+      if (k >= 0) g += EJ(r, k) * s.efc_force[r];
     }
     s.v2[l] = g;
   }
@@ -1054,18 +1312,17 @@ __device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
       if (s.efc_type[i] != 6) continue;
       const int dim = s.con[s.efc_id[i]].dim;
       for (int j = i; j < i + 2 * (dim - 1); j += 2) {
+        // one pair of opposing pyramid edges; sparse rows have <= 16 slots = one DPP row
         const int t0 = s.efc_t0[j], t1 = s.efc_t1[j], w = row_width(m, t0, t1);
-        T r0 = 0, r1 = 0, a00 = 0, a01 = 0, a10 = 0, a11 = 0;
-        if (l < w) {
-          const int d = slot_dof(m, t0, t1, l);
-          const T J0 = s.efc_J[j][l], J1 = s.efc_J[j + 1][l];
-          const T W0 = s.efc_W[j][l], W1 = s.efc_W[j + 1][l];
-          r0 = J0 * s.v2[d]; r1 = J1 * s.v2[d];
-          a00 = J0 * W0; a01 = J0 * W1; a10 = J1 * W0; a11 = J1 * W1;
-        }
-        r0 = wsum(r0); r1 = wsum(r1); a00 = wsum(a00); a01 = wsum(a01); a10 = wsum(a10); a11 = wsum(a11);
-        r0 += s.efc_bb[j];
-        r1 += s.efc_bb[j + 1];
+        const bool on = l < w;
+        const int d = on ? slot_dof(m, t0, t1, l) : 0;
+        const T J0 = on ? EJ(j, l) : T(0), J1 = on ? EJ(j + 1, l) : T(0);
+        const T W0 = on ? EW(j, l) : T(0), W1 = on ? EW(j + 1, l) : T(0);
+        const T vd = on ? s.v2[d] : T(0);
+        const T r0 = rowsum16(J0 * vd) + s.efc_bb[j];
+        const T r1 = rowsum16(J1 * vd) + s.efc_bb[j + 1];
+        const T a00 = rowsum16(J0 * W0), a01 = rowsum16(J0 * W1);
+        const T a10 = rowsum16(J1 * W0), a11 = rowsum16(J1 * W1);
         const T f0 = s.efc_force[j], f1 = s.efc_force[j + 1];
         const T bc0 = r0 - (a00 * f0 + a01 * f1), bc1 = r1 - (a10 * f0 + a11 * f1);
         const T mid = T(0.5) * (f0 + f1);
@@ -1077,12 +1334,7 @@ __device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
           if (y < -mid) y = -mid; else if (y > mid) y = mid;
           n0 = mid + y; n1 = mid - y;
         }
-        const T df0 = n0 - f0, df1 = n1 - f1;
-        if (l < w) {
-          const int d = slot_dof(m, t0, t1, l);
-          s.v2[d] += s.efc_W[j][l] * df0 + s.efc_W[j + 1][l] * df1;
-        }
-        wsync();
+        if (on) s.v2[d] += W0 * (n0 - f0) + W1 * (n1 - f1);
         if (l == 0) { s.efc_force[j] = n0; s.efc_force[j + 1] = n1; }
         wsync();
       }
@@ -1103,7 +1355,7 @@ __device__ void st_finish_accel(const DevPhys<T>& m, Env<T>& s) {
       int k = -1;
       if (t0 == t) k = l - m.tree_dofadr[t0];
       else if (t1 == t) k = m.tree_dofnum[t0] + l - m.tree_dofadr[t1];
-      if (k >= 0) g += s.efc_J[r][k] * s.efc_force[r];
+      if (k >= 0) g += EJ(r, k) * s.efc_force[r];
     }
     s.v2[l] = s.qfrc_smooth[l] + g;
   }
@@ -1173,18 +1425,39 @@ __device__ void st_euler(const DevPhys<T>& m, Env<T>& s) {
 }
 
 // ============================================================================ forward / kernel
+// stage timer (diagnostic instantiation only: TIMED = true); cycles accumulate in prof[stage]
+#define PNP_NSTAGE 12
+struct StageClock {
+  unsigned long long* prof;
+  unsigned long long t;
+  __device__ void start() { if (prof) t = __builtin_amdgcn_s_memtime(); }
+  __device__ void lap(int k) {
+    if (!prof) return;
+    __syncthreads();
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) prof[k] += n - t;
+    t = n;
+  }
+};
+
+template <typename T>
+__device__ void forward(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
+  st_kinematics(m, s);      clk.lap(1);
+  st_compos_crb(m, s);      clk.lap(2);
+  st_factor_M(m, s);        clk.lap(3);
+  st_collision(m, s);       clk.lap(4);
+  st_constraints(m, s);     clk.lap(5);
+  st_velocity(m, s);        clk.lap(6);
+  st_actuation_smooth(m, s); clk.lap(7);
+  st_newton(m, s);          clk.lap(8);
+  st_noslip(m, s);          clk.lap(9);
+  st_finish_accel(m, s);    clk.lap(10);
+}
+
 template <typename T>
 __device__ void forward(const DevPhys<T>& m, Env<T>& s) {
-  st_kinematics(m, s);
-  st_compos_crb(m, s);
-  st_factor_M(m, s);
-  st_collision(m, s);
-  st_constraints(m, s);
-  st_velocity(m, s);
-  st_actuation_smooth(m, s);
-  st_newton(m, s);
-  st_noslip(m, s);
-  st_finish_accel(m, s);
+  StageClock clk{nullptr, 0};
+  forward(m, s, clk);
 }
 
 template <typename T>
@@ -1201,23 +1474,32 @@ __device__ void check_state(const DevPhys<T>& m, Env<T>& s) {
 }
 
 template <typename T>
-__device__ void mj_step_dev(const DevPhys<T>& m, Env<T>& s) {
+__device__ void mj_step_dev(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
+  clk.start();
   check_state(m, s);
-  forward(m, s);
+  clk.lap(0);
+  forward(m, s, clk);
   const int l = lane_id();
   const uint64_t bad = __ballot(l < m.nv && is_bad(s.qacc[l]));
   if (bad) {
     if (l == 0) s.warn |= 4u;
     wsync();
     reset_state(m, s);
-    forward(m, s);
+    forward(m, s, clk);
   }
   st_euler(m, s);
+  clk.lap(11);
 }
 
 template <typename T>
 __device__ void load_env(const DevPhys<T>& m, Env<T>& s, const pnp_state_t<T>& st, int b) {
   const int l = lane_id();
+  if (l < PH_MAXT) {
+    s.c_tree_dofadr[l] = m.tree_dofadr[l];
+    s.c_tree_dofnum[l] = m.tree_dofnum[l];
+    s.c_tree_moff[l] = m.tree_moff[l];
+  }
+  if (l < PH_MAXV) s.c_dof_tree[l] = l < m.nv ? m.dof_tree[l] : 0;
   if (l < m.nq) s.qpos[l] = st.qpos[(size_t)b * m.nq + l];
   if (l < m.nv) { s.qvel[l] = st.qvel[(size_t)b * m.nv + l]; s.qacc_ws[l] = st.qacc_warmstart[(size_t)b * m.nv + l]; }
   if (l < m.nu) s.ctrl[l] = st.ctrl[(size_t)b * m.nu + l];
@@ -1238,15 +1520,17 @@ __device__ void store_env(const DevPhys<T>& m, const Env<T>& s, const pnp_state_
   if (l == 0) { st.time[b] = s.time; st.warn[b] = s.warn; }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(NT) step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st, int B, int nsub) {
+template <typename T, bool TIMED>
+__global__ void __launch_bounds__(NT) step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st, int B, int nsub,
+                                                 unsigned long long* __restrict__ prof) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
   const DevPhys<T>& m = *mp;
   const int b = blockIdx.x;
   if (b >= B) return;
+  StageClock clk{TIMED ? prof + (size_t)b * PNP_NSTAGE : nullptr, 0};
   load_env(m, s, st, b);
-  for (int k = 0; k < nsub; k++) mj_step_dev(m, s);
+  for (int k = 0; k < nsub; k++) mj_step_dev(m, s, clk);
   store_env(m, s, st, b);
 }
 
@@ -1273,6 +1557,7 @@ __global__ void __launch_bounds__(NT) forward_debug_kernel(const DevPhys<T>* __r
     o[PNP_DBG_ACT + l] = s.qfrc_act[l];
     o[PNP_DBG_QACC_SMOOTH + l] = s.qacc_smooth[l];
     o[PNP_DBG_QACC + l] = s.qacc[l];
+    o[PNP_DBG_QACC_NEWTON + l] = s.x[l];
   }
   if (l == 0) {
     o[PNP_DBG_COUNTS + 0] = s.ncon;
@@ -1298,14 +1583,14 @@ __global__ void __launch_bounds__(NT) forward_debug_kernel(const DevPhys<T>* __r
     const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
     double* Jr = o + PNP_DBG_EFC_J + r * nv;
     for (int k = 0; k < nv; k++) Jr[k] = 0;
-    for (int k = 0; k < w; k++) Jr[slot_dof(m, t0, t1, k)] = s.efc_J[r][k];
+    for (int k = 0; k < w; k++) Jr[slot_dof(m, t0, t1, k)] = EJ(r, k);
   }
 }
 
 // ============================================================================ host launchers
 template <typename T>
 static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B, int32_t nsub, void* stream,
-                           double* dbg) {
+                           double* dbg, unsigned long long* prof = nullptr) {
   if (!model || !st || B < 0 || nsub < 0) { pnp_set_error("pnp_step: bad argument"); return PNP_ERR_ARG; }
   if (B == 0 || (nsub == 0 && !dbg)) return PNP_OK;
   if (!st->qpos || !st->qvel || !st->ctrl || !st->mocap_pos || !st->mocap_quat || !st->qacc_warmstart ||
@@ -1325,12 +1610,12 @@ static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B
     hipLaunchKernelGGL(k, dim3(B), dim3(NT), lds, (hipStream_t)stream, dm, *st, B, dbg);
     return pnp_check_launch("forward_debug_kernel");
   }
-  auto k = step_kernel<T>;
+  auto k = prof ? step_kernel<T, true> : step_kernel<T, false>;
   if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
     pnp_set_error("pnp_step: LDS %zu B not available", lds);
     return PNP_ERR_HIP;
   }
-  hipLaunchKernelGGL(k, dim3(B), dim3(NT), lds, (hipStream_t)stream, dm, *st, B, nsub);
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), lds, (hipStream_t)stream, dm, *st, B, nsub, prof);
   return pnp_check_launch("step_kernel");
 }
 
@@ -1349,6 +1634,13 @@ extern "C" int32_t pnp_forward_debug_f64(pnp_model* model, const pnp_state_f64* 
   if (!dbg) { pnp_set_error("pnp_forward_debug: null dbg"); return PNP_ERR_ARG; }
   return launch_step<double>(model, reinterpret_cast<const pnp_state_t<double>*>(st), B, 0, stream, dbg);
 }
+extern "C" int32_t pnp_step_profile(pnp_model* model, const pnp_state* st, int32_t B, int32_t nsub,
+                                    unsigned long long* stage_cycles, void* stream) {
+  if (!stage_cycles) { pnp_set_error("pnp_step_profile: null stage_cycles"); return PNP_ERR_ARG; }
+  return launch_step<float>(model, reinterpret_cast<const pnp_state_t<float>*>(st), B, nsub, stream, nullptr,
+                            stage_cycles);
+}
+
 extern "C" int32_t pnp_step_lds_bytes(int32_t fp64) {
   return fp64 ? (int32_t)sizeof(Env<double>) : (int32_t)sizeof(Env<float>);
 }

@@ -16,7 +16,7 @@ EXPORTS = [
     "pnp_abi_version", "pnp_model_desc_size", "pnp_last_error", "pnp_model_create",
     "pnp_model_destroy", "pnp_site_kinematics", "pnp_site_kinematics_f64", "pnp_jac_site",
     "pnp_jac_site_f64", "pnp_ik_dls", "pnp_ik_dls_f64", "pnp_step", "pnp_step_f64",
-    "pnp_forward_debug", "pnp_forward_debug_f64", "pnp_step_lds_bytes",
+    "pnp_forward_debug", "pnp_forward_debug_f64", "pnp_step_lds_bytes", "pnp_step_profile",
 ]
 
 STATE_FIELDS = ("qpos", "qvel", "ctrl", "mocap_pos", "mocap_quat", "qacc_warmstart", "time", "warn")
@@ -28,7 +28,8 @@ class PnpState(C.Structure):
 
 # debug record layout (include/pnp.h PNP_DBG_*)
 DBG = dict(QM=0, BIAS=1296, ACT=1332, QACC_SMOOTH=1368, QACC=1404, COUNTS=1440, CON=1444, CON_STRIDE=16,
-           EFC_FORCE=1892, EFC_POS=2020, EFC_D=2148, EFC_AREF=2276, EFC_TYPE=2404, EFC_J=2532, SIZE=7168)
+           EFC_FORCE=1892, EFC_POS=2020, EFC_D=2148, EFC_AREF=2276, EFC_TYPE=2404, EFC_J=2532,
+           QACC_NEWTON=7140, SIZE=7184)
 
 _lib = None
 
@@ -74,6 +75,8 @@ def load():
         f = getattr(L, name)
         f.argtypes = [P, C.POINTER(PnpState), I32, P, P]
         f.restype = I32
+    L.pnp_step_profile.argtypes = [P, C.POINTER(PnpState), I32, I32, P, P]
+    L.pnp_step_profile.restype = I32
     L.pnp_step_lds_bytes.argtypes = [I32]
     L.pnp_step_lds_bytes.restype = I32
     if L.pnp_abi_version() != ABI_VERSION:

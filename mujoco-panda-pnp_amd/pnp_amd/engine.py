@@ -119,6 +119,19 @@ class Engine:
         _lib.check(fn(self._h, C.byref(S), B, int(nsub), _stream()), "pnp_step")
         return st
 
+    STAGES = ("check", "kinematics", "compos_crb", "factor_M", "collision", "constraints", "velocity_rne",
+              "actuation_smooth", "newton", "noslip", "finish_accel", "euler")
+
+    def step_profile(self, st, nsub=1):
+        """Diagnostic timed instantiation of pnp_step: per-stage shader cycles [B, 12] (uint64)."""
+        S, B, dt = self._state_struct(st)
+        if dt != torch.float32:
+            raise TypeError("step_profile times the fp32 product kernel")
+        prof = torch.zeros(B, len(self.STAGES), dtype=torch.int64, device=self.device)
+        _lib.check(self.lib.pnp_step_profile(self._h, C.byref(S), B, int(nsub), _ptr(prof), _stream()),
+                   "pnp_step_profile")
+        return prof
+
     def forward_debug(self, st):
         """One mj_forward per env; returns the PNP_DBG_* record [B, PNP_DBG_SIZE] (float64)."""
         S, B, dt = self._state_struct(st)

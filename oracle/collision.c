@@ -328,6 +328,9 @@ int orc_collide_pair(Mdl* m, const orc_data* d, int g1, int g2, orc_contact* out
   if (n > cap) n = cap;
   for (int k = 0; k < n; k++) {
     out[k] = tmp[k];
+    /* colliders set the normal only; complete the tangent frame (mju_makeFrame, as
+       mj_collideGeoms does before the contact enters the constraint Jacobian) */
+    sp_makeframe(out[k].frame);
     contact_params(m, out + k, g1, g2);
   }
   return n;

@@ -272,7 +272,10 @@ static double impedance(const double* si, double x) {
   x = fabs(x);
   if (width <= ORC_MINVAL || x >= width) return dmax;
   double y = x / width;
-  if (power != 1) {
+  if (power == 2) {
+    if (y <= mid) y = y * y / mid;
+    else y = 1 - (1 - y) * (1 - y) / (1 - mid);
+  } else if (power != 1) {
     if (y <= mid) y = pow(y, power) / pow(mid, power - 1);
     else y = 1 - pow(1 - y, power) / pow(1 - mid, power - 1);
   }
@@ -681,6 +684,7 @@ void orc_forward(Mdl* m, orc_data* d) {
     return;
   }
   solve_newton(m, d);
+  memcpy(d->qacc_newton, d->qacc, nv * sizeof(double));
   solve_noslip(m, d, m->noslip_iterations);
   for (int i = 0; i < nv; i++) {
     double s = 0;
@@ -830,7 +834,7 @@ int orc_field(Mdl* m, const orc_data* d, const char* name, double* out, int cap)
   double tmp[ORC_MAXEFC * 4];
 #define F(nm, ptr, cnt) else if (!strcmp(name, nm)) { src = (ptr); n = (cnt); }
   if (0) {}
-  F("qpos", d->qpos, m->nq) F("qvel", d->qvel, nv) F("qacc", d->qacc, nv)
+  F("qpos", d->qpos, m->nq) F("qvel", d->qvel, nv) F("qacc", d->qacc, nv) F("qacc_newton", d->qacc_newton, nv)
   F("qacc_smooth", d->qacc_smooth, nv) F("qacc_warmstart", d->qacc_warmstart, nv)
   F("xpos", d->xpos, 3 * m->nbody) F("xquat", d->xquat, 4 * m->nbody) F("xmat", d->xmat, 9 * m->nbody)
   F("xipos", d->xipos, 3 * m->nbody) F("ximat", d->ximat, 9 * m->nbody)

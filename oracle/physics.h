@@ -70,7 +70,7 @@ typedef struct {
   double actuator_force[ORC_MAXU], qfrc_actuator[ORC_MAXV];
   double qfrc_smooth[ORC_MAXV], qacc_smooth[ORC_MAXV];
   double efc_force[ORC_MAXEFC], efc_b[ORC_MAXEFC];
-  double qfrc_constraint[ORC_MAXV], qacc[ORC_MAXV];
+  double qfrc_constraint[ORC_MAXV], qacc[ORC_MAXV], qacc_newton[ORC_MAXV];
   int solver_iter;
   double solver_improvement, solver_gradient;
 } orc_data;

@@ -63,6 +63,18 @@ def main():
             errs["qacc"] = max(errs["qacc"], rel(g[D["QACC"]:D["QACC"] + nv], f["qacc"]))
             errs["efc_force"] = max(errs["efc_force"], rel(g[D["EFC_FORCE"]:D["EFC_FORCE"] + nefc], f["efc_force"]))
             errs["efc_pos"] = max(errs["efc_pos"], rel(g[D["EFC_POS"]:D["EFC_POS"] + nefc], f["efc_pos"]))
+        if dt == torch.float32:
+            for b in range(min(B, 4)):
+                f = oracle_forward(st, b, ["qacc", "qacc_smooth", "qacc_newton"])
+                gn = dbg[b][D["QACC_NEWTON"]:D["QACC_NEWTON"] + nv]
+                en = np.abs(gn - f["qacc_newton"])
+                print(f"  env {b}: newton x err arm {en[:9].max():.2e} cubes {en[9:27].max():.2e} dummy {en[27:33].max():.2e}")
+                g = dbg[b][D["QACC"]:D["QACC"] + nv]
+                e = np.abs(g - f["qacc"])
+                k = int(e.argmax())
+                print(f"  env {b}: worst dof {k} ({m.names_jnt[m.dof_jntid[k]]}) gpu {g[k]:.6g} ref {f['qacc'][k]:.6g}; "
+                      f"per-tree max err: arm {e[:9].max():.2e} c1 {e[9:15].max():.2e} c2 {e[15:21].max():.2e} "
+                      f"c3 {e[21:27].max():.2e} dummy {e[27:33].max():.2e}")
         print(dt, "count mismatches", cnt_mis, {k: f"{v:.2e}" for k, v in errs.items()},
               "gpu iters", dbg[:, D["COUNTS"] + 2].mean(), flush=True)
     # one and ten steps
@@ -89,5 +101,22 @@ def main():
         print(f"B={B2} nsub={nsub}: {t * 1e3:.1f} ms -> {B2 * nsub / t / 1e6:.3f} M env-steps/s", flush=True)
 
 
+
+
+def profile_stages(B=4096, nsub=10):
+    eng = get_engine()
+    st = PS.settled_states(64, seed=0, nsettle=50)
+    PS.random_ctrl(st)
+    big = {k: torch.cat([v] * (B // 64)) for k, v in to_dev(st, torch.float32).items()}
+    prof = eng.step_profile(big, nsub).cpu().numpy().astype(np.float64)
+    tot = prof.sum(1).mean()
+    print(f"per env per sub-step: {tot / nsub:.0f} cycles")
+    for k, name in enumerate(eng.STAGES):
+        print(f"  {name:18s} {prof[:, k].mean() / nsub:10.0f} cycles  {100 * prof[:, k].mean() / tot:5.1f}%")
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 2 and sys.argv[2] == "prof":
+        profile_stages()
+    else:
+        main()
