@@ -1,20 +1,27 @@
 #!/usr/bin/env python3
-"""Benchmark of the batched DLS-IK hot path (BASELINE.json configs[1], "C2": 4096 Panda
-instances, IK-only, free space, one MI355X per rank).
+"""Benchmark of the batched env-step hot path (BASELINE.json metric "env-steps/sec @4096
+envs/GPU, 1/2/4/8 MI355X; DLS-IK solves/sec").
 
-A "step" = one batched JacobianIKController.solve over the rank's 4096 envs (one launch of
-pnp_ik_dls: every solve runs to convergence or max_iters inside the kernel).  Inputs are
-synthetic (Philox, seed 20250808, counter = global env index, so rank r owns envs
-[r*B, (r+1)*B) and inputs are identical at any GPU count), resident in HBM before timing.
+Default workload (--workload step) = BASELINE configs[2] "C3" at N=1 and configs[3] "C4" at N>1:
+4096 shelf_pnp envs per GPU, full mj_step (kinematics, CRBA, collision, constraints, RNE,
+Newton + noslip, Euler), random ctrl.  A "step" = one launch of pnp_step over the rank's envs
+with nsub = 25 fused sub-steps (the reference's mj_step(nstep=n_substeps=25),
+envs/panda_env.py:355-358) and a fresh ctrl ~ U(actuator_ctrlrange) per step (a table of 64
+Philox draws, cycled, resident in HBM).  value = env-steps (= mj_step's) per second, all ranks.
+Inputs: the reference's reset distribution (Philox, seed 20250808, counter = global env index;
+rank r owns envs [r*B, (r+1)*B)), settled by 250 untimed sub-steps like _env_setup.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--regime waypoint|ik_test]
+--workload ik = configs[1] "C2": one batched JacobianIKController.solve over 4096 envs per step.
+The step workload also times C2 briefly and reports it under "ik".
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload step|ik]
     torchrun --nproc-per-node N bench.py --gpus N ...    (one process per GPU)
 
-Rank 0 prints ONE JSON line.  `value` = all ranks' solves / max-over-ranks wall time.
-`roofline` prices the ik_dls kernel at its algorithmic 89 B/solve against HBM peak, with the
-kernel's average duration from HIP events on the launch stream.  `cpu_baseline` (rank 0, N=1)
-times the CPU oracle (fp64 C restatement of the same solve, all allowed host threads) on a
-bounded sample of the same inputs.
+Rank 0 prints ONE JSON line.  `roofline` prices the dominant kernel at its algorithmic bytes
+(state read + written once per launch) against HBM peak, with its average duration from HIP
+events on the launch stream.  `cpu_baseline` (rank 0, N=1) times the fp64 CPU oracle (C
+restatement of the same algorithms, all allowed host threads) on a bounded sample of the same
+inputs.
 """
 from __future__ import annotations
 
@@ -36,6 +43,12 @@ from pnp_amd.engine import get_engine  # noqa: E402
 BASELINE_METRIC = "env-steps/sec @4096 envs/GPU, 1/2/4/8 MI355X; DLS-IK solves/sec"
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 IK_BYTES_PER_SOLVE = 89         # q_init 28 + target 12 in; q 28 + final_pos 12 + err 4 + iters 4 + flags 1 out
+# env-step launch: read qpos 37 + qvel 33 + ctrl 9 + mocap 7 + qacc_warmstart 33 + time 1 + warn 1
+# words, write qpos 37 + qvel 33 + qacc_warmstart 33 + time 1 + warn 1 words (fp32 / u32)
+STEP_BYTES_PER_ENV = 4 * (37 + 33 + 9 + 3 + 4 + 33 + 1 + 1) + 4 * (37 + 33 + 33 + 1 + 1)
+NSUB = 25                       # panda_env.py n_substeps
+NSETTLE = 250                   # _env_setup settle sub-steps (panda_env.py:124-141)
+NCTRL = 64                      # distinct per-step ctrl draws, cycled
 
 
 def host_threads():
@@ -44,7 +57,135 @@ def host_threads():
     return max(1, min(n, cap, 16))
 
 
-def make_inputs(engine, model, rank, B, regime):
+def _oracle():
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    return O
+
+
+def _timed(fn, steps, warmup, dist):
+    """W untimed + K timed calls bracketed by barrier + synchronize; returns (wall s, avg event ms)."""
+    for i in range(warmup):
+        fn(i)
+    torch.cuda.synchronize()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        starts[i].record()
+        fn(warmup + i)
+        ends[i].record()
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    if dist:
+        t = torch.tensor([elapsed, kern_ms], device="cuda", dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    return elapsed, kern_ms
+
+
+def _traffic(name, B):
+    f = os.path.join(ROOT, "profiles", name)
+    if os.path.exists(f):
+        with open(f) as fh:
+            tr = json.load(fh)
+        if tr.get("batch") == B:
+            return tr.get("hbm_bytes_per_launch"), tr.get("source")
+    return None, None
+
+
+# ----------------------------------------------------------------------------- C3 / C4 env-step
+def step_inputs(engine, model, rank, B):
+    idx = np.arange(rank * B, (rank + 1) * B)
+    q = torch.as_tensor(np.tile(model.qpos0, (1, 1)), dtype=torch.float64, device=engine.device)
+    q[:, :9] = torch.as_tensor(workloads.NEUTRAL, dtype=torch.float64)
+    sx, sm = engine.site_kinematics(q.contiguous())
+    host = workloads.c3_reset(model, idx, sx[0].cpu().numpy(), sm[0].cpu().numpy())
+    st = {}
+    for k, v in host.items():
+        dt = torch.int32 if k == "warn" else torch.float32
+        st[k] = torch.as_tensor(v.astype(np.int32) if k == "warn" else v, dtype=dt, device=engine.device).contiguous()
+    for _ in range(NSETTLE // NSUB):    # same launch shape as the timed steps (profiles agree)
+        engine.step(st, NSUB)
+    ctrl = torch.as_tensor(np.stack([workloads.c3_ctrl(model, idx, s) for s in range(NCTRL)]),
+                           dtype=torch.float32, device=engine.device).contiguous()
+    return st, ctrl
+
+
+def step_cpu_baseline(st, ctrl, budget_s):
+    """fp64 oracle mj_step x NSUB on host threads, over a bounded sample of the same settled envs."""
+    O = _oracle()
+    nth = host_threads()
+    n = min(st["qpos"].shape[0], 256)
+    sample = {k: (v[:n].cpu().numpy().astype(np.uint32) if k == "warn" else v[:n].double().cpu().numpy())
+              for k, v in st.items()}
+    ctab = ctrl[:, :n].double().cpu().numpy()
+    O.step({k: v[:8].copy() for k, v in sample.items()}, nsub=1, nthreads=1)   # load / warm
+    done, reps, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        sample["ctrl"] = np.ascontiguousarray(ctab[reps % NCTRL])
+        O.step(sample, nsub=NSUB, nthreads=nth)
+        done += n * NSUB
+        reps += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "env-steps/s", "cores": nth, "kind": "port",
+            "sample": f"{reps} steps x {n} envs x {NSUB} sub-steps of the same settled C3 envs "
+                      f"(envs 0..{n - 1}), fp64 oracle oracle/physics.c, {nth} pthreads, {dt:.1f} s"}
+
+
+def run_step(args, engine, model, rank, world, dist):
+    B = args.batch
+    st, ctrl = step_inputs(engine, model, rank, B)
+    torch.cuda.synchronize()
+
+    def fn(i):
+        st["ctrl"] = ctrl[i % NCTRL]
+        engine.step(st, NSUB)
+
+    elapsed, kern_ms = _timed(fn, args.steps, args.warmup, dist)
+    warn = int(st["warn"].max())
+    finite = bool(torch.isfinite(st["qpos"]).all())
+    total = B * world * args.steps * NSUB
+    achieved = STEP_BYTES_PER_ENV * B / (kern_ms * 1e-3) / 1e9
+    traffic, src = _traffic("pmc_traffic_step.json", B)
+    rec = {
+        "metric": BASELINE_METRIC,
+        "value": total / elapsed,
+        "unit": "env-steps/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (reset distribution + random ctrl; Philox seed 20250808, counter = global env index)",
+        "config": {
+            "workload": ("C3: 4096 shelf_pnp envs full mj_step per MI355X, random ctrl" if world == 1 else
+                         f"C4: {B * world} shelf_pnp envs sharded over {world} MI355X, random ctrl"),
+            "envs_per_gpu": B, "global_envs": B * world, "sub_steps_per_step": NSUB,
+            "parallelism": f"env-shard x{world} (no collective on the data path)",
+        },
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": src,
+                     "kernel": "step_kernel<float, false>", "kernel_avg_ms": kern_ms,
+                     "algorithmic_bytes_per_launch": STEP_BYTES_PER_ENV * B},
+        "state_ok": {"max_warn": warn, "finite": finite},
+        "host_cores": len(os.sched_getaffinity(0)),
+    }
+    if not args.no_ik:
+        ik = run_ik(args, engine, model, rank, world, dist, steps=50, warmup=5, baseline=False)
+        rec["ik"] = {k: ik[k] for k in ("value", "unit", "ms_per_step")}
+        rec["ik"].update(roofline_frac=ik["roofline"]["frac"], workload=ik["config"]["workload"])
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rec["cpu_baseline"] = step_cpu_baseline(st, ctrl, args.cpu_budget)
+    return rec
+
+
+# ----------------------------------------------------------------------------- C2 IK
+def ik_inputs(engine, model, rank, B, regime):
     idx = np.arange(rank * B, (rank + 1) * B)
     q, delta = workloads.ik_inputs(model, idx, regime=regime)
     dev = engine.device
@@ -56,15 +197,12 @@ def make_inputs(engine, model, rank, B, regime):
     return qf[:, :7].contiguous(), target, q, (sx[:, s].double().cpu().numpy() + delta)
 
 
-def cpu_baseline(q_host, tgt_host, prm, budget_s=12.0):
-    """Oracle (fp64 C restatement) on host threads over a bounded sample of the same inputs."""
-    sys.path.insert(0, ROOT)
-    from oracle import oracle as O
+def ik_cpu_baseline(q_host, tgt_host, prm, budget_s):
+    O = _oracle()
     nth = host_threads()
     n = min(len(q_host), 4096)
     O.ik_dls(q_host[:64], tgt_host[:64], nthreads=1, **prm)  # load / warm
-    done, t0 = 0, time.perf_counter()
-    reps = 0
+    done, reps, t0 = 0, 0, time.perf_counter()
     while True:
         O.ik_dls(q_host[:n], tgt_host[:n], nthreads=nth, **prm)
         done += n
@@ -77,14 +215,58 @@ def cpu_baseline(q_host, tgt_host, prm, budget_s=12.0):
                       f"oracle/oracle.c, {nth} pthreads, {dt:.1f} s"}
 
 
+def run_ik(args, engine, model, rank, world, dist, steps=None, warmup=None, baseline=True):
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
+    B = args.batch
+    prm = workloads.IK_PARAMS[args.params]
+    q0, tgt, q_host, tgt_host = ik_inputs(engine, model, rank, B, args.regime)
+    dev = engine.device
+    out = dict(q=torch.empty(B, 7, device=dev), final_pos=torch.empty(B, 3, device=dev),
+               pos_error=torch.empty(B, device=dev), iterations=torch.empty(B, dtype=torch.int32, device=dev),
+               flags=torch.empty(B, dtype=torch.uint8, device=dev))
+    elapsed, kern_ms = _timed(lambda i: engine.ik_dls_into(q0, tgt, out, **prm), steps, warmup, dist)
+    iters = out["iterations"].cpu().numpy()
+    fl = out["flags"].cpu().numpy()
+    achieved = IK_BYTES_PER_SOLVE * B / (kern_ms * 1e-3) / 1e9
+    traffic, src = _traffic("pmc_traffic_ik.json", B)
+    rec = {
+        "metric": BASELINE_METRIC,
+        "value": B * world * steps / elapsed,
+        "unit": "solves/s",
+        "n_gpus": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": elapsed / steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (Philox seed 20250808, counter = global env index)",
+        "config": {
+            "workload": "C2: 4096 Panda instances, IK-only DLS (skills/ik_solver.py) batched per MI355X, free space",
+            "envs_per_gpu": B, "global_envs": B * world, "regime": args.regime,
+            "ik_params": prm, "parallelism": f"env-shard x{world} (no collective on the data path)",
+        },
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": src,
+                     "kernel": "ik_dls_kernel<float, true>", "kernel_avg_ms": kern_ms,
+                     "algorithmic_bytes_per_launch": IK_BYTES_PER_SOLVE * B},
+        "ik_stats": {"mean_iterations": float(iters.mean()), "max_iterations": int(iters.max()),
+                     "converged_frac": float((fl & 1).astype(bool).mean()),
+                     "dls_iterations_per_s": float(iters.sum()) * world * steps / elapsed},
+        "host_cores": len(os.sched_getaffinity(0)),
+    }
+    if baseline and rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rec["cpu_baseline"] = ik_cpu_baseline(q_host, tgt_host, prm, args.cpu_budget)
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=4096, help="envs (IK solves) per GPU")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--workload", default="step", choices=("step", "ik"))
     ap.add_argument("--regime", default="waypoint", choices=sorted(workloads.IK_REGIMES))
     ap.add_argument("--params", default="default", choices=sorted(workloads.IK_PARAMS))
+    ap.add_argument("--no-ik", action="store_true", help="step workload: skip the secondary C2 timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -100,83 +282,12 @@ def main():
         torch.cuda.set_device(0)
     engine = get_engine()
     model = engine.model
-    B = args.batch
-    prm = workloads.IK_PARAMS[args.params]
-    q0, tgt, q_host, tgt_host = make_inputs(engine, model, rank, B, args.regime)
-    dev = engine.device
-    out = dict(q=torch.empty(B, 7, device=dev), final_pos=torch.empty(B, 3, device=dev),
-               pos_error=torch.empty(B, device=dev), iterations=torch.empty(B, dtype=torch.int32, device=dev),
-               flags=torch.empty(B, dtype=torch.uint8, device=dev))
-
-    def step():
-        engine.ik_dls_into(q0, tgt, out, **prm)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    if dist:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        starts[i].record()
-        step()
-        ends[i].record()
-    torch.cuda.synchronize()
-    if dist:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
-    if dist:
-        t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-
-    iters = out["iterations"].cpu().numpy()
-    fl = out["flags"].cpu().numpy()
-    total_solves = B * world * args.steps
-    value = total_solves / elapsed
-    achieved = IK_BYTES_PER_SOLVE * B / (kern_ms * 1e-3) / 1e9
-    record = {
-        "metric": BASELINE_METRIC,
-        "value": value,
-        "unit": "solves/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (Philox seed 20250808, counter = global env index)",
-        "config": {
-            "workload": "C2: 4096 Panda instances, IK-only DLS (skills/ik_solver.py) batched per MI355X, free space",
-            "envs_per_gpu": B, "global_envs": B * world, "regime": args.regime,
-            "ik_params": prm, "parallelism": f"env-shard x{world} (no collective on the data path)",
-        },
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                     "kernel": "ik_dls_kernel<float, true>", "kernel_avg_ms": kern_ms,
-                     "algorithmic_bytes_per_launch": IK_BYTES_PER_SOLVE * B},
-        "ik_stats": {"mean_iterations": float(iters.mean()), "max_iterations": int(iters.max()),
-                     "converged_frac": float((fl & 1).astype(bool).mean()),
-                     "dls_iterations_per_s": float(iters.sum()) * world * args.steps / elapsed},
-        "host_cores": len(os.sched_getaffinity(0)),
-    }
-    traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic_ik.json")
-    if os.path.exists(traffic_file):
-        with open(traffic_file) as f:
-            tr = json.load(f)
-        if tr.get("batch") == B:
-            record["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
-            record["roofline"]["traffic_source"] = tr.get("source")
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        record["cpu_baseline"] = cpu_baseline(q_host, tgt_host, prm, args.cpu_budget)
+    if args.workload == "step":
+        rec = run_step(args, engine, model, rank, world, dist)
+    else:
+        rec = run_ik(args, engine, model, rank, world, dist)
     if rank == 0:
-        print(json.dumps(record), flush=True)
+        print(json.dumps(rec), flush=True)
     if dist:
         torch.distributed.destroy_process_group()
 

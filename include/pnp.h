@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 2
+#define PNP_ABI_VERSION 3
 
 #define PNP_OK 0
 #define PNP_ERR_ARG -1
@@ -223,16 +223,16 @@ int32_t pnp_step_f64(pnp_model* model, const pnp_state_f64* state, int32_t B, in
 #define PNP_DBG_QACC_SMOOTH 1368
 #define PNP_DBG_QACC 1404
 #define PNP_DBG_COUNTS 1440     /* ncon, nefc, solver iterations, warn */
-#define PNP_DBG_CON 1444        /* ncon x 16: pos3 frame9 dist geom1 geom2 dim */
+#define PNP_DBG_CON 1444        /* ncon (<= 48) x 16: pos3 frame9 dist geom1 geom2 dim */
 #define PNP_DBG_CON_STRIDE 16
-#define PNP_DBG_EFC_FORCE 1892  /* nefc (<= 128) */
-#define PNP_DBG_EFC_POS 2020
-#define PNP_DBG_EFC_D 2148
-#define PNP_DBG_EFC_AREF 2276
-#define PNP_DBG_EFC_TYPE 2404
-#define PNP_DBG_EFC_J 2532      /* nefc x nv dense */
-#define PNP_DBG_QACC_NEWTON 7140 /* Newton result before no-slip */
-#define PNP_DBG_SIZE 7184
+#define PNP_DBG_EFC_FORCE 2212  /* nefc (<= 208) */
+#define PNP_DBG_EFC_POS 2420
+#define PNP_DBG_EFC_D 2628
+#define PNP_DBG_EFC_AREF 2836
+#define PNP_DBG_EFC_TYPE 3044
+#define PNP_DBG_EFC_J 3252      /* nefc x nv dense */
+#define PNP_DBG_QACC_NEWTON 10740 /* Newton result before no-slip */
+#define PNP_DBG_SIZE 10776
 int32_t pnp_forward_debug(pnp_model* model, const pnp_state* state, int32_t B, double* dbg, void* stream);
 int32_t pnp_forward_debug_f64(pnp_model* model, const pnp_state_f64* state, int32_t B, double* dbg,
                               void* stream);

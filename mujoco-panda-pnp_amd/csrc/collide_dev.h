@@ -134,23 +134,32 @@ __device__ void c_sphere_box(const T* p1, T r, const T* p2, const T* R2, const T
   out.emit(dist, pos, n);
 }
 
+// Liang-Barsky clip of the 2D segment p0 -> p1 to |x| <= A, |y| <= B (closed); false if empty
 template <typename T>
-__device__ int c_clip(T (*poly)[3], int np, int axis, T sgn, T lim, T (*out)[3]) {
-  int no = 0;
-  for (int i = 0; i < np; i++) {
-    const T* a = poly[i];
-    const T* b = poly[(i + 1) % np];
-    const T da = sgn * a[axis] - lim, db = sgn * b[axis] - lim;
-    if (da <= 0) { out[no][0] = a[0]; out[no][1] = a[1]; out[no][2] = a[2]; no++; }
-    if ((da < 0 && db > 0) || (da > 0 && db < 0)) {
-      const T t = da / (da - db);
-      for (int k = 0; k < 3; k++) out[no][k] = a[k] + t * (b[k] - a[k]);
-      no++;
+__device__ __forceinline__ bool c_clip_seg(const T* p0, const T* p1, T A, T B, T& t0, T& t1) {
+  const T dx = p1[0] - p0[0], dy = p1[1] - p0[1];
+  const T pp[4] = {-dx, dx, -dy, dy}, qq[4] = {p0[0] + A, A - p0[0], p0[1] + B, B - p0[1]};
+  T a = 0, b = 1;
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (pp[k] == T(0)) {
+      ok &= !(qq[k] < T(0));
+    } else {
+      const T r = qq[k] / pp[k];
+      if (pp[k] < T(0)) a = r > a ? r : a;
+      else b = r < b ? r : b;
     }
   }
-  return no;
+  t0 = a;
+  t1 = b;
+  return ok && !(a > b);
 }
 
+// Reference face on box r (axis ia, outward normal nr), incident box i (oracle/collision.c
+// box_face_contacts, same vertex order): clipped incident-edge points, then reference corners
+// strictly inside the incident face.  Fully unrolled: every array index is a compile-time
+// constant, so the polygon lives in VGPRs (no private-memory scratch).
 template <typename T, class S>
 __device__ void c_box_face(const T* pr, const T* Rr, const T* sr, int ia, const T* nr, const T* pi, const T* Ri,
                            const T* si, const T* nframe, T margin, S& out) {
@@ -164,30 +173,49 @@ __device__ void c_box_face(const T* pr, const T* Rr, const T* sr, int ia, const 
     const T a = fabs(Ri[j] * nr[0] + Ri[3 + j] * nr[1] + Ri[6 + j] * nr[2]);
     if (a > best) { best = a; ja = j; }
   }
+  const int ju = ja == 0 ? 1 : ja == 1 ? 2 : 0, jv = ja == 0 ? 2 : ja == 1 ? 0 : 1;
   const T bj[3] = {Ri[ja], Ri[3 + ja], Ri[6 + ja]};
   const T sg = t_dot3(bj, nr) > 0 ? T(-1) : T(1);
-  const int ju = (ja + 1) % 3, jv = (ja + 2) % 3;
   const T bu[3] = {Ri[ju], Ri[3 + ju], Ri[6 + ju]}, bv[3] = {Ri[jv], Ri[3 + jv], Ri[6 + jv]};
-  T poly[8][3], tmp[8][3];
+  const T hj = si[ja], hu = si[ju], hv = si[jv];
   const T su[4] = {1, -1, -1, 1}, sv[4] = {1, 1, -1, -1};
+  T P[4][3];
+#pragma unroll
   for (int q = 0; q < 4; q++) {
     T w[3];
-    for (int k = 0; k < 3; k++) w[k] = pi[k] + sg * bj[k] * si[ja] + su[q] * bu[k] * si[ju] + sv[q] * bv[k] * si[jv] - cref[k];
-    poly[q][0] = t_dot3(w, u); poly[q][1] = t_dot3(w, v); poly[q][2] = t_dot3(w, nr);
+#pragma unroll
+    for (int k = 0; k < 3; k++) w[k] = pi[k] + sg * bj[k] * hj + su[q] * bu[k] * hu + sv[q] * bv[k] * hv - cref[k];
+    P[q][0] = t_dot3(w, u); P[q][1] = t_dot3(w, v); P[q][2] = t_dot3(w, nr);
   }
-  int np = 4;
-  np = c_clip(poly, np, 0, T(1), sr[iu], tmp);
-  np = c_clip(tmp, np, 0, T(-1), sr[iu], poly);
-  np = c_clip(poly, np, 1, T(1), sr[iv], tmp);
-  np = c_clip(tmp, np, 1, T(-1), sr[iv], poly);
+  const T A = sr[iu], B = sr[iv];
   int cnt = 0;
-  for (int q = 0; q < np && cnt < 8; q++) {
-    const T dist = poly[q][2];
-    if (dist > margin) continue;
+  auto emit = [&](T x, T y, T z) {
+    if (cnt >= 8 || z > margin) return;
     T pos[3];
-    for (int k = 0; k < 3; k++) pos[k] = cref[k] + u[k] * poly[q][0] + v[k] * poly[q][1] + nr[k] * poly[q][2] * T(0.5);
-    out.emit(dist, pos, nframe);
+#pragma unroll
+    for (int k = 0; k < 3; k++) pos[k] = cref[k] + u[k] * x + v[k] * y + nr[k] * z * T(0.5);
+    out.emit(z, pos, nframe);
     cnt++;
+  };
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const T* p0 = P[e];
+    const T* p1 = P[(e + 1) & 3];
+    T t0, t1;
+    if (!c_clip_seg(p0, p1, A, B, t0, t1)) continue;
+    emit(p0[0] + t0 * (p1[0] - p0[0]), p0[1] + t0 * (p1[1] - p0[1]), p0[2] + t0 * (p1[2] - p0[2]));
+    if (t1 < T(1)) emit(p0[0] + t1 * (p1[0] - p0[0]), p0[1] + t1 * (p1[1] - p0[1]), p0[2] + t1 * (p1[2] - p0[2]));
+  }
+  const T e1[3] = {P[1][0] - P[0][0], P[1][1] - P[0][1], P[1][2] - P[0][2]};
+  const T e3[3] = {P[3][0] - P[0][0], P[3][1] - P[0][1], P[3][2] - P[0][2]};
+  const T det = e1[0] * e3[1] - e1[1] * e3[0];
+  if (fabs(det) > T(1e-12) * (fabs(e1[0]) + fabs(e1[1])) * (fabs(e3[0]) + fabs(e3[1]))) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const T cx = su[q] * A - P[0][0], cy = sv[q] * B - P[0][1];
+      const T al = (cx * e3[1] - cy * e3[0]) / det, be = (e1[0] * cy - e1[1] * cx) / det;
+      if (al > 0 && al < 1 && be > 0 && be < 1) emit(su[q] * A, sv[q] * B, P[0][2] + al * e1[2] + be * e3[2]);
+    }
   }
 }
 

@@ -50,39 +50,42 @@ struct Env {
   T qpos[PH_MAXQ], qvel[PH_MAXV], ctrl[PH_MAXU], mocap_pos[6], mocap_quat[8], qacc_ws[PH_MAXV];
   T time;
   uint32_t warn;
-  int ncon, nefc, ne, nlive, nisland, solver_iter;
-  // ---- position stage
-  T xpos[PH_MAXB][3], xquat[PH_MAXB][4], xmat[PH_MAXB][9], xipos[PH_MAXB][3];
-  T xanchor[PH_MAXJ][3], xaxis[PH_MAXJ][3];
-  T gpos[PH_MAXG][3], gmat[PH_MAXG][9];
-  T subcom[PH_MAXB][3];
-  T cinert[PH_MAXB][10], crb[PH_MAXB][10], cdof[PH_MAXV][6], cvel[PH_MAXB][6], cdofdot[PH_MAXV][6];
-  T scr6[PH_MAXB > PH_MAXV ? PH_MAXB : PH_MAXV][6];   // per-body / per-dof 6-vector scratch
-  T scr6b[PH_MAXB][6];
+  int ncon, nefc, ne, nisland, solver_iter;
+  // ---- position / velocity-stage working set (kinematics -> collision -> constraints -> RNE).
+  // Dead once the solver starts, so it shares storage with the Newton Hessian H and the no-slip
+  // W = M^-1 J^T (those two lifetimes do not overlap either).
+  union {
+    struct {
+      T xpos[PH_MAXB][3], xquat[PH_MAXB][4], xmat[PH_MAXB][9], xipos[PH_MAXB][3];
+      T xanchor[PH_MAXJ][3], xaxis[PH_MAXJ][3];
+      T gpos[PH_MAXG][3], gmat[PH_MAXG][9];
+      T subcom[PH_MAXB][3];
+      T cinert[PH_MAXB][10], crb[PH_MAXB][10], cdof[PH_MAXV][6], cvel[PH_MAXB][6], cdofdot[PH_MAXV][6];
+      T scr6[PH_MAXB > PH_MAXV ? PH_MAXB : PH_MAXV][6];   // per-body / per-dof 6-vector scratch
+      T scr6b[PH_MAXB][6];
+      short live[PH_MAXPAIR];   // broadphase survivors: every candidate pair fits
+      Con<T> con[PH_MAXCON];
+    };
+    T H[PH_MAXV][PH_MAXV];
+    T efc_Wv[PH_MAXJSLOT];
+  };
   T M[PH_MAXMBLK];    // per-tree dense blocks
   T L[PH_MAXMBLK];    // Cholesky factors of the blocks
   // ---- vectors
   T qfrc_bias[PH_MAXV], qfrc_passive[PH_MAXV], qfrc_act[PH_MAXV], qfrc_smooth[PH_MAXV];
   T qacc_smooth[PH_MAXV], qacc[PH_MAXV], x[PH_MAXV], grad[PH_MAXV], p[PH_MAXV], v1[PH_MAXV], v2[PH_MAXV];
-  // ---- collision
-  Con<T> con[PH_MAXCON];
-  // ---- constraints (sparse rows)
-  int efc_t0[PH_MAXEFC], efc_t1[PH_MAXEFC], efc_type[PH_MAXEFC], efc_id[PH_MAXEFC];
+  // ---- constraints (sparse rows over <= 2 trees; t1 = -1 for single-tree rows)
+  signed char efc_t0[PH_MAXEFC], efc_t1[PH_MAXEFC], efc_type[PH_MAXEFC];
+  unsigned char efc_id[PH_MAXEFC], efc_act[PH_MAXEFC];
   int efc_off[PH_MAXEFC + 1];   // packed rows: slots [efc_off[r], efc_off[r+1])
   T efc_Jv[PH_MAXJSLOT];
   T efc_pos[PH_MAXEFC], efc_D[PH_MAXEFC], efc_aref[PH_MAXEFC], efc_bb[PH_MAXEFC];
   T efc_force[PH_MAXEFC], efc_jar[PH_MAXEFC], efc_Jp[PH_MAXEFC];
-  int efc_act[PH_MAXEFC];
   int lim_count[PH_MAXJ];
   int con_rbase[PH_MAXCON], con_sbase[PH_MAXCON], con_t[PH_MAXCON][2];
-  // ---- Newton Hessian; its storage is reused by the broadphase survivor list (collision stage)
-  // and by W = M^-1 J^T (no-slip stage): the three lifetimes do not overlap
-  union {
-    T H[PH_MAXV][PH_MAXV];
-    T efc_Wv[PH_MAXJSLOT];
-    int live[PH_MAXLIVE];
-  };
-  int tree_island[PH_MAXT], isl_n[PH_MAXT], isl_dof[PH_MAXT][PH_MAXV];
+  unsigned char con_dim[PH_MAXCON];
+  int tree_island[PH_MAXT], isl_n[PH_MAXT];
+  unsigned char isl_dof[PH_MAXT][PH_MAXV];
   int isl_eoff[PH_MAXT + 1], isl_roff[PH_MAXT + 1];
   short isl_row[PH_MAXEFC];
   T isl_alpha[PH_MAXT];        // per-island line-search step (also the warm-start choice)
@@ -513,10 +516,9 @@ __device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
     }
     const uint64_t bal = __ballot(keep);
     const int pos = nlive + __popcll(bal & ((1ull << l) - 1));
-    if (keep && pos < PH_MAXLIVE) s.live[pos] = pi;
+    if (keep) s.live[pos] = (short)pi;
     nlive += __popcll(bal);
   }
-  if (nlive > PH_MAXLIVE) { if (l == 0) s.warn |= 8u; nlive = PH_MAXLIVE; }
   wsync();
   // narrowphase in two passes (count, then write at the scanned offset): contact order = pair order
   int ncon = 0;
@@ -734,6 +736,7 @@ __device__ void st_constraints(const DevPhys<T>& m, Env<T>& s) {
     s.con_sbase[l] = sbase;
     s.con_t[l][0] = t0c;
     s.con_t[l][1] = t1c;
+    s.con_dim[l] = (unsigned char)s.con[l].dim;
   }
   if (__ballot(l < nc && !fits) && l == 0) s.warn |= 16u;
   wsync();
@@ -900,18 +903,30 @@ __device__ void st_actuation_smooth(const DevPhys<T>& m, Env<T>& s) {
 }
 
 // ============================================================================ Newton solver
-static_assert(PH_MAXEFC <= 2 * NT, "two constraint rows per lane");
+constexpr int RPL = (PH_MAXEFC + NT - 1) / NT;   // constraint rows per lane
 
-// Island-segmented wave sum: lane I (< nis) receives the sum over islands-I items of the three
-// per-lane items (one dof, two rows; island -1 = no item).  The cost separates over islands
+// Island-segmented wave sum: lane I (< nis) receives the sum of the island-I items of every
+// lane (one dof item, RPL row items; island -1 = no item).  The cost separates over islands
 // (block-diagonal M, every row inside one island), so the solver runs per island: a single
 // global cost would hide the 1e-10 improvements of the 4 mg dummy island under the arm's cost in
 // fp32, and a single global step length would tie every island to the arm's line search.
 template <typename T>
-__device__ __forceinline__ T isl_wsum(T v0, int i0, T v1, int i1, T v2, int i2, int nis) {
+__device__ __forceinline__ T isl_wsum(T vd, int id, const T (&vr)[RPL], const int (&ir)[RPL], int nis) {
   T out = 0;
   for (int I = 0; I < nis; I++) {
-    const T t = wsum((i0 == I ? v0 : T(0)) + (i1 == I ? v1 : T(0)) + (i2 == I ? v2 : T(0)));
+    T v = id == I ? vd : T(0);
+#pragma unroll
+    for (int k = 0; k < RPL; k++) v += ir[k] == I ? vr[k] : T(0);
+    const T t = wsum(v);
+    if (lane_id() == I) out = t;
+  }
+  return out;
+}
+template <typename T>
+__device__ __forceinline__ T isl_wsum(T vd, int id, int nis) {
+  T out = 0;
+  for (int I = 0; I < nis; I++) {
+    const T t = wsum(id == I ? vd : T(0));
     if (lane_id() == I) out = t;
   }
   return out;
@@ -923,15 +938,17 @@ __device__ T eval_cost(const DevPhys<T>& m, Env<T>& s, const T* x, bool store) {
   const int l = lane_id();
   if (l < m.nv) s.v1[l] = x[l] - s.qacc_smooth[l];
   wsync();
-  T cd = 0, cr[2] = {T(0), T(0)};
-  int di = -1, ri[2] = {-1, -1};
+  T cd = 0, cr[RPL];
+  int di = -1, ri[RPL];
   if (l < m.nv) {
     cd = T(0.5) * s.v1[l] * mulM_row(m, s, l, s.v1);
     di = s.tree_island[m.dof_tree[l]];
   }
 #pragma unroll
-  for (int k = 0; k < 2; k++) {
+  for (int k = 0; k < RPL; k++) {
     const int r = l + k * NT;
+    cr[k] = 0;
+    ri[k] = -1;
     if (r >= s.nefc) continue;
     const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
     T v = -s.efc_aref[r];
@@ -941,7 +958,7 @@ __device__ T eval_cost(const DevPhys<T>& m, Env<T>& s, const T* x, bool store) {
     if (a) cr[k] = T(0.5) * s.efc_D[r] * v * v;
     ri[k] = s.tree_island[t0];
   }
-  const T c = isl_wsum(cd, di, cr[0], ri[0], cr[1], ri[1], s.nisland);
+  const T c = isl_wsum(cd, di, cr, ri, s.nisland);
   wsync();
   return c;
 }
@@ -1015,7 +1032,7 @@ __device__ void build_islands(const DevPhys<T>& m, Env<T>& s) {
 // with 1e-5 constraint terms, and unscaled fp32 Cholesky would lose most digits there.
 template <typename T, int N>
 __device__ void island_newton_dir_reg(Env<T>& s, int I, int n) {
-  const int* idx = s.isl_dof[I];
+  const unsigned char* idx = s.isl_dof[I];
   int id[N];
 #pragma unroll
   for (int a = 0; a < N; a++) id[a] = a < n ? idx[a] : 0;
@@ -1069,7 +1086,7 @@ __device__ void island_newton_dir_reg(Env<T>& s, int I, int n) {
 // generic (merged islands of any size): in-place Cholesky through the dof list, LDS resident
 template <typename T>
 __device__ void island_newton_dir_lds(Env<T>& s, int I, int n) {
-  const int* idx = s.isl_dof[I];
+  const unsigned char* idx = s.isl_dof[I];
   for (int jj = 0; jj < n; jj++) {
     const int j = idx[jj];
     T sjj = s.H[j][j];
@@ -1106,15 +1123,16 @@ template <typename T>
 __device__ void line_search(const DevPhys<T>& m, Env<T>& s, bool done) {
   const int l = lane_id();
   const int nis = s.nisland;
-  int di = -1, ri[2] = {-1, -1};
+  int di = -1, ri[RPL];
   T A0 = 0, B0 = 0;
   if (l < m.nv) {
     s.v1[l] = s.x[l] - s.qacc_smooth[l];
     di = s.tree_island[m.dof_tree[l]];
   }
 #pragma unroll
-  for (int k = 0; k < 2; k++) {
+  for (int k = 0; k < RPL; k++) {
     const int r = l + k * NT;
+    ri[k] = -1;
     if (r >= s.nefc) continue;
     const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
     T v = 0;
@@ -1128,23 +1146,24 @@ __device__ void line_search(const DevPhys<T>& m, Env<T>& s, bool done) {
     A0 = mp * s.p[l];
     B0 = mp * s.v1[l];
   }
-  A0 = isl_wsum(A0, di, T(0), -1, T(0), -1, nis);
-  B0 = isl_wsum(B0, di, T(0), -1, T(0), -1, nis);
+  A0 = isl_wsum(A0, di, nis);
+  B0 = isl_wsum(B0, di, nis);
   bool fin = l >= nis || done;
   T lo = 0, hi = T(-1), a = fin ? T(0) : T(1);
   if (l < nis) s.isl_alpha[l] = a;
   for (int it = 0; it < 60; it++) {
     wsync();
-    T d1r[2] = {T(0), T(0)}, d2r[2] = {T(0), T(0)};
+    T d1r[RPL], d2r[RPL];
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < RPL; k++) {
       const int r = l + k * NT;
+      d1r[k] = d2r[k] = 0;
       if (r >= s.nefc) continue;
       const T jp = s.efc_Jp[r], v = s.efc_jar[r] + s.isl_alpha[ri[k]] * jp;
       if (r < s.ne || v < 0) { d1r[k] = s.efc_D[r] * v * jp; d2r[k] = s.efc_D[r] * jp * jp; }
     }
-    T d1 = isl_wsum(T(0), -1, d1r[0], ri[0], d1r[1], ri[1], nis) + A0 * a + B0;
-    T d2 = isl_wsum(T(0), -1, d2r[0], ri[0], d2r[1], ri[1], nis) + A0;
+    T d1 = isl_wsum(T(0), -1, d1r, ri, nis) + A0 * a + B0;
+    T d2 = isl_wsum(T(0), -1, d2r, ri, nis) + A0;
     if (!fin) {
       if (!(d2 > T(0))) { a = 0; fin = true; }
       else if (d1 == T(0)) fin = true;
@@ -1240,15 +1259,18 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s) {
     // island converged: its step did not change its active set (then its piecewise quadratic
     // was a single quadratic along the step and x is that quadratic's exact minimiser), or its
     // cost stopped decreasing
-    int ci[2] = {-1, -1};
+    int ci[RPL];
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < RPL; k++) {
       const int r = l + k * NT;
-      if (r < s.nefc && (T)s.efc_act[r] != s.efc_Jp[r]) ci[k] = s.tree_island[s.efc_t0[r]];
+      ci[k] = r < s.nefc && (T)s.efc_act[r] != s.efc_Jp[r] ? s.tree_island[s.efc_t0[r]] : -1;
     }
     bool changed = false;
     for (int I = 0; I < s.nisland; I++) {
-      const bool any = __ballot(ci[0] == I || ci[1] == I) != 0;
+      bool mine = false;
+#pragma unroll
+      for (int k = 0; k < RPL; k++) mine |= ci[k] == I;
+      const bool any = __ballot(mine) != 0;
       if (l == I) changed = any;
     }
     if (!done) {
@@ -1310,7 +1332,7 @@ __device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
   for (int iter = 0; iter < m.noslip_iterations; iter++) {
     for (int i = s.ne; i < s.nefc; i++) {
       if (s.efc_type[i] != 6) continue;
-      const int dim = s.con[s.efc_id[i]].dim;
+      const int dim = s.con_dim[s.efc_id[i]];
       for (int j = i; j < i + 2 * (dim - 1); j += 2) {
         // one pair of opposing pyramid edges; sparse rows have <= 16 slots = one DPP row
         const int t0 = s.efc_t0[j], t1 = s.efc_t1[j], w = row_width(m, t0, t1);
@@ -1440,12 +1462,28 @@ struct StageClock {
   }
 };
 
+// debug record of the contacts (PNP_DBG_CON): written right after collision, because the contact
+// list shares storage with the solver's scratch
 template <typename T>
-__device__ void forward(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
+__device__ void dump_contacts(const DevPhys<T>& m, const Env<T>& s, double* o) {
+  for (int c = lane_id(); c < s.ncon; c += NT) {
+    double* q = o + PNP_DBG_CON + c * PNP_DBG_CON_STRIDE;
+    for (int t = 0; t < 3; t++) q[t] = s.con[c].pos[t];
+    for (int t = 0; t < 9; t++) q[3 + t] = s.con[c].frame[t];
+    q[12] = s.con[c].dist;
+    q[13] = m.geom_id[s.con[c].g1];
+    q[14] = m.geom_id[s.con[c].g2];
+    q[15] = s.con[c].dim;
+  }
+}
+
+template <typename T>
+__device__ void forward(const DevPhys<T>& m, Env<T>& s, StageClock& clk, double* dbg = nullptr) {
   st_kinematics(m, s);      clk.lap(1);
   st_compos_crb(m, s);      clk.lap(2);
   st_factor_M(m, s);        clk.lap(3);
   st_collision(m, s);       clk.lap(4);
+  if (dbg) dump_contacts(m, s, dbg);
   st_constraints(m, s);     clk.lap(5);
   st_velocity(m, s);        clk.lap(6);
   st_actuation_smooth(m, s); clk.lap(7);
@@ -1514,10 +1552,7 @@ __device__ void store_env(const DevPhys<T>& m, const Env<T>& s, const pnp_state_
   const int l = lane_id();
   if (l < m.nq) st.qpos[(size_t)b * m.nq + l] = s.qpos[l];
   if (l < m.nv) { st.qvel[(size_t)b * m.nv + l] = s.qvel[l]; st.qacc_warmstart[(size_t)b * m.nv + l] = s.qacc_ws[l]; }
-  if (l < m.nu) st.ctrl[(size_t)b * m.nu + l] = s.ctrl[l];
-  if (l < 3 * m.nmocap) st.mocap_pos[(size_t)b * 3 * m.nmocap + l] = s.mocap_pos[l];
-  if (l < 4 * m.nmocap) st.mocap_quat[(size_t)b * 4 * m.nmocap + l] = s.mocap_quat[l];
-  if (l == 0) { st.time[b] = s.time; st.warn[b] = s.warn; }
+  if (l == 0) { st.time[b] = s.time; st.warn[b] = s.warn; }   // ctrl / mocap are inputs only
 }
 
 template <typename T, bool TIMED>
@@ -1544,8 +1579,9 @@ __global__ void __launch_bounds__(NT) forward_debug_kernel(const DevPhys<T>* __r
   const int b = blockIdx.x;
   if (b >= B) return;
   load_env(m, s, st, b);
-  forward(m, s);
   double* o = dbg + (size_t)b * PNP_DBG_SIZE;
+  StageClock clk{nullptr, 0};
+  forward(m, s, clk, o);
   const int l = lane_id();
   const int nv = m.nv;
   for (int e = l; e < nv * nv; e += NT) {
@@ -1564,15 +1600,6 @@ __global__ void __launch_bounds__(NT) forward_debug_kernel(const DevPhys<T>* __r
     o[PNP_DBG_COUNTS + 1] = s.nefc;
     o[PNP_DBG_COUNTS + 2] = s.solver_iter;
     o[PNP_DBG_COUNTS + 3] = s.warn;
-  }
-  for (int c = l; c < s.ncon; c += NT) {
-    double* q = o + PNP_DBG_CON + c * PNP_DBG_CON_STRIDE;
-    for (int t = 0; t < 3; t++) q[t] = s.con[c].pos[t];
-    for (int t = 0; t < 9; t++) q[3 + t] = s.con[c].frame[t];
-    q[12] = s.con[c].dist;
-    q[13] = m.geom_id[s.con[c].g1];
-    q[14] = m.geom_id[s.con[c].g2];
-    q[15] = s.con[c].dim;
   }
   for (int r = l; r < s.nefc; r += NT) {
     o[PNP_DBG_EFC_FORCE + r] = s.efc_force[r];

@@ -9,7 +9,7 @@ from .model import PnpIKParams, PnpModelDesc
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpnp.so")
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # every symbol include/pnp.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -28,8 +28,8 @@ class PnpState(C.Structure):
 
 # debug record layout (include/pnp.h PNP_DBG_*)
 DBG = dict(QM=0, BIAS=1296, ACT=1332, QACC_SMOOTH=1368, QACC=1404, COUNTS=1440, CON=1444, CON_STRIDE=16,
-           EFC_FORCE=1892, EFC_POS=2020, EFC_D=2148, EFC_AREF=2276, EFC_TYPE=2404, EFC_J=2532,
-           QACC_NEWTON=7140, SIZE=7184)
+           EFC_FORCE=2212, EFC_POS=2420, EFC_D=2628, EFC_AREF=2836, EFC_TYPE=3044, EFC_J=3252,
+           QACC_NEWTON=10740, SIZE=10776)
 
 _lib = None
 

@@ -11,7 +11,7 @@
  *   plane-sphere, plane-box (corners below the plane, deepest-first as MuJoCo, <= 4),
  *   plane-mesh (hull vertices below the plane, <= 4 deepest), sphere-sphere, sphere-box,
  *   box-box (separating-axis test over 15 axes, reference/incident face clipping, edge-edge),
- *   convex mesh pairs (mesh-*): GJK distance + EPA penetration on the convex hulls.
+ *   convex mesh pairs (mesh-*): convex.c.
  * Contact parameters (mj_contactParam): condim and friction = max, solref/solimp mixed by
  * solmix, margin/gap = max.
  */
@@ -149,33 +149,42 @@ static int sphere_box(const double* p1, double r, const double* p2, const double
   return 1;
 }
 
-/* Sutherland-Hodgman: clip polygon (in a 2D frame) against x_k*sgn <= lim */
-static int clip_poly(double (*poly)[3], int np, int axis, double sgn, double lim, double (*out)[3]) {
-  int no = 0;
-  for (int i = 0; i < np; i++) {
-    const double* a = poly[i];
-    const double* b = poly[(i + 1) % np];
-    double da = sgn * a[axis] - lim, db = sgn * b[axis] - lim;
-    if (da <= 0) { memcpy(out[no++], a, 3 * sizeof(double)); }
-    if ((da < 0 && db > 0) || (da > 0 && db < 0)) {
-      double t = da / (da - db);
-      for (int k = 0; k < 3; k++) out[no][k] = a[k] + t * (b[k] - a[k]);
-      no++;
+/* Liang-Barsky: clip the 2D segment p0 -> p1 (x, y = coords 0, 1) to |x| <= A, |y| <= B (closed);
+ * returns 0 when nothing is left, else the parameter interval [t0, t1] */
+static int clip_seg(const double* p0, const double* p1, double A, double B, double* t0, double* t1) {
+  const double dx = p1[0] - p0[0], dy = p1[1] - p0[1];
+  const double pp[4] = {-dx, dx, -dy, dy}, qq[4] = {p0[0] + A, A - p0[0], p0[1] + B, B - p0[1]};
+  double a = 0, b = 1;
+  for (int k = 0; k < 4; k++) {
+    if (pp[k] == 0) {
+      if (qq[k] < 0) return 0;
+    } else {
+      const double r = qq[k] / pp[k];
+      if (pp[k] < 0) { if (r > a) a = r; } else { if (r < b) b = r; }
     }
   }
-  return no;
+  if (a > b) return 0;
+  *t0 = a;
+  *t1 = b;
+  return 1;
 }
 
-/* reference face on box r (axis ia, outward normal nr), incident box i; normal_out = frame normal */
+/* Reference face on box r (axis ia, outward normal nr), incident box i; nframe = contact normal.
+ * The incident face (the face of box i most anti-parallel to nr) is expressed in the reference
+ * face frame (u, v, depth along nr) and intersected with the reference rectangle.  The vertices
+ * of that convex polygon are emitted in a fixed order: for each incident edge e = 0..3 its clipped
+ * start point and, when the edge leaves the rectangle, its exit point; then the reference corners
+ * strictly inside the incident face (depth from the incident plane).  This is the vertex set
+ * reference-face clipping (Sutherland-Hodgman) produces, computed without a variable-length
+ * polygon so the device version stays in registers; points deeper than margin are dropped.
+ * Not MuJoCo's mjc_BoxBox contact reduction: parity with MuJoCo here is unpinned. */
 static int box_face_contacts(const double* pr, const double* Rr, const double* sr, int ia, const double* nr,
                              const double* pi, const double* Ri, const double* si, const double* nframe,
                              double margin, orc_contact* c) {
-  /* reference frame: u, v = the other two axes of the reference box */
   int iu = (ia + 1) % 3, iv = (ia + 2) % 3;
   double u[3] = {Rr[iu], Rr[3 + iu], Rr[6 + iu]}, v[3] = {Rr[iv], Rr[3 + iv], Rr[6 + iv]};
   double cref[3];
   for (int k = 0; k < 3; k++) cref[k] = pr[k] + nr[k] * sr[ia];
-  /* incident face: box i face most anti-parallel to nr */
   int ja = 0;
   double best = -1;
   for (int j = 0; j < 3; j++) {
@@ -186,26 +195,52 @@ static int box_face_contacts(const double* pr, const double* Rr, const double* s
   double sg = dot3(bj, nr) > 0 ? -1 : 1;
   int ju = (ja + 1) % 3, jv = (ja + 2) % 3;
   double bu[3] = {Ri[ju], Ri[3 + ju], Ri[6 + ju]}, bv[3] = {Ri[jv], Ri[3 + jv], Ri[6 + jv]};
-  double poly[8][3], tmp[8][3];
   static const double su[4] = {1, -1, -1, 1}, sv[4] = {1, 1, -1, -1};
+  double P[4][3];
   for (int q = 0; q < 4; q++) {
     double w[3];
     for (int k = 0; k < 3; k++) w[k] = pi[k] + sg * bj[k] * si[ja] + su[q] * bu[k] * si[ju] + sv[q] * bv[k] * si[jv] - cref[k];
-    poly[q][0] = dot3(w, u); poly[q][1] = dot3(w, v); poly[q][2] = dot3(w, nr);
+    P[q][0] = dot3(w, u); P[q][1] = dot3(w, v); P[q][2] = dot3(w, nr);
   }
-  int np = 4;
-  np = clip_poly(poly, np, 0, 1, sr[iu], tmp);
-  np = clip_poly(tmp, np, 0, -1, sr[iu], poly);
-  np = clip_poly(poly, np, 1, 1, sr[iv], tmp);
-  np = clip_poly(tmp, np, 1, -1, sr[iv], poly);
+  const double A = sr[iu], B = sr[iv];
+  double pts[12][3];
+  int np = 0;
+  for (int e = 0; e < 4; e++) {
+    const double* p0 = P[e];
+    const double* p1 = P[(e + 1) & 3];
+    double t0, t1;
+    if (!clip_seg(p0, p1, A, B, &t0, &t1)) continue;
+    for (int k = 0; k < 3; k++) pts[np][k] = p0[k] + t0 * (p1[k] - p0[k]);
+    np++;
+    if (t1 < 1) {
+      for (int k = 0; k < 3; k++) pts[np][k] = p0[k] + t1 * (p1[k] - p0[k]);
+      np++;
+    }
+  }
+  /* reference corners inside the incident parallelogram P0 + a (P1 - P0) + b (P3 - P0) */
+  const double e1[3] = {P[1][0] - P[0][0], P[1][1] - P[0][1], P[1][2] - P[0][2]};
+  const double e3[3] = {P[3][0] - P[0][0], P[3][1] - P[0][1], P[3][2] - P[0][2]};
+  const double det = e1[0] * e3[1] - e1[1] * e3[0];
+  if (fabs(det) > 1e-12 * (fabs(e1[0]) + fabs(e1[1])) * (fabs(e3[0]) + fabs(e3[1]))) {
+    for (int q = 0; q < 4; q++) {
+      const double cx = su[q] * A - P[0][0], cy = sv[q] * B - P[0][1];
+      const double al = (cx * e3[1] - cy * e3[0]) / det, be = (e1[0] * cy - e1[1] * cx) / det;
+      if (al > 0 && al < 1 && be > 0 && be < 1) {
+        pts[np][0] = su[q] * A;
+        pts[np][1] = sv[q] * B;
+        pts[np][2] = P[0][2] + al * e1[2] + be * e3[2];
+        np++;
+      }
+    }
+  }
   int cnt = 0;
   for (int q = 0; q < np && cnt < 8; q++) {
-    double dist = poly[q][2];
+    double dist = pts[q][2];
     if (dist > margin) continue;
     c[cnt].dist = dist;
     set_normal(c + cnt, nframe);
     for (int k = 0; k < 3; k++)
-      c[cnt].pos[k] = cref[k] + u[k] * poly[q][0] + v[k] * poly[q][1] + nr[k] * poly[q][2] * 0.5;
+      c[cnt].pos[k] = cref[k] + u[k] * pts[q][0] + v[k] * pts[q][1] + nr[k] * pts[q][2] * 0.5;
     cnt++;
   }
   return cnt;

@@ -72,7 +72,7 @@ def test_library_loads_and_exports_header_symbols():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_lib.EXPORTS)
-    assert L.pnp_abi_version() == 2
+    assert L.pnp_abi_version() == _lib.ABI_VERSION == 3
     from pnp_amd.model import PnpModelDesc
     assert L.pnp_model_desc_size() == C.sizeof(PnpModelDesc)
 
@@ -95,3 +95,12 @@ def test_product_package_never_imports_oracle():
             if f.endswith((".py", ".hip", ".cpp", ".h")):
                 txt = open(os.path.join(dp, f)).read()
                 assert "import oracle" not in txt and "from oracle" not in txt and "liboracle" not in txt, f
+
+
+def test_debug_layout_matches_header():
+    """pnp_amd._lib.DBG mirrors the PNP_DBG_* offsets of include/pnp.h."""
+    import re
+    from pnp_amd import _lib
+    hdr = open(os.path.join(ROOT, "include", "pnp.h")).read()
+    defs = {k: int(v) for k, v in re.findall(r"#define PNP_DBG_(\w+) (\d+)", hdr)}
+    assert defs == _lib.DBG

@@ -1,0 +1,124 @@
+"""CPU checks of the fp64 mj_step oracle (oracle/physics.c, collision.c).
+
+Dynamics parity against MuJoCo itself is unpinned: the reference's dynamics live in MuJoCo 2.3.3,
+which is not installed, and the reference's tests hold no dynamics vectors.  So the
+oracle is checked here against independent restatements and physical invariants instead:
+
+* the CRBA mass matrix against the Jacobian sum sum_b J_b^T m_b J_b + J_r^T I J_r + armature;
+* the RNE bias at rest against the gravity-only generalised force sum_b Jp_b^T m_b (-g);
+* exact semi-implicit Euler free fall of the unconstrained dummy sphere;
+* a cube sliding on a shelf board stops after about v^2 / (2 mu g);
+* mj_checkPos / mj_checkVel reset the env and raise the warning bit (mj_resetData semantics);
+* bit-identical results across worker-thread counts.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from pnp_amd import setconst
+
+import physics_states as PS
+
+
+def _row(st, b):
+    return {k: st[k][b] for k in O.STATE_KEYS}
+
+
+def _random_arm(model, n, seed):
+    st = PS.reset_states(n, seed=seed, model=model)
+    rng = np.random.default_rng(seed)
+    lo, hi = model.jnt_range[:9, 0], model.jnt_range[:9, 1]
+    st["qpos"][:, :9] = rng.uniform(lo, hi, size=(n, 9))
+    return st
+
+
+def test_mass_matrix_matches_jacobian_sum(model):
+    st = _random_arm(model, 6, seed=11)
+    raw = model.__dict__
+    for b in range(6):
+        f = O.forward_fields(_row(st, b), ["qM"], model=model)
+        M = f["qM"].reshape(model.nv, model.nv)
+        Mj = setconst.mass_matrix(raw, st["qpos"][b])
+        assert np.abs(M - Mj).max() <= 1e-12 * max(1.0, np.abs(Mj).max())
+        assert np.allclose(M, M.T, atol=0, rtol=0)
+
+
+def test_bias_at_rest_is_gravity(model):
+    st = _random_arm(model, 4, seed=12)
+    raw = model.__dict__
+    g = np.array([0.0, 0.0, -9.81])
+    for b in range(4):
+        f = O.forward_fields(_row(st, b), ["qfrc_bias"], model=model)
+        Jp, _, _, _ = setconst.body_jacobians(raw, st["qpos"][b])
+        want = np.zeros(model.nv)
+        for i in range(1, model.nbody):
+            want -= model.body_mass[i] * Jp[i].T @ g
+        assert np.abs(f["qfrc_bias"] - want).max() <= 1e-10 * max(1.0, np.abs(want).max())
+
+
+def test_dummy_free_fall_is_semi_implicit_euler(model):
+    st = PS.reset_states(1, seed=0, model=model)
+    a = int(model.jnt_qposadr[model.joint_id("obj_joint")])
+    d = int(model.jnt_dofadr[model.joint_id("obj_joint")])
+    st["qpos"][0, a:a + 3] = [2.0, 2.0, 3.0]          # far from every other geom
+    st["qvel"][0, d:d + 3] = [0.1, -0.2, 0.3]
+    z0, vz0 = 3.0, 0.3
+    h = model.opt_timestep
+    n = 20
+    O.step(st, nsub=n, model=model)
+    vz = vz0 - 9.81 * h * n
+    z = z0 + h * sum(vz0 - 9.81 * h * k for k in range(1, n + 1))
+    assert abs(st["qvel"][0, d + 2] - vz) < 1e-12
+    assert abs(st["qpos"][0, a + 2] - z) < 1e-12
+    assert abs(st["qpos"][0, a] - (2.0 + 0.1 * h * n)) < 1e-12
+    assert st["time"][0] == pytest.approx(h * n, abs=1e-15)
+
+
+def test_cube_on_shelf_stops_by_friction(model):
+    st = PS.settled_states(1, seed=0, nsettle=100, model=model)
+    j = model.joint_id("cube2_joint")
+    a, d = int(model.jnt_qposadr[j]), int(model.jnt_dofadr[j])
+    x0 = st["qpos"][0, a]
+    v0 = 0.3
+    st["qvel"][0, d] = v0
+    O.step(st, nsub=60, model=model)
+    assert abs(st["qvel"][0, d]) < 1e-3, "cube still sliding after 0.12 s"
+    slide = st["qpos"][0, a] - x0
+    coulomb = v0 ** 2 / (2 * 1.0 * 9.81)              # mu = 1 (max-mixed cube/shelf friction)
+    assert 0.5 * coulomb < slide < 2.0 * coulomb
+    assert st["warn"][0] == 0
+
+
+def test_bad_qpos_resets_env_and_warns(model):
+    st = PS.settled_states(2, seed=0, nsettle=10, model=model)
+    st["qpos"][1, 3] = np.nan
+    O.step(st, nsub=1, model=model)
+    assert st["warn"][1] & 1                          # PNP_WARN_BADQPOS
+    assert st["warn"][0] == 0
+    assert np.isfinite(st["qpos"]).all()
+
+
+def test_bad_qvel_resets_env_and_warns(model):
+    st = PS.settled_states(1, seed=0, nsettle=10, model=model)
+    st["qvel"][0, 12] = 1e11
+    O.step(st, nsub=1, model=model)
+    assert st["warn"][0] & 2                          # PNP_WARN_BADQVEL
+    assert np.isfinite(st["qvel"]).all() and np.abs(st["qvel"]).max() < 1e3
+
+
+def test_step_threads_bit_identical(model):
+    st = PS.settled_states(8, seed=3, nsettle=20, model=model)
+    PS.random_ctrl(st, model=model)
+    a, b = PS.copy_state(st), PS.copy_state(st)
+    O.step(a, nsub=5, nthreads=1, model=model)
+    O.step(b, nsub=5, nthreads=4, model=model)
+    for k in O.STATE_KEYS:
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_settled_scene_is_at_rest(model):
+    st = PS.settled_states(4, seed=5, nsettle=250, model=model)
+    for name in ("cube1_joint", "cube2_joint", "cube3_joint"):
+        d = int(model.jnt_dofadr[model.joint_id(name)])
+        assert np.abs(st["qvel"][:, d:d + 6]).max() < 5e-3, name
+    assert (st["warn"] == 0).all()
