@@ -246,6 +246,93 @@ int32_t pnp_step_profile(pnp_model* model, const pnp_state* state, int32_t B, in
 /* LDS bytes one env occupies in the step kernel (fp64 != 0: the debug instantiation). */
 int32_t pnp_step_lds_bytes(int32_t fp64);
 
+/* ------------------------------------------------------------------ gym env (FrankaEnv) */
+/* Batched FrankaShelfPNPEnv: the reference's gym surface (envs/panda_env.py, envs/shelf_pnp.py)
+ * with the whole gym step fused into one launch per batch.  Replaces, per env:
+ *   pnp_env_init   FrankaEnv.__init__ -> _initialize_simulation / _env_setup (panda_env.py:106-141)
+ *                  + _initialize_multi_object_task (:100-104)
+ *   pnp_env_reset  FrankaEnv.reset -> _reset_sim (:366-391), _sample_object (:146-158),
+ *                  _sample_goal (:360-364), then _get_obs (:279-301)
+ *   pnp_env_step   FrankaEnv.step (:163-196): clip, _set_action (:250-277), _mujoco_step (10 x
+ *                  mj_step(nstep=25), :355-358), _get_obs, _is_success (:303-306),
+ *                  compute_reward (:205-245), task sequencing, TimeLimit(300) truncation
+ *                  (__init__.py:15).
+ * "data.site_*" semantics are kept: the observation's positions / Jacobians come from the
+ * kinematics of the last forward (the pre-integration qpos of the last sub-step, or the reset
+ * state), velocities are J * qvel with the integrated qvel, finger width reads integrated qpos. */
+#define PNP_MAX_TASKS 4
+#define PNP_OBS_DIM 19
+typedef struct pnp_env_params {
+  int32_t n_substeps;          /* 25 (shelf_pnp.py:19) */
+  int32_t n_calls;             /* 10 mj_step calls per gym step (panda_env.py:357) */
+  int32_t reward_dense;        /* 1: dense reward, 0: sparse */
+  int32_t max_episode_steps;   /* TimeLimit (300); <= 0: never truncate */
+  int32_t n_tasks;             /* len(task_sequence) (3) */
+  int32_t ee_site;             /* ee_center_site */
+  int32_t obj_site[PNP_MAX_TASKS];     /* "<obj>_site" per task */
+  int32_t target_site[PNP_MAX_TASKS];  /* "target_<obj>" per task */
+  int32_t obj_qadr[PNP_MAX_TASKS];     /* qpos address of "<obj>_joint" (free joint) */
+  int32_t finger_qadr[2];      /* finger_joint1 / finger_joint2 qpos addresses */
+  int32_t neutral_qadr[9];     /* arm + gripper joint qpos addresses (set_joint_neutral) */
+  int32_t height_qadr;         /* qpos address of obj_joint (initial_object_height = z) */
+  int32_t arm_ctrl_n;          /* ctrl[0:arm_ctrl_n] = neutral at setup (7) */
+  double neutral[9];           /* neutral_joint_values (panda_env.py:64-66) */
+  double distance_threshold;   /* 0.05 */
+  double high_pick_z;          /* 0.35 */
+  double grip_width;           /* 0.045 */
+  double reach_thresh;         /* 0.05: gripped needs d_reach < this; reach penalty cap */
+  double lift_height;          /* 0.04 */
+  double obj_x_range, obj_y_range;   /* 0.02, 0.2 (shelf_pnp.py:23-24) */
+  double pos_scale;            /* 0.05 (ee target = ee_pos + pos_scale * a[0:3]) */
+  double rot_scale;            /* 0.1 (delta euler) */
+  double finger_scale;         /* 0.2 (finger width += finger_scale * a[6]) */
+  uint32_t seed_lo, seed_hi;   /* Philox key of the reset draws */
+} pnp_env_params;
+/* sizeof(pnp_env_params) (binding layout check) */
+int32_t pnp_env_params_size(void);
+/* Per-env episode state, device SoA (float or double like the sim state; ints as given). */
+typedef struct pnp_env_state {
+  void* goal;            /* [B*3] desired goal */
+  int32_t* task;         /* [B] current_task_index */
+  int32_t* elapsed;      /* [B] TimeLimit step counter */
+  void* qpos_kin;        /* [B*nq] qpos of the last forward (what data.site_* were computed at) */
+  void* obj_height0;     /* [B] initial_object_height */
+  void* init_mocap;      /* [B*7] initial mocap pos (3) + grasp quat (4) */
+  void* init_qvel;       /* [B*nv] */
+  void* init_time;       /* [B] */
+  uint32_t* episode;     /* [B] resets so far: Philox counter of the reset draws */
+  uint32_t* env_index;   /* [B] global env index: Philox counter (shard-invariant) */
+} pnp_env_state;
+/* Outputs (any pointer may be NULL to skip it). */
+typedef struct pnp_env_out {
+  void* obs;             /* [B*19] observation */
+  void* achieved_goal;   /* [B*3] */
+  void* desired_goal;    /* [B*3] (goal before this step's task update) */
+  void* reward;          /* [B] */
+  void* is_success;      /* [B] 1.0 / 0.0 */
+  uint8_t* terminated;   /* [B] */
+  uint8_t* truncated;    /* [B] */
+} pnp_env_out;
+int32_t pnp_env_init(pnp_model* model, const pnp_state* state, const pnp_env_params* params,
+                     const pnp_env_state* env, int32_t B, void* stream);
+int32_t pnp_env_init_f64(pnp_model* model, const pnp_state_f64* state, const pnp_env_params* params,
+                         const pnp_env_state* env, int32_t B, void* stream);
+/* mask[B] (uint8, NULL = every env): envs to reset; obs / achieved_goal / desired_goal of the
+ * reset envs are written to out (other envs' outputs untouched). */
+int32_t pnp_env_reset(pnp_model* model, const pnp_state* state, const pnp_env_params* params,
+                      const pnp_env_state* env, const uint8_t* mask, const pnp_env_out* out, int32_t B,
+                      void* stream);
+int32_t pnp_env_reset_f64(pnp_model* model, const pnp_state_f64* state, const pnp_env_params* params,
+                          const pnp_env_state* env, const uint8_t* mask, const pnp_env_out* out, int32_t B,
+                          void* stream);
+/* action[B*7] (same dtype as the state), clipped to [-1, 1] like the action space. */
+int32_t pnp_env_step(pnp_model* model, const pnp_state* state, const pnp_env_params* params,
+                     const pnp_env_state* env, const float* action, const pnp_env_out* out, int32_t B,
+                     void* stream);
+int32_t pnp_env_step_f64(pnp_model* model, const pnp_state_f64* state, const pnp_env_params* params,
+                         const pnp_env_state* env, const double* action, const pnp_env_out* out, int32_t B,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

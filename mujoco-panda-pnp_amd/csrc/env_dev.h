@@ -1,0 +1,514 @@
+// env_dev.h — the reference's gym surface as fused device code (included by step.hip, whose Env,
+// stages and mj_step_dev it uses).  One 64-lane wave per env, like the step kernel.
+//
+//   env_init_kernel   FrankaEnv._env_setup + _initialize_multi_object_task (envs/panda_env.py:100-141)
+//   env_reset_kernel  _reset_sim / _sample_object / _sample_goal / _get_obs (:146-158, :279-301, :360-391)
+//   env_step_kernel   FrankaEnv.step (:163-196): clip -> _set_action (:250-277) -> 10 x mj_step(nstep=25)
+//                     (:355-358) -> _get_obs -> _is_success (:303-306) -> compute_reward (:205-245)
+//                     -> task sequencing -> TimeLimit(max_episode_steps=300) (__init__.py:15)
+//
+// gymnasium_robotics.utils.rotations (euler2quat, quat_mul, mat2euler) and MuJoCo's mju_mat2Quat
+// are restated from their published definitions (third-party, absent here).
+#pragma once
+
+#define PNP_RESET_STREAM 0x40000000u   // Philox stream word of the reset draws: | episode
+
+// ---------------------------------------------------------------- Philox4x32-10 (pnp_amd/rng.py)
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    const uint64_t p0 = (uint64_t)c[0] * 0xD2511F53ull, p1 = (uint64_t)c[2] * 0xCD9E8D57ull;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0, hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+// rng.uniform(env, ndraw, seed, stream)[draw]: counter (env_lo, draw / 4, stream, env_hi = 0)
+__device__ __forceinline__ double philox_uniform(uint32_t env, int draw, uint32_t stream, uint32_t k0, uint32_t k1) {
+  uint32_t c[4] = {env, (uint32_t)(draw >> 2), stream, 0u};
+  philox4x32_10(c, k0, k1);
+  return (double)c[draw & 3] * (1.0 / 4294967296.0);
+}
+
+// ---------------------------------------------------------------- rotations
+// gymnasium_robotics rotations.euler2quat (static x-y-z = roll, pitch, yaw), wxyz
+template <typename T>
+__device__ void g_euler2quat(const T e[3], T q[4]) {
+  T si, ci, sj, cj, sk, ck;
+  d_sincos(e[2] * T(0.5), &si, &ci);
+  d_sincos(-e[1] * T(0.5), &sj, &cj);
+  d_sincos(e[0] * T(0.5), &sk, &ck);
+  const T cc = ci * ck, cs = ci * sk, sc = si * ck, ss = si * sk;
+  q[0] = cj * cc + sj * ss;
+  q[1] = cj * cs - sj * sc;
+  q[2] = -(cj * ss + sj * cc);
+  q[3] = cj * sc - sj * cs;
+}
+// rotations.quat_mul(q0, q1) (Hamilton product, wxyz)
+template <typename T>
+__device__ void g_quat_mul(const T a[4], const T b[4], T r[4]) {
+  r[0] = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  r[1] = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  r[2] = a[0] * b[2] + a[2] * b[0] + a[3] * b[1] - a[1] * b[3];
+  r[3] = a[0] * b[3] + a[3] * b[0] + a[1] * b[2] - a[2] * b[1];
+}
+// rotations.mat2euler (row-major R), with its 4 * float64-eps gimbal test
+template <typename T>
+__device__ void g_mat2euler(const T R[9], T e[3]) {
+  const T cy = PM<T>::sqrt_(R[8] * R[8] + R[5] * R[5]);
+  const bool ok = (double)cy > 4.0 * 2.220446049250313e-16;
+  e[2] = ok ? -atan2(R[1], R[0]) : -atan2(-R[3], R[4]);
+  e[1] = -atan2(-R[2], cy);
+  e[0] = ok ? -atan2(R[5], R[8]) : T(0);
+}
+// MuJoCo mju_mat2Quat (largest-component branch, then normalised)
+template <typename T>
+__device__ void g_mat2quat(const T m[9], T q[4]) {
+  if (m[0] + m[4] + m[8] > 0) {
+    q[0] = T(0.5) * PM<T>::sqrt_(1 + m[0] + m[4] + m[8]);
+    q[1] = T(0.25) * (m[7] - m[5]) / q[0];
+    q[2] = T(0.25) * (m[2] - m[6]) / q[0];
+    q[3] = T(0.25) * (m[3] - m[1]) / q[0];
+  } else if (m[0] > m[4] && m[0] > m[8]) {
+    q[1] = T(0.5) * PM<T>::sqrt_(1 + m[0] - m[4] - m[8]);
+    q[0] = T(0.25) * (m[7] - m[5]) / q[1];
+    q[2] = T(0.25) * (m[1] + m[3]) / q[1];
+    q[3] = T(0.25) * (m[2] + m[6]) / q[1];
+  } else if (m[4] > m[8]) {
+    q[2] = T(0.5) * PM<T>::sqrt_(1 - m[0] + m[4] - m[8]);
+    q[0] = T(0.25) * (m[2] - m[6]) / q[2];
+    q[1] = T(0.25) * (m[1] + m[3]) / q[2];
+    q[3] = T(0.25) * (m[5] + m[7]) / q[2];
+  } else {
+    q[3] = T(0.5) * PM<T>::sqrt_(1 - m[0] - m[4] + m[8]);
+    q[0] = T(0.25) * (m[3] - m[1]) / q[3];
+    q[1] = T(0.25) * (m[2] + m[6]) / q[3];
+    q[2] = T(0.25) * (m[5] + m[7]) / q[3];
+  }
+  t_normalize4(q);
+}
+
+// ---------------------------------------------------------------- typed views of the C structs
+template <typename T>
+struct EnvSoA {
+  T* goal; int32_t* task; int32_t* elapsed; T* qpos_kin; T* obj_height0; T* init_mocap; T* init_qvel;
+  T* init_time; uint32_t* episode; uint32_t* env_index;
+};
+template <typename T>
+struct EnvOutT {
+  T* obs; T* ag; T* dg; T* reward; T* success; uint8_t* terminated; uint8_t* truncated;
+};
+
+// site frame from the body frames of the last st_kinematics (mj_kinematics site pass)
+template <typename T>
+__device__ void site_frame(const DevPhys<T>& m, const Env<T>& s, int site, T pos[3], T mat[9]) {
+  const int b = m.site_bodyid[site];
+  T v[3], q[4];
+  d_mulmatvec3(v, s.xmat[b], m.site_pos[site]);
+  for (int t = 0; t < 3; t++) pos[t] = s.xpos[b][t] + v[t];
+  d_mulquat(q, s.xquat[b], m.site_quat[site]);
+  d_quat2mat(mat, q);
+}
+// mj_jacSite(site) * qvel (gymnasium_robotics get_site_xvelp / xvelr); needs st_compos_crb
+// (subtree COM, cdof); lane-uniform result
+template <typename T>
+__device__ void site_vel(const DevPhys<T>& m, Env<T>& s, int site, const T pt[3], T vp[3], T vr[3]) {
+  const int l = lane_id();
+  T jp[3] = {0, 0, 0}, jr[3] = {0, 0, 0};
+  if (l < m.nv) jac_col(m, s, m.site_bodyid[site], l, pt, jp, jr);
+  const T qv = l < m.nv ? s.qvel[l] : T(0);
+  for (int t = 0; t < 3; t++) {
+    vp[t] = wsum(jp[t] * qv);
+    vr[t] = wsum(jr[t] * qv);
+  }
+}
+
+// forward kinematics (+ comPos for Jacobians) at qk, keeping s.qpos: s.qpos_pre holds s.qpos
+template <typename T>
+__device__ void kin_at(const DevPhys<T>& m, Env<T>& s, const T* qk, bool jac) {
+  const int l = lane_id();
+  if (l < m.nq) { s.qpos_pre[l] = s.qpos[l]; s.qpos[l] = qk[l]; }
+  wsync();
+  st_kinematics(m, s);
+  if (jac) st_compos_crb(m, s);
+  if (l < m.nq) s.qpos[l] = s.qpos_pre[l];
+  wsync();
+}
+
+
+// _get_obs on the current kinematics (positions) and s.qvel; width = finger qpos sum of the
+// integrated state.  Writes obs / achieved / desired goal of env b; returns ee / object data.
+template <typename T>
+__device__ void env_observe(const DevPhys<T>& m, Env<T>& s, const pnp_env_params& prm, int task, const T goal[3],
+                            const EnvOutT<T>& out, int b, T width, T ee_p[3], T ee_R[9], T ob_p[3]) {
+  const int l = lane_id();
+  const int ti = task < prm.n_tasks ? task : prm.n_tasks - 1;   // current_target_object
+  T ob_R[9], ee_vp[3], ee_vr[3], ob_vp[3], ob_vr[3], eul[3];
+  site_frame(m, s, prm.ee_site, ee_p, ee_R);
+  site_frame(m, s, prm.obj_site[ti], ob_p, ob_R);
+  site_vel(m, s, prm.ee_site, ee_p, ee_vp, ee_vr);
+  site_vel(m, s, prm.obj_site[ti], ob_p, ob_vp, ob_vr);
+  g_mat2euler(ob_R, eul);
+  const T dt = m.timestep * T(prm.n_substeps);   // MujocoRobotEnv.dt
+  if (l == 0) {
+    if (out.obs) {
+      T* o = out.obs + (size_t)b * PNP_OBS_DIM;
+      for (int t = 0; t < 3; t++) {
+        o[t] = ee_p[t];
+        o[3 + t] = ee_vp[t] * dt;
+        o[7 + t] = ob_p[t];
+        o[10 + t] = eul[t];
+        o[13 + t] = ob_vp[t] * dt;
+        o[16 + t] = ob_vr[t] * dt;
+      }
+      o[6] = width;
+    }
+    if (out.ag)
+      for (int t = 0; t < 3; t++) out.ag[(size_t)b * 3 + t] = ob_p[t];
+    if (out.dg)
+      for (int t = 0; t < 3; t++) out.dg[(size_t)b * 3 + t] = goal[t];
+  }
+}
+
+template <typename T>
+__device__ void store_controls(const DevPhys<T>& m, const Env<T>& s, const pnp_state_t<T>& st, int b) {
+  const int l = lane_id();
+  if (l < m.nu) st.ctrl[(size_t)b * m.nu + l] = s.ctrl[l];
+  if (l < 3 * m.nmocap) st.mocap_pos[(size_t)b * 3 * m.nmocap + l] = s.mocap_pos[l];
+  if (l < 4 * m.nmocap) st.mocap_quat[(size_t)b * 4 * m.nmocap + l] = s.mocap_quat[l];
+}
+
+// ---------------------------------------------------------------- init (_env_setup)
+template <typename T>
+__global__ void __launch_bounds__(NT) env_init_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
+                                                      pnp_env_params prm, EnvSoA<T> es, int B) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
+  const DevPhys<T>& m = *mp;
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  const int l = lane_id();
+  load_env(m, s, st, b);
+  // set_joint_neutral; ctrl[0:7] = neutral[:7]; (welds already at identity relpose)
+  if (l == 0) {
+    for (int i = 0; i < 9; i++) s.qpos[prm.neutral_qadr[i]] = (T)prm.neutral[i];
+    for (int i = 0; i < prm.arm_ctrl_n; i++) s.ctrl[i] = (T)prm.neutral[i];
+  }
+  wsync();
+  // mj_forward -> initial mocap = ee_center_site pose (get_site_xpos, get_ee_orientation)
+  st_kinematics(m, s);
+  T ee_p[3], ee_R[9], ee_q[4], goal[3], gR[9];
+  site_frame(m, s, prm.ee_site, ee_p, ee_R);
+  g_mat2quat(ee_R, ee_q);
+  site_frame(m, s, prm.target_site[0], goal, gR);
+  if (l == 0) {
+    for (int t = 0; t < 3; t++) s.mocap_pos[t] = ee_p[t];
+    for (int t = 0; t < 4; t++) s.mocap_quat[t] = ee_q[t];
+  }
+  wsync();
+  // _mujoco_step(): 10 x mj_step(nstep = n_substeps)
+  StageClock clk{nullptr, 0};
+  const int nsub = prm.n_substeps * prm.n_calls;
+  for (int k = 0; k < nsub; k++) mj_step_dev(m, s, clk, k == nsub - 1 ? s.qpos_pre : nullptr);
+  store_env(m, s, st, b);
+  store_controls(m, s, st, b);
+  if (l < m.nq) es.qpos_kin[(size_t)b * m.nq + l] = s.qpos_pre[l];
+  if (l < m.nv) es.init_qvel[(size_t)b * m.nv + l] = s.qvel[l];
+  if (l < 3) es.init_mocap[(size_t)b * 7 + l] = s.mocap_pos[l];
+  if (l < 4) es.init_mocap[(size_t)b * 7 + 3 + l] = s.mocap_quat[l];
+  if (l < 3) es.goal[(size_t)b * 3 + l] = goal[l];
+  if (l == 0) {
+    es.obj_height0[b] = s.qpos[prm.height_qadr + 2];
+    es.init_time[b] = s.time;
+    es.task[b] = 0;
+    es.elapsed[b] = 0;
+    es.episode[b] = 0;
+  }
+}
+
+// ---------------------------------------------------------------- reset (_reset_sim + _get_obs)
+template <typename T>
+__global__ void __launch_bounds__(NT) env_reset_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
+                                                       pnp_env_params prm, EnvSoA<T> es,
+                                                       const uint8_t* __restrict__ mask, EnvOutT<T> out, int B) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
+  const DevPhys<T>& m = *mp;
+  const int b = blockIdx.x;
+  if (b >= B || (mask && !mask[b])) return;
+  const int l = lane_id();
+  load_env(m, s, st, b);
+  // _sample_object centres: the objects' site_xpos as of the last forward (not refreshed by
+  // set_joint_neutral / set_mocap_pose, which only write qpos / mocap)
+  kin_at(m, s, es.qpos_kin + (size_t)b * m.nq, false);
+  T ctr[PNP_MAX_TASKS][3];
+#pragma unroll
+  for (int k = 0; k < PNP_MAX_TASKS; k++) {
+    T R[9];
+    if (k < prm.n_tasks) site_frame(m, s, prm.obj_site[k], ctr[k], R);
+  }
+  const uint32_t ep = es.episode[b], env = es.env_index[b];
+  if (l == 0) {
+    s.time = es.init_time[b];
+    for (int i = 0; i < 9; i++) s.qpos[prm.neutral_qadr[i]] = (T)prm.neutral[i];
+    for (int t = 0; t < 3; t++) s.mocap_pos[t] = es.init_mocap[(size_t)b * 7 + t];
+    for (int t = 0; t < 4; t++) s.mocap_quat[t] = es.init_mocap[(size_t)b * 7 + 3 + t];
+    for (int k = 0; k < prm.n_tasks; k++) {
+      // x = centre + np.random.uniform(-r, r) = centre + (-r + (r - -r) * u)
+      const double ux = philox_uniform(env, 2 * k, PNP_RESET_STREAM | ep, prm.seed_lo, prm.seed_hi);
+      const double uy = philox_uniform(env, 2 * k + 1, PNP_RESET_STREAM | ep, prm.seed_lo, prm.seed_hi);
+      const double xr = prm.obj_x_range, yr = prm.obj_y_range;
+      T* q = s.qpos + prm.obj_qadr[k];
+      q[0] = ctr[k][0] + (T)(-xr + (xr - -xr) * ux);
+      q[1] = ctr[k][1] + (T)(-yr + (yr - -yr) * uy);
+      q[2] = ctr[k][2];
+      q[3] = 1; q[4] = 0; q[5] = 0; q[6] = 0;
+    }
+    es.task[b] = 0;
+    es.elapsed[b] = 0;
+    es.episode[b] = ep + 1;
+  }
+  if (l < m.nv) s.qvel[l] = es.init_qvel[(size_t)b * m.nv + l];
+  wsync();
+  // _initialize_multi_object_task + mj_forward
+  st_kinematics(m, s);
+  st_compos_crb(m, s);
+  T goal[3], gR[9];
+  site_frame(m, s, prm.target_site[0], goal, gR);
+  if (l < 3) es.goal[(size_t)b * 3 + l] = goal[l];
+  if (l < m.nq) es.qpos_kin[(size_t)b * m.nq + l] = s.qpos[l];
+  T ee_p[3], ee_R[9], ob_p[3];
+  env_observe(m, s, prm, 0, goal, out, b, s.qpos[prm.finger_qadr[0]] + s.qpos[prm.finger_qadr[1]], ee_p, ee_R, ob_p);
+  store_env(m, s, st, b);
+  store_controls(m, s, st, b);
+}
+
+// ---------------------------------------------------------------- step (FrankaEnv.step)
+template <typename T>
+__global__ void __launch_bounds__(NT) env_step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
+                                                      pnp_env_params prm, EnvSoA<T> es, const T* __restrict__ action,
+                                                      EnvOutT<T> out, int B) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
+  const DevPhys<T>& m = *mp;
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  const int l = lane_id();
+  load_env(m, s, st, b);
+  // ---- _set_action: ee pose from the last forward's site frame
+  kin_at(m, s, es.qpos_kin + (size_t)b * m.nq, false);
+  T ee_p[3], ee_R[9], ee_q[4];
+  site_frame(m, s, prm.ee_site, ee_p, ee_R);
+  g_mat2quat(ee_R, ee_q);
+  if (l == 0) {
+    T a[7];
+    for (int k = 0; k < 7; k++) a[k] = fmin(fmax(action[(size_t)b * 7 + k], T(-1)), T(1));
+    const T width = s.qpos[prm.finger_qadr[0]] + s.qpos[prm.finger_qadr[1]] + a[6] * (T)prm.finger_scale;
+    const T half = fmin(fmax(width / T(2), m.act_ctrlrange[m.nu - 1][0]), m.act_ctrlrange[m.nu - 1][1]);
+    s.ctrl[m.nu - 2] = half;
+    s.ctrl[m.nu - 1] = half;
+    T de[3], dq[4], tq[4];
+    for (int t = 0; t < 3; t++) {
+      s.mocap_pos[t] = ee_p[t] + (T)prm.pos_scale * a[t];
+      de[t] = fmin(fmax(a[3 + t], T(-1)), T(1)) * (T)prm.rot_scale;
+    }
+    s.mocap_pos[2] = fmax(T(0), s.mocap_pos[2]);
+    g_euler2quat(de, dq);
+    g_quat_mul(dq, ee_q, tq);
+    for (int t = 0; t < 4; t++) s.mocap_quat[t] = tq[t];
+  }
+  wsync();
+  // ---- _mujoco_step: n_calls x mj_step(nstep = n_substeps)
+  StageClock clk{nullptr, 0};
+  const int nsub = prm.n_substeps * prm.n_calls;
+  for (int k = 0; k < nsub; k++) mj_step_dev(m, s, clk, k == nsub - 1 ? s.qpos_pre : nullptr);
+  store_env(m, s, st, b);
+  store_controls(m, s, st, b);
+  const T width = s.qpos[prm.finger_qadr[0]] + s.qpos[prm.finger_qadr[1]];
+  if (l < m.nq) es.qpos_kin[(size_t)b * m.nq + l] = s.qpos_pre[l];
+  // ---- _get_obs at data.site_* (kinematics of qpos_pre) with the integrated qvel
+  if (l < m.nq) { const T t = s.qpos[l]; s.qpos[l] = s.qpos_pre[l]; s.qpos_pre[l] = t; }
+  wsync();
+  st_kinematics(m, s);
+  st_compos_crb(m, s);
+  const int task = es.task[b];
+  T dg[3];
+  for (int t = 0; t < 3; t++) dg[t] = es.goal[(size_t)b * 3 + t];
+  T ob_p[3];
+  env_observe(m, s, prm, task, dg, out, b, width, ee_p, ee_R, ob_p);
+  // ---- _is_success / compute_reward (before the task update)
+  const T dr[3] = {ee_p[0] - ob_p[0], ee_p[1] - ob_p[1], ee_p[2] - ob_p[2]};
+  const T dp[3] = {ob_p[0] - dg[0], ob_p[1] - dg[1], ob_p[2] - dg[2]};
+  const T d_reach = PM<T>::sqrt_(dr[0] * dr[0] + dr[1] * dr[1] + dr[2] * dr[2]);
+  const T d_place = PM<T>::sqrt_(dp[0] * dp[0] + dp[1] * dp[1] + dp[2] * dp[2]);
+  const bool placed = d_place < (T)prm.distance_threshold;
+  const bool gripped = width < (T)prm.grip_width && d_reach < (T)prm.reach_thresh;
+  const bool lifted = gripped && ob_p[2] - es.obj_height0[b] > (T)prm.lift_height;
+  T eq[4];
+  g_mat2quat(ee_R, eq);
+  T need[4] = {1, 0, 0, 0};   // VERTICAL_QUAT = euler2quat(0)
+  if (ob_p[2] > (T)prm.high_pick_z) {
+    const T hz[3] = {T(-1.5707963267948966), 0, 0};   // HORIZONTAL_QUAT = euler2quat([-pi/2, 0, 0])
+    g_euler2quat(hz, need);
+  }
+  const T ori_err = T(1) - fabs(eq[0] * need[0] + eq[1] * need[1] + eq[2] * need[2] + eq[3] * need[3]);
+  T reward;
+  if (!prm.reward_dense) {
+    reward = placed ? T(0) : T(-1);
+  } else {
+    reward = T(-0.003) - fmin(d_reach, (T)prm.reach_thresh);
+    if (gripped) reward += T(2) + (T(1) - ori_err);
+    if (lifted) reward += T(4);
+    if (placed) reward += T(10);
+    reward += T(0.5) * (T(task) / T(prm.n_tasks));
+  }
+  // ---- task sequencing, TimeLimit
+  bool terminated = false;
+  int ntask = task;
+  T goal[3] = {dg[0], dg[1], dg[2]};
+  if (placed) {
+    ntask = task + 1;
+    if (ntask < prm.n_tasks) {
+      T gR[9];
+      site_frame(m, s, prm.target_site[ntask], goal, gR);
+    } else {
+      terminated = true;
+    }
+  }
+  const int elapsed = es.elapsed[b] + 1;
+  const bool truncated = prm.max_episode_steps > 0 && elapsed >= prm.max_episode_steps;
+  if (l == 0) {
+    es.task[b] = ntask;
+    es.elapsed[b] = elapsed;
+    for (int t = 0; t < 3; t++) es.goal[(size_t)b * 3 + t] = goal[t];
+    if (out.reward) out.reward[b] = reward;
+    if (out.success) out.success[b] = placed ? T(1) : T(0);
+    if (out.terminated) out.terminated[b] = terminated;
+    if (out.truncated) out.truncated[b] = truncated;
+  }
+}
+
+// ---------------------------------------------------------------- host launchers
+template <typename T>
+static EnvSoA<T> env_view(const pnp_env_state* e) {
+  return EnvSoA<T>{(T*)e->goal, e->task, e->elapsed, (T*)e->qpos_kin, (T*)e->obj_height0, (T*)e->init_mocap,
+                   (T*)e->init_qvel, (T*)e->init_time, e->episode, e->env_index};
+}
+template <typename T>
+static EnvOutT<T> out_view(const pnp_env_out* o) {
+  if (!o) return EnvOutT<T>{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  return EnvOutT<T>{(T*)o->obs, (T*)o->achieved_goal, (T*)o->desired_goal, (T*)o->reward, (T*)o->is_success,
+                    o->terminated, o->truncated};
+}
+
+static int32_t env_check(pnp_model* model, const void* st, const pnp_env_params* p, const pnp_env_state* e,
+                         int32_t B, const char* fn) {
+  if (!model || !st || !p || !e || B < 0) { pnp_set_error("%s: bad argument", fn); return PNP_ERR_ARG; }
+  const DevModel<double>& h = model->h;
+  bool ok = p->n_tasks >= 1 && p->n_tasks <= PNP_MAX_TASKS && p->n_substeps >= 1 && p->n_calls >= 1 &&
+            p->ee_site >= 0 && p->ee_site < h.nsite && h.nmocap == 1 && model->nu >= 2 &&
+            p->arm_ctrl_n >= 0 && p->arm_ctrl_n <= model->nu;
+  for (int k = 0; k < p->n_tasks && ok; k++)
+    ok = p->obj_site[k] >= 0 && p->obj_site[k] < h.nsite && p->target_site[k] >= 0 && p->target_site[k] < h.nsite &&
+         p->obj_qadr[k] >= 0 && p->obj_qadr[k] + 7 <= h.nq;
+  for (int k = 0; k < 9 && ok; k++) ok = p->neutral_qadr[k] >= 0 && p->neutral_qadr[k] < h.nq;
+  ok = ok && p->finger_qadr[0] >= 0 && p->finger_qadr[0] < h.nq && p->finger_qadr[1] >= 0 &&
+       p->finger_qadr[1] < h.nq && p->height_qadr >= 0 && p->height_qadr + 3 <= h.nq;
+  if (!ok) { pnp_set_error("%s: env params do not fit the model", fn); return PNP_ERR_ARG; }
+  if (B == 0) return PNP_OK;
+  if (!e->goal || !e->task || !e->elapsed || !e->qpos_kin || !e->obj_height0 || !e->init_mocap || !e->init_qvel ||
+      !e->init_time || !e->episode || !e->env_index) {
+    pnp_set_error("%s: null env state buffer", fn);
+    return PNP_ERR_ARG;
+  }
+  return PNP_OK;
+}
+
+template <typename T, typename K>
+static int32_t env_prep(pnp_model* model, const pnp_state_t<T>* st, K kernel, const DevPhys<T>** dm, const char* fn) {
+  if (!st->qpos || !st->qvel || !st->ctrl || !st->mocap_pos || !st->mocap_quat || !st->qacc_warmstart || !st->time ||
+      !st->warn) {
+    pnp_set_error("%s: null state buffer", fn);
+    return PNP_ERR_ARG;
+  }
+  *dm = phys_image<T>(model);
+  if (!*dm) { pnp_set_error("%s: model has no physics image (%s)", fn, model->phys_err); return PNP_ERR_MODEL; }
+  if (hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(Env<T>)) !=
+      hipSuccess) {
+    pnp_set_error("%s: LDS %zu B not available", fn, sizeof(Env<T>));
+    return PNP_ERR_HIP;
+  }
+  return PNP_OK;
+}
+
+template <typename T>
+static int32_t launch_env_init(pnp_model* model, const pnp_state_t<T>* st, const pnp_env_params* p,
+                               const pnp_env_state* e, int32_t B, void* stream) {
+  int32_t rc = env_check(model, st, p, e, B, "pnp_env_init");
+  if (rc || B == 0) return rc;
+  const DevPhys<T>* dm;
+  auto k = env_init_kernel<T>;
+  if ((rc = env_prep(model, st, k, &dm, "pnp_env_init"))) return rc;
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), sizeof(Env<T>), (hipStream_t)stream, dm, *st, *p, env_view<T>(e), B);
+  return pnp_check_launch("env_init_kernel");
+}
+template <typename T>
+static int32_t launch_env_reset(pnp_model* model, const pnp_state_t<T>* st, const pnp_env_params* p,
+                                const pnp_env_state* e, const uint8_t* mask, const pnp_env_out* o, int32_t B,
+                                void* stream) {
+  int32_t rc = env_check(model, st, p, e, B, "pnp_env_reset");
+  if (rc || B == 0) return rc;
+  const DevPhys<T>* dm;
+  auto k = env_reset_kernel<T>;
+  if ((rc = env_prep(model, st, k, &dm, "pnp_env_reset"))) return rc;
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), sizeof(Env<T>), (hipStream_t)stream, dm, *st, *p, env_view<T>(e), mask,
+                     out_view<T>(o), B);
+  return pnp_check_launch("env_reset_kernel");
+}
+template <typename T>
+static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const pnp_env_params* p,
+                               const pnp_env_state* e, const T* action, const pnp_env_out* o, int32_t B,
+                               void* stream) {
+  int32_t rc = env_check(model, st, p, e, B, "pnp_env_step");
+  if (rc || B == 0) return rc;
+  if (!action) { pnp_set_error("pnp_env_step: null action"); return PNP_ERR_ARG; }
+  const DevPhys<T>* dm;
+  auto k = env_step_kernel<T>;
+  if ((rc = env_prep(model, st, k, &dm, "pnp_env_step"))) return rc;
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), sizeof(Env<T>), (hipStream_t)stream, dm, *st, *p, env_view<T>(e), action,
+                     out_view<T>(o), B);
+  return pnp_check_launch("env_step_kernel");
+}
+
+extern "C" int32_t pnp_env_params_size(void) { return (int32_t)sizeof(pnp_env_params); }
+
+extern "C" int32_t pnp_env_init(pnp_model* model, const pnp_state* st, const pnp_env_params* p,
+                                const pnp_env_state* e, int32_t B, void* stream) {
+  return launch_env_init<float>(model, reinterpret_cast<const pnp_state_t<float>*>(st), p, e, B, stream);
+}
+extern "C" int32_t pnp_env_init_f64(pnp_model* model, const pnp_state_f64* st, const pnp_env_params* p,
+                                    const pnp_env_state* e, int32_t B, void* stream) {
+  return launch_env_init<double>(model, reinterpret_cast<const pnp_state_t<double>*>(st), p, e, B, stream);
+}
+extern "C" int32_t pnp_env_reset(pnp_model* model, const pnp_state* st, const pnp_env_params* p,
+                                 const pnp_env_state* e, const uint8_t* mask, const pnp_env_out* o, int32_t B,
+                                 void* stream) {
+  return launch_env_reset<float>(model, reinterpret_cast<const pnp_state_t<float>*>(st), p, e, mask, o, B, stream);
+}
+extern "C" int32_t pnp_env_reset_f64(pnp_model* model, const pnp_state_f64* st, const pnp_env_params* p,
+                                     const pnp_env_state* e, const uint8_t* mask, const pnp_env_out* o, int32_t B,
+                                     void* stream) {
+  return launch_env_reset<double>(model, reinterpret_cast<const pnp_state_t<double>*>(st), p, e, mask, o, B, stream);
+}
+extern "C" int32_t pnp_env_step(pnp_model* model, const pnp_state* st, const pnp_env_params* p,
+                                const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
+                                void* stream) {
+  return launch_env_step<float>(model, reinterpret_cast<const pnp_state_t<float>*>(st), p, e, action, o, B, stream);
+}
+extern "C" int32_t pnp_env_step_f64(pnp_model* model, const pnp_state_f64* st, const pnp_env_params* p,
+                                    const pnp_env_state* e, const double* action, const pnp_env_out* o, int32_t B,
+                                    void* stream) {
+  return launch_env_step<double>(model, reinterpret_cast<const pnp_state_t<double>*>(st), p, e, action, o, B, stream);
+}

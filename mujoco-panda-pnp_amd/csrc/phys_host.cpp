@@ -16,7 +16,7 @@ int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
   memset(d, 0, sizeof(*d));
   if (s->nbody > PH_MAXB || s->njnt > PH_MAXJ || s->nv > PH_MAXV || s->nq > PH_MAXQ || s->nu > PH_MAXU ||
       s->neq > 4 || s->nmocap > 2 || s->nbody > 32 || s->nv > 64 || s->nmesh > PH_MAXMESH ||
-      s->nmeshvert > PH_MAXMESHV) {
+      s->nmeshvert > PH_MAXMESHV || s->nsite > PH_MAXS) {
     snprintf(err, errlen, "model exceeds the step kernel's compiled capacity");
     return -1;
   }
@@ -243,6 +243,13 @@ int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
   }
   for (int b = 0; b < s->nbody; b++)
     if (s->body_mocapid[b] >= 0) d->mocap_body[s->body_mocapid[b]] = b;
+  // ---- sites
+  d->nsite = s->nsite;
+  for (int i = 0; i < s->nsite; i++) {
+    d->site_bodyid[i] = s->site_bodyid[i];
+    for (int k = 0; k < 3; k++) d->site_pos[i][k] = (T)s->site_pos[3 * i + k];
+    for (int k = 0; k < 4; k++) d->site_quat[i][k] = (T)s->site_quat[4 * i + k];
+  }
   return 0;
 }
 

@@ -24,6 +24,7 @@
 #define PH_MAXT 8
 #define PH_MAXTDOF 16     // dofs per tree (arm 9)
 #define PH_MAXG 48        // collidable geoms
+#define PH_MAXS 12        // sites
 #define PH_MAXPAIR 1024
 #define PH_MAXMESHV 1400
 #define PH_MAXMESH 16
@@ -84,4 +85,8 @@ struct DevPhys {
   T eq_solref[4][2], eq_solimp[4][5], eq_data[4][11];
   // mocap defaults (mj_resetData)
   int mocap_body[4];
+  // sites (gym observation / action frames)
+  int nsite;
+  int site_bodyid[PH_MAXS];
+  T site_pos[PH_MAXS][3], site_quat[PH_MAXS][4];
 };

@@ -116,6 +116,7 @@ extern "C" int32_t pnp_model_create(const pnp_model_desc* desc, pnp_model** out)
   m->p_f32 = nullptr;
   m->p_f64 = nullptr;
   m->phys_err[0] = 0;
+  m->nu = desc->nu;
   DevPhys<float>* pf = new (std::nothrow) DevPhys<float>();
   DevPhys<double>* pd = new (std::nothrow) DevPhys<double>();
   if (pf && pd && build_phys(desc, pf, m->phys_err, sizeof(m->phys_err)) == 0 &&

@@ -66,6 +66,7 @@ struct pnp_model {
   DevPhys<float>* p_f32;    // step-kernel images (null if the model is outside its capacity)
   DevPhys<double>* p_f64;
   char phys_err[160];
+  int nu;                   // actuators (gym env ABI validation)
 };
 
 template <typename T> struct pnp_state_t {  // same layout as pnp_state / pnp_state_f64

@@ -89,6 +89,7 @@ struct Env {
   int isl_eoff[PH_MAXT + 1], isl_roff[PH_MAXT + 1];
   short isl_row[PH_MAXEFC];
   T isl_alpha[PH_MAXT];        // per-island line-search step (also the warm-start choice)
+  T qpos_pre[PH_MAXQ];         // gym env: qpos of the last forward (pre-integration)
   T red[8];
 };
 
@@ -1511,8 +1512,10 @@ __device__ void check_state(const DevPhys<T>& m, Env<T>& s) {
   }
 }
 
+// save_qpos (gym env, last sub-step): the qpos the forward ran at, i.e. where MuJoCo's
+// data.site_* / Jacobians stay after mj_step returns
 template <typename T>
-__device__ void mj_step_dev(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
+__device__ void mj_step_dev(const DevPhys<T>& m, Env<T>& s, StageClock& clk, T* save_qpos = nullptr) {
   clk.start();
   check_state(m, s);
   clk.lap(0);
@@ -1524,6 +1527,10 @@ __device__ void mj_step_dev(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
     wsync();
     reset_state(m, s);
     forward(m, s, clk);
+  }
+  if (save_qpos) {
+    if (l < m.nq) save_qpos[l] = s.qpos[l];
+    wsync();
   }
   st_euler(m, s);
   clk.lap(11);
@@ -1671,3 +1678,6 @@ extern "C" int32_t pnp_step_profile(pnp_model* model, const pnp_state* st, int32
 extern "C" int32_t pnp_step_lds_bytes(int32_t fp64) {
   return fp64 ? (int32_t)sizeof(Env<double>) : (int32_t)sizeof(Env<float>);
 }
+
+// ============================================================================ gym env (fused)
+#include "env_dev.h"

@@ -17,6 +17,8 @@ EXPORTS = [
     "pnp_model_destroy", "pnp_site_kinematics", "pnp_site_kinematics_f64", "pnp_jac_site",
     "pnp_jac_site_f64", "pnp_ik_dls", "pnp_ik_dls_f64", "pnp_step", "pnp_step_f64",
     "pnp_forward_debug", "pnp_forward_debug_f64", "pnp_step_lds_bytes", "pnp_step_profile",
+    "pnp_env_params_size", "pnp_env_init", "pnp_env_init_f64", "pnp_env_reset", "pnp_env_reset_f64",
+    "pnp_env_step", "pnp_env_step_f64",
 ]
 
 STATE_FIELDS = ("qpos", "qvel", "ctrl", "mocap_pos", "mocap_quat", "qacc_warmstart", "time", "warn")
@@ -24,6 +26,37 @@ STATE_FIELDS = ("qpos", "qvel", "ctrl", "mocap_pos", "mocap_quat", "qacc_warmsta
 
 class PnpState(C.Structure):
     _fields_ = [(f, C.c_void_p) for f in STATE_FIELDS]
+
+
+MAX_TASKS = 4
+OBS_DIM = 19
+
+
+class PnpEnvParams(C.Structure):
+    """include/pnp.h pnp_env_params."""
+    _fields_ = [("n_substeps", C.c_int32), ("n_calls", C.c_int32), ("reward_dense", C.c_int32),
+                ("max_episode_steps", C.c_int32), ("n_tasks", C.c_int32), ("ee_site", C.c_int32),
+                ("obj_site", C.c_int32 * MAX_TASKS), ("target_site", C.c_int32 * MAX_TASKS),
+                ("obj_qadr", C.c_int32 * MAX_TASKS), ("finger_qadr", C.c_int32 * 2),
+                ("neutral_qadr", C.c_int32 * 9), ("height_qadr", C.c_int32), ("arm_ctrl_n", C.c_int32),
+                ("neutral", C.c_double * 9), ("distance_threshold", C.c_double), ("high_pick_z", C.c_double),
+                ("grip_width", C.c_double), ("reach_thresh", C.c_double), ("lift_height", C.c_double),
+                ("obj_x_range", C.c_double), ("obj_y_range", C.c_double), ("pos_scale", C.c_double),
+                ("rot_scale", C.c_double), ("finger_scale", C.c_double), ("seed_lo", C.c_uint32),
+                ("seed_hi", C.c_uint32)]
+
+
+ENV_STATE_FIELDS = ("goal", "task", "elapsed", "qpos_kin", "obj_height0", "init_mocap", "init_qvel", "init_time",
+                    "episode", "env_index")
+ENV_OUT_FIELDS = ("obs", "achieved_goal", "desired_goal", "reward", "is_success", "terminated", "truncated")
+
+
+class PnpEnvState(C.Structure):
+    _fields_ = [(f, C.c_void_p) for f in ENV_STATE_FIELDS]
+
+
+class PnpEnvOut(C.Structure):
+    _fields_ = [(f, C.c_void_p) for f in ENV_OUT_FIELDS]
 
 
 # debug record layout (include/pnp.h PNP_DBG_*)
@@ -79,8 +112,25 @@ def load():
     L.pnp_step_profile.restype = I32
     L.pnp_step_lds_bytes.argtypes = [I32]
     L.pnp_step_lds_bytes.restype = I32
+    L.pnp_env_params_size.restype = I32
+    SP, EP, ES, EO = C.POINTER(PnpState), C.POINTER(PnpEnvParams), C.POINTER(PnpEnvState), C.POINTER(PnpEnvOut)
+    for name in ("pnp_env_init", "pnp_env_init_f64"):
+        f = getattr(L, name)
+        f.argtypes = [P, SP, EP, ES, I32, P]
+        f.restype = I32
+    for name in ("pnp_env_reset", "pnp_env_reset_f64"):
+        f = getattr(L, name)
+        f.argtypes = [P, SP, EP, ES, P, EO, I32, P]
+        f.restype = I32
+    for name in ("pnp_env_step", "pnp_env_step_f64"):
+        f = getattr(L, name)
+        f.argtypes = [P, SP, EP, ES, P, EO, I32, P]
+        f.restype = I32
     if L.pnp_abi_version() != ABI_VERSION:
         raise PnpError(f"libpnp ABI {L.pnp_abi_version()} != binding ABI {ABI_VERSION}")
+    if L.pnp_env_params_size() != C.sizeof(PnpEnvParams):
+        raise PnpError(f"pnp_env_params size mismatch: lib {L.pnp_env_params_size()} vs "
+                       f"binding {C.sizeof(PnpEnvParams)}")
     if L.pnp_model_desc_size() != C.sizeof(PnpModelDesc):
         raise PnpError(f"pnp_model_desc size mismatch: lib {L.pnp_model_desc_size()} vs "
                        f"binding {C.sizeof(PnpModelDesc)}")

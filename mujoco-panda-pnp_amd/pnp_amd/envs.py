@@ -1,0 +1,321 @@
+"""Batched FrankaShelfPNP gym envs on the GPU (reference panda_mujoco_gym/envs/panda_env.py,
+envs/shelf_pnp.py, __init__.py registration).
+
+``BatchedFrankaShelfPNPEnv``  B envs on one device; one fused HIP launch per gym step
+                              (pnp_env_step: _set_action -> 250 mj_step -> obs / reward / success
+                              / task sequencing / TimeLimit), vector-env auto-reset.
+``FrankaShelfPNPEnv``         the single-env gymnasium surface (reset / step / the helper methods
+                              the skills and behaviour tree call), numpy in / out, B = 1 on the
+                              device (fp64 by default, like MuJoCo's mjtNum).
+``make(env_id)``              gym.make replacement for FrankaShelfPNP{Dense,Sparse}-v0
+                              (max_episode_steps = 300).
+
+Everything runs through libpnp.so; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+
+import numpy as np
+import torch
+
+from . import _lib, rng
+from .engine import _ptr, _stream, get_engine
+
+NEUTRAL = (0.00, 0.41, 0.00, -1.85, 0.00, 2.26, 0.79, 0.00, 0.00)   # panda_env.py:64-66
+ENV_IDS = ("FrankaShelfPNPSparse-v0", "FrankaShelfPNPDense-v0")     # __init__.py:6-18
+
+
+@dataclasses.dataclass
+class EnvConfig:
+    """FrankaShelfPNPEnv constructor values (shelf_pnp.py:11-25, panda_env.py:32-46, 205-277)."""
+    reward_type: str = "dense"
+    n_substeps: int = 25
+    n_calls: int = 10
+    max_episode_steps: int = 300
+    task_sequence: tuple = ("cube1", "cube2", "cube3")
+    distance_threshold: float = 0.05
+    obj_x_range: float = 0.02
+    obj_y_range: float = 0.2
+    high_pick_z: float = 0.35
+    grip_width: float = 0.045
+    reach_thresh: float = 0.05
+    lift_height: float = 0.04
+    pos_scale: float = 0.05
+    rot_scale: float = 0.1
+    finger_scale: float = 0.2
+    seed: int = rng.SEED
+
+
+def env_params(model, cfg: EnvConfig) -> _lib.PnpEnvParams:
+    if cfg.reward_type not in ("dense", "sparse"):
+        raise ValueError(f"reward_type must be 'dense' or 'sparse', got {cfg.reward_type!r}")
+    n = len(cfg.task_sequence)
+    if not 1 <= n <= _lib.MAX_TASKS:
+        raise ValueError(f"task_sequence must have 1..{_lib.MAX_TASKS} objects")
+    q = lambda j: int(model.jnt_qposadr[model.joint_id(j)])
+    p = _lib.PnpEnvParams()
+    p.n_substeps, p.n_calls = cfg.n_substeps, cfg.n_calls
+    p.reward_dense = int(cfg.reward_type == "dense")
+    p.max_episode_steps, p.n_tasks = cfg.max_episode_steps, n
+    p.ee_site = model.site_id("ee_center_site")
+    for k, o in enumerate(cfg.task_sequence):
+        p.obj_site[k] = model.site_id(f"{o}_site")
+        p.target_site[k] = model.site_id(f"target_{o}")
+        p.obj_qadr[k] = q(f"{o}_joint")
+    p.finger_qadr[0], p.finger_qadr[1] = q("finger_joint1"), q("finger_joint2")
+    for i, j in enumerate([f"joint{i}" for i in range(1, 8)] + ["finger_joint1", "finger_joint2"]):
+        p.neutral_qadr[i] = q(j)
+        p.neutral[i] = NEUTRAL[i]
+    p.height_qadr = q("obj_joint")
+    p.arm_ctrl_n = 7
+    for f in ("distance_threshold", "high_pick_z", "grip_width", "reach_thresh", "lift_height", "obj_x_range",
+              "obj_y_range", "pos_scale", "rot_scale", "finger_scale"):
+        setattr(p, f, float(getattr(cfg, f)))
+    p.seed_lo, p.seed_hi = cfg.seed & 0xFFFFFFFF, (cfg.seed >> 32) & 0xFFFFFFFF
+    return p
+
+
+class Box:
+    """Minimal gymnasium.spaces.Box stand-in (gymnasium is not a dependency)."""
+
+    def __init__(self, low, high, shape, dtype=np.float32, seed=None):
+        self.shape, self.dtype = tuple(shape), np.dtype(dtype)
+        self.low = np.full(shape, low, dtype=self.dtype)
+        self.high = np.full(shape, high, dtype=self.dtype)
+        self._rng = np.random.default_rng(seed)
+
+    def sample(self):
+        return self._rng.uniform(self.low, self.high).astype(self.dtype)
+
+    def contains(self, x):
+        x = np.asarray(x)
+        return x.shape == self.shape and bool(np.all(x >= self.low) and np.all(x <= self.high))
+
+    def seed(self, seed=None):
+        self._rng = np.random.default_rng(seed)
+
+
+class BatchedFrankaShelfPNPEnv:
+    """``num_envs`` FrankaShelfPNPEnv instances on one GPU.
+
+    Global env indices ``env_offset + arange(num_envs)`` key the reset draws, so a batch sharded
+    over ranks (rank r: env_offset = r * num_envs) reproduces the single-device batch exactly.
+    """
+
+    def __init__(self, num_envs, reward_type="dense", device=None, dtype=torch.float32, env_offset=0,
+                 autoreset=True, config: EnvConfig | None = None, engine=None):
+        self.engine = engine or get_engine(device)
+        self.model = m = self.engine.model
+        self.cfg = dataclasses.replace(config or EnvConfig(), reward_type=reward_type)
+        self.params = env_params(m, self.cfg)
+        self.num_envs = B = int(num_envs)
+        self.dtype, self.device = dtype, self.engine.device
+        self.autoreset = autoreset
+        self.task_sequence = list(self.cfg.task_sequence)
+        self.action_space = Box(-1.0, 1.0, (7,))
+        dev, dt = self.device, dtype
+        self.state = self.engine.new_state(B, dtype)
+        z = lambda *s, d=dt: torch.zeros(*s, dtype=d, device=dev)
+        self.env = dict(goal=z(B, 3), task=z(B, d=torch.int32), elapsed=z(B, d=torch.int32),
+                        qpos_kin=z(B, m.nq), obj_height0=z(B), init_mocap=z(B, 7), init_qvel=z(B, m.nv),
+                        init_time=z(B), episode=z(B, d=torch.int32),
+                        env_index=torch.arange(env_offset, env_offset + B, dtype=torch.int32, device=dev))
+        self.out = dict(obs=z(B, _lib.OBS_DIM), achieved_goal=z(B, 3), desired_goal=z(B, 3), reward=z(B),
+                        is_success=z(B), terminated=z(B, d=torch.uint8), truncated=z(B, d=torch.uint8))
+        self._S, _, _ = self.engine._state_struct(self.state)
+        self._E = _lib.PnpEnvState(*[self.env[k].data_ptr() for k in _lib.ENV_STATE_FIELDS])
+        self._O = _lib.PnpEnvOut(*[self.out[k].data_ptr() for k in _lib.ENV_OUT_FIELDS])
+        f64 = dt == torch.float64
+        L = self.engine.lib
+        self._init = L.pnp_env_init_f64 if f64 else L.pnp_env_init
+        self._reset = L.pnp_env_reset_f64 if f64 else L.pnp_env_reset
+        self._step = L.pnp_env_step_f64 if f64 else L.pnp_env_step
+        h = self.engine._h
+        _lib.check(self._init(h, C.byref(self._S), C.byref(self.params), C.byref(self._E), B, _stream()),
+                   "pnp_env_init")
+
+    # ---------------------------------------------------------------- gym surface
+    def _obs(self):
+        return {"observation": self.out["obs"], "achieved_goal": self.out["achieved_goal"],
+                "desired_goal": self.out["desired_goal"]}
+
+    def reset(self, mask=None):
+        """Reset every env (mask None) or the envs where mask != 0; returns the obs dict (device
+        tensors, views of the output buffers: copy before the next call)."""
+        mp = None
+        if mask is not None:
+            mask = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+            if mask.shape != (self.num_envs,):
+                raise ValueError(f"mask must have shape ({self.num_envs},)")
+            mp = _ptr(mask)
+        _lib.check(self._reset(self.engine._h, C.byref(self._S), C.byref(self.params), C.byref(self._E), mp,
+                               C.byref(self._O), self.num_envs, _stream()), "pnp_env_reset")
+        self._keep = mask
+        return self._obs()
+
+    def step(self, actions):
+        """actions [B, 7] -> (obs, reward, terminated, truncated, info).  With autoreset, envs that
+        ended are reset in the same call: obs holds their first observation, and
+        info["final_observation"] / info["final_achieved_goal"] the terminal ones."""
+        a = torch.as_tensor(actions, device=self.device).to(self.dtype).contiguous()
+        if a.shape != (self.num_envs, 7):
+            raise ValueError("Action dimension mismatch")          # panda_env.py:165-166
+        _lib.check(self._step(self.engine._h, C.byref(self._S), C.byref(self.params), C.byref(self._E), _ptr(a),
+                              C.byref(self._O), self.num_envs, _stream()), "pnp_env_step")
+        reward = self.out["reward"].clone()
+        term = self.out["terminated"].bool()
+        trunc = self.out["truncated"].bool()
+        info = {"is_success": self.out["is_success"].clone()}
+        if self.autoreset:
+            done = term | trunc
+            info["final_observation"] = self.out["obs"].clone()
+            info["final_achieved_goal"] = self.out["achieved_goal"].clone()
+            info["final_desired_goal"] = self.out["desired_goal"].clone()
+            if bool(done.any()):
+                self.reset(done)
+        obs = {k: v.clone() for k, v in self._obs().items()}
+        return obs, reward, term, trunc, info
+
+    # ---------------------------------------------------------------- helpers (panda_env.py:317-352)
+    def _site_frames(self):
+        """site_xpos / site_xmat of the last forward (data.site_*)."""
+        return self.engine.site_kinematics(self.env["qpos_kin"], self.state["mocap_pos"], self.state["mocap_quat"])
+
+    def get_ee_position(self):
+        sx, _ = self._site_frames()
+        return sx[:, self.params.ee_site]
+
+    def get_ee_orientation(self):
+        """mju_mat2Quat(site_xmat[ee]) per env (wxyz)."""
+        _, sm = self._site_frames()
+        return mat2quat_batch(sm[:, self.params.ee_site])
+
+    def get_fingers_width(self):
+        q = self.state["qpos"]
+        return q[:, self.params.finger_qadr[0]] + q[:, self.params.finger_qadr[1]]
+
+    def set_mocap_pose(self, pos, quat):
+        self.state["mocap_pos"].copy_(torch.as_tensor(pos, dtype=self.dtype, device=self.device).reshape(-1, 3))
+        self.state["mocap_quat"].copy_(torch.as_tensor(quat, dtype=self.dtype, device=self.device).reshape(-1, 4))
+
+    @property
+    def current_task_index(self):
+        return self.env["task"]
+
+    @property
+    def goal(self):
+        return self.env["goal"]
+
+
+def mat2quat_batch(R):
+    """mju_mat2Quat on [N, 9] row-major matrices (torch, device): host-side helper for the facade's
+    accessors (the kernels carry their own copy)."""
+    R = R.reshape(-1, 9)
+    q = torch.zeros(R.shape[0], 4, dtype=R.dtype, device=R.device)
+    t = R[:, 0] + R[:, 4] + R[:, 8]
+    c0 = t > 0
+    c1 = ~c0 & (R[:, 0] > R[:, 4]) & (R[:, 0] > R[:, 8])
+    c2 = ~c0 & ~c1 & (R[:, 4] > R[:, 8])
+    c3 = ~c0 & ~c1 & ~c2
+    s = torch.sqrt(torch.clamp(1 + R[:, 0] + R[:, 4] + R[:, 8], min=0)) * 0.5
+    q[c0, 0] = s[c0]
+    q[c0, 1] = 0.25 * (R[c0, 7] - R[c0, 5]) / s[c0]
+    q[c0, 2] = 0.25 * (R[c0, 2] - R[c0, 6]) / s[c0]
+    q[c0, 3] = 0.25 * (R[c0, 3] - R[c0, 1]) / s[c0]
+    s = torch.sqrt(torch.clamp(1 + R[:, 0] - R[:, 4] - R[:, 8], min=0)) * 0.5
+    q[c1, 1] = s[c1]
+    q[c1, 0] = 0.25 * (R[c1, 7] - R[c1, 5]) / s[c1]
+    q[c1, 2] = 0.25 * (R[c1, 1] + R[c1, 3]) / s[c1]
+    q[c1, 3] = 0.25 * (R[c1, 2] + R[c1, 6]) / s[c1]
+    s = torch.sqrt(torch.clamp(1 - R[:, 0] + R[:, 4] - R[:, 8], min=0)) * 0.5
+    q[c2, 2] = s[c2]
+    q[c2, 0] = 0.25 * (R[c2, 2] - R[c2, 6]) / s[c2]
+    q[c2, 1] = 0.25 * (R[c2, 1] + R[c2, 3]) / s[c2]
+    q[c2, 3] = 0.25 * (R[c2, 5] + R[c2, 7]) / s[c2]
+    s = torch.sqrt(torch.clamp(1 - R[:, 0] - R[:, 4] + R[:, 8], min=0)) * 0.5
+    q[c3, 3] = s[c3]
+    q[c3, 0] = 0.25 * (R[c3, 3] - R[c3, 1]) / s[c3]
+    q[c3, 1] = 0.25 * (R[c3, 2] + R[c3, 6]) / s[c3]
+    q[c3, 2] = 0.25 * (R[c3, 5] + R[c3, 7]) / s[c3]
+    return q / torch.linalg.norm(q, dim=1, keepdim=True)
+
+
+class FrankaShelfPNPEnv:
+    """Single-env gymnasium surface of FrankaShelfPNPEnv (numpy in / out), B = 1 on the device.
+
+    reset(seed=None) -> (obs, {});  step(a) -> (obs, reward, terminated, truncated, info), with
+    TimeLimit(max_episode_steps) truncation and no auto-reset (gym semantics).  Also the helper
+    methods the skills / behaviour tree use: get_ee_position, get_ee_orientation,
+    get_fingers_width, set_mocap_pose, home_pos, task_sequence, action_space, unwrapped.
+    """
+
+    metadata = {"render_modes": [], "render_fps": 20}
+
+    def __init__(self, reward_type="dense", render_mode=None, device=None, dtype=torch.float64,
+                 max_episode_steps=300, config: EnvConfig | None = None):
+        if render_mode not in (None,):
+            raise ValueError("rendering is not part of this engine (render_mode must be None)")
+        cfg = dataclasses.replace(config or EnvConfig(), max_episode_steps=max_episode_steps)
+        self._b = BatchedFrankaShelfPNPEnv(1, reward_type, device=device, dtype=dtype, autoreset=False, config=cfg)
+        self.render_mode = None
+        self.reward_type = reward_type
+        self.task_sequence = self._b.task_sequence
+        self.action_space = Box(-1.0, 1.0, (7,))
+        self.home_pos = None
+        self.dt = self._b.model.opt_timestep * cfg.n_substeps
+
+    @property
+    def unwrapped(self):
+        return self
+
+    def _np_obs(self, obs):
+        return {k: v[0].double().cpu().numpy() for k, v in obs.items()}
+
+    def reset(self, seed=None, options=None):
+        if seed is not None:
+            self.action_space.seed(seed)
+        obs = self._np_obs(self._b.reset())
+        self.home_pos = self.get_ee_position().copy()               # panda_env.py:387-391
+        return obs, {}
+
+    def step(self, action):
+        a = np.asarray(action)
+        if a.shape != self.action_space.shape:
+            raise ValueError("Action dimension mismatch")
+        obs, r, term, trunc, info = self._b.step(torch.as_tensor(a[None], dtype=self._b.dtype))
+        return (self._np_obs(obs), np.float32(r[0].item()), bool(term[0]), bool(trunc[0]),
+                {"is_success": np.float32(info["is_success"][0].item())})
+
+    def close(self):
+        pass
+
+    # ---------------------------------------------------------------- helpers
+    def get_ee_position(self):
+        return self._b.get_ee_position()[0].double().cpu().numpy()
+
+    def get_ee_orientation(self):
+        return self._b.get_ee_orientation()[0].double().cpu().numpy()
+
+    def get_fingers_width(self):
+        return float(self._b.get_fingers_width()[0])
+
+    def set_mocap_pose(self, pos, quat):
+        self._b.set_mocap_pose(np.asarray(pos)[None], np.asarray(quat)[None])
+
+    @property
+    def current_task_index(self):
+        return int(self._b.env["task"][0])
+
+    @property
+    def goal(self):
+        return self._b.env["goal"][0].double().cpu().numpy()
+
+
+def make(env_id, **kwargs):
+    """gym.make("FrankaShelfPNP{Dense,Sparse}-v0") replacement (__init__.py:6-18)."""
+    if env_id not in ENV_IDS:
+        raise KeyError(f"unknown env id {env_id!r}; registered: {ENV_IDS}")
+    reward_type = "dense" if env_id == "FrankaShelfPNPDense-v0" else "sparse"
+    return FrankaShelfPNPEnv(reward_type=reward_type, **kwargs)

@@ -257,6 +257,25 @@ void orc_jac_site(const pnp_model_desc* m, const double* xanchor, const double* 
   }
 }
 
+/* mj_jacSite rotational part (jacr, 3 x nv row-major): hinge -> xaxis, slide -> 0, free joint ->
+ * 0 for the translational dofs and the body-frame axes (columns of xmat) for the rotational ones */
+void orc_jac_site_rot(const pnp_model_desc* m, const double* xaxis, const double* xmat, int site, double* jacr) {
+  int nv = m->nv;
+  memset(jacr, 0, 3 * nv * sizeof(double));
+  for (int b = m->site_bodyid[site]; b > 0; b = m->body_parentid[b]) {
+    for (int j = m->body_jntadr[b]; j >= 0 && j < m->body_jntadr[b] + m->body_jntnum[b]; j++) {
+      int d = m->jnt_dofadr[j], t = m->jnt_type[j];
+      if (t == 3) {
+        for (int k = 0; k < 3; k++) jacr[k * nv + d] = xaxis[3 * j + k];
+      } else if (t == 0) {
+        const double* R = xmat + 9 * b;
+        for (int k = 0; k < 3; k++)
+          for (int r = 0; r < 3; r++) jacr[r * nv + d + 3 + k] = R[3 * r + k];
+      }
+    }
+  }
+}
+
 /* ------------------------------------------------------------------ DLS IK */
 typedef struct {
   double* xpos; double* xquat; double* xmat; double* xanchor; double* xaxis;
@@ -436,6 +455,24 @@ int orc_jac_site_batch(const pnp_model_desc* m, int site, const double* qpos, do
     orc_kinematics(m, qpos + (size_t)b * m->nq, NULL, NULL, s.xpos, s.xquat, s.xmat, s.xanchor,
                    s.xaxis, s.site_xpos, NULL);
     orc_jac_site(m, s.xanchor, s.xaxis, s.xmat, s.site_xpos, site, jacp + (size_t)b * 3 * m->nv);
+  }
+  scratch_free(&s);
+  return 0;
+}
+
+/* Batched site frames + full site Jacobian (jacp, jacr: 3 x nv per env) at qpos (mocap pose
+ * from mocap_pos / mocap_quat when given). */
+int orc_site_jac2_batch(const pnp_model_desc* m, int site, const double* qpos, const double* mocap_pos,
+                        const double* mocap_quat, double* site_xpos, double* site_xmat, double* jacp,
+                        double* jacr, int B) {
+  orc_scratch s;
+  if (scratch_alloc(m, &s)) return -1;
+  for (int b = 0; b < B; b++) {
+    orc_kinematics(m, qpos + (size_t)b * m->nq, mocap_pos ? mocap_pos + (size_t)b * 3 * m->nmocap : NULL,
+                   mocap_quat ? mocap_quat + (size_t)b * 4 * m->nmocap : NULL, s.xpos, s.xquat, s.xmat,
+                   s.xanchor, s.xaxis, site_xpos + (size_t)b * 3 * m->nsite, site_xmat + (size_t)b * 9 * m->nsite);
+    orc_jac_site(m, s.xanchor, s.xaxis, s.xmat, site_xpos + (size_t)b * 3 * m->nsite, site, jacp + (size_t)b * 3 * m->nv);
+    orc_jac_site_rot(m, s.xaxis, s.xmat, site, jacr + (size_t)b * 3 * m->nv);
   }
   scratch_free(&s);
   return 0;

@@ -41,6 +41,8 @@ def lib():
         L.orc_site_kinematics_batch.restype = C.c_int
         L.orc_jac_site_batch.argtypes = [P, C.c_int, P, P, C.c_int]
         L.orc_jac_site_batch.restype = C.c_int
+        L.orc_site_jac2_batch.argtypes = [P, C.c_int, P, P, P, P, P, P, P, C.c_int]
+        L.orc_site_jac2_batch.restype = C.c_int
         L.orc_mat2quat.argtypes = [P, P]
         L.orc_mat2quat.restype = None
         _lib = L
@@ -101,6 +103,23 @@ def jac_site(qpos, site="ee_center_site", model=None):
     if rc:
         raise RuntimeError("orc_jac_site_batch failed")
     return jac
+
+
+def site_jac2(qpos, site, mocap_pos=None, mocap_quat=None, model=None):
+    """Site frames of every site and the full mj_jacSite (jacp, jacr) of `site` at qpos:
+    returns site_xpos [B,nsite,3], site_xmat [B,nsite,9], jacp [B,3,nv], jacr [B,3,nv]."""
+    m = model or load_model()
+    qpos = np.ascontiguousarray(qpos, np.float64).reshape(-1, m.nq)
+    B = qpos.shape[0]
+    mp = None if mocap_pos is None else np.ascontiguousarray(mocap_pos, np.float64).reshape(B, -1)
+    mq = None if mocap_quat is None else np.ascontiguousarray(mocap_quat, np.float64).reshape(B, -1)
+    sx, sm = np.zeros((B, m.nsite, 3)), np.zeros((B, m.nsite, 9))
+    jp, jr = np.zeros((B, 3, m.nv)), np.zeros((B, 3, m.nv))
+    sid = site if isinstance(site, (int, np.integer)) else m.site_id(site)
+    rc = lib().orc_site_jac2_batch(_desc_ptr(m), int(sid), _p(qpos), _p(mp), _p(mq), _p(sx), _p(sm), _p(jp), _p(jr), B)
+    if rc:
+        raise RuntimeError("orc_site_jac2_batch failed")
+    return sx, sm, jp, jr
 
 
 def mat2quat(mat):

@@ -1,0 +1,233 @@
+"""GPU parity of the fused gym env (libpnp.so pnp_env_init / pnp_env_reset / pnp_env_step through
+the C ABI, via pnp_amd.envs) against the CPU env oracle (oracle/env_oracle.py: the reference's
+FrankaEnv logic over the fp64 physics oracle).
+
+The scene is chaotic over a full gym step: the fp64 oracle itself turns a 1e-12 velocity
+perturbation into 1e-4 .. 4e-3 within 200-250 sub-steps (tests/test_env_oracle.py pins this), so
+no two implementations — MuJoCo included — agree to 1e-8 over 250 sub-steps.  The env logic
+(_set_action, _get_obs, reward, success, task sequencing, TimeLimit, reset draws) is therefore
+checked exactly on a short-physics configuration (n_calls = 2 x n_substeps = 2 sub-steps per gym
+step, inside the divergence horizon), and the full configuration with bounds:
+  * short physics, fp64: observation / state within 1e-9, rewards within 1e-9, flags identical;
+  * short physics, fp32: observation within 1e-4, rewards within 1e-4, flags identical;
+  * full 250 sub-steps, one gym step from the same state: observation within 5e-3, flags identical.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle.env_oracle import EnvConfig as OCfg, EnvOracle
+
+pytestmark = pytest.mark.gpu
+
+B = 4
+
+
+def _env(dtype, B=B, **cfg):
+    from pnp_amd.envs import BatchedFrankaShelfPNPEnv, EnvConfig
+    return BatchedFrankaShelfPNPEnv(B, dtype=dtype, autoreset=False, config=EnvConfig(**cfg))
+
+
+def _actions(n, seed):
+    return np.random.default_rng(seed).uniform(-1, 1, size=(n, 7)).astype(np.float32).astype(np.float64)
+
+
+SHORT = dict(n_substeps=2, n_calls=2)
+
+
+@pytest.fixture(scope="module")
+def pair64(model):
+    return _env(torch.float64), EnvOracle(B, model=model)
+
+
+@pytest.fixture(scope="module")
+def short64(model):
+    return _env(torch.float64, **SHORT), EnvOracle(B, cfg=OCfg(**SHORT), model=model)
+
+
+def test_init_matches_oracle(pair64):
+    g, o = pair64
+    np.testing.assert_allclose(g.state["qpos"].cpu().numpy(), o.st["qpos"], atol=1e-9)
+    np.testing.assert_allclose(g.env["qpos_kin"].cpu().numpy(), o.qpos_kin, atol=1e-9)
+    np.testing.assert_allclose(g.env["obj_height0"].cpu().numpy(), o.obj_height0, atol=1e-9)
+    np.testing.assert_allclose(g.env["init_qvel"].cpu().numpy(), o.init_qvel, atol=1e-8)
+    np.testing.assert_allclose(g.env["init_mocap"].cpu().numpy(), o.init_mocap, atol=1e-12)
+    np.testing.assert_allclose(g.env["goal"].cpu().numpy(), o.goal, atol=1e-12)
+    assert np.allclose(g.env["init_time"].cpu().numpy(), 0.5)
+    # the dummy object rests on the floor: initial_object_height ~ its radius (App. B quirk 4)
+    assert np.all(np.abs(o.obj_height0 - 0.001) < 5e-4)
+
+
+def test_reset_matches_oracle_f64(pair64):
+    g, o = pair64
+    obs = g.reset()
+    ref = o.reset()
+    for b in range(B):
+        np.testing.assert_allclose(obs["observation"][b].cpu().numpy(), ref[b]["observation"], atol=1e-9)
+        np.testing.assert_allclose(obs["desired_goal"][b].cpu().numpy(), ref[b]["desired_goal"], atol=1e-12)
+    np.testing.assert_allclose(g.state["qpos"].cpu().numpy(), o.st["qpos"], atol=1e-12)   # same Philox draws
+
+
+def _compare_steps(g, o, nsteps, tol, seed0=10):
+    for k in range(nsteps):
+        a = _actions(B, seed0 + k)
+        obs, r, term, trunc, info = g.step(torch.as_tensor(a, dtype=g.dtype))
+        res = o.step(a)
+        for b in range(B):
+            np.testing.assert_allclose(obs["observation"][b].double().cpu().numpy(), res[b]["obs"]["observation"],
+                                       atol=tol)
+            np.testing.assert_allclose(obs["desired_goal"][b].double().cpu().numpy(), res[b]["obs"]["desired_goal"],
+                                       atol=tol)
+            np.testing.assert_allclose(float(r[b]), res[b]["reward"], atol=tol)
+            assert float(info["is_success"][b]) == res[b]["is_success"]
+            assert bool(term[b]) == res[b]["terminated"] and bool(trunc[b]) == res[b]["truncated"]
+        np.testing.assert_allclose(g.state["ctrl"].double().cpu().numpy(), o.st["ctrl"], atol=tol)
+        np.testing.assert_allclose(g.state["mocap_pos"].double().cpu().numpy(), o.st["mocap_pos"], atol=tol)
+        np.testing.assert_allclose(g.state["mocap_quat"].double().cpu().numpy(), o.st["mocap_quat"], atol=tol)
+
+
+def test_env_logic_short_physics_f64(short64):
+    g, o = short64
+    g.reset()
+    o.reset()
+    _compare_steps(g, o, 5, 1e-9)
+    np.testing.assert_allclose(g.state["qpos"].cpu().numpy(), o.st["qpos"], atol=1e-9)
+    np.testing.assert_allclose(g.env["qpos_kin"].cpu().numpy(), o.qpos_kin, atol=1e-9)
+    assert np.array_equal(g.env["task"].cpu().numpy(), o.task)
+    assert np.array_equal(g.env["elapsed"].cpu().numpy(), o.elapsed)
+
+
+def _sync_oracle(g, o):
+    for k in ("qpos", "qvel", "ctrl", "mocap_pos", "mocap_quat", "qacc_warmstart", "time"):
+        o.st[k][:] = g.state[k].double().cpu().numpy()
+    o.qpos_kin[:] = g.env["qpos_kin"].double().cpu().numpy()
+    o.goal[:] = g.env["goal"].double().cpu().numpy()
+
+
+def test_env_logic_short_physics_f32(model):
+    g = _env(torch.float32, **SHORT)
+    o = EnvOracle(B, cfg=OCfg(**SHORT), model=model)
+    g.reset()
+    o.reset()
+    _sync_oracle(g, o)
+    _compare_steps(g, o, 3, 1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_full_gym_step_bounded(model, dtype):
+    g = _env(dtype)
+    o = EnvOracle(B, model=model)
+    g.reset()
+    o.reset()
+    _sync_oracle(g, o)
+    a = _actions(B, 3)
+    a[:, 6] = 1.0
+    obs, r, term, trunc, info = g.step(torch.as_tensor(a, dtype=dtype))
+    res = o.step(a)
+    for b in range(B):
+        np.testing.assert_allclose(obs["observation"][b].double().cpu().numpy(), res[b]["obs"]["observation"], atol=5e-3)
+        np.testing.assert_allclose(float(r[b]), res[b]["reward"], atol=5e-3)
+        assert bool(term[b]) == res[b]["terminated"]
+
+
+def _place_cube(g, o, k):
+    """Put task object k exactly on its target site (placed = True at the next step's obs)."""
+    m = o.m
+    a = o.obj_qadr[k]
+    tgt = o.goal[0].copy()
+    for st_q in (o.st["qpos"],):
+        st_q[:, a:a + 3] = tgt
+        st_q[:, a + 3:a + 7] = [1, 0, 0, 0]
+    g.state["qpos"].copy_(torch.as_tensor(o.st["qpos"], dtype=g.dtype))
+    return m
+
+
+def test_task_sequencing_and_termination(model):
+    g = _env(torch.float64, B=2, **SHORT)
+    o = EnvOracle(2, cfg=OCfg(**SHORT), model=model)
+    g.reset()
+    o.reset()
+    seen = []
+    for k in range(3):
+        g.env["task"].fill_(k)
+        o.task[:] = k
+        sx, _, _, _ = o._frames(0, o.ee)
+        o.goal[:] = sx[o.target_site[k]]
+        g.env["goal"].copy_(torch.as_tensor(o.goal, dtype=g.dtype))
+        _place_cube(g, o, k)
+        a = np.zeros((2, 7))
+        obs, r, term, trunc, info = g.step(torch.as_tensor(a, dtype=torch.float64))
+        res = o.step(a)
+        seen.append((float(info["is_success"][0]), bool(term[0]), int(g.env["task"][0])))
+        for b in range(2):
+            assert float(info["is_success"][b]) == res[b]["is_success"]
+            assert bool(term[b]) == res[b]["terminated"]
+            np.testing.assert_allclose(float(r[b]), res[b]["reward"], atol=1e-8)
+            np.testing.assert_allclose(g.env["goal"][b].cpu().numpy(), o.goal[b], atol=1e-12)
+            assert int(g.env["task"][b]) == int(o.task[b])
+    # a cube dropped on its target is placed: success, task index advances, last one terminates
+    assert [s[0] for s in seen] == [1.0, 1.0, 1.0]
+    assert [s[1] for s in seen] == [False, False, True]
+    assert [s[2] for s in seen] == [1, 2, 3]
+
+
+def test_truncation_autoreset_and_mask(model):
+    from pnp_amd.envs import BatchedFrankaShelfPNPEnv, EnvConfig
+    g = BatchedFrankaShelfPNPEnv(3, dtype=torch.float32, autoreset=True, config=EnvConfig(max_episode_steps=2))
+    first = {k: v.clone() for k, v in g.reset().items()}
+    a = torch.zeros(3, 7)
+    _, _, _, trunc, _ = g.step(a)
+    assert not trunc.any()
+    obs, _, _, trunc, info = g.step(a)
+    assert trunc.all()
+    assert "final_observation" in info
+    assert torch.equal(g.env["elapsed"], torch.zeros(3, dtype=torch.int32, device=g.device))
+    assert torch.equal(g.env["episode"].cpu(), torch.full((3,), 2, dtype=torch.int32))
+    # the new episode's objects are re-drawn around the objects' current positions
+    assert not torch.equal(obs["observation"], first["observation"])
+    # masked reset touches only the selected env
+    before = g.state["qpos"].clone()
+    g.reset(torch.tensor([0, 1, 0], dtype=torch.uint8))
+    assert torch.equal(g.state["qpos"][0], before[0]) and torch.equal(g.state["qpos"][2], before[2])
+    assert not torch.equal(g.state["qpos"][1], before[1])
+
+
+def test_shard_invariant_resets():
+    """Envs [2, 4) of a 4-env batch == a 2-env batch with env_offset 2 (Philox by global index)."""
+    from pnp_amd.envs import BatchedFrankaShelfPNPEnv
+    full = BatchedFrankaShelfPNPEnv(4, dtype=torch.float32, autoreset=False)
+    half = BatchedFrankaShelfPNPEnv(2, dtype=torch.float32, autoreset=False, env_offset=2)
+    a = full.reset()["observation"].clone()
+    b = half.reset()["observation"].clone()
+    assert torch.equal(a[2:], b)
+    act = torch.as_tensor(_actions(4, 5), dtype=torch.float32, device=full.device)
+    oa = full.step(act)[0]["observation"]
+    ob = half.step(act[2:])[0]["observation"]
+    assert torch.equal(oa[2:], ob)
+
+
+def test_single_env_facade_envs_test():
+    """reference test/envs_test.py equivalent: reset + 20 random steps per id, obs shapes / bounds,
+    reset on done, double close; plus reward_test.py:118-126 (static steps -> total < 0)."""
+    from pnp_amd.envs import ENV_IDS, make
+    for env_id in ENV_IDS:
+        env = make(env_id)
+        obs, info = env.reset(seed=0)
+        assert obs["observation"].shape == (19,) and obs["achieved_goal"].shape == (3,)
+        assert np.allclose(env.home_pos, [1.23843967, 0.0, 0.49740014], atol=1e-6)
+        total = 0.0
+        for _ in range(20):
+            obs, r, term, trunc, info = env.step(env.action_space.sample())
+            assert np.all(np.isfinite(obs["observation"]))
+            assert isinstance(r, np.float32) and "is_success" in info
+            if term or trunc:
+                env.reset()
+        env.reset()
+        for _ in range(5):
+            _, r, _, _, _ = env.step(np.zeros(7, np.float32))
+            total += float(r)
+        assert total < 0
+        with pytest.raises(ValueError):
+            env.step(np.zeros(6))
+        env.close()
+        env.close()
