@@ -12,7 +12,8 @@ Inputs: the reference's reset distribution (Philox, seed 20250808, counter = glo
 rank r owns envs [r*B, (r+1)*B)), settled by 250 untimed sub-steps like _env_setup.
 
 --workload ik = configs[1] "C2": one batched JacobianIKController.solve over 4096 envs per step.
-The step workload also times C2 briefly and reports it under "ik".
+The step workload also times C2 briefly ("ik") and the fused gym step of C5's env side ("gym":
+FrankaEnv.step = set_action + 250 sub-steps + obs / reward, one launch).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload step|ik]
     torchrun --nproc-per-node N bench.py --gpus N ...    (one process per GPU)
@@ -175,6 +176,8 @@ def run_step(args, engine, model, rank, world, dist):
         "state_ok": {"max_warn": warn, "finite": finite},
         "host_cores": len(os.sched_getaffinity(0)),
     }
+    if not args.no_gym:
+        rec["gym"] = run_gym(engine, B, rank, world, dist)
     if not args.no_ik:
         ik = run_ik(args, engine, model, rank, world, dist, steps=50, warmup=5, baseline=False)
         rec["ik"] = {k: ik[k] for k in ("value", "unit", "ms_per_step")}
@@ -182,6 +185,22 @@ def run_step(args, engine, model, rank, world, dist):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = step_cpu_baseline(st, ctrl, args.cpu_budget)
     return rec
+
+
+# ----------------------------------------------------------------------------- fused gym step
+def run_gym(engine, B, rank, world, dist, steps=3, warmup=1):
+    """C5's env side: FrankaShelfPNPDense env.step over B envs per GPU as ONE fused launch
+    (set_action + 250 sub-steps + obs / reward / success / sequencing), random actions."""
+    from pnp_amd.envs import BatchedFrankaShelfPNPEnv
+    env = BatchedFrankaShelfPNPEnv(B, engine=engine, env_offset=rank * B, autoreset=False)
+    env.reset()
+    acts = torch.as_tensor(np.random.default_rng(7 + rank).uniform(-1, 1, size=(4, B, 7)), dtype=torch.float32,
+                           device=engine.device)
+    elapsed, kern_ms = _timed(lambda i: env.step(acts[i % 4]), steps, warmup, dist)
+    sub = env.cfg.n_substeps * env.cfg.n_calls
+    return {"gym_steps_per_s": B * world * steps / elapsed, "env_steps_per_s": B * world * steps * sub / elapsed,
+            "ms_per_gym_step": elapsed / steps * 1e3, "kernel_avg_ms": kern_ms, "sub_steps_per_gym_step": sub,
+            "kernel": "env_step_kernel<float>", "workload": f"{B} FrankaShelfPNPDense envs per GPU, random actions"}
 
 
 # ----------------------------------------------------------------------------- C2 IK
@@ -267,6 +286,7 @@ def main():
     ap.add_argument("--regime", default="waypoint", choices=sorted(workloads.IK_REGIMES))
     ap.add_argument("--params", default="default", choices=sorted(workloads.IK_PARAMS))
     ap.add_argument("--no-ik", action="store_true", help="step workload: skip the secondary C2 timing")
+    ap.add_argument("--no-gym", action="store_true", help="step workload: skip the secondary fused gym-step timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()

@@ -303,16 +303,19 @@ __global__ void __launch_bounds__(NT) env_step_kernel(const DevPhys<T>* __restri
   site_frame(m, s, prm.ee_site, ee_p, ee_R);
   g_mat2quat(ee_R, ee_q);
   if (l == 0) {
-    T a[7];
-    for (int k = 0; k < 7; k++) a[k] = fmin(fmax(action[(size_t)b * 7 + k], T(-1)), T(1));
-    const T width = s.qpos[prm.finger_qadr[0]] + s.qpos[prm.finger_qadr[1]] + a[6] * (T)prm.finger_scale;
+    // the action space is float32: np.clip(action, low, high) and the scalings 0.05 * a, 0.2 * a,
+    // clip(a, -1, 1) * 0.1 happen in float32 in the reference (NumPy scalar promotion), before
+    // meeting the float64 state; __fmul_rn keeps the product out of any FMA contraction
+    float a[7];
+    for (int k = 0; k < 7; k++) a[k] = fminf(fmaxf((float)action[(size_t)b * 7 + k], -1.0f), 1.0f);
+    const T width = s.qpos[prm.finger_qadr[0]] + s.qpos[prm.finger_qadr[1]] + (T)__fmul_rn(a[6], (float)prm.finger_scale);
     const T half = fmin(fmax(width / T(2), m.act_ctrlrange[m.nu - 1][0]), m.act_ctrlrange[m.nu - 1][1]);
     s.ctrl[m.nu - 2] = half;
     s.ctrl[m.nu - 1] = half;
     T de[3], dq[4], tq[4];
     for (int t = 0; t < 3; t++) {
-      s.mocap_pos[t] = ee_p[t] + (T)prm.pos_scale * a[t];
-      de[t] = fmin(fmax(a[3 + t], T(-1)), T(1)) * (T)prm.rot_scale;
+      s.mocap_pos[t] = ee_p[t] + (T)__fmul_rn((float)prm.pos_scale, a[t]);
+      de[t] = (T)__fmul_rn(fminf(fmaxf(a[3 + t], -1.0f), 1.0f), (float)prm.rot_scale);
     }
     s.mocap_pos[2] = fmax(T(0), s.mocap_pos[2]);
     g_euler2quat(de, dq);
@@ -383,7 +386,7 @@ __global__ void __launch_bounds__(NT) env_step_kernel(const DevPhys<T>* __restri
     es.task[b] = ntask;
     es.elapsed[b] = elapsed;
     for (int t = 0; t < 3; t++) es.goal[(size_t)b * 3 + t] = goal[t];
-    if (out.reward) out.reward[b] = reward;
+    if (out.reward) out.reward[b] = (T)(float)reward;   // compute_reward returns np.float32
     if (out.success) out.success[b] = placed ? T(1) : T(0);
     if (out.terminated) out.terminated[b] = terminated;
     if (out.truncated) out.truncated[b] = truncated;

@@ -1202,6 +1202,10 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s) {
   wsync();
   T cost = eval_cost(m, s, s.x, true);   // island l's cost on lane l
   bool done = l >= s.nisland;
+  int unchanged = 0;                      // consecutive steps that kept the island's active set
+  // gradient floor of a converged island (scaled like the oracle: 1 / (meaninertia * nv))
+  const T gscale = T(1) / (m.meaninertia * T(m.nv > 1 ? m.nv : 1));
+  const T gtol = T(100) * PM<T>::eps();
   int it = 0;
   const int nent = s.isl_eoff[s.nisland];
   for (; it < m.iterations; it++) {
@@ -1218,6 +1222,15 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s) {
         if (k >= 0) g += EJ(r, k) * s.efc_D[r] * s.efc_jar[r];
       }
       s.grad[l] = g;
+    }
+    {
+      // an island whose last step kept its active set is at that quadratic's minimiser up to
+      // the rounding of one Cholesky solve (cond(H) eps); it is done once its gradient is at the
+      // floor, otherwise it takes one more (refining) Newton step
+      const T g2 = isl_wsum(l < m.nv ? s.grad[l] * s.grad[l] : T(0), l < m.nv ? s.tree_island[m.dof_tree[l]] : -1,
+                            s.nisland);
+      if (!done && unchanged >= 1 && PM<T>::sqrt_(g2) * gscale < gtol) done = true;
+      if (!__ballot(!done)) break;
     }
     // Hessian island blocks (lower triangle entries, lane per entry): M + sum_active D J J^T
     for (int e = l; e < nent; e += NT) {
@@ -1257,9 +1270,9 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s) {
     for (int r = l; r < s.nefc; r += NT) s.efc_Jp[r] = (T)s.efc_act[r];
     wsync();
     const T nc = eval_cost(m, s, s.x, true);
-    // island converged: its step did not change its active set (then its piecewise quadratic
-    // was a single quadratic along the step and x is that quadratic's exact minimiser), or its
-    // cost stopped decreasing
+    // island converged: two consecutive steps kept its active set (then its piecewise quadratic
+    // is a single quadratic there and x its minimiser, refined once), or its cost stopped
+    // decreasing
     int ci[RPL];
 #pragma unroll
     for (int k = 0; k < RPL; k++) {
@@ -1276,7 +1289,8 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s) {
     }
     if (!done) {
       const T impr = cost - nc;
-      if (!changed || !(impr > 0) || !(s.isl_alpha[l] > T(0))) done = true;
+      unchanged = changed ? 0 : unchanged + 1;
+      if (unchanged >= 2 || !(impr > 0) || !(s.isl_alpha[l] > T(0))) done = true;
       cost = nc;
     }
     if (!__ballot(!done)) { it++; break; }

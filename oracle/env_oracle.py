@@ -203,16 +203,20 @@ class EnvOracle:
     # ---------------------------------------------------------------- step (panda_env.py:163-277)
     def step(self, actions):
         cfg, st = self.cfg, self.st
-        actions = np.clip(np.asarray(actions, np.float64), -1.0, 1.0)
+        # float32 action space: the clip and the action scalings run in float32 (NumPy promotes
+        # float32 array * python float to float32), then meet the float64 state
+        f32 = np.float32
+        actions = np.clip(np.asarray(actions, f32), f32(-1.0), f32(1.0))
         for b in range(self.B):                                    # _set_action (:250-277)
             a = actions[b]
             sx, sm, _, _ = self._frames(b, self.ee)
-            width = st["qpos"][b, self.finger_qadr[0]] + st["qpos"][b, self.finger_qadr[1]] + a[6] * cfg.finger_scale
+            width = (st["qpos"][b, self.finger_qadr[0]] + st["qpos"][b, self.finger_qadr[1]]
+                     + np.float64(a[6] * f32(cfg.finger_scale)))
             lo, hi = self.m.actuator_ctrlrange[-1]
             st["ctrl"][b, -2:] = np.clip(width / 2, lo, hi)
-            pos = sx[self.ee] + cfg.pos_scale * a[:3]
+            pos = sx[self.ee] + (f32(cfg.pos_scale) * a[:3]).astype(np.float64)
             pos[2] = max(0.0, pos[2])
-            dq = euler2quat(np.clip(a[3:6], -1.0, 1.0) * cfg.rot_scale)
+            dq = euler2quat((np.clip(a[3:6], f32(-1.0), f32(1.0)) * f32(cfg.rot_scale)).astype(np.float64))
             st["mocap_pos"][b] = pos
             st["mocap_quat"][b] = quat_mul(dq, O.mat2quat(sm[self.ee]))
         self._advance(np.arange(self.B))
@@ -240,6 +244,7 @@ class EnvOracle:
                 if placed:
                     reward += 10.0
                 reward += 0.5 * (task / len(self.obj_site))
+            reward = float(np.float32(reward))                     # compute_reward returns np.float32
             terminated = False
             if placed:                                             # task sequencing (:183-193)
                 self.task[b] = task + 1

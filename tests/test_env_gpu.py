@@ -231,3 +231,51 @@ def test_single_env_facade_envs_test():
             env.step(np.zeros(6))
         env.close()
         env.close()
+
+
+class _GpuAdapter:
+    """pnp_amd.envs B = 1 env behind the golden replay interface (tests/test_env_oracle.py)."""
+
+    def __init__(self, env_index, cfg, dtype):
+        from pnp_amd.envs import BatchedFrankaShelfPNPEnv, EnvConfig
+        rt = cfg.pop("reward_type")
+        self.g = BatchedFrankaShelfPNPEnv(1, reward_type=rt, dtype=dtype, env_offset=env_index, autoreset=False,
+                                          config=EnvConfig(**cfg))
+
+    def _np(self, t):
+        return t.double().cpu().numpy()
+
+    def init_values(self):
+        return float(self.g.env["obj_height0"][0]), self._np(self.g.env["init_mocap"][0])
+
+    def reset(self):
+        obs = self.g.reset()
+        return self._np(obs["observation"][0]), self._np(self.g.env["goal"][0])
+
+    def place(self):
+        g = self.g
+        k = min(int(g.env["task"][0]), len(g.task_sequence) - 1)
+        a = g.params.obj_qadr[k]
+        q = g.state["qpos"]
+        q[0, a:a + 3] = g.env["goal"][0]
+        q[0, a + 3:a + 7] = torch.tensor([1.0, 0, 0, 0], dtype=q.dtype)
+        g.env["qpos_kin"][0] = q[0]
+
+    def step(self, a):
+        g = self.g
+        obs, r, term, trunc, info = g.step(torch.as_tensor(np.asarray(a)[None], dtype=g.dtype))
+        return dict(obs=self._np(obs["observation"][0]), reward=float(r[0]), success=float(info["is_success"][0]),
+                    terminated=bool(term[0]), ctrl=self._np(g.state["ctrl"][0]), mocap_pos=self._np(g.state["mocap_pos"][0]),
+                    mocap_quat=self._np(g.state["mocap_quat"][0]), task=int(g.env["task"][0]),
+                    goal=self._np(g.env["goal"][0]))
+
+
+def _close(a, b, tol, what):
+    np.testing.assert_allclose(np.asarray(a, np.float64), np.asarray(b, np.float64), atol=tol, rtol=0, err_msg=what)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-9), (torch.float32, 2e-4)])
+def test_gpu_env_matches_reference_env_golden(dtype, tol):
+    """The fused env kernel against the reference's own FrankaEnv code (golden fixture)."""
+    from test_env_oracle import replay_golden
+    replay_golden(lambda idx, cfg: _GpuAdapter(idx, dict(cfg), dtype), _close, tol)

@@ -88,3 +88,80 @@ def test_scene_is_chaotic_over_a_gym_step(model):
     O.step(Bs, nsub=250, nthreads=8, model=model)
     growth = np.abs(A["qvel"] - Bs["qvel"]).max() / 1e-12
     assert growth > 1e5
+
+
+# ---------------------------------------------------------------- reference golden vectors
+import os  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "env_golden.npz")
+
+
+def replay_golden(make_env, check, tol):
+    """Replays tests/golden/env_golden.npz (the reference's own FrankaEnv code, stub-imported,
+    see make_env_golden.py) through an env adapter: make_env(env_index, cfg) -> adapter with
+    .init_values(), .reset() -> (obs, goal), .place(), .step(action) -> dict."""
+    G = np.load(GOLDEN)
+    n_sub = int(G["n_substeps"])
+    for i in range(len(G["env_index"])):
+        cfg = dict(reward_type="dense" if G["reward_dense"][i] else "sparse", n_substeps=n_sub, n_calls=10)
+        env = make_env(int(G["env_index"][i]), cfg)
+        h0, mocap = env.init_values()
+        check(h0, G["obj_height0"][i], tol, "obj_height0")
+        check(mocap, G["init_mocap"][i], tol, "init_mocap")
+        obs, goal = env.reset()
+        check(obs, G["reset_obs"][i], tol, "reset obs")
+        check(goal, G["reset_goal"][i], tol, "reset goal")
+        for k in range(G["actions"].shape[1]):
+            if G["place"][i][k]:
+                env.place()
+            r = env.step(G["actions"][i][k])
+            tag = f"episode {i} step {k}"
+            check(r["obs"], G["obs"][i][k], tol, tag + " obs")
+            check(r["reward"], G["reward"][i][k], tol, tag + " reward")
+            assert r["success"] == G["success"][i][k], tag
+            assert r["terminated"] == bool(G["terminated"][i][k]), tag
+            check(r["ctrl"], G["ctrl"][i][k], tol, tag + " ctrl")
+            check(r["mocap_pos"], G["mocap_pos"][i][k], tol, tag + " mocap_pos")
+            check(r["mocap_quat"], G["mocap_quat"][i][k], tol, tag + " mocap_quat")
+            assert r["task"] == int(G["task"][i][k]), tag
+            check(r["goal"], G["goal"][i][k], tol, tag + " goal")
+
+
+def _close(a, b, tol, what):
+    np.testing.assert_allclose(np.asarray(a, np.float64), np.asarray(b, np.float64), atol=tol, rtol=0, err_msg=what)
+
+
+class _OracleAdapter:
+    def __init__(self, env_index, cfg, model):
+        self.e = EnvOracle(1, cfg=EnvConfig(**cfg), env_index=[env_index], model=model)
+
+    def init_values(self):
+        return self.e.obj_height0[0], self.e.init_mocap[0]
+
+    def reset(self):
+        r = self.e.reset()[0]
+        return r["observation"], self.e.goal[0]
+
+    def place(self):
+        e = self.e
+        a = e.obj_qadr[min(int(e.task[0]), len(e.obj_qadr) - 1)]
+        e.st["qpos"][0, a:a + 7] = np.concatenate([e.goal[0], [1, 0, 0, 0]])
+        e.qpos_kin[0] = e.st["qpos"][0]
+
+    def step(self, a):
+        e = self.e
+        r = e.step(np.asarray(a)[None])[0]
+        return dict(obs=r["obs"]["observation"], reward=r["reward"], success=r["is_success"],
+                    terminated=r["terminated"], ctrl=e.st["ctrl"][0], mocap_pos=e.st["mocap_pos"][0],
+                    mocap_quat=e.st["mocap_quat"][0], task=int(e.task[0]), goal=e.goal[0])
+
+
+def test_golden_fixture_covers_paths():
+    G = np.load(GOLDEN)
+    assert G["success"].sum() >= 3 and G["terminated"].sum() >= 1
+    assert (~G["reward_dense"]).any() and G["reward_dense"].any()
+    assert len(set(G["env_index"].tolist())) >= 3
+
+
+def test_oracle_matches_reference_env_golden(model):
+    replay_golden(lambda idx, cfg: _OracleAdapter(idx, cfg, model), _close, 1e-12)
