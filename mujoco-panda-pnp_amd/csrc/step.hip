@@ -66,8 +66,15 @@ struct Env {
       short live[PH_MAXPAIR];   // broadphase survivors: every candidate pair fits
       Con<T> con[PH_MAXCON];
     };
-    T H[PH_MAXV][PH_MAXV];
-    T efc_Wv[PH_MAXJSLOT];
+    struct {                   // Newton: island Hessian blocks + per-row scratch
+      T H[PH_MAXV][PH_MAXV];
+      T ntmp[PH_MAXEFC];
+    };
+    struct {                   // no-slip: W = M^-1 J^T and the per-group pair lists
+      T efc_Wv[PH_MAXJSLOT];
+      short ns_list[4][PH_MAXEFC / 2];
+      int ns_len[4];
+    };
   };
   T M[PH_MAXMBLK];    // per-tree dense blocks
   T L[PH_MAXMBLK];    // Cholesky factors of the blocks
@@ -89,8 +96,25 @@ struct Env {
   int isl_eoff[PH_MAXT + 1], isl_roff[PH_MAXT + 1];
   short isl_row[PH_MAXEFC];
   T isl_alpha[PH_MAXT];        // per-island line-search step (also the warm-start choice)
+  T isl_cost[PH_MAXT], isl_val[PH_MAXT];   // per-island reductions (cost, |grad|^2 ...)
+  int isl_flag[PH_MAXT];       // per-island: done (Newton), active set changed
+  int isl_hvalid[PH_MAXT];     // per-island: H block is current for the island's active set
   T qpos_pre[PH_MAXQ];         // gym env: qpos of the last forward (pre-integration)
   T red[8];
+};
+
+// stage timer (diagnostic instantiation only: TIMED = true); cycles accumulate in prof[stage]
+struct StageClock {
+  unsigned long long* prof;
+  unsigned long long t;
+  __device__ void start() { if (prof) t = __builtin_amdgcn_s_memtime(); }
+  __device__ void lap(int k) {
+    if (!prof) return;
+    __syncthreads();
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) prof[k] += n - t;
+    t = n;
+  }
 };
 
 // ============================================================================ small helpers
@@ -904,64 +928,50 @@ __device__ void st_actuation_smooth(const DevPhys<T>& m, Env<T>& s) {
 }
 
 // ============================================================================ Newton solver
-constexpr int RPL = (PH_MAXEFC + NT - 1) / NT;   // constraint rows per lane
-
-// Island-segmented wave sum: lane I (< nis) receives the sum of the island-I items of every
-// lane (one dof item, RPL row items; island -1 = no item).  The cost separates over islands
-// (block-diagonal M, every row inside one island), so the solver runs per island: a single
-// global cost would hide the 1e-10 improvements of the 4 mg dummy island under the arm's cost in
-// fp32, and a single global step length would tie every island to the arm's line search.
+// Island reductions.  The cost separates over islands (block-diagonal M, every row inside one
+// island), so the solver runs per island: a single global cost would hide the 1e-10
+// improvements of the 4 mg dummy island under the arm's cost in fp32, and a single global step
+// length would tie every island to the arm's line search.  Island I is reduced on DPP row
+// (I & 3): 16 lanes sum its dofs / rows, rowsum16 finishes; the four rows run concurrently.
 template <typename T>
-__device__ __forceinline__ T isl_wsum(T vd, int id, const T (&vr)[RPL], const int (&ir)[RPL], int nis) {
-  T out = 0;
-  for (int I = 0; I < nis; I++) {
-    T v = id == I ? vd : T(0);
-#pragma unroll
-    for (int k = 0; k < RPL; k++) v += ir[k] == I ? vr[k] : T(0);
-    const T t = wsum(v);
-    if (lane_id() == I) out = t;
-  }
-  return out;
+__device__ __forceinline__ T group_sum(const Env<T>& s, int I, const T* vd, const T* vr) {
+  const int q = lane_id() & 15;
+  T acc = 0;
+  const int n = s.isl_n[I];
+  if (vd)
+    for (int c = q; c < n; c += 16) acc += vd[s.isl_dof[I][c]];
+  if (vr)
+    for (int rr = s.isl_roff[I] + q; rr < s.isl_roff[I + 1]; rr += 16) acc += vr[s.isl_row[rr]];
+  return rowsum16(acc);
 }
+// out[I] = group_sum for every island (vd / vr in LDS)
 template <typename T>
-__device__ __forceinline__ T isl_wsum(T vd, int id, int nis) {
-  T out = 0;
-  for (int I = 0; I < nis; I++) {
-    const T t = wsum(id == I ? vd : T(0));
-    if (lane_id() == I) out = t;
+__device__ __forceinline__ void island_sums(Env<T>& s, const T* vd, const T* vr, T* out) {
+  const int l = lane_id();
+  for (int I = l >> 4; I < s.nisland; I += 4) {
+    const T c = group_sum(s, I, vd, vr);
+    if ((l & 15) == 0) out[I] = c;
   }
-  return out;
+  wsync();
 }
 
-// jar = J x - aref, active set; returns island l's cost on lane l (< nisland)
+// jar = J x - aref, active set (store), per-island cost -> out[I]
 template <typename T>
-__device__ T eval_cost(const DevPhys<T>& m, Env<T>& s, const T* x, bool store) {
+__device__ void eval_cost(const DevPhys<T>& m, Env<T>& s, const T* x, bool store, T* out) {
   const int l = lane_id();
   if (l < m.nv) s.v1[l] = x[l] - s.qacc_smooth[l];
   wsync();
-  T cd = 0, cr[RPL];
-  int di = -1, ri[RPL];
-  if (l < m.nv) {
-    cd = T(0.5) * s.v1[l] * mulM_row(m, s, l, s.v1);
-    di = s.tree_island[m.dof_tree[l]];
-  }
-#pragma unroll
-  for (int k = 0; k < RPL; k++) {
-    const int r = l + k * NT;
-    cr[k] = 0;
-    ri[k] = -1;
-    if (r >= s.nefc) continue;
+  if (l < m.nv) s.v2[l] = T(0.5) * s.v1[l] * mulM_row(m, s, l, s.v1);
+  for (int r = l; r < s.nefc; r += NT) {
     const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
     T v = -s.efc_aref[r];
     for (int q = 0; q < w; q++) v += EJ(r, q) * x[slot_dof(m, t0, t1, q)];
     const int a = r < s.ne || v < 0;
     if (store) { s.efc_jar[r] = v; s.efc_act[r] = a; }
-    if (a) cr[k] = T(0.5) * s.efc_D[r] * v * v;
-    ri[k] = s.tree_island[t0];
+    s.ntmp[r] = a ? T(0.5) * s.efc_D[r] * v * v : T(0);
   }
-  const T c = isl_wsum(cd, di, cr, ri, s.nisland);
   wsync();
-  return c;
+  island_sums(s, s.v2, s.ntmp, out);
 }
 
 template <typename T>
@@ -972,48 +982,87 @@ __device__ __forceinline__ int row_slot_(const Env<T>& s, int t0, int t1, int tr
 }
 #define row_slot(m, t0, t1, tree, dof) row_slot_(s, t0, t1, tree, dof)
 
-// Islands = trees joined by constraint rows (union-find over <= 8 trees, one lane), their dof
-// lists, the rows of each island (CSR, wave ballots) and the island Hessian entry offsets.
+// OR over the wave (DPP butterfly in each row of 16, then the four rows)
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) | (uint32_t)__builtin_amdgcn_readlane((int)v, 16) |
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) | (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
+// Islands = trees joined by constraint rows.  Only contact and equality rows can span two trees;
+// their tree pairs form an 8 x 8 bit matrix (row t = bits 8t..8t+7) whose transitive closure
+// (three boolean squarings) gives the components; island ids follow the lowest tree of each
+// component, dofs keep increasing order inside an island (trees are contiguous dof ranges).
+// Then the rows of each island (CSR, wave ballots) and the island Hessian entry offsets.
 template <typename T>
 __device__ void build_islands(const DevPhys<T>& m, Env<T>& s) {
   const int l = lane_id();
+  uint64_t e = 0;
+  if (l < s.ncon && s.con_rbase[l] >= 0 && s.con_t[l][1] >= 0) {
+    const int a = s.con_t[l][0], b = s.con_t[l][1];
+    e = (1ull << (8 * a + b)) | (1ull << (8 * b + a));
+  }
+  for (int r = l; r < s.ne; r += NT) {
+    const int a = s.efc_t0[r], b = s.efc_t1[r];
+    if (a >= 0 && b >= 0) e |= (1ull << (8 * a + b)) | (1ull << (8 * b + a));
+  }
+  uint64_t R = ((uint64_t)wave_or((uint32_t)(e >> 32)) << 32) | wave_or((uint32_t)e);
+  R |= 0x8040201008040201ull;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    uint64_t R2 = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+      const uint32_t row = (uint32_t)(R >> (8 * t)) & 0xFFu;
+      uint64_t acc = 0;
+#pragma unroll
+      for (int j = 0; j < 8; j++)
+        if (row >> j & 1u) acc |= (R >> (8 * j)) & 0xFFull;
+      R2 |= acc << (8 * t);
+    }
+    R = R2;
+  }
+  const int nt = m.ntree;
+  uint32_t roots = 0;
+#pragma unroll
+  for (int t = 0; t < 8; t++)
+    if (t < nt && __builtin_ctz((uint32_t)(R >> (8 * t)) & 0xFFu) == t) roots |= 1u << t;
+  const int nis = __builtin_popcount(roots);
+  auto island_of = [&](int t) {
+    const int low = __builtin_ctz((uint32_t)(R >> (8 * t)) & 0xFFu);
+    return __builtin_popcount(roots & ((1u << low) - 1u));
+  };
+  if (l < nt) s.tree_island[l] = island_of(l);
+  if (l < m.nv) {
+    const int t = s.c_dof_tree[l];
+    const uint32_t comp = (uint32_t)(R >> (8 * t)) & 0xFFu;
+    int pos = l - s.c_tree_dofadr[t];
+    for (int u = 0; u < t; u++)
+      if (comp >> u & 1u) pos += s.c_tree_dofnum[u];
+    s.isl_dof[island_of(t)][pos] = (unsigned char)l;
+  }
+  if (l < nis) {
+    int n = 0;
+    for (int t = 0; t < nt; t++)
+      if (island_of(t) == l) n += s.c_tree_dofnum[t];
+    s.isl_n[l] = n;
+  }
+  if (l == 0) s.nisland = nis;
+  wsync();
   if (l == 0) {
-    int par[PH_MAXT];
-    for (int t = 0; t < m.ntree; t++) par[t] = t;
-    for (int r = 0; r < s.nefc; r++) {
-      int a = s.efc_t0[r], b = s.efc_t1[r];
-      if (a < 0 || b < 0) continue;
-      while (par[a] != a) a = par[a];
-      while (par[b] != b) b = par[b];
-      if (a != b) par[a > b ? a : b] = a < b ? a : b;
-    }
-    int nis = 0, id[PH_MAXT];
-    for (int t = 0; t < m.ntree; t++) {
-      int r = t;
-      while (par[r] != r) r = par[r];
-      if (r == t) { id[t] = nis; s.isl_n[nis] = 0; nis++; }
-    }
-    for (int t = 0; t < m.ntree; t++) {
-      int r = t;
-      while (par[r] != r) r = par[r];
-      s.tree_island[t] = id[r];
-    }
-    for (int i = 0; i < m.nv; i++) {
-      const int isl = s.tree_island[m.dof_tree[i]];
-      s.isl_dof[isl][s.isl_n[isl]++] = i;
-    }
     int eo = 0;
     for (int I = 0; I < nis; I++) {
       s.isl_eoff[I] = eo;
       eo += s.isl_n[I] * (s.isl_n[I] + 1) / 2;
     }
     s.isl_eoff[nis] = eo;
-    s.nisland = nis;
   }
-  wsync();
   // rows grouped by island (stable, row order kept inside an island)
   int off = 0;
-  for (int I = 0; I < s.nisland; I++) {
+  for (int I = 0; I < nis; I++) {
     if (l == 0) s.isl_roff[I] = off;
     for (int base = 0; base < s.nefc; base += NT) {
       const int r = base + l;
@@ -1023,7 +1072,7 @@ __device__ void build_islands(const DevPhys<T>& m, Env<T>& s) {
       off += __popcll(bal);
     }
   }
-  if (l == 0) s.isl_roff[s.nisland] = off;
+  if (l == 0) s.isl_roff[nis] = off;
   wsync();
 }
 
@@ -1118,73 +1167,60 @@ __device__ void island_newton_dir_lds(Env<T>& s, int I, int n) {
 }
 
 // Exact minimiser of each island's convex piecewise quadratic phi_I(a) = cost_I(x + a p)
-// (semi-smooth Newton on phi', bracketed); lane I owns island I's bracket.  Islands with
-// done != 0 keep a = 0.  Leaves the step lengths in s.isl_alpha.
+// (semi-smooth Newton on phi', bracketed), island I on DPP row (I & 3): its rows are summed by
+// the row's 16 lanes and its bracket iterates independently of the other islands.  Islands with
+// isl_flag set (done) keep a = 0.  Leaves the step lengths in s.isl_alpha.
 template <typename T>
-__device__ void line_search(const DevPhys<T>& m, Env<T>& s, bool done) {
+__device__ void line_search(const DevPhys<T>& m, Env<T>& s) {
   const int l = lane_id();
-  const int nis = s.nisland;
-  int di = -1, ri[RPL];
-  T A0 = 0, B0 = 0;
-  if (l < m.nv) {
-    s.v1[l] = s.x[l] - s.qacc_smooth[l];
-    di = s.tree_island[m.dof_tree[l]];
-  }
-#pragma unroll
-  for (int k = 0; k < RPL; k++) {
-    const int r = l + k * NT;
-    ri[k] = -1;
-    if (r >= s.nefc) continue;
+  if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
+  for (int r = l; r < s.nefc; r += NT) {
     const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
     T v = 0;
     for (int q = 0; q < w; q++) v += EJ(r, q) * s.p[slot_dof(m, t0, t1, q)];
     s.efc_Jp[r] = v;
-    ri[k] = s.tree_island[t0];
   }
   wsync();
   if (l < m.nv) {
     const T mp = mulM_row(m, s, l, s.p);
-    A0 = mp * s.p[l];
-    B0 = mp * s.v1[l];
+    s.v2[l] = mp * s.p[l];
+    s.grad[l] = mp * s.v1[l];   // the gradient is no longer needed this iteration
   }
-  A0 = isl_wsum(A0, di, nis);
-  B0 = isl_wsum(B0, di, nis);
-  bool fin = l >= nis || done;
-  T lo = 0, hi = T(-1), a = fin ? T(0) : T(1);
-  if (l < nis) s.isl_alpha[l] = a;
-  for (int it = 0; it < 60; it++) {
-    wsync();
-    T d1r[RPL], d2r[RPL];
-#pragma unroll
-    for (int k = 0; k < RPL; k++) {
-      const int r = l + k * NT;
-      d1r[k] = d2r[k] = 0;
-      if (r >= s.nefc) continue;
-      const T jp = s.efc_Jp[r], v = s.efc_jar[r] + s.isl_alpha[ri[k]] * jp;
-      if (r < s.ne || v < 0) { d1r[k] = s.efc_D[r] * v * jp; d2r[k] = s.efc_D[r] * jp * jp; }
+  wsync();
+  const int q = l & 15;
+  for (int I = l >> 4; I < s.nisland; I += 4) {
+    if (s.isl_flag[I]) {
+      if (q == 0) s.isl_alpha[I] = 0;
+      continue;
     }
-    T d1 = isl_wsum(T(0), -1, d1r, ri, nis) + A0 * a + B0;
-    T d2 = isl_wsum(T(0), -1, d2r, ri, nis) + A0;
-    if (!fin) {
-      if (!(d2 > T(0))) { a = 0; fin = true; }
-      else if (d1 == T(0)) fin = true;
-      else {
-        if (d1 > 0) hi = a; else lo = a;
-        T an = a - d1 / d2;
-        if (!(an > lo) || (hi >= T(0) && !(an < hi))) an = hi >= T(0) ? T(0.5) * (lo + hi) : T(2) * a;
-        if (an == a || (hi >= T(0) && hi - lo <= PM<T>::eps() * hi)) fin = true;
-        a = an;
+    const T A0 = group_sum(s, I, s.v2, (const T*)nullptr), B0 = group_sum(s, I, s.grad, (const T*)nullptr);
+    const int r0 = s.isl_roff[I], r1 = s.isl_roff[I + 1];
+    T lo = 0, hi = T(-1), a = 1;
+    for (int it = 0; it < 60; it++) {
+      T d1 = 0, d2 = 0;
+      for (int rr = r0 + q; rr < r1; rr += 16) {
+        const int r = s.isl_row[rr];
+        const T jp = s.efc_Jp[r], v = s.efc_jar[r] + a * jp;
+        if (r < s.ne || v < 0) { d1 += s.efc_D[r] * v * jp; d2 += s.efc_D[r] * jp * jp; }
       }
+      d1 = rowsum16(d1) + A0 * a + B0;
+      d2 = rowsum16(d2) + A0;
+      if (!(d2 > T(0))) { a = 0; break; }
+      if (d1 == T(0)) break;
+      if (d1 > 0) hi = a; else lo = a;
+      T an = a - d1 / d2;
+      if (!(an > lo) || (hi >= T(0) && !(an < hi))) an = hi >= T(0) ? T(0.5) * (lo + hi) : T(2) * a;
+      const bool fin = an == a || (hi >= T(0) && hi - lo <= PM<T>::eps() * hi);
+      a = an;
+      if (fin) break;
     }
-    wsync();
-    if (l < nis) s.isl_alpha[l] = a;
-    if (!__ballot(!fin)) break;
+    if (q == 0) s.isl_alpha[I] = a;
   }
   wsync();
 }
 
 template <typename T>
-__device__ void st_newton(const DevPhys<T>& m, Env<T>& s) {
+__device__ void st_newton(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
   const int l = lane_id();
   if (s.nefc == 0) {
     if (l < m.nv) s.qacc[l] = s.qacc_smooth[l];
@@ -1193,14 +1229,43 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s) {
     return;
   }
   build_islands(m, s);
-  // warm start per island: the better of qacc_warmstart and qacc_smooth
-  const T cws = eval_cost(m, s, s.qacc_ws, false);
-  const T csm = eval_cost(m, s, s.qacc_smooth, false);
-  if (l < s.nisland) s.isl_alpha[l] = cws < csm ? T(1) : T(0);
+  // warm start per island: the better of qacc_warmstart and qacc_smooth (MuJoCo chooses for the
+  // whole problem; per island the minimiser is the same and the start is better).  One pass:
+  // cost(qacc_smooth) has no dof term and its jar is efc_bb (= J qacc_smooth - aref, same
+  // arithmetic), and the chosen start's jar / active set are kept instead of re-evaluated.
+  if (l < m.nv) s.v1[l] = s.qacc_ws[l] - s.qacc_smooth[l];
+  wsync();
+  if (l < m.nv) s.v2[l] = T(0.5) * s.v1[l] * mulM_row(m, s, l, s.v1);
+  for (int r = l; r < s.nefc; r += NT) {
+    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
+    T v = -s.efc_aref[r];
+    for (int q = 0; q < w; q++) v += EJ(r, q) * s.qacc_ws[slot_dof(m, t0, t1, q)];
+    const T bs = s.efc_bb[r];
+    s.efc_jar[r] = v;
+    s.ntmp[r] = r < s.ne || v < 0 ? T(0.5) * s.efc_D[r] * v * v : T(0);
+    s.efc_Jp[r] = r < s.ne || bs < 0 ? T(0.5) * s.efc_D[r] * bs * bs : T(0);
+  }
+  wsync();
+  island_sums(s, s.v2, s.ntmp, s.isl_val);
+  island_sums(s, (const T*)nullptr, s.efc_Jp, s.isl_cost);
+  if (l < PH_MAXT) {
+    const bool ws = l < s.nisland && s.isl_val[l] < s.isl_cost[l];
+    s.isl_alpha[l] = ws ? T(1) : T(0);
+    if (ws) s.isl_cost[l] = s.isl_val[l];
+    s.isl_flag[l] = 0;
+    s.isl_hvalid[l] = 0;
+  }
   wsync();
   if (l < m.nv) s.x[l] = s.isl_alpha[s.tree_island[m.dof_tree[l]]] != T(0) ? s.qacc_ws[l] : s.qacc_smooth[l];
+  for (int r = l; r < s.nefc; r += NT) {
+    const T v = s.isl_alpha[s.tree_island[s.efc_t0[r]]] != T(0) ? s.efc_jar[r] : s.efc_bb[r];
+    s.efc_jar[r] = v;
+    s.efc_act[r] = r < s.ne || v < 0;
+  }
   wsync();
-  T cost = eval_cost(m, s, s.x, true);   // island l's cost on lane l
+  clk.lap(8);
+  // lane I (< nisland) keeps island I's convergence state
+  T cost = l < s.nisland ? s.isl_cost[l] : T(0);
   bool done = l >= s.nisland;
   int unchanged = 0;                      // consecutive steps that kept the island's active set
   // gradient floor of a converged island (scaled like the oracle: 1 / (meaninertia * nv))
@@ -1222,20 +1287,23 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s) {
         if (k >= 0) g += EJ(r, k) * s.efc_D[r] * s.efc_jar[r];
       }
       s.grad[l] = g;
+      s.v2[l] = g * g;
     }
-    {
-      // an island whose last step kept its active set is at that quadratic's minimiser up to
-      // the rounding of one Cholesky solve (cond(H) eps); it is done once its gradient is at the
-      // floor, otherwise it takes one more (refining) Newton step
-      const T g2 = isl_wsum(l < m.nv ? s.grad[l] * s.grad[l] : T(0), l < m.nv ? s.tree_island[m.dof_tree[l]] : -1,
-                            s.nisland);
-      if (!done && unchanged >= 1 && PM<T>::sqrt_(g2) * gscale < gtol) done = true;
-      if (!__ballot(!done)) break;
-    }
-    // Hessian island blocks (lower triangle entries, lane per entry): M + sum_active D J J^T
+    wsync();
+    // an island whose last step kept its active set is at that quadratic's minimiser up to the
+    // rounding of one Cholesky solve (cond(H) eps): done once its gradient is at the floor,
+    // otherwise it takes one more (refining) Newton step
+    island_sums(s, s.v2, (const T*)nullptr, s.isl_val);
+    if (!done && unchanged >= 1 && PM<T>::sqrt_(s.isl_val[l]) * gscale < gtol) done = true;
+    if (l < PH_MAXT) s.isl_flag[l] = done;
+    wsync();
+    if (!__ballot(!done)) { clk.lap(9); break; }
+    // Hessian island blocks (lower triangle, lane per entry): M + sum_active D J J^T; blocks of
+    // islands whose active set is unchanged since their last assembly are reused as they are
     for (int e = l; e < nent; e += NT) {
       int I = 0;
       while (e >= s.isl_eoff[I + 1]) I++;
+      if (s.isl_flag[I] || s.isl_hvalid[I]) continue;
       const int le = e - s.isl_eoff[I];
       int a = (int)((PM<float>::sqrt_(8.0f * le + 1.0f) - 1.0f) * 0.5f);
       while (a * (a + 1) / 2 > le) a--;
@@ -1256,45 +1324,56 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s) {
       s.H[j][i] = h;
     }
     wsync();
-    // Newton direction per island (lane per island)
-    if (l < s.nisland && !done) {
+    clk.lap(9);
+    // Newton direction per island (lane per island); the register path leaves H intact, the
+    // in-place LDS path (merged islands > 9 dofs) consumes it
+    if (!done) {
       const int n = s.isl_n[l];
       if (n <= 6) island_newton_dir_reg<T, 6>(s, l, n);
       else if (n <= 9) island_newton_dir_reg<T, 9>(s, l, n);
       else island_newton_dir_lds(s, l, n);
+      s.isl_hvalid[l] = n <= 9;
     }
     wsync();
-    line_search(m, s, done);
+    clk.lap(10);
+    line_search(m, s);
+    clk.lap(11);
     if (l < m.nv) s.x[l] += s.isl_alpha[s.tree_island[m.dof_tree[l]]] * s.p[l];
     // remember the active set the step was computed with
     for (int r = l; r < s.nefc; r += NT) s.efc_Jp[r] = (T)s.efc_act[r];
     wsync();
-    const T nc = eval_cost(m, s, s.x, true);
+    eval_cost(m, s, s.x, true, s.isl_cost);
+    // active-set change per island (rows of island I on DPP row I & 3)
+    {
+      const int q = l & 15;
+      for (int I = l >> 4; I < s.nisland; I += 4) {
+        bool ch = false;
+        for (int rr = s.isl_roff[I] + q; rr < s.isl_roff[I + 1]; rr += 16) {
+          const int r = s.isl_row[rr];
+          ch |= (T)s.efc_act[r] != s.efc_Jp[r];
+        }
+        const bool any = ((__ballot(ch) >> (l & 48)) & 0xFFFFull) != 0;
+        if (q == 0) s.isl_val[I] = any ? T(1) : T(0);
+      }
+    }
+    wsync();
     // island converged: two consecutive steps kept its active set (then its piecewise quadratic
     // is a single quadratic there and x its minimiser, refined once), or its cost stopped
     // decreasing
-    int ci[RPL];
-#pragma unroll
-    for (int k = 0; k < RPL; k++) {
-      const int r = l + k * NT;
-      ci[k] = r < s.nefc && (T)s.efc_act[r] != s.efc_Jp[r] ? s.tree_island[s.efc_t0[r]] : -1;
-    }
-    bool changed = false;
-    for (int I = 0; I < s.nisland; I++) {
-      bool mine = false;
-#pragma unroll
-      for (int k = 0; k < RPL; k++) mine |= ci[k] == I;
-      const bool any = __ballot(mine) != 0;
-      if (l == I) changed = any;
-    }
     if (!done) {
+      const bool changed = s.isl_val[l] != T(0);
+      const T nc = s.isl_cost[l];
       const T impr = cost - nc;
       unchanged = changed ? 0 : unchanged + 1;
+      if (changed) s.isl_hvalid[l] = 0;
       if (unchanged >= 2 || !(impr > 0) || !(s.isl_alpha[l] > T(0))) done = true;
       cost = nc;
     }
+    wsync();
+    clk.lap(12);
     if (!__ballot(!done)) { it++; break; }
   }
+  clk.lap(12);
   if (l == 0) s.solver_iter = it;
   for (int r = l; r < s.nefc; r += NT) s.efc_force[r] = s.efc_act[r] ? -s.efc_D[r] * s.efc_jar[r] : T(0);
   if (l < m.nv) s.qacc[l] = s.x[l];
@@ -1329,53 +1408,73 @@ __device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
       base += n;
     }
   }
-  // v = M^-1 J^T f (all rows)
+  // v = M^-1 J^T f over the dof's island rows
   if (l < m.nv) {
-    const int t = m.dof_tree[l];
+    const int t = m.dof_tree[l], I = s.tree_island[t];
     T g = 0;
-    for (int r = 0; r < s.nefc; r++) {
-      const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
-      int k = -1;
-      if (t0 == t) k = l - m.tree_dofadr[t0];
-      else if (t1 == t) k = m.tree_dofnum[t0] + l - m.tree_dofadr[t1];
+    for (int rr = s.isl_roff[I]; rr < s.isl_roff[I + 1]; rr++) {
+      const int r = s.isl_row[rr];
+      const int k = row_slot(m, s.efc_t0[r], s.efc_t1[r], t, l);
       if (k >= 0) g += EJ(r, k) * s.efc_force[r];
     }
     s.v2[l] = g;
   }
+  // Pair lists: islands are independent under Gauss-Seidel (block-diagonal M, rows inside one
+  // island), so island I runs on DPP row (I mod 4) — 16 lanes, one slot per lane — in its own
+  // row order, and up to 4 pairs are updated at once; each island sees exactly the sequential
+  // order, so the result equals the one-pair-at-a-time sweep.
+  const int grp = l >> 4, q = l & 15;
+  {
+    int len = 0;
+    for (int I = grp; I < s.nisland; I += 4) {
+      for (int base = s.isl_roff[I]; base < s.isl_roff[I + 1]; base += 16) {
+        const int rr = base + q;
+        bool start = false;
+        int r = 0;
+        if (rr < s.isl_roff[I + 1]) {
+          r = s.isl_row[rr];
+          start = s.efc_type[r] == 6 && ((r - s.con_rbase[s.efc_id[r]]) & 1) == 0;
+        }
+        const uint32_t bits = (uint32_t)(__ballot(start) >> (16 * grp)) & 0xFFFFu;
+        if (start) s.ns_list[grp][len + __popc(bits & ((1u << q) - 1u))] = (short)r;
+        len += __popc(bits);
+      }
+    }
+    if (q == 0) s.ns_len[grp] = len;
+  }
   wsync();
   solve_M(m, s, s.v2, s.v2);
+  const int glen = s.ns_len[grp];
+  const int maxlen = max(max(s.ns_len[0], s.ns_len[1]), max(s.ns_len[2], s.ns_len[3]));
   for (int iter = 0; iter < m.noslip_iterations; iter++) {
-    for (int i = s.ne; i < s.nefc; i++) {
-      if (s.efc_type[i] != 6) continue;
-      const int dim = s.con_dim[s.efc_id[i]];
-      for (int j = i; j < i + 2 * (dim - 1); j += 2) {
-        // one pair of opposing pyramid edges; sparse rows have <= 16 slots = one DPP row
-        const int t0 = s.efc_t0[j], t1 = s.efc_t1[j], w = row_width(m, t0, t1);
-        const bool on = l < w;
-        const int d = on ? slot_dof(m, t0, t1, l) : 0;
-        const T J0 = on ? EJ(j, l) : T(0), J1 = on ? EJ(j + 1, l) : T(0);
-        const T W0 = on ? EW(j, l) : T(0), W1 = on ? EW(j + 1, l) : T(0);
-        const T vd = on ? s.v2[d] : T(0);
-        const T r0 = rowsum16(J0 * vd) + s.efc_bb[j];
-        const T r1 = rowsum16(J1 * vd) + s.efc_bb[j + 1];
-        const T a00 = rowsum16(J0 * W0), a01 = rowsum16(J0 * W1);
-        const T a10 = rowsum16(J1 * W0), a11 = rowsum16(J1 * W1);
-        const T f0 = s.efc_force[j], f1 = s.efc_force[j + 1];
-        const T bc0 = r0 - (a00 * f0 + a01 * f1), bc1 = r1 - (a10 * f0 + a11 * f1);
-        const T mid = T(0.5) * (f0 + f1);
-        const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;
-        T n0, n1;
-        if (K1 < T(1e-15)) { n0 = n1 = mid; }
-        else {
-          T y = -K0 / K1;
-          if (y < -mid) y = -mid; else if (y > mid) y = mid;
-          n0 = mid + y; n1 = mid - y;
-        }
-        if (on) s.v2[d] += W0 * (n0 - f0) + W1 * (n1 - f1);
-        if (l == 0) { s.efc_force[j] = n0; s.efc_force[j + 1] = n1; }
-        wsync();
+    for (int k = 0; k < maxlen; k++) {
+      // one pair of opposing pyramid edges per group; sparse rows have <= 16 slots = one DPP row
+      const bool act = k < glen;
+      const int j = act ? s.ns_list[grp][k] : 0;
+      const int t0 = s.efc_t0[j], t1 = s.efc_t1[j], w = row_width(m, t0, t1);
+      const bool on = act && q < w;
+      const int d = on ? slot_dof(m, t0, t1, q) : 0;
+      const T J0 = on ? EJ(j, q) : T(0), J1 = on ? EJ(j + 1, q) : T(0);
+      const T W0 = on ? EW(j, q) : T(0), W1 = on ? EW(j + 1, q) : T(0);
+      const T vd = on ? s.v2[d] : T(0);
+      const T r0 = rowsum16(J0 * vd) + s.efc_bb[j];
+      const T r1 = rowsum16(J1 * vd) + s.efc_bb[j + 1];
+      const T a00 = rowsum16(J0 * W0), a01 = rowsum16(J0 * W1);
+      const T a10 = rowsum16(J1 * W0), a11 = rowsum16(J1 * W1);
+      const T f0 = s.efc_force[j], f1 = s.efc_force[j + 1];
+      const T bc0 = r0 - (a00 * f0 + a01 * f1), bc1 = r1 - (a10 * f0 + a11 * f1);
+      const T mid = T(0.5) * (f0 + f1);
+      const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;
+      T n0, n1;
+      if (K1 < T(1e-15)) { n0 = n1 = mid; }
+      else {
+        T y = -K0 / K1;
+        if (y < -mid) y = -mid; else if (y > mid) y = mid;
+        n0 = mid + y; n1 = mid - y;
       }
-      i += 2 * (dim - 1) - 1;
+      if (on) s.v2[d] += W0 * (n0 - f0) + W1 * (n1 - f1);
+      if (act && q == 0) { s.efc_force[j] = n0; s.efc_force[j + 1] = n1; }
+      wsync();
     }
   }
 }
@@ -1385,13 +1484,12 @@ __device__ void st_finish_accel(const DevPhys<T>& m, Env<T>& s) {
   const int l = lane_id();
   if (s.nefc == 0) return;
   if (l < m.nv) {
-    const int t = m.dof_tree[l];
+    // J^T f over the dof's island rows (the other rows do not touch it)
+    const int t = m.dof_tree[l], I = s.tree_island[t];
     T g = 0;
-    for (int r = 0; r < s.nefc; r++) {
-      const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
-      int k = -1;
-      if (t0 == t) k = l - m.tree_dofadr[t0];
-      else if (t1 == t) k = m.tree_dofnum[t0] + l - m.tree_dofadr[t1];
+    for (int rr = s.isl_roff[I]; rr < s.isl_roff[I + 1]; rr++) {
+      const int r = s.isl_row[rr];
+      const int k = row_slot(m, s.efc_t0[r], s.efc_t1[r], t, l);
       if (k >= 0) g += EJ(r, k) * s.efc_force[r];
     }
     s.v2[l] = s.qfrc_smooth[l] + g;
@@ -1462,20 +1560,6 @@ __device__ void st_euler(const DevPhys<T>& m, Env<T>& s) {
 }
 
 // ============================================================================ forward / kernel
-// stage timer (diagnostic instantiation only: TIMED = true); cycles accumulate in prof[stage]
-#define PNP_NSTAGE 12
-struct StageClock {
-  unsigned long long* prof;
-  unsigned long long t;
-  __device__ void start() { if (prof) t = __builtin_amdgcn_s_memtime(); }
-  __device__ void lap(int k) {
-    if (!prof) return;
-    __syncthreads();
-    const unsigned long long n = __builtin_amdgcn_s_memtime();
-    if (threadIdx.x == 0) prof[k] += n - t;
-    t = n;
-  }
-};
 
 // debug record of the contacts (PNP_DBG_CON): written right after collision, because the contact
 // list shares storage with the solver's scratch
@@ -1502,9 +1586,9 @@ __device__ void forward(const DevPhys<T>& m, Env<T>& s, StageClock& clk, double*
   st_constraints(m, s);     clk.lap(5);
   st_velocity(m, s);        clk.lap(6);
   st_actuation_smooth(m, s); clk.lap(7);
-  st_newton(m, s);          clk.lap(8);
-  st_noslip(m, s);          clk.lap(9);
-  st_finish_accel(m, s);    clk.lap(10);
+  st_newton(m, s, clk);     // laps 8..12 inside
+  st_noslip(m, s);          clk.lap(13);
+  st_finish_accel(m, s);    clk.lap(14);
 }
 
 template <typename T>
@@ -1547,7 +1631,7 @@ __device__ void mj_step_dev(const DevPhys<T>& m, Env<T>& s, StageClock& clk, T* 
     wsync();
   }
   st_euler(m, s);
-  clk.lap(11);
+  clk.lap(15);
 }
 
 template <typename T>

@@ -120,7 +120,8 @@ class Engine:
         return st
 
     STAGES = ("check", "kinematics", "compos_crb", "factor_M", "collision", "constraints", "velocity_rne",
-              "actuation_smooth", "newton", "noslip", "finish_accel", "euler")
+              "actuation_smooth", "newton_setup", "newton_grad_hess", "newton_dir", "newton_linesearch",
+              "newton_update", "noslip", "finish_accel", "euler")
 
     def step_profile(self, st, nsub=1):
         """Diagnostic timed instantiation of pnp_step: per-stage shader cycles [B, 12] (uint64)."""
