@@ -85,10 +85,20 @@ def _timed(fn, steps, warmup, dist):
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
     if dist:
-        t = torch.tensor([elapsed, kern_ms], device="cuda", dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        elapsed, kern_ms = reduce_max([elapsed, kern_ms], "cuda")
     return elapsed, kern_ms
+
+
+def reduce_max(values, device):
+    """MAX of each value over all ranks (the slowest rank sets the job's time)."""
+    t = torch.tensor(values, device=device, dtype=torch.float64)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return [float(v) for v in t]
+
+
+def shard_range(rank, B):
+    """Global env indices of rank r: [r*B, (r+1)*B) (inputs depend only on the global index)."""
+    return np.arange(rank * B, (rank + 1) * B)
 
 
 def _traffic(name, B):
@@ -103,7 +113,7 @@ def _traffic(name, B):
 
 # ----------------------------------------------------------------------------- C3 / C4 env-step
 def step_inputs(engine, model, rank, B):
-    idx = np.arange(rank * B, (rank + 1) * B)
+    idx = shard_range(rank, B)
     q = torch.as_tensor(np.tile(model.qpos0, (1, 1)), dtype=torch.float64, device=engine.device)
     q[:, :9] = torch.as_tensor(workloads.NEUTRAL, dtype=torch.float64)
     sx, sm = engine.site_kinematics(q.contiguous())
@@ -205,7 +215,7 @@ def run_gym(engine, B, rank, world, dist, steps=3, warmup=1):
 
 # ----------------------------------------------------------------------------- C2 IK
 def ik_inputs(engine, model, rank, B, regime):
-    idx = np.arange(rank * B, (rank + 1) * B)
+    idx = shard_range(rank, B)
     q, delta = workloads.ik_inputs(model, idx, regime=regime)
     dev = engine.device
     qf = torch.as_tensor(np.tile(model.qpos0, (B, 1)), dtype=torch.float32, device=dev)

@@ -1,0 +1,82 @@
+"""Multi-rank path on CPU (gloo, world size 2, 127.0.0.1): the env shards of bench.py /
+pnp_amd.envs reproduce the single-process batch bitwise, and the job time is the max over ranks.
+(The GPU data path has no collective)"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+B = 24
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _inputs(rank, sx, sm):
+    import bench
+    from pnp_amd import workloads
+    from pnp_amd.model import load_model
+    m = load_model()
+    idx = bench.shard_range(rank, B)
+    st = workloads.c3_reset(m, idx, sx, sm)
+    ctrl = np.stack([workloads.c3_ctrl(m, idx, s) for s in range(3)])
+    q, d = workloads.ik_inputs(m, idx)
+    return dict(qpos=st["qpos"], mocap=st["mocap_pos"], ctrl=ctrl, q=q, d=d)
+
+
+def _worker(rank, world, port, sx, sm, out):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "mujoco-panda-pnp_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    mine = _inputs(rank, sx, sm)
+    got = [None] * world
+    dist.all_gather_object(got, mine)
+    t = bench.reduce_max([1.0 + rank, 10.0 - rank], "cpu")
+    if rank == 0:
+        out.put((got, t))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_shards_match_global_batch(model):
+    from oracle import oracle as O
+    q = model.qpos0.copy()
+    q[:9] = [0.00, 0.41, 0.00, -1.85, 0.00, 2.26, 0.79, 0.00, 0.00]
+    sx, sm = O.site_kinematics(q[None], model=model)
+    sx, sm = sx[0], sm[0]
+    ctx = mp.get_context("spawn")
+    out = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, sx, sm, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, t = out.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert t == [2.0, 10.0]                     # max over ranks
+    # global batch of 2B envs generated in one process == the two shards concatenated
+    import bench
+    from pnp_amd import workloads
+    idx = np.arange(2 * B)
+    st = workloads.c3_reset(model, idx, sx, sm)
+    ctrl = np.stack([workloads.c3_ctrl(model, idx, s) for s in range(3)])
+    qi, d = workloads.ik_inputs(model, idx)
+    cat = lambda k, ax=0: np.concatenate([g[k] for g in got], axis=ax)
+    assert np.array_equal(cat("qpos"), st["qpos"])
+    assert np.array_equal(cat("mocap"), st["mocap_pos"])
+    assert np.array_equal(cat("ctrl", 1), ctrl)
+    assert np.array_equal(cat("q"), qi) and np.array_equal(cat("d"), d)
+    assert not np.array_equal(got[0]["qpos"], got[1]["qpos"])   # shards differ
+    assert bench.shard_range(1, 4096)[0] == 4096
