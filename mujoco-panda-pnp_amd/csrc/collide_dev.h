@@ -134,6 +134,9 @@ __device__ void c_sphere_box(const T* p1, T r, const T* p2, const T* R2, const T
   out.emit(dist, pos, n);
 }
 
+// 1 um band of oracle/collision.c BB_TOL (identical boxes face to face: robust decisions)
+#define C_BB_TOL 1e-6
+
 // Liang-Barsky clip of the 2D segment p0 -> p1 to |x| <= A, |y| <= B (closed); false if empty
 template <typename T>
 __device__ __forceinline__ bool c_clip_seg(const T* p0, const T* p1, T A, T B, T& t0, T& t1) {
@@ -187,10 +190,10 @@ __device__ void c_box_face(const T* pr, const T* Rr, const T* sr, int ia, const 
     for (int k = 0; k < 3; k++) w[k] = pi[k] + sg * bj[k] * hj + su[q] * bu[k] * hu + sv[q] * bv[k] * hv - cref[k];
     P[q][0] = t_dot3(w, u); P[q][1] = t_dot3(w, v); P[q][2] = t_dot3(w, nr);
   }
-  const T A = sr[iu], B = sr[iv];
+  const T A = sr[iu] + T(C_BB_TOL), B = sr[iv] + T(C_BB_TOL);   // rectangle grown by the band
   int cnt = 0;
   auto emit = [&](T x, T y, T z) {
-    if (cnt >= 8 || z > margin) return;
+    if (cnt >= 8 || z > margin + T(C_BB_TOL)) return;
     T pos[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) pos[k] = cref[k] + u[k] * x + v[k] * y + nr[k] * z * T(0.5);
@@ -210,11 +213,14 @@ __device__ void c_box_face(const T* pr, const T* Rr, const T* sr, int ia, const 
   const T e3[3] = {P[3][0] - P[0][0], P[3][1] - P[0][1], P[3][2] - P[0][2]};
   const T det = e1[0] * e3[1] - e1[1] * e3[0];
   if (fabs(det) > T(1e-12) * (fabs(e1[0]) + fabs(e1[1])) * (fabs(e3[0]) + fabs(e3[1]))) {
+    const T ta = T(C_BB_TOL) / PM<T>::sqrt_(e1[0] * e1[0] + e1[1] * e1[1]);
+    const T tb = T(C_BB_TOL) / PM<T>::sqrt_(e3[0] * e3[0] + e3[1] * e3[1]);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      const T cx = su[q] * A - P[0][0], cy = sv[q] * B - P[0][1];
+      const T cx = su[q] * sr[iu] - P[0][0], cy = sv[q] * sr[iv] - P[0][1];
       const T al = (cx * e3[1] - cy * e3[0]) / det, be = (e1[0] * cy - e1[1] * cx) / det;
-      if (al > 0 && al < 1 && be > 0 && be < 1) emit(su[q] * A, sv[q] * B, P[0][2] + al * e1[2] + be * e3[2]);
+      if (al > ta && al < 1 - ta && be > tb && be < 1 - tb)
+        emit(su[q] * sr[iu], sv[q] * sr[iv], P[0][2] + al * e1[2] + be * e3[2]);
     }
   }
 }
@@ -241,7 +247,7 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
     const T ra = s1[0] * fabs(AB[0][j]) + s1[1] * fabs(AB[1][j]) + s1[2] * fabs(AB[2][j]);
     const T sep = fabs(tl) - ra - s2[j];
     if (sep > margin) return;
-    if (sep > best) { best = sep; btype = 1; bj = j; for (int k = 0; k < 3; k++) bestn[k] = tl >= 0 ? Bm[j][k] : -Bm[j][k]; }
+    if (sep > best + T(C_BB_TOL)) { best = sep; btype = 1; bj = j; for (int k = 0; k < 3; k++) bestn[k] = tl >= 0 ? Bm[j][k] : -Bm[j][k]; }
   }
   for (int i = 0; i < 3; i++)
     for (int j = 0; j < 3; j++) {
@@ -289,6 +295,314 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
 }
 
 // mju_makeFrame: complete the contact frame from its normal (colliders set the normal only)
+// ---------------------------------------------------------------- convex pairs (MPR)
+// oracle/convex.c restated on the device (MuJoCo 2.3.3 mjc_Convex = libccd ccdMPRPenetration):
+// same control flow, tolerances scaled to T's epsilon; the portal lives in registers (every
+// index below is a compile-time constant).
+template <typename T>
+struct CShape {
+  int type, mesh;
+  T pos[3], R[9], size[3], margin;
+};
+template <typename T>
+struct SVert {
+  T v[3], v1[3], v2[3];
+};
+template <typename T> __device__ __forceinline__ T ccd_eps() { return PM<T>::eps(); }
+template <typename T> __device__ __forceinline__ bool ccd_zero(T x) { return fabs(x) < ccd_eps<T>(); }
+template <typename T>
+__device__ __forceinline__ bool ccd_eq(T a, T b) {
+  const T ab = fabs(a - b);
+  if (ab < ccd_eps<T>()) return true;
+  a = fabs(a);
+  b = fabs(b);
+  return b > a ? ab < ccd_eps<T>() * b : ab < ccd_eps<T>() * a;
+}
+template <typename T> __device__ __forceinline__ T cd3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+template <typename T>
+__device__ __forceinline__ void cc3(T* r, const T* a, const T* b) {
+  const T t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+template <typename T> __device__ __forceinline__ void cs3(T* r, const T* a, const T* b) { r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2]; }
+template <typename T>
+__device__ __forceinline__ void cnorm(T* v) {
+  const T n = PM<T>::sqrt_(cd3(v, v));
+  v[0] /= n; v[1] /= n; v[2] /= n;
+}
+template <typename T>
+__device__ void c_support(const DevPhys<T>& m, const CShape<T>& s, const T* d, T* out) {
+  T ld[3];
+  for (int k = 0; k < 3; k++) ld[k] = s.R[k] * d[0] + s.R[3 + k] * d[1] + s.R[6 + k] * d[2];
+  T lp[3];
+  if (s.type == 2) {
+    for (int k = 0; k < 3; k++) lp[k] = ld[k] * s.size[0];
+  } else if (s.type == 6) {
+    for (int k = 0; k < 3; k++) lp[k] = ld[k] >= T(-1e-12) ? s.size[k] : -s.size[k];
+  } else {
+    // first vertex within the tie band of the maximum (oracle/convex.c support)
+    const int a = m.mesh_vertadr[s.mesh], n = m.mesh_vertnum[s.mesh];
+    T bd = T(-1e30);
+    for (int i = 0; i < n; i++) {
+      const T* V = m.mesh_vert[a + i];
+      bd = fmax(bd, V[0] * ld[0] + V[1] * ld[1] + V[2] * ld[2]);
+    }
+    int best = 0;
+    for (int i = 0; i < n; i++) {
+      const T* V = m.mesh_vert[a + i];
+      if (V[0] * ld[0] + V[1] * ld[1] + V[2] * ld[2] >= bd - T(1e-9)) { best = i; break; }
+    }
+    const T* V = m.mesh_vert[a + best];
+    lp[0] = V[0]; lp[1] = V[1]; lp[2] = V[2];
+  }
+  for (int k = 0; k < 3; k++)
+    out[k] = s.pos[k] + s.R[3 * k] * lp[0] + s.R[3 * k + 1] * lp[1] + s.R[3 * k + 2] * lp[2] + T(0.5) * s.margin * d[k];
+}
+template <typename T>
+__device__ __forceinline__ void c_mksupport(const DevPhys<T>& m, const CShape<T>& a, const CShape<T>& b, const T* d, SVert<T>& v) {
+  const T nd[3] = {-d[0], -d[1], -d[2]};
+  c_support(m, a, d, v.v1);
+  c_support(m, b, nd, v.v2);
+  cs3(v.v, v.v1, v.v2);
+}
+template <typename T>
+__device__ __forceinline__ void c_portal_dir(const SVert<T>& p1, const SVert<T>& p2, const SVert<T>& p3, T* dir) {
+  T a[3], b[3];
+  cs3(a, p2.v, p1.v);
+  cs3(b, p3.v, p1.v);
+  cc3(dir, a, b);
+  cnorm(dir);
+}
+template <typename T>
+__device__ __forceinline__ bool c_reach_tol(const SVert<T>& p1, const SVert<T>& p2, const SVert<T>& p3, const SVert<T>& v4,
+                                            const T* dir, T tol) {
+  const T dv4 = cd3(v4.v, dir);
+  T t1 = dv4 - cd3(p1.v, dir), t2 = dv4 - cd3(p2.v, dir), t3 = dv4 - cd3(p3.v, dir);
+  t1 = t1 < t2 ? t1 : t2;
+  t1 = t1 < t3 ? t1 : t3;
+  return ccd_eq(t1, tol) || t1 < tol;
+}
+template <typename T>
+__device__ __forceinline__ void c_expand(SVert<T>& p0, SVert<T>& p1, SVert<T>& p2, SVert<T>& p3, const SVert<T>& v4) {
+  T v4v0[3];
+  cc3(v4v0, v4.v, p0.v);
+  if (cd3(p1.v, v4v0) > 0) {
+    if (cd3(p2.v, v4v0) > 0) p1 = v4;
+    else p3 = v4;
+  } else {
+    if (cd3(p3.v, v4v0) > 0) p2 = v4;
+    else p1 = v4;
+  }
+}
+template <typename T>
+__device__ T c_seg_dist2(const T* P, const T* x0, const T* b, T* w) {
+  T d[3], a[3];
+  cs3(d, b, x0);
+  cs3(a, x0, P);
+  const T t = -cd3(a, d) / cd3(d, d);
+  if (t < 0 || ccd_zero(t)) {
+    w[0] = x0[0]; w[1] = x0[1]; w[2] = x0[2];
+  } else if (t > 1 || ccd_eq(t, T(1))) {
+    w[0] = b[0]; w[1] = b[1]; w[2] = b[2];
+  } else {
+    for (int k = 0; k < 3; k++) w[k] = d[k] * t + x0[k];
+  }
+  T e[3];
+  cs3(e, w, P);
+  return cd3(e, e);
+}
+template <typename T>
+__device__ T c_tri_dist2(const T* P, const T* x0, const T* B, const T* C, T* w) {
+  T d1[3], d2[3], a[3];
+  cs3(d1, B, x0);
+  cs3(d2, C, x0);
+  cs3(a, x0, P);
+  const T v = cd3(d1, d1), ww = cd3(d2, d2), p = cd3(a, d1), q = cd3(a, d2), r = cd3(d1, d2);
+  const T det = ww * v - r * r;
+  T s, t;
+  if (ccd_zero(det)) {
+    s = t = T(-1);
+  } else {
+    s = (q * r - ww * p) / det;
+    t = (-s * r - q) / ww;
+  }
+  if ((ccd_zero(s) || s > 0) && (ccd_eq(s, T(1)) || s < 1) && (ccd_zero(t) || t > 0) && (ccd_eq(t, T(1)) || t < 1) &&
+      (ccd_eq(t + s, T(1)) || t + s < 1)) {
+    for (int k = 0; k < 3; k++) w[k] = x0[k] + d1[k] * s + d2[k] * t;
+    T e[3];
+    cs3(e, w, P);
+    return cd3(e, e);
+  }
+  T w2[3];
+  T dist = c_seg_dist2(P, x0, B, w);
+  T dist2 = c_seg_dist2(P, x0, C, w2);
+  if (dist2 < dist) { dist = dist2; w[0] = w2[0]; w[1] = w2[1]; w[2] = w2[2]; }
+  dist2 = c_seg_dist2(P, B, C, w2);
+  if (dist2 < dist) { dist = dist2; w[0] = w2[0]; w[1] = w2[1]; w[2] = w2[2]; }
+  return dist;
+}
+
+// ccdMPRPenetration: true and (depth, dir, pos) on intersection
+template <typename T>
+__device__ bool c_mpr(const DevPhys<T>& m, const CShape<T>& A, const CShape<T>& Bs, T& depth, T* dir, T* pos) {
+  const T tol = T(1e-6);   // mjOption mpr_tolerance
+  SVert<T> p0, p1, p2, p3, v4;
+  T d[3], va[3], vb[3], dot;
+  // ---- discover portal
+  for (int k = 0; k < 3; k++) { p0.v1[k] = A.pos[k]; p0.v2[k] = Bs.pos[k]; }
+  cs3(p0.v, p0.v1, p0.v2);
+  if (p0.v[0] == 0 && p0.v[1] == 0 && p0.v[2] == 0) p0.v[0] += ccd_eps<T>() * T(10);
+  d[0] = -p0.v[0]; d[1] = -p0.v[1]; d[2] = -p0.v[2];
+  cnorm(d);
+  c_mksupport(m, A, Bs, d, p1);
+  dot = cd3(p1.v, d);
+  if (ccd_zero(dot) || dot < 0) return false;
+  cc3(d, p0.v, p1.v);
+  if (ccd_zero(cd3(d, d))) {
+    for (int k = 0; k < 3; k++) pos[k] = T(0.5) * (p1.v1[k] + p1.v2[k]);
+    if (p1.v[0] == 0 && p1.v[1] == 0 && p1.v[2] == 0) {   // touching on v1
+      depth = 0;
+      dir[0] = dir[1] = dir[2] = 0;
+      return true;
+    }
+    for (int k = 0; k < 3; k++) dir[k] = p1.v[k];          // origin on the segment v0-v1
+    depth = PM<T>::sqrt_(cd3(dir, dir));
+    cnorm(dir);
+    return true;
+  }
+  cnorm(d);
+  c_mksupport(m, A, Bs, d, p2);
+  dot = cd3(p2.v, d);
+  if (ccd_zero(dot) || dot < 0) return false;
+  cs3(va, p1.v, p0.v);
+  cs3(vb, p2.v, p0.v);
+  cc3(d, va, vb);
+  cnorm(d);
+  if (cd3(d, p0.v) > 0) {
+    const SVert<T> t = p1;
+    p1 = p2;
+    p2 = t;
+    d[0] = -d[0]; d[1] = -d[1]; d[2] = -d[2];
+  }
+  bool found = false;
+  for (int guard = 0; guard < 1000 && !found; guard++) {
+    c_mksupport(m, A, Bs, d, p3);
+    dot = cd3(p3.v, d);
+    if (ccd_zero(dot) || dot < 0) return false;
+    bool cont = false;
+    cc3(va, p1.v, p3.v);
+    dot = cd3(va, p0.v);
+    if (dot < 0 && !ccd_zero(dot)) { p2 = p3; cont = true; }
+    if (!cont) {
+      cc3(va, p3.v, p2.v);
+      dot = cd3(va, p0.v);
+      if (dot < 0 && !ccd_zero(dot)) { p1 = p3; cont = true; }
+    }
+    if (!cont) {
+      found = true;
+    } else {
+      cs3(va, p1.v, p0.v);
+      cs3(vb, p2.v, p0.v);
+      cc3(d, va, vb);
+      cnorm(d);
+    }
+  }
+  if (!found) return false;
+  // ---- refine until the portal contains the origin
+  bool inside = false;
+  for (int guard = 0; guard < 1000 && !inside; guard++) {
+    c_portal_dir(p1, p2, p3, d);
+    dot = cd3(d, p1.v);
+    if (ccd_zero(dot) || dot > 0) { inside = true; break; }
+    c_mksupport(m, A, Bs, d, v4);
+    dot = cd3(v4.v, d);
+    if (!(ccd_zero(dot) || dot > 0) || c_reach_tol(p1, p2, p3, v4, d, tol)) return false;
+    c_expand(p0, p1, p2, p3, v4);
+  }
+  if (!inside) return false;
+  // ---- penetration: refine towards the surface
+  for (int it = 0;; it++) {
+    c_portal_dir(p1, p2, p3, d);
+    c_mksupport(m, A, Bs, d, v4);
+    if (c_reach_tol(p1, p2, p3, v4, d, tol) || it > 50) {
+      const T O[3] = {0, 0, 0};
+      depth = PM<T>::sqrt_(c_tri_dist2(O, p1.v, p2.v, p3.v, dir));
+      if (ccd_zero(depth)) dir[0] = dir[1] = dir[2] = 0;
+      else cnorm(dir);
+      // contact position: barycentric mix of the supports (findPos)
+      T vec[3], b0, b1, b2, b3;
+      c_portal_dir(p1, p2, p3, d);
+      cc3(vec, p1.v, p2.v); b0 = cd3(vec, p3.v);
+      cc3(vec, p3.v, p2.v); b1 = cd3(vec, p0.v);
+      cc3(vec, p0.v, p1.v); b2 = cd3(vec, p3.v);
+      cc3(vec, p2.v, p1.v); b3 = cd3(vec, p0.v);
+      T sum = b0 + b1 + b2 + b3;
+      if (ccd_zero(sum) || sum < 0) {
+        b0 = 0;
+        cc3(vec, p2.v, p3.v); b1 = cd3(vec, d);
+        cc3(vec, p3.v, p1.v); b2 = cd3(vec, d);
+        cc3(vec, p1.v, p2.v); b3 = cd3(vec, d);
+        sum = b1 + b2 + b3;
+      }
+      const T inv = T(1) / sum;
+      for (int k = 0; k < 3; k++) {
+        const T q1 = b0 * p0.v1[k] + b1 * p1.v1[k] + b2 * p2.v1[k] + b3 * p3.v1[k];
+        const T q2 = b0 * p0.v2[k] + b1 * p1.v2[k] + b2 * p2.v2[k] + b3 * p3.v2[k];
+        pos[k] = T(0.5) * (q1 * inv + q2 * inv);
+      }
+      return true;
+    }
+    c_expand(p0, p1, p2, p3, v4);
+  }
+}
+
+// oriented-box separating-axis test (15 axes), boxes inflated by margin
+template <typename T>
+__device__ bool c_obb_disjoint(const T* p1, const T* R1, const T* h1, const T* p2, const T* R2, const T* h2, T margin) {
+  T A[3][3], B[3][3], Tv[3];
+  for (int i = 0; i < 3; i++)
+    for (int k = 0; k < 3; k++) { A[i][k] = R1[3 * k + i]; B[i][k] = R2[3 * k + i]; }
+  cs3(Tv, p2, p1);
+#pragma unroll
+  for (int a = 0; a < 15; a++) {
+    T L[3];
+    if (a < 3) { L[0] = A[a][0]; L[1] = A[a][1]; L[2] = A[a][2]; }
+    else if (a < 6) { L[0] = B[a - 3][0]; L[1] = B[a - 3][1]; L[2] = B[a - 3][2]; }
+    else cc3(L, A[(a - 6) / 3], B[(a - 6) % 3]);
+    const T len2 = cd3(L, L);
+    if (len2 < T(1e-12)) continue;
+    T ra = 0, rb = 0;
+    for (int k = 0; k < 3; k++) { ra += h1[k] * fabs(cd3(A[k], L)); rb += h2[k] * fabs(cd3(B[k], L)); }
+    if (fabs(cd3(Tv, L)) > ra + rb + margin * PM<T>::sqrt_(len2)) return true;
+  }
+  return false;
+}
+
+// mjc_Convex for (sphere | box | mesh) x mesh: at most one contact
+template <typename T>
+__device__ bool c_convex(const DevPhys<T>& m, const Env<T>& s, int g1, int g2, T margin, T& dist, T* pos, T* nrm) {
+  CShape<T> sh[2];
+  T bp[2][3];
+  const int gs[2] = {g1, g2};
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const int g = gs[i];
+    sh[i].type = m.geom_type[g];
+    sh[i].mesh = m.geom_dataid[g];
+    sh[i].margin = margin;
+    for (int k = 0; k < 3; k++) { sh[i].pos[k] = s.gpos[g][k]; sh[i].size[k] = m.geom_size[g][k]; }
+    for (int k = 0; k < 9; k++) sh[i].R[k] = s.gmat[g][k];
+    const T* c = m.geom_aabb[g];
+    for (int k = 0; k < 3; k++) bp[i][k] = sh[i].pos[k] + sh[i].R[3 * k] * c[0] + sh[i].R[3 * k + 1] * c[1] + sh[i].R[3 * k + 2] * c[2];
+  }
+  if (c_obb_disjoint(bp[0], sh[0].R, m.geom_aabb[g1] + 3, bp[1], sh[1].R, m.geom_aabb[g2] + 3, margin)) return false;
+  T depth;
+  if (!c_mpr(m, sh[0], sh[1], depth, nrm, pos)) return false;
+  if (nrm[0] == 0 && nrm[1] == 0 && nrm[2] == 0) return false;
+  dist = margin - depth;
+  return true;
+}
+
 template <typename T>
 __device__ void t_makeframe(T f[9]) {
   t_normalize3(f);
@@ -340,4 +654,8 @@ __device__ void collide_pair(const DevPhys<T>& m, const Env<T>& s, int pair, S& 
   else if (t1 == 2 && t2 == 2) c_sphere_sphere(p1, s1[0], p2, s2[0], margin, out);
   else if (t1 == 2 && t2 == 6) c_sphere_box(p1, s1[0], p2, R2, s2, margin, out);
   else if (t1 == 6 && t2 == 6) c_box_box(p1, R1, s1, p2, R2, s2, margin, out);
+  else if (t2 == 7 && t1 != 0) {
+    T dist, pos[3], nrm[3];
+    if (c_convex(m, s, g1, g2, margin, dist, pos, nrm)) out.emit(dist, pos, nrm);
+  }
 }

@@ -152,8 +152,6 @@ int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
       ne++;
     }
   d->nmentry = ne;
-  T mi = 0;
-  d->meaninertia = mi;
   // ---- collidable geoms + pairs
   int ng = 0, map[512];
   for (int g = 0; g < s->ngeom && g < 512; g++) {
@@ -179,6 +177,26 @@ int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
     d->geom_gap[ng] = (T)s->geom_gap[g];
     d->geom_solmix[ng] = (T)s->geom_solmix[g];
     d->geom_rbound[ng] = (T)s->geom_rbound[g];
+    {   // geom-frame bounding box (oracle/convex.c local_box)
+      double c[3] = {0, 0, 0}, h[3] = {0, 0, 0};
+      const int ty = s->geom_type[g];
+      if (ty == 2) {
+        h[0] = h[1] = h[2] = s->geom_size[3 * g];
+      } else if (ty == 6) {
+        for (int k = 0; k < 3; k++) h[k] = s->geom_size[3 * g + k];
+      } else if (ty == 7 && s->geom_dataid[g] >= 0) {
+        const int mesh = s->geom_dataid[g];
+        const double* V = s->mesh_vert + 3 * s->mesh_vertadr[mesh];
+        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+        for (int i = 0; i < s->mesh_vertnum[mesh]; i++)
+          for (int k = 0; k < 3; k++) {
+            lo[k] = V[3 * i + k] < lo[k] ? V[3 * i + k] : lo[k];
+            hi[k] = V[3 * i + k] > hi[k] ? V[3 * i + k] : hi[k];
+          }
+        for (int k = 0; k < 3; k++) { c[k] = 0.5 * (lo[k] + hi[k]); h[k] = 0.5 * (hi[k] - lo[k]); }
+      }
+      for (int k = 0; k < 3; k++) { d->geom_aabb[ng][k] = (T)c[k]; d->geom_aabb[ng][3 + k] = (T)h[k]; }
+    }
     if (s->geom_type[g] != 0 && s->geom_type[g] != 2 && s->geom_type[g] != 6 && s->geom_type[g] != 7) {
       snprintf(err, errlen, "geom type %d not supported by the step kernel", s->geom_type[g]);
       return -1;

@@ -40,7 +40,6 @@ struct DevPhys {
   int nq, nv, nu, nbody, njnt, ngeom, npair, nmocap, neq, ntree, nmentry;
   T timestep, gravity[3];
   int noslip_iterations, iterations;
-  T meaninertia;
   // bodies
   int body_parentid[PH_MAXB], body_rootid[PH_MAXB], body_weldid[PH_MAXB], body_mocapid[PH_MAXB];
   int body_jntadr[PH_MAXB], body_jntnum[PH_MAXB], body_dofadr[PH_MAXB], body_dofnum[PH_MAXB];
@@ -71,6 +70,7 @@ struct DevPhys {
   T geom_size[PH_MAXG][3], geom_pos[PH_MAXG][3], geom_quat[PH_MAXG][4], geom_friction[PH_MAXG][3];
   T geom_solref[PH_MAXG][2], geom_solimp[PH_MAXG][5], geom_margin[PH_MAXG], geom_gap[PH_MAXG];
   T geom_solmix[PH_MAXG], geom_rbound[PH_MAXG];
+  T geom_aabb[PH_MAXG][6];   // geom-frame bounding box: centre (3), half extents (3) (OBB pre-test)
   int pair_g1[PH_MAXPAIR], pair_g2[PH_MAXPAIR];   // compact geom ids, g1 has the lower type
   // meshes (convex hulls)
   int mesh_vertadr[PH_MAXMESH], mesh_vertnum[PH_MAXMESH];

@@ -1268,8 +1268,10 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
   T cost = l < s.nisland ? s.isl_cost[l] : T(0);
   bool done = l >= s.nisland;
   int unchanged = 0;                      // consecutive steps that kept the island's active set
-  // gradient floor of a converged island (scaled like the oracle: 1 / (meaninertia * nv))
-  const T gscale = T(1) / (m.meaninertia * T(m.nv > 1 ? m.nv : 1));
+  // gradient floor of a converged island, scaled like the oracle: 1 / (meaninertia * nv) with
+  // meaninertia = mean of diag(M) of this step
+  const T meaninertia = wsum(l < m.nv ? s.M[mblk(m, l, l)] : T(0)) / T(m.nv);
+  const T gscale = T(1) / (meaninertia * T(m.nv > 1 ? m.nv : 1));
   const T gtol = T(100) * PM<T>::eps();
   int it = 0;
   const int nent = s.isl_eoff[s.nisland];

@@ -149,6 +149,12 @@ static int sphere_box(const double* p1, double r, const double* p2, const double
   return 1;
 }
 
+/* 1 um band that moves box-box decisions off exact configurations: identical boxes pressed face
+ * to face (the closed gripper's finger pads) put every clip / corner / SAT-tie / inclusion test
+ * exactly on its boundary, where rounding (FMA or not) would decide.  Applied identically by
+ * the device colliders. */
+#define BB_TOL 1e-6
+
 /* Liang-Barsky: clip the 2D segment p0 -> p1 (x, y = coords 0, 1) to |x| <= A, |y| <= B (closed);
  * returns 0 when nothing is left, else the parameter interval [t0, t1] */
 static int clip_seg(const double* p0, const double* p1, double A, double B, double* t0, double* t1) {
@@ -202,7 +208,7 @@ static int box_face_contacts(const double* pr, const double* Rr, const double* s
     for (int k = 0; k < 3; k++) w[k] = pi[k] + sg * bj[k] * si[ja] + su[q] * bu[k] * si[ju] + sv[q] * bv[k] * si[jv] - cref[k];
     P[q][0] = dot3(w, u); P[q][1] = dot3(w, v); P[q][2] = dot3(w, nr);
   }
-  const double A = sr[iu], B = sr[iv];
+  const double A = sr[iu] + BB_TOL, B = sr[iv] + BB_TOL;   /* rectangle grown by the band */
   double pts[12][3];
   int np = 0;
   for (int e = 0; e < 4; e++) {
@@ -222,12 +228,14 @@ static int box_face_contacts(const double* pr, const double* Rr, const double* s
   const double e3[3] = {P[3][0] - P[0][0], P[3][1] - P[0][1], P[3][2] - P[0][2]};
   const double det = e1[0] * e3[1] - e1[1] * e3[0];
   if (fabs(det) > 1e-12 * (fabs(e1[0]) + fabs(e1[1])) * (fabs(e3[0]) + fabs(e3[1]))) {
+    /* corners more than the band inside the incident face (in its edge coordinates) */
+    const double ta = BB_TOL / sqrt(e1[0] * e1[0] + e1[1] * e1[1]), tb = BB_TOL / sqrt(e3[0] * e3[0] + e3[1] * e3[1]);
     for (int q = 0; q < 4; q++) {
-      const double cx = su[q] * A - P[0][0], cy = sv[q] * B - P[0][1];
+      const double cx = su[q] * sr[iu] - P[0][0], cy = sv[q] * sr[iv] - P[0][1];
       const double al = (cx * e3[1] - cy * e3[0]) / det, be = (e1[0] * cy - e1[1] * cx) / det;
-      if (al > 0 && al < 1 && be > 0 && be < 1) {
-        pts[np][0] = su[q] * A;
-        pts[np][1] = sv[q] * B;
+      if (al > ta && al < 1 - ta && be > tb && be < 1 - tb) {
+        pts[np][0] = su[q] * sr[iu];
+        pts[np][1] = sv[q] * sr[iv];
         pts[np][2] = P[0][2] + al * e1[2] + be * e3[2];
         np++;
       }
@@ -236,7 +244,7 @@ static int box_face_contacts(const double* pr, const double* Rr, const double* s
   int cnt = 0;
   for (int q = 0; q < np && cnt < 8; q++) {
     double dist = pts[q][2];
-    if (dist > margin) continue;
+    if (dist > margin + BB_TOL) continue;
     c[cnt].dist = dist;
     set_normal(c + cnt, nframe);
     for (int k = 0; k < 3; k++)
@@ -268,7 +276,8 @@ static int box_box(const double* p1, const double* R1, const double* s1, const d
     double ra = s1[0] * fabs(AB[0][j]) + s1[1] * fabs(AB[1][j]) + s1[2] * fabs(AB[2][j]);
     double sep = fabs(tl) - ra - s2[j];
     if (sep > margin) return 0;
-    if (sep > best) { best = sep; btype = 1; bj = j; for (int k = 0; k < 3; k++) bestn[k] = tl >= 0 ? B[j][k] : -B[j][k]; }
+    /* box 2's faces replace box 1's only when clearly better (ties: identical boxes face to face) */
+    if (sep > best + BB_TOL) { best = sep; btype = 1; bj = j; for (int k = 0; k < 3; k++) bestn[k] = tl >= 0 ? B[j][k] : -B[j][k]; }
   }
   for (int i = 0; i < 3; i++)
     for (int j = 0; j < 3; j++) {

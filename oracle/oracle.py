@@ -146,6 +146,8 @@ def _phys_lib():
         L.orc_step.argtypes = [P, P]
         L.orc_field.argtypes = [P, P, C.c_char_p, P, C.c_int]
         L.orc_field.restype = C.c_int
+        L.orc_convex_probe.argtypes = [P, P, C.c_int, C.c_int, P, P, P]
+        L.orc_convex_probe.restype = C.c_int
         L._phys_ready = True
     return L
 
@@ -192,5 +194,27 @@ def forward_fields(state_row, fields, model=None, do_step=False):
                 raise KeyError(f)
             out[f] = buf[:n].copy()
         return out
+    finally:
+        L.orc_data_free(d)
+
+
+def convex_probe(state_row, g1, g2, model=None):
+    """MPR (convex.c) on geoms g1, g2 after one forward at state_row: (dist, pos, normal) or None,
+    plus the geom frames used: returns (hit, geom_xpos [ngeom,3], geom_xmat [ngeom,9])."""
+    m = model or load_model()
+    L = _phys_lib()
+    d = L.orc_data_new()
+    try:
+        arrs = [np.ascontiguousarray(state_row[k], np.float64) for k in STATE_KEYS[:6]]
+        L.orc_set_state(_desc_ptr(m), d, *[_p(a) for a in arrs])
+        L.orc_forward(_desc_ptr(m), d)
+        dist, pos, nrm = np.zeros(1), np.zeros(3), np.zeros(3)
+        hit = L.orc_convex_probe(_desc_ptr(m), d, int(g1), int(g2), _p(dist), _p(pos), _p(nrm))
+        buf = np.zeros(200000)
+        n = L.orc_field(_desc_ptr(m), d, b"geom_xpos", _p(buf), buf.size)
+        gx = buf[:n].reshape(-1, 3).copy()
+        n = L.orc_field(_desc_ptr(m), d, b"geom_xmat", _p(buf), buf.size)
+        gm = buf[:n].reshape(-1, 9).copy()
+        return ((float(dist[0]), pos, nrm) if hit else None), gx, gm
     finally:
         L.orc_data_free(d)

@@ -122,3 +122,67 @@ def test_settled_scene_is_at_rest(model):
         d = int(model.jnt_dofadr[model.joint_id(name)])
         assert np.abs(st["qvel"][:, d:d + 6]).max() < 5e-3, name
     assert (st["warn"] == 0).all()
+
+
+# ---------------------------------------------------------------- convex (MPR) narrowphase
+def _gid(model, name):
+    return list(model.names_geom).index(name)
+
+
+def test_mpr_matches_sat_on_resting_cube(model):
+    """MPR (convex.c) on a box-box pair equals the exact SAT face-contact depth and normal."""
+    st = PS.settled_states(2, seed=0, nsettle=100, model=model)
+    for b in range(2):
+        row = _row(st, b)
+        f = O.forward_fields(row, ["contact", "ncon"], model=model)
+        c = f["contact"].reshape(int(f["ncon"][0]), 30)
+        g1, g2 = _gid(model, "shelf_board2"), _gid(model, "cube1_geom")
+        sat = c[(c[:, 27] == g1) & (c[:, 28] == g2)]
+        hit, _, _ = O.convex_probe(row, g1, g2, model=model)
+        assert hit is not None and len(sat)
+        assert abs(hit[0] - sat[:, 12].min()) < 1e-9
+        assert np.allclose(hit[2], [0, 0, 1], atol=1e-9)
+
+
+def _hand_in_cube(model):
+    st = PS.reset_states(1, seed=0, model=model)
+    sx, _ = O.site_kinematics(st["qpos"], model=model)
+    a = int(model.jnt_qposadr[model.joint_id("cube1_joint")])
+    st["qpos"][0, a:a + 3] = sx[0, model.site_id("ee_center_site")] + [0.0, 0.0, 0.075]   # into the palm
+    return st
+
+
+def test_mpr_depth_is_the_support_gap(model):
+    """At MPR's termination the depth equals the Minkowski support gap along its direction,
+    h(dir) = max_a a.dir - min_b b.dir, within mpr_tolerance."""
+    st = _hand_in_cube(model)
+    row = _row(st, 0)
+    g_box, g_mesh = _gid(model, "cube1_geom"), 69           # the hand's collision mesh
+    assert model.geom_type[g_mesh] == 7 and model.geom_type[g_box] == 6
+    hit, gx, gm = O.convex_probe(row, g_box, g_mesh, model=model)
+    assert hit is not None, "hand mesh and cube overlap"
+    dist, pos, n = hit
+    R = gm[g_box].reshape(3, 3)
+    s = model.geom_size[g_box]
+    corners = np.array([[i, j, k] for i in (-1, 1) for j in (-1, 1) for k in (-1, 1)]) * s
+    wa = gx[g_box] + corners @ R.T
+    mesh = int(model.geom_dataid[g_mesh])
+    V = model.mesh_vert[model.mesh_vertadr[mesh]:model.mesh_vertadr[mesh] + model.mesh_vertnum[mesh]]
+    wb = gx[g_mesh] + V @ gm[g_mesh].reshape(3, 3).T
+    h = (wa @ n).max() - (wb @ n).min()
+    assert np.isclose(np.linalg.norm(n), 1.0)
+    assert -dist <= h + 1e-12 and h - (-dist) < 2e-6
+    # the contact point lies between the two bodies' support planes along n
+    assert (wb @ n).min() - 1e-9 <= pos @ n <= (wa @ n).max() + 1e-9
+
+
+def test_mpr_separated_and_contact_list(model):
+    st = _hand_in_cube(model)
+    f = O.forward_fields(_row(st, 0), ["contact", "ncon"], model=model)
+    c = f["contact"].reshape(int(f["ncon"][0]), 30)
+    g_box = _gid(model, "cube1_geom")
+    mesh_rows = c[(c[:, 27] == g_box) & np.isin(c[:, 28], np.nonzero(model.geom_type == 7)[0])]
+    assert len(mesh_rows) >= 1 and np.all(mesh_rows[:, 12] < 0)        # box-mesh contacts present
+    far = PS.reset_states(1, seed=0, model=model)
+    hit, _, _ = O.convex_probe(_row(far, 0), g_box, 69, model=model)
+    assert hit is None
