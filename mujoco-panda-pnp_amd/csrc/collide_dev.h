@@ -3,19 +3,15 @@
 // contact point midway between the surfaces, MuJoCo mj_contactParam mixing):
 //   plane-sphere, plane-box (corners below the plane, <= 4), plane-mesh (<= 4 deepest hull
 //   vertices), sphere-sphere, sphere-box, box-box (SAT over 15 axes + reference/incident face
-//   clipping, edge-edge).  Convex mesh vs non-plane: not yet (as in the oracle: no contact).
+//   clipping, edge-edge), and (sphere | box | mesh) x mesh by MPR (oracle/convex.c).
 // One lane runs one candidate pair; results stay in the lane's registers/scratch until the
 // wave-wide scan places them.
 #pragma once
 
-// Colliders emit contacts into a sink: CountSink only counts (phase 1 of the wave-wide ordered
-// placement), LdsSink writes straight into the env's LDS contact list (phase 2).  No per-lane
-// contact arrays, so nothing spills to scratch.
-template <typename T>
-struct CountSink {
-  int n = 0;
-  __device__ __forceinline__ void emit(T, const T*, const T*) { n++; }
-};
+// Colliders emit contacts into a sink that writes straight into the env's LDS contact list and
+// counts; with cap = 0 it only counts (phase 1 of the wave-wide ordered placement).  One sink
+// type = one copy of every collider in the kernel (instruction-cache footprint), and no
+// per-lane contact arrays, so nothing spills to scratch.
 template <typename T>
 struct LdsSink {
   Con<T>* base;
@@ -299,10 +295,19 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
 // oracle/convex.c restated on the device (MuJoCo 2.3.3 mjc_Convex = libccd ccdMPRPenetration):
 // same control flow, tolerances scaled to T's epsilon; the portal lives in registers (every
 // index below is a compile-time constant).
+//
+// Wave-cooperative: the whole wave runs MPR on ONE pair (every lane holds the same portal, so
+// all branches are uniform) and splits each mesh support map over its 64 lanes.  Lane l keeps
+// hull vertices l, l+64, l+128 in registers for the whole MPR run (C_WV per lane; larger hulls
+// stream the rest from global memory), a support is three dot products, a DPP max and a ballot
+// for the first vertex inside the tie band -- instead of 2 x nvert dependent global loads on a
+// single lane.
+constexpr int C_WV = 3;
 template <typename T>
 struct CShape {
-  int type, mesh;
+  int type, mesh, vadr, nvert;
   T pos[3], R[9], size[3], margin;
+  T wv[C_WV][3];   // mesh: vertices lane + 64 j (local frame)
 };
 template <typename T>
 struct SVert {
@@ -330,6 +335,59 @@ __device__ __forceinline__ void cnorm(T* v) {
   const T n = PM<T>::sqrt_(cd3(v, v));
   v[0] /= n; v[1] /= n; v[2] /= n;
 }
+// max over the wave (all 64 lanes active), wave-uniform result
+template <typename T>
+__device__ __forceinline__ T c_wave_max(T v) {
+  v = fmax(v, dpp_f<0xB1>(v));
+  v = fmax(v, dpp_f<0x4E>(v));
+  v = fmax(v, dpp_f<0x141>(v));
+  v = fmax(v, dpp_f<0x140>(v));
+  return fmax(fmax(rdlane(v, 0), rdlane(v, 16)), fmax(rdlane(v, 32), rdlane(v, 48)));
+}
+template <typename T>
+__device__ void c_load_shape(const DevPhys<T>& m, CShape<T>& sh) {
+  const int l = threadIdx.x;
+  sh.vadr = sh.type == 7 ? m.mesh_vertadr[sh.mesh] : 0;
+  sh.nvert = sh.type == 7 ? m.mesh_vertnum[sh.mesh] : 0;
+#pragma unroll
+  for (int j = 0; j < C_WV; j++) {
+    const int i = 64 * j + l;
+    for (int k = 0; k < 3; k++) sh.wv[j][k] = i < sh.nvert ? m.mesh_vert[sh.vadr + i][k] : T(0);
+  }
+}
+// first vertex within the tie band of the maximum (oracle/convex.c support), wave-cooperative
+template <typename T>
+__device__ int c_mesh_argmax(const DevPhys<T>& m, const CShape<T>& s, const T* ld) {
+  const int l = threadIdx.x, n = s.nvert;
+  T dv[C_WV], bd = T(-1e30);
+#pragma unroll
+  for (int j = 0; j < C_WV; j++) {
+    dv[j] = 64 * j + l < n ? s.wv[j][0] * ld[0] + s.wv[j][1] * ld[1] + s.wv[j][2] * ld[2] : T(-1e30);
+    bd = fmax(bd, dv[j]);
+  }
+  for (int i = 64 * C_WV + l; i < n; i += 64) {
+    const T* V = m.mesh_vert[s.vadr + i];
+    bd = fmax(bd, V[0] * ld[0] + V[1] * ld[1] + V[2] * ld[2]);
+  }
+  bd = c_wave_max(bd);
+  const T lo = bd - T(1e-9);
+#pragma unroll
+  for (int j = 0; j < C_WV; j++) {
+    const uint64_t b = __ballot(64 * j + l < n && dv[j] >= lo);
+    if (b) return 64 * j + __ffsll((unsigned long long)b) - 1;
+  }
+  for (int base = 64 * C_WV; base < n; base += 64) {
+    const int i = base + l;
+    bool ok = false;
+    if (i < n) {
+      const T* V = m.mesh_vert[s.vadr + i];
+      ok = V[0] * ld[0] + V[1] * ld[1] + V[2] * ld[2] >= lo;
+    }
+    const uint64_t b = __ballot(ok);
+    if (b) return base + __ffsll((unsigned long long)b) - 1;
+  }
+  return 0;
+}
 template <typename T>
 __device__ void c_support(const DevPhys<T>& m, const CShape<T>& s, const T* d, T* out) {
   T ld[3];
@@ -340,19 +398,7 @@ __device__ void c_support(const DevPhys<T>& m, const CShape<T>& s, const T* d, T
   } else if (s.type == 6) {
     for (int k = 0; k < 3; k++) lp[k] = ld[k] >= T(-1e-12) ? s.size[k] : -s.size[k];
   } else {
-    // first vertex within the tie band of the maximum (oracle/convex.c support)
-    const int a = m.mesh_vertadr[s.mesh], n = m.mesh_vertnum[s.mesh];
-    T bd = T(-1e30);
-    for (int i = 0; i < n; i++) {
-      const T* V = m.mesh_vert[a + i];
-      bd = fmax(bd, V[0] * ld[0] + V[1] * ld[1] + V[2] * ld[2]);
-    }
-    int best = 0;
-    for (int i = 0; i < n; i++) {
-      const T* V = m.mesh_vert[a + i];
-      if (V[0] * ld[0] + V[1] * ld[1] + V[2] * ld[2] >= bd - T(1e-9)) { best = i; break; }
-    }
-    const T* V = m.mesh_vert[a + best];
+    const T* V = m.mesh_vert[s.vadr + c_mesh_argmax(m, s, ld)];
     lp[0] = V[0]; lp[1] = V[1]; lp[2] = V[2];
   }
   for (int k = 0; k < 3; k++)
@@ -578,11 +624,34 @@ __device__ bool c_obb_disjoint(const T* p1, const T* R1, const T* h1, const T* p
   return false;
 }
 
-// mjc_Convex for (sphere | box | mesh) x mesh: at most one contact
+// convex pair: (sphere | box | mesh) x mesh (g1 has the lower type)
 template <typename T>
-__device__ bool c_convex(const DevPhys<T>& m, const Env<T>& s, int g1, int g2, T margin, T& dist, T* pos, T* nrm) {
-  CShape<T> sh[2];
+__device__ __forceinline__ bool c_is_convex_pair(const DevPhys<T>& m, int g1, int g2) {
+  return m.geom_type[g2] == 7 && m.geom_type[g1] != 0;
+}
+
+// oriented bounding boxes of a convex pair disjoint (broadphase: such pairs cannot touch, MPR
+// would find no contact)
+template <typename T>
+__device__ __forceinline__ bool c_convex_obb_disjoint(const DevPhys<T>& m, const Env<T>& s, int g1, int g2, T margin) {
   T bp[2][3];
+  const int gs[2] = {g1, g2};
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const int g = gs[i];
+    const T* c = m.geom_aabb[g];
+    const T* R = s.gmat[g];
+    for (int k = 0; k < 3; k++) bp[i][k] = s.gpos[g][k] + R[3 * k] * c[0] + R[3 * k + 1] * c[1] + R[3 * k + 2] * c[2];
+  }
+  return c_obb_disjoint(bp[0], s.gmat[g1], m.geom_aabb[g1] + 3, bp[1], s.gmat[g2], m.geom_aabb[g2] + 3, margin);
+}
+
+// mjc_Convex by MPR (the OBB pre-test ran in the broadphase): at most one contact.  Wave-uniform
+// call: every lane passes the same pair and gets the same result.
+template <typename T>
+__device__ __forceinline__ bool c_convex(const DevPhys<T>& m, const Env<T>& s, int g1, int g2, T margin,
+                                                    T& dist, T* pos, T* nrm) {
+  CShape<T> sh[2];
   const int gs[2] = {g1, g2};
 #pragma unroll
   for (int i = 0; i < 2; i++) {
@@ -592,10 +661,8 @@ __device__ bool c_convex(const DevPhys<T>& m, const Env<T>& s, int g1, int g2, T
     sh[i].margin = margin;
     for (int k = 0; k < 3; k++) { sh[i].pos[k] = s.gpos[g][k]; sh[i].size[k] = m.geom_size[g][k]; }
     for (int k = 0; k < 9; k++) sh[i].R[k] = s.gmat[g][k];
-    const T* c = m.geom_aabb[g];
-    for (int k = 0; k < 3; k++) bp[i][k] = sh[i].pos[k] + sh[i].R[3 * k] * c[0] + sh[i].R[3 * k + 1] * c[1] + sh[i].R[3 * k + 2] * c[2];
+    c_load_shape(m, sh[i]);
   }
-  if (c_obb_disjoint(bp[0], sh[0].R, m.geom_aabb[g1] + 3, bp[1], sh[1].R, m.geom_aabb[g2] + 3, margin)) return false;
   T depth;
   if (!c_mpr(m, sh[0], sh[1], depth, nrm, pos)) return false;
   if (nrm[0] == 0 && nrm[1] == 0 && nrm[2] == 0) return false;
@@ -654,8 +721,5 @@ __device__ void collide_pair(const DevPhys<T>& m, const Env<T>& s, int pair, S& 
   else if (t1 == 2 && t2 == 2) c_sphere_sphere(p1, s1[0], p2, s2[0], margin, out);
   else if (t1 == 2 && t2 == 6) c_sphere_box(p1, s1[0], p2, R2, s2, margin, out);
   else if (t1 == 6 && t2 == 6) c_box_box(p1, R1, s1, p2, R2, s2, margin, out);
-  else if (t2 == 7 && t1 != 0) {
-    T dist, pos[3], nrm[3];
-    if (c_convex(m, s, g1, g2, margin, dist, pos, nrm)) out.emit(dist, pos, nrm);
-  }
+  // convex pairs: st_collision's MPR pass
 }

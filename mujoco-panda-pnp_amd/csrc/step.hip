@@ -51,6 +51,8 @@ struct Env {
   T time;
   uint32_t warn;
   int ncon, nefc, ne, nisland, solver_iter;
+  int nlive, ncon_raw;     // collision: broadphase survivors, contacts before the capacity cap
+  int nconvex;             // collision: live convex (MPR) pairs
   // ---- position / velocity-stage working set (kinematics -> collision -> constraints -> RNE).
   // Dead once the solver starts, so it shares storage with the Newton Hessian H and the no-slip
   // W = M^-1 J^T (those two lifetimes do not overlap either).
@@ -538,6 +540,8 @@ __device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
         T v[3] = {s.gpos[g1][0] - s.gpos[g2][0], s.gpos[g1][1] - s.gpos[g2][1], s.gpos[g1][2] - s.gpos[g2][2]};
         keep = t_dot3(v, v) <= (r1 + r2 + mg) * (r1 + r2 + mg);
       }
+      // convex (MPR) pairs also need overlapping oriented bounding boxes
+      if (keep && c_is_convex_pair(m, g1, g2)) keep = !c_convex_obb_disjoint(m, s, g1, g2, mg);
     }
     const uint64_t bal = __ballot(keep);
     const int pos = nlive + __popcll(bal & ((1ull << l) - 1));
@@ -545,12 +549,18 @@ __device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
     nlive += __popcll(bal);
   }
   wsync();
-  // narrowphase in two passes (count, then write at the scanned offset): contact order = pair order
-  int ncon = 0;
+  // narrowphase in two passes (count, then write at the scanned offset).  Contact order: the
+  // primitive pairs in pair order, then the convex (MPR) pairs in pair order — MPR runs in a loop
+  // of its own, so its portal state never shares a register allocation with the rest of the
+  // stage (a call or inlined MPR inside the main loop slowed the whole step by 17-20 %).
+  int ncon = 0, nconvex = 0;
   for (int base = 0; base < nlive; base += NT) {
     const int k = base + l;
-    CountSink<T> cs;
-    if (k < nlive) collide_pair(m, s, s.live[k], cs);
+    LdsSink<T> cs{nullptr, 0};   // count only
+    const int pair = k < nlive ? s.live[k] : 0;
+    const bool cvx = k < nlive && c_is_convex_pair(m, m.pair_g1[pair], m.pair_g2[pair]);
+    nconvex += __popcll(__ballot(cvx));
+    if (k < nlive && !cvx) collide_pair(m, s, pair, cs);
     int incl = cs.n;
     for (int o = 1; o < 64; o <<= 1) {
       const int y = __shfl_up(incl, o);
@@ -561,12 +571,51 @@ __device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
     if (cs.n) {
       LdsSink<T> ls{s.con + off, PH_MAXCON - off};
       if (ls.cap > 0) {
-        collide_pair(m, s, s.live[k], ls);
-        const int g1 = m.pair_g1[s.live[k]], g2 = m.pair_g2[s.live[k]];
+        collide_pair(m, s, pair, ls);
+        const int g1 = m.pair_g1[pair], g2 = m.pair_g2[pair];
         for (int c = 0; c < cs.n && c < ls.cap; c++) c_params(m, s.con[off + c], g1, g2);
       }
     }
     ncon += total;
+  }
+  if (l == 0) {
+    s.nlive = nlive;
+    s.ncon_raw = ncon;
+    s.nconvex = nconvex;
+    s.ncon = min(ncon, PH_MAXCON);
+    if (ncon > PH_MAXCON) s.warn |= 8u;
+  }
+  wsync();
+}
+
+// Convex (MPR) pairs of the live list, appended after the primitive contacts.  A stage of its
+// own, out of line, and only called when the broadphase kept a convex pair: MPR's portal state
+// then never shares a register allocation with the rest of the step, and steps without convex
+// candidates pay neither its frame nor its callee-saved registers (inlined, or called
+// unconditionally, it slowed the whole step by 17-20 %).
+template <typename T>
+__device__ __attribute__((noinline)) void st_collision_convex(const DevPhys<T>& m, Env<T>& s) {
+  const int l = lane_id();
+  const int nlive = s.nlive;
+  int ncon = s.ncon_raw;
+  for (int base = 0; base < nlive; base += NT) {
+    const int k = base + l;
+    const int pair = k < nlive ? s.live[k] : 0;
+    uint64_t todo = __ballot(k < nlive && c_is_convex_pair(m, m.pair_g1[pair], m.pair_g2[pair]));
+    while (todo) {                                  // the wave takes the pairs one at a time, in order
+      const int src = __ffsll((unsigned long long)todo) - 1;
+      todo &= todo - 1;
+      const int p = __builtin_amdgcn_readlane(pair, src);
+      const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
+      T dist = 0, pos[3] = {0, 0, 0}, nrm[3] = {0, 0, 0};
+      if (!c_convex(m, s, g1, g2, fmax(m.geom_margin[g1], m.geom_margin[g2]), dist, pos, nrm)) continue;
+      if (l == 0 && ncon < PH_MAXCON) {
+        LdsSink<T> ls{s.con + ncon, 1};
+        ls.emit(dist, pos, nrm);
+        c_params(m, s.con[ncon], g1, g2);
+      }
+      ncon++;
+    }
   }
   if (l == 0) {
     if (ncon > PH_MAXCON) s.warn |= 8u;
@@ -1330,9 +1379,10 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
     // Newton direction per island (lane per island); the register path leaves H intact, the
     // in-place LDS path (merged islands > 9 dofs) consumes it
     if (!done) {
+      // one unrolled register variant (islands of <= 9 dofs padded with identity): lanes holding
+      // 6- and 9-dof islands run the same code instead of two divergent copies
       const int n = s.isl_n[l];
-      if (n <= 6) island_newton_dir_reg<T, 6>(s, l, n);
-      else if (n <= 9) island_newton_dir_reg<T, 9>(s, l, n);
+      if (n <= 9) island_newton_dir_reg<T, 9>(s, l, n);
       else island_newton_dir_lds(s, l, n);
       s.isl_hvalid[l] = n <= 9;
     }
@@ -1583,7 +1633,9 @@ __device__ void forward(const DevPhys<T>& m, Env<T>& s, StageClock& clk, double*
   st_kinematics(m, s);      clk.lap(1);
   st_compos_crb(m, s);      clk.lap(2);
   st_factor_M(m, s);        clk.lap(3);
-  st_collision(m, s);       clk.lap(4);
+  st_collision(m, s);
+  if (s.nconvex) st_collision_convex(m, s);
+  clk.lap(4);
   if (dbg) dump_contacts(m, s, dbg);
   st_constraints(m, s);     clk.lap(5);
   st_velocity(m, s);        clk.lap(6);

@@ -380,24 +380,36 @@ int orc_collide_pair(Mdl* m, const orc_data* d, int g1, int g2, orc_contact* out
   return n;
 }
 
+/* convex (MPR) pair: (sphere | box | mesh) x mesh */
+static int is_convex_pair(Mdl* m, int g1, int g2) {
+  int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  int lo = t1 < t2 ? t1 : t2, hi = t1 < t2 ? t2 : t1;
+  return hi == T_MESH && lo != T_PLANE;
+}
+
+/* Contact order: the primitive pairs in pair order, then the convex (MPR) pairs in pair order
+ * (MuJoCo's order follows its sweep-and-prune output, not geom ids; this is the order the
+ * device kernel produces, and the Gauss-Seidel noslip sweep depends on it). */
 int orc_collision(Mdl* m, orc_data* d) {
   d->ncon = 0;
-  for (int g1 = 0; g1 < m->ngeom; g1++) {
-    if (!m->geom_contype[g1] && !m->geom_conaffinity[g1]) continue;
-    for (int g2 = g1 + 1; g2 < m->ngeom; g2++) {
-      if (!m->geom_contype[g2] && !m->geom_conaffinity[g2]) continue;
-      if (geom_filter_skip(m, g1, g2)) continue;
-      double r1 = m->geom_rbound[g1], r2 = m->geom_rbound[g2];
-      double margin = fmax(m->geom_margin[g1], m->geom_margin[g2]);
-      if (r1 > 0 && r2 > 0) {
-        const double *a = d->geom_xpos + 3 * g1, *b = d->geom_xpos + 3 * g2;
-        double v[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
-        if (sqrt(dot3(v, v)) > r1 + r2 + margin) continue;
+  for (int pass = 0; pass < 2; pass++)
+    for (int g1 = 0; g1 < m->ngeom; g1++) {
+      if (!m->geom_contype[g1] && !m->geom_conaffinity[g1]) continue;
+      for (int g2 = g1 + 1; g2 < m->ngeom; g2++) {
+        if (!m->geom_contype[g2] && !m->geom_conaffinity[g2]) continue;
+        if (geom_filter_skip(m, g1, g2)) continue;
+        if (is_convex_pair(m, g1, g2) != pass) continue;
+        double r1 = m->geom_rbound[g1], r2 = m->geom_rbound[g2];
+        double margin = fmax(m->geom_margin[g1], m->geom_margin[g2]);
+        if (r1 > 0 && r2 > 0) {
+          const double *a = d->geom_xpos + 3 * g1, *b = d->geom_xpos + 3 * g2;
+          double v[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+          if (sqrt(dot3(v, v)) > r1 + r2 + margin) continue;
+        }
+        int room = ORC_MAXCON - d->ncon;
+        if (room <= 0) { d->warn |= ORC_WARN_CONTACTFULL; return d->ncon; }
+        d->ncon += orc_collide_pair(m, d, g1, g2, d->contact + d->ncon, room);
       }
-      int room = ORC_MAXCON - d->ncon;
-      if (room <= 0) { d->warn |= ORC_WARN_CONTACTFULL; return d->ncon; }
-      d->ncon += orc_collide_pair(m, d, g1, g2, d->contact + d->ncon, room);
     }
-  }
   return d->ncon;
 }

@@ -103,13 +103,28 @@ def main():
 
 
 
-def profile_stages(B=4096, nsub=10):
+def profile_stages(B=4096, nsub=10, bench_inputs=False):
     eng = get_engine()
-    st = PS.settled_states(64, seed=0, nsettle=50)
-    PS.random_ctrl(st)
-    big = {k: torch.cat([v] * (B // 64)) for k, v in to_dev(st, torch.float32).items()}
+    if bench_inputs:
+        import bench
+        big, ctrl = bench.step_inputs(eng, eng.model, 0, B)
+        big["ctrl"] = ctrl[0]
+    else:
+        st = PS.settled_states(64, seed=0, nsettle=50)
+        PS.random_ctrl(st)
+        big = {k: torch.cat([v] * (B // 64)) for k, v in to_dev(st, torch.float32).items()}
+    keep = {k: v.clone() for k, v in big.items()}
     prof = eng.step_profile(big, nsub).cpu().numpy().astype(np.float64)
     tot = prof.sum(1).mean()
+    for rep in range(3):                         # the timed (non-profiling) kernel on the same inputs
+        st2 = {k: v.clone() for k, v in keep.items()}
+        torch.cuda.synchronize()
+        t = time.time()
+        eng.step(st2, nsub)
+        torch.cuda.synchronize()
+        t = time.time() - t
+        print(f"step_kernel B={B} nsub={nsub}: {t * 1e3:.2f} ms -> {B * nsub / t / 1e6:.3f} M env-steps/s; "
+              f"implied resident waves {B * nsub * tot / nsub / t / 2.4e9:.0f} (at 2.4 GHz)")
     print(f"per env per sub-step: {tot / nsub:.0f} cycles")
     for k, name in enumerate(eng.STAGES):
         print(f"  {name:18s} {prof[:, k].mean() / nsub:10.0f} cycles  {100 * prof[:, k].mean() / tot:5.1f}%")
@@ -117,6 +132,6 @@ def profile_stages(B=4096, nsub=10):
 
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[2] == "prof":
-        profile_stages()
+        profile_stages(bench_inputs=len(sys.argv) > 3 and sys.argv[3] == "bench")
     else:
         main()
