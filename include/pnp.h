@@ -171,6 +171,16 @@ int32_t pnp_jac_site(pnp_model* model, int32_t site_id, const float* qpos, float
 int32_t pnp_jac_site_f64(pnp_model* model, int32_t site_id, const double* qpos, double* jacp,
                          int32_t B, void* stream);
 
+/* Full mj_jacSite (reference skills/ik_solver.py:70-72, and gymnasium-robotics get_site_xvelp /
+ * get_site_xvelr behind envs/panda_env.py:285-293): translational and rotational Jacobians of a
+ * site, mocap bodies placed from mocap_pos / mocap_quat (either may be NULL: model pose).
+ *   qpos[B*nq] -> jacp[B*3*nv], jacr[B*3*nv] (row-major 3 x nv per env; either may be NULL). */
+int32_t pnp_jac_site_full(pnp_model* model, int32_t site_id, const float* qpos, const float* mocap_pos,
+                          const float* mocap_quat, float* jacp, float* jacr, int32_t B, void* stream);
+int32_t pnp_jac_site_full_f64(pnp_model* model, int32_t site_id, const double* qpos,
+                              const double* mocap_pos, const double* mocap_quat, double* jacp,
+                              double* jacr, int32_t B, void* stream);
+
 /* Batched JacobianIKController.solve (reference skills/ik_solver.py:35-101), one solve per env:
  *   q_init[B*7], target[B*3] -> q_out[B*7], final_pos[B*3], pos_error[B], iterations[B],
  *   flags[B] (PNP_IK_CONVERGED | PNP_IK_SUCCESS).

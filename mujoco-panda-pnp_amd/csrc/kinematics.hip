@@ -1,4 +1,4 @@
-// kinematics.hip — batched mj_kinematics (site frames) and mj_jacSite (jacp), one thread per env.
+// kinematics.hip — batched mj_kinematics (site frames) and mj_jacSite (jacp / jacr), one thread per env.
 //
 // Reference call sites replaced: skills/ik_solver.py:58-59 and 70-72 (mj_kinematics, site_xpos,
 // mj_jacSite), envs/panda_env.py:285-293 and 337-346 (site_xpos / site_xmat / jacSite reads of
@@ -123,43 +123,59 @@ __global__ void __launch_bounds__(64) site_kinematics_kernel(
   }
 }
 
+// mj_jacSite: translational (jacp) and rotational (jacr) Jacobian of `site` over all dofs.  A dof
+// moves the site only if its joint is an ancestor of the site's body; free / ball joints turn
+// about the body frame's axes (columns of xmat), as cdof does.
 template <typename T>
 __global__ void __launch_bounds__(64) jac_site_kernel(const DevModel<T>* __restrict__ mp, int site,
                                                      const T* __restrict__ qpos,
-                                                     T* __restrict__ jacp, int B) {
+                                                     const T* __restrict__ mocap_pos,
+                                                     const T* __restrict__ mocap_quat,
+                                                     T* __restrict__ jacp, T* __restrict__ jacr, int B) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const DevModel<T>& m = *mp;
   T xpos[PNP_MAXBODY][3], xquat[PNP_MAXBODY][4], xanchor[PNP_MAXJNT][3], xaxis[PNP_MAXJNT][3];
-  d_kinematics<T>(m, qpos + (size_t)b * m.nq, nullptr, nullptr, xpos, xquat, xanchor, xaxis);
+  d_kinematics<T>(m, qpos + (size_t)b * m.nq, mocap_pos ? mocap_pos + (size_t)b * 3 * m.nmocap : nullptr,
+                  mocap_quat ? mocap_quat + (size_t)b * 4 * m.nmocap : nullptr, xpos, xquat, xanchor, xaxis);
   const int sb = m.site_bodyid[site];
   T bm[9], v[3], pt[3];
   d_quat2mat(bm, xquat[sb]);
   d_mulmatvec3(v, bm, m.site_pos[site]);
   pt[0] = xpos[sb][0] + v[0]; pt[1] = xpos[sb][1] + v[1]; pt[2] = xpos[sb][2] + v[2];
   const int nv = m.nv;
-  T* J = jacp + (size_t)b * 3 * nv;
-  for (int k = 0; k < 3 * nv; k++) J[k] = 0;
+  T* Jp = jacp ? jacp + (size_t)b * 3 * nv : nullptr;
+  T* Jr = jacr ? jacr + (size_t)b * 3 * nv : nullptr;
+  for (int k = 0; k < 3 * nv; k++) {
+    if (Jp) Jp[k] = 0;
+    if (Jr) Jr[k] = 0;
+  }
+  // one rotational axis a at dof d: jacr column a, jacp column a x (site - anchor)
+  auto put = [&](int d, const T* a, const T* r) {
+    if (Jp) {
+      Jp[0 * nv + d] = a[1] * r[2] - a[2] * r[1];
+      Jp[1 * nv + d] = a[2] * r[0] - a[0] * r[2];
+      Jp[2 * nv + d] = a[0] * r[1] - a[1] * r[0];
+    }
+    if (Jr) { Jr[0 * nv + d] = a[0]; Jr[1 * nv + d] = a[1]; Jr[2 * nv + d] = a[2]; }
+  };
   for (int bd = sb; bd > 0; bd = m.body_parentid[bd]) {
     for (int j = m.body_jntadr[bd]; j >= 0 && j < m.body_jntadr[bd] + m.body_jntnum[bd]; j++) {
       const int d = m.jnt_dofadr[j], t = m.jnt_type[j];
-      const T* ax = xaxis[j];
       const T r[3] = {pt[0] - xanchor[j][0], pt[1] - xanchor[j][1], pt[2] - xanchor[j][2]};
       if (t == 3) {
-        J[0 * nv + d] = ax[1] * r[2] - ax[2] * r[1];
-        J[1 * nv + d] = ax[2] * r[0] - ax[0] * r[2];
-        J[2 * nv + d] = ax[0] * r[1] - ax[1] * r[0];
+        put(d, xaxis[j], r);
       } else if (t == 2) {
-        J[0 * nv + d] = ax[0]; J[1 * nv + d] = ax[1]; J[2 * nv + d] = ax[2];
-      } else if (t == 0) {
+        if (Jp) { Jp[0 * nv + d] = xaxis[j][0]; Jp[1 * nv + d] = xaxis[j][1]; Jp[2 * nv + d] = xaxis[j][2]; }
+      } else {   // free (3 translational + 3 rotational dofs) or ball (3 rotational)
         T R[9];
         d_quat2mat(R, xquat[bd]);
-        for (int k = 0; k < 3; k++) J[k * nv + d + k] = 1;
+        const int dr = t == 0 ? d + 3 : d;
+        if (t == 0 && Jp)
+          for (int k = 0; k < 3; k++) Jp[k * nv + d + k] = 1;
         for (int k = 0; k < 3; k++) {
           const T a[3] = {R[0 + k], R[3 + k], R[6 + k]};
-          J[0 * nv + d + 3 + k] = a[1] * r[2] - a[2] * r[1];
-          J[1 * nv + d + 3 + k] = a[2] * r[0] - a[0] * r[2];
-          J[2 * nv + d + 3 + k] = a[0] * r[1] - a[1] * r[0];
+          put(dr + k, a, r);
         }
       }
     }
@@ -186,7 +202,21 @@ static int32_t launch_jac_site(pnp_model* model, int32_t site, const T* qpos, T*
   }
   if (B == 0) return PNP_OK;
   hipLaunchKernelGGL(jac_site_kernel<T>, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, dm,
-                     site, qpos, jacp, B);
+                     site, qpos, (const T*)nullptr, (const T*)nullptr, jacp, (T*)nullptr, B);
+  return pnp_check_launch("jac_site_kernel");
+}
+
+template <typename T>
+static int32_t launch_jac_site_full(pnp_model* model, int32_t site, const T* qpos, const T* mocap_pos,
+                                    const T* mocap_quat, T* jacp, T* jacr, int32_t B, void* stream,
+                                    const DevModel<T>* dm) {
+  if (!model || !qpos || (!jacp && !jacr) || B < 0 || site < 0 || site >= model->h.nsite) {
+    pnp_set_error("pnp_jac_site_full: bad argument");
+    return PNP_ERR_ARG;
+  }
+  if (B == 0) return PNP_OK;
+  hipLaunchKernelGGL(jac_site_kernel<T>, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, dm,
+                     site, qpos, mocap_pos, mocap_quat, jacp, jacr, B);
   return pnp_check_launch("jac_site_kernel");
 }
 
@@ -213,4 +243,18 @@ extern "C" int32_t pnp_jac_site(pnp_model* model, int32_t site_id, const float* 
 extern "C" int32_t pnp_jac_site_f64(pnp_model* model, int32_t site_id, const double* qpos,
                                     double* jacp, int32_t B, void* stream) {
   return launch_jac_site<double>(model, site_id, qpos, jacp, B, stream, model ? model->d_f64 : nullptr);
+}
+
+extern "C" int32_t pnp_jac_site_full(pnp_model* model, int32_t site_id, const float* qpos,
+                                     const float* mocap_pos, const float* mocap_quat, float* jacp,
+                                     float* jacr, int32_t B, void* stream) {
+  return launch_jac_site_full<float>(model, site_id, qpos, mocap_pos, mocap_quat, jacp, jacr, B, stream,
+                                     model ? model->d_f32 : nullptr);
+}
+
+extern "C" int32_t pnp_jac_site_full_f64(pnp_model* model, int32_t site_id, const double* qpos,
+                                         const double* mocap_pos, const double* mocap_quat,
+                                         double* jacp, double* jacr, int32_t B, void* stream) {
+  return launch_jac_site_full<double>(model, site_id, qpos, mocap_pos, mocap_quat, jacp, jacr, B, stream,
+                                      model ? model->d_f64 : nullptr);
 }

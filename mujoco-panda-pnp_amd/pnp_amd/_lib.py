@@ -15,7 +15,7 @@ ABI_VERSION = 4
 EXPORTS = [
     "pnp_abi_version", "pnp_model_desc_size", "pnp_last_error", "pnp_model_create",
     "pnp_model_destroy", "pnp_site_kinematics", "pnp_site_kinematics_f64", "pnp_jac_site",
-    "pnp_jac_site_f64", "pnp_ik_dls", "pnp_ik_dls_f64", "pnp_step", "pnp_step_f64",
+    "pnp_jac_site_f64", "pnp_jac_site_full", "pnp_jac_site_full_f64", "pnp_ik_dls", "pnp_ik_dls_f64", "pnp_step", "pnp_step_f64",
     "pnp_forward_debug", "pnp_forward_debug_f64", "pnp_step_lds_bytes", "pnp_step_profile",
     "pnp_env_params_size", "pnp_env_init", "pnp_env_init_f64", "pnp_env_reset", "pnp_env_reset_f64",
     "pnp_env_step", "pnp_env_step_f64",
@@ -95,6 +95,10 @@ def load():
     for name in ("pnp_jac_site", "pnp_jac_site_f64"):
         f = getattr(L, name)
         f.argtypes = [P, I32, P, P, I32, P]
+        f.restype = I32
+    for name in ("pnp_jac_site_full", "pnp_jac_site_full_f64"):
+        f = getattr(L, name)
+        f.argtypes = [P, I32, P, P, P, P, P, I32, P]
         f.restype = I32
     for name in ("pnp_ik_dls", "pnp_ik_dls_f64"):
         f = getattr(L, name)

@@ -86,6 +86,24 @@ class Engine:
         _lib.check(fn(self._h, sid, _ptr(qpos), _ptr(jac), B, _stream()), "pnp_jac_site")
         return jac
 
+    def jac_site_full(self, qpos, site, mocap_pos=None, mocap_quat=None, want_jacp=True, want_jacr=True):
+        """mj_jacSite: (jacp [B, 3, nv], jacr [B, 3, nv]) of `site` (either None when not wanted)."""
+        m = self.model
+        dt = qpos.dtype
+        _need(qpos, dt, (m.nq,), "qpos")
+        B = qpos.shape[0]
+        if mocap_pos is not None:
+            _need(mocap_pos, dt, (m.nmocap * 3,), "mocap_pos")
+        if mocap_quat is not None:
+            _need(mocap_quat, dt, (m.nmocap * 4,), "mocap_quat")
+        jp = torch.empty(B, 3, m.nv, dtype=dt, device=qpos.device) if want_jacp else None
+        jr = torch.empty(B, 3, m.nv, dtype=dt, device=qpos.device) if want_jacr else None
+        fn = self.lib.pnp_jac_site_full if dt == torch.float32 else self.lib.pnp_jac_site_full_f64
+        sid = site if isinstance(site, int) else m.site_id(site)
+        _lib.check(fn(self._h, sid, _ptr(qpos), _ptr(mocap_pos), _ptr(mocap_quat), _ptr(jp), _ptr(jr), B,
+                      _stream()), "pnp_jac_site_full")
+        return jp, jr
+
     # ------------------------------------------------------------------ physics
     def new_state(self, B, dtype=torch.float32):
         """Model-default state (mj_resetData) for B envs: dict of device tensors (SoA)."""

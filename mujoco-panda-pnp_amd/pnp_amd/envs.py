@@ -247,28 +247,52 @@ class FrankaShelfPNPEnv:
 
     reset(seed=None) -> (obs, {});  step(a) -> (obs, reward, terminated, truncated, info), with
     TimeLimit(max_episode_steps) truncation and no auto-reset (gym semantics).  Also the helper
-    methods the skills / behaviour tree use: get_ee_position, get_ee_orientation,
-    get_fingers_width, set_mocap_pose, home_pos, task_sequence, action_space, unwrapped.
+    methods the skills / behaviour tree use (get_ee_position, get_ee_orientation,
+    get_fingers_width, set_mocap_pose, set_joint_neutral, home_pos, task_sequence, action_space)
+    and the MuJoCo-binding objects behind ``unwrapped`` (``model``, ``data``, ``_mujoco``,
+    ``_utils``: pnp_amd/mjshim.py) that reference code such as skills/base.py:41-44 and
+    skills/move.py:79-85 reaches through.
+
+    ``self.data`` (MjData, host) is the state of record between calls, as MjData is for the
+    reference: writes to it are seen by the next step / mj_step, and every device call uploads it,
+    runs, and downloads the result in place.
     """
 
     metadata = {"render_modes": [], "render_fps": 20}
 
     def __init__(self, reward_type="dense", render_mode=None, device=None, dtype=torch.float64,
                  max_episode_steps=300, config: EnvConfig | None = None):
+        from .mjshim import MjData, MujocoShim, UtilsShim
         if render_mode not in (None,):
             raise ValueError("rendering is not part of this engine (render_mode must be None)")
         cfg = dataclasses.replace(config or EnvConfig(), max_episode_steps=max_episode_steps)
         self._b = BatchedFrankaShelfPNPEnv(1, reward_type, device=device, dtype=dtype, autoreset=False, config=cfg)
+        self.model = self._b.model
+        self.data = MjData(self.model)
+        self._mujoco = MujocoShim(self._b.engine, dtype)
+        self._utils = UtilsShim(self._mujoco)
         self.render_mode = None
         self.reward_type = reward_type
         self.task_sequence = self._b.task_sequence
         self.action_space = Box(-1.0, 1.0, (7,))
         self.home_pos = None
         self.dt = self._b.model.opt_timestep * cfg.n_substeps
+        self.neutral_joint_values = np.array(NEUTRAL)
+        self._pull()
 
     @property
     def unwrapped(self):
         return self
+
+    # ---------------------------------------------------------------- mirror <-> device
+    def _push(self):
+        self._mujoco.upload(self.data, self._b.state)
+        self._b.env["qpos_kin"][0].copy_(torch.from_numpy(np.asarray(self.data.qpos_kin, np.float64)))
+
+    def _pull(self):
+        self._mujoco.download(self.data, self._b.state)
+        self.data.qpos_kin = self._b.env["qpos_kin"][0].double().cpu().numpy()
+        self._mujoco.frames(self.data)
 
     def _np_obs(self, obs):
         return {k: v[0].double().cpu().numpy() for k, v in obs.items()}
@@ -276,7 +300,9 @@ class FrankaShelfPNPEnv:
     def reset(self, seed=None, options=None):
         if seed is not None:
             self.action_space.seed(seed)
+        self._push()
         obs = self._np_obs(self._b.reset())
+        self._pull()
         self.home_pos = self.get_ee_position().copy()               # panda_env.py:387-391
         return obs, {}
 
@@ -284,25 +310,37 @@ class FrankaShelfPNPEnv:
         a = np.asarray(action)
         if a.shape != self.action_space.shape:
             raise ValueError("Action dimension mismatch")
+        self._push()
         obs, r, term, trunc, info = self._b.step(torch.as_tensor(a[None], dtype=self._b.dtype))
+        self._pull()
         return (self._np_obs(obs), np.float32(r[0].item()), bool(term[0]), bool(trunc[0]),
                 {"is_success": np.float32(info["is_success"][0].item())})
 
     def close(self):
         pass
 
-    # ---------------------------------------------------------------- helpers
+    # ---------------------------------------------------------------- helpers (panda_env.py:317-352)
     def get_ee_position(self):
-        return self._b.get_ee_position()[0].double().cpu().numpy()
+        return self._utils.get_site_xpos(self.model, self.data, "ee_center_site")
 
     def get_ee_orientation(self):
-        return self._b.get_ee_orientation()[0].double().cpu().numpy()
+        q = np.zeros(4)
+        self._mujoco.mju_mat2Quat(q, self.data.site_xmat[self.model.site_id("ee_center_site")])
+        return q
 
     def get_fingers_width(self):
-        return float(self._b.get_fingers_width()[0])
+        """finger_joint1 + finger_joint2 qpos, a shape-(1,) array like the reference's."""
+        return (self._utils.get_joint_qpos(self.model, self.data, "finger_joint1")
+                + self._utils.get_joint_qpos(self.model, self.data, "finger_joint2"))
 
     def set_mocap_pose(self, pos, quat):
-        self._b.set_mocap_pose(np.asarray(pos)[None], np.asarray(quat)[None])
+        self._utils.set_mocap_pos(self.model, self.data, "panda_mocap", pos)
+        self._utils.set_mocap_quat(self.model, self.data, "panda_mocap", quat)
+
+    def set_joint_neutral(self):
+        names = [f"joint{i}" for i in range(1, 8)] + ["finger_joint1", "finger_joint2"]
+        for name, v in zip(names, self.neutral_joint_values):
+            self._utils.set_joint_qpos(self.model, self.data, name, v)
 
     @property
     def current_task_index(self):

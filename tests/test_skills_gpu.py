@@ -1,0 +1,109 @@
+"""The facade's MuJoCo-binding surface (pnp_amd/mjshim.py) and the skills on the device.
+
+* mj_step / mj_forward / mj_jacSite / mju_mat2Quat / mujoco_utils accessors against the oracle;
+* the reference skills' golden episode (tests/golden/make_skill_golden.py) replayed with
+  pnp_amd.skills on the real facade (FrankaShelfPNPEnv, fp64 device physics, the product IK
+  kernel inside MoveIKSkill).  Tick counts and done flags must match exactly; trajectories
+  within 1e-6 (fp64 device vs fp64 oracle over ~300 sub-steps: measured well below that).
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+import skill_harness as H
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def env():
+    from pnp_amd.envs import EnvConfig, FrankaShelfPNPEnv
+    e = FrankaShelfPNPEnv(config=EnvConfig(n_substeps=1))
+    e.reset()
+    return e
+
+
+def _oracle_state(d):
+    st = {k: np.array(v, np.float64)[None] for k, v in
+          (("qpos", d.qpos), ("qvel", d.qvel), ("ctrl", d.ctrl), ("mocap_pos", d.mocap_pos.reshape(-1)),
+           ("mocap_quat", d.mocap_quat.reshape(-1)), ("qacc_warmstart", d.qacc_warmstart))}
+    st["time"] = np.array([d.time])
+    st["warn"] = np.array([d.warn], np.uint32)
+    return st
+
+
+def test_binding_surface(env):
+    u = env.unwrapped
+    assert u.model is env.model and u.data is env.data
+    for f in ("mj_step", "mj_forward", "mj_kinematics", "mj_jacSite", "mju_mat2Quat", "mj_resetData"):
+        assert callable(getattr(u._mujoco, f))
+    d2 = copy.deepcopy(env.data)                      # skills/move.py:83-84
+    d2.qpos[:7] += 0.1
+    assert not np.allclose(d2.qpos[:7], env.data.qpos[:7])
+
+
+def test_mj_step_matches_oracle(env, model):
+    from pnp_amd.mjshim import MjData
+    d = copy.deepcopy(env.data)
+    d.ctrl[:] = model.actuator_ctrlrange[:, 0] + 0.3 * np.diff(model.actuator_ctrlrange, axis=1)[:, 0]
+    ref = _oracle_state(d)
+    env._mujoco.mj_step(env.model, d, nstep=7)
+    pre = {k: v.copy() for k, v in ref.items()}
+    O.step(pre, nsub=6, model=model)
+    qk = pre["qpos"][0].copy()
+    O.step(pre, nsub=1, model=model)
+    assert isinstance(d, MjData)
+    np.testing.assert_allclose(d.qpos, pre["qpos"][0], atol=1e-10, rtol=0)
+    np.testing.assert_allclose(d.qvel, pre["qvel"][0], atol=1e-8, rtol=0)
+    assert d.time == pytest.approx(pre["time"][0], abs=1e-12)
+    np.testing.assert_allclose(d.qpos_kin, qk, atol=1e-10, rtol=0)    # site_* = last forward
+    sx, sm = O.site_kinematics(qk[None], pre["mocap_pos"], pre["mocap_quat"], model=model)
+    np.testing.assert_allclose(d.site_xpos, sx[0], atol=1e-10, rtol=0)
+    np.testing.assert_allclose(d.site_xmat, sm[0].reshape(-1, 9), atol=1e-10, rtol=0)
+
+
+def test_mj_jacsite_and_velocities(env, model):
+    d = copy.deepcopy(env.data)
+    d.qvel[:] = np.random.default_rng(1).normal(size=model.nv)
+    env._mujoco.mj_forward(env.model, d)
+    for name in ("ee_center_site", "cube1_site", "cube3_site"):
+        sid = model.site_id(name)
+        jp, jr = np.zeros((3, model.nv)), np.zeros((3, model.nv))
+        env._mujoco.mj_jacSite(env.model, d, jp, jr, sid)
+        _, _, rjp, rjr = O.site_jac2(d.qpos[None], name, d.mocap_pos.reshape(1, -1), d.mocap_quat.reshape(1, -1),
+                                     model=model)
+        np.testing.assert_allclose(jp, rjp[0], atol=1e-12, rtol=0)
+        np.testing.assert_allclose(jr, rjr[0], atol=1e-12, rtol=0)
+        np.testing.assert_allclose(env._utils.get_site_xvelp(env.model, d, name), rjp[0] @ d.qvel, atol=1e-12)
+        np.testing.assert_allclose(env._utils.get_site_xvelr(env.model, d, name), rjr[0] @ d.qvel, atol=1e-12)
+    q = np.zeros(4)
+    env._mujoco.mju_mat2Quat(q, d.site_xmat[model.site_id("ee_center_site")].reshape(9, 1))
+    np.testing.assert_allclose(q, O.mat2quat(d.site_xmat[model.site_id("ee_center_site")]), atol=1e-14)
+
+
+def test_data_writes_reach_the_device(env):
+    """data is the state of record: a qpos write before step() is what the kernel integrates."""
+    from pnp_amd.envs import EnvConfig, FrankaShelfPNPEnv
+    e = FrankaShelfPNPEnv(config=EnvConfig(n_substeps=1))
+    e.reset()
+    e.set_mocap_pose(e.get_ee_position() + [0, 0, 0.05], e.get_ee_orientation())
+    e.unwrapped._mujoco.mj_step(e.model, e.data, nstep=50)
+    assert e.get_ee_position()[2] > e.home_pos[2] + 0.005         # the weld pulled the hand up
+    e.set_joint_neutral()
+    e.unwrapped._mujoco.mj_forward(e.model, e.data)
+    np.testing.assert_allclose(e.get_ee_position(), e.home_pos, atol=1e-10)
+    assert e.get_fingers_width().shape == (1,)
+
+
+def test_skills_replay_reference_episode_on_device():
+    from pnp_amd.envs import EnvConfig, FrankaShelfPNPEnv
+    G = H.load_golden()
+    env = FrankaShelfPNPEnv(config=EnvConfig(n_substeps=int(G["n_substeps"])), dtype=torch.float64)
+    env.reset()
+    np.testing.assert_allclose(env.data.qpos, G["reset_qpos"], atol=1e-12, rtol=0)
+    out = H.run_episode(env, G)
+    worst = H.compare(out, G, 1e-6)
+    print("skill episode worst |diff|:", {k: f"{v:.1e}" for k, v in worst.items()})
