@@ -646,6 +646,25 @@ __device__ __forceinline__ bool c_convex_obb_disjoint(const DevPhys<T>& m, const
   return c_obb_disjoint(bp[0], s.gmat[g1], m.geom_aabb[g1] + 3, bp[1], s.gmat[g2], m.geom_aabb[g2] + 3, margin);
 }
 
+// plane pairs: the other geom's oriented bounding box lies entirely beyond the plane (by more
+// than the margin, plus 1 um of slack) -- no vertex / corner / surface point can reach it, so the
+// pair cannot produce a contact.  Exact cull: the contact set is unchanged.
+template <typename T>
+__device__ __forceinline__ bool c_plane_obb_clear(const DevPhys<T>& m, const Env<T>& s, int gp, int g, T margin) {
+  const T* Rp = s.gmat[gp];
+  const T n[3] = {Rp[2], Rp[5], Rp[8]};
+  const T* R = s.gmat[g];
+  const T* c = m.geom_aabb[g];
+  T d = 0, ext = 0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const T ck = s.gpos[g][k] + R[3 * k] * c[0] + R[3 * k + 1] * c[1] + R[3 * k + 2] * c[2];
+    d += n[k] * (ck - s.gpos[gp][k]);
+    ext += c[3 + k] * fabs(n[0] * R[k] + n[1] * R[3 + k] + n[2] * R[6 + k]);
+  }
+  return d - ext > margin + T(1e-6);
+}
+
 // mjc_Convex by MPR (the OBB pre-test ran in the broadphase): at most one contact.  Wave-uniform
 // call: every lane passes the same pair and gets the same result.
 template <typename T>

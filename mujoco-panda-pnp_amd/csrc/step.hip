@@ -526,7 +526,7 @@ __device__ T mulM_row(const DevPhys<T>& m, const Env<T>& s, int i, const T* v) {
 template <typename T>
 __device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
   const int l = lane_id();
-  // broadphase: bounding spheres; survivors compacted in pair order
+  // broadphase: bounding spheres (+ exact box tests, below); survivors compacted in pair order
   int nlive = 0;
   for (int base = 0; base < m.npair; base += NT) {
     const int pi = base + l;
@@ -540,8 +540,10 @@ __device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
         T v[3] = {s.gpos[g1][0] - s.gpos[g2][0], s.gpos[g1][1] - s.gpos[g2][1], s.gpos[g1][2] - s.gpos[g2][2]};
         keep = t_dot3(v, v) <= (r1 + r2 + mg) * (r1 + r2 + mg);
       }
-      // convex (MPR) pairs also need overlapping oriented bounding boxes
+      // convex (MPR) pairs also need overlapping oriented bounding boxes; plane pairs (no
+      // bounding sphere on the plane side) need the other geom's box to reach the plane
       if (keep && c_is_convex_pair(m, g1, g2)) keep = !c_convex_obb_disjoint(m, s, g1, g2, mg);
+      else if (keep && m.geom_type[g1] == 0 && m.geom_type[g2] != 0) keep = !c_plane_obb_clear(m, s, g1, g2, mg);
     }
     const uint64_t bal = __ballot(keep);
     const int pos = nlive + __popcll(bal & ((1ull << l) - 1));

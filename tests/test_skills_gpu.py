@@ -107,3 +107,38 @@ def test_skills_replay_reference_episode_on_device():
     out = H.run_episode(env, G)
     worst = H.compare(out, G, 1e-6)
     print("skill episode worst |diff|:", {k: f"{v:.1e}" for k, v in worst.items()})
+
+
+def test_batched_moveik_planner_matches_sequential(model):
+    """BatchedMoveIKPlanner (one IK launch per round for all envs) == plan_ik_waypoints per env
+    with the single-solve JacobianIKController (the fallback logic is covered on the CPU by
+    tests/test_skills_oracle.py::test_batched_planner_fallbacks_match_sequential)."""
+    from pnp_amd.engine import get_engine
+    from pnp_amd.ik_solver import JacobianIKController
+    from pnp_amd.skills import plan_ik_waypoints
+    from pnp_amd.skills.batched import BatchedMoveIKPlanner
+    from pnp_amd.workloads import NEUTRAL
+    eng = get_engine()
+    rng = np.random.default_rng(7)
+    B = 12
+    qpos = np.tile(model.qpos0, (B, 1))
+    qpos[:, :9] = NEUTRAL
+    qpos[:, :7] += rng.uniform(-0.3, 0.3, size=(B, 7))
+    sx, sm = eng.site_kinematics(torch.as_tensor(qpos, dtype=torch.float64, device=eng.device))
+    ee = model.site_id("ee_center_site")
+    start = sx[:, ee].cpu().numpy()
+    quat = np.tile([1.0, 0, 0, 0], (B, 1))
+    tgt = start + rng.uniform(-0.08, 0.08, size=(B, 3))
+    logs = [[] for _ in range(B)]
+    planner = BatchedMoveIKPlanner()
+    got = planner.plan(start, quat, qpos[:, :7], tgt, logs=logs)
+    ik = JacobianIKController(model)
+    for b in range(B):
+        lb = []
+        pos, qt = plan_ik_waypoints(ik, start[b], quat[b], qpos[b, :7], tgt[b], log=lb.append)
+        assert len(got[b][0]) == len(pos), b
+        np.testing.assert_allclose(np.array(got[b][0]), np.array(pos), atol=1e-12, rtol=0)
+        np.testing.assert_allclose(np.array(got[b][1]), np.array(qt), atol=0, rtol=0)
+        assert logs[b] == lb, b
+    n_solves = sum(len(p) for p, _ in got)
+    assert planner.launches < n_solves                             # batching saved launches

@@ -80,3 +80,43 @@ def test_gripper_width_fallback():
             return float("nan")
 
     assert GripperSkill.close(WithWidth())._current_width() == 0.0
+
+
+def test_batched_planner_fallbacks_match_sequential():
+    """BatchedMoveIKPlanner's lockstep state machine == plan_ik_waypoints per env, driven by a
+    scripted solver with a wall at x = 0.05 (targets beyond it exhaust retries and fallbacks)."""
+    from pnp_amd.ik_solver import IKResult
+    from pnp_amd.skills import plan_ik_waypoints
+    from pnp_amd.skills.batched import BatchedMoveIKPlanner
+
+    def fake(goal, q):
+        ok = goal[0] <= 0.05
+        return np.asarray(q) + 0.001 * goal.sum(), np.asarray(goal, float), 0.0 if ok else 1.0, ok
+
+    class Seq:
+        def solve(self, goal, q):
+            qn, fp, err, ok = fake(np.asarray(goal), q)
+            return IKResult(bool(ok), qn, fp, err, 10, bool(ok))
+
+    def batch(goals, qs):
+        r = [fake(g, q) for g, q in zip(goals, qs)]
+        return (np.array([x[0] for x in r]), np.array([x[1] for x in r]), np.array([x[2] for x in r]),
+                np.array([x[3] for x in r]))
+
+    rng = np.random.default_rng(3)
+    B = 10
+    start = np.zeros((B, 3))
+    tgt = np.concatenate([rng.uniform(-0.04, 0.04, size=(5, 3)),                 # reachable
+                          [[0.2, 0, 0], [0.2, 0.1, 0], [0.3, -0.2, 0.1], [0.06, 0.0, 0.0], [0.1, 0.3, -0.2]]])
+    quat = np.tile([1.0, 0, 0, 0], (B, 1))
+    q0 = np.zeros((B, 7))
+    logs = [[] for _ in range(B)]
+    planner = BatchedMoveIKPlanner(solve_fn=batch)
+    got = planner.plan(start, quat, q0, tgt, logs=logs)
+    for b in range(B):
+        lb = []
+        pos, qt = plan_ik_waypoints(Seq(), start[b], quat[b], q0[b], tgt[b], log=lb.append)
+        assert len(got[b][0]) == len(pos), b
+        np.testing.assert_array_equal(np.array(got[b][0]), np.array(pos))
+        assert logs[b] == lb, (b, logs[b], lb)
+    assert sum(bool(lg) for lg in logs) >= 4
