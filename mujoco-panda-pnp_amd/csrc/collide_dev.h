@@ -28,6 +28,25 @@ struct LdsSink {
   }
 };
 
+// staging sink (single-pass narrowphase): a wave-wide LDS slot counter; each contact records its
+// producing lane and its number within the pair so it can be placed in order afterwards
+template <typename T>
+struct StageSink {
+  int* counter;
+  T (*val)[7];
+  unsigned short* key;
+  int lane, n = 0;
+  __device__ __forceinline__ void emit(T dist, const T pos[3], const T nrm[3]) {
+    const int slot = atomicAdd(counter, 1);
+    if (slot < 64 && n < 16) {
+      val[slot][0] = dist;
+      for (int k = 0; k < 3; k++) { val[slot][1 + k] = pos[k]; val[slot][4 + k] = nrm[k]; }
+      key[slot] = (unsigned short)(lane * 16 + n);
+    }
+    n++;
+  }
+};
+
 template <typename T, class S>
 __device__ void c_plane_sphere(const T* p1, const T* R1, const T* p2, T r, T margin, S& out) {
   const T n[3] = {R1[2], R1[5], R1[8]}, v[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};

@@ -221,6 +221,12 @@ int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
       if (s->geom_type[a] > s->geom_type[b]) { int t = a; a = b; b = t; }
       d->pair_g1[np] = map[a];
       d->pair_g2[np] = map[b];
+      const double ra = s->geom_rbound[a], rb = s->geom_rbound[b];
+      const double mg = s->geom_margin[a] > s->geom_margin[b] ? s->geom_margin[a] : s->geom_margin[b];
+      d->pair_reach[np] = (T)(ra > 0 && rb > 0 ? ra + rb + mg : -1.0);
+      d->pair_margin[np] = (T)mg;
+      const int ta = s->geom_type[a], tb = s->geom_type[b];
+      d->pair_kind[np] = tb == 7 && ta != 0 ? PH_PAIR_CONVEX : (ta == 0 && tb != 0 ? PH_PAIR_PLANE : PH_PAIR_PRIM);
       np++;
     }
   }

@@ -26,6 +26,9 @@
 #define PH_MAXG 48        // collidable geoms
 #define PH_MAXS 12        // sites
 #define PH_MAXPAIR 1024
+#define PH_PAIR_PRIM 0     // primitive collider, sphere test only
+#define PH_PAIR_CONVEX 1   // MPR pair: + oriented bounding boxes overlap
+#define PH_PAIR_PLANE 2    // plane vs geom: + the geom's box reaches the plane
 #define PH_MAXMESHV 1400
 #define PH_MAXMESH 16
 #define PH_MAXCON 48      // contacts per env (lane per contact: <= 64)
@@ -72,6 +75,10 @@ struct DevPhys {
   T geom_solmix[PH_MAXG], geom_rbound[PH_MAXG];
   T geom_aabb[PH_MAXG][6];   // geom-frame bounding box: centre (3), half extents (3) (OBB pre-test)
   int pair_g1[PH_MAXPAIR], pair_g2[PH_MAXPAIR];   // compact geom ids, g1 has the lower type
+  // broadphase table: bounding-sphere reach r1 + r2 + margin (< 0: a geom has no bounding sphere,
+  // i.e. a plane), the pair margin, and the exact box test the pair gets (PH_PAIR_*)
+  T pair_reach[PH_MAXPAIR], pair_margin[PH_MAXPAIR];
+  unsigned char pair_kind[PH_MAXPAIR];
   // meshes (convex hulls)
   int mesh_vertadr[PH_MAXMESH], mesh_vertnum[PH_MAXMESH];
   T mesh_vert[PH_MAXMESHV][3];

@@ -87,7 +87,14 @@ struct Env {
   signed char efc_t0[PH_MAXEFC], efc_t1[PH_MAXEFC], efc_type[PH_MAXEFC];
   unsigned char efc_id[PH_MAXEFC], efc_act[PH_MAXEFC];
   int efc_off[PH_MAXEFC + 1];   // packed rows: slots [efc_off[r], efc_off[r+1])
-  T efc_Jv[PH_MAXJSLOT];
+  union {
+    T efc_Jv[PH_MAXJSLOT];
+    struct {                   // collision: single-pass contact staging (rows are rebuilt after it)
+      T cst_val[NT][7];        // dist, pos[3], normal[3]
+      unsigned short cst_key[NT];   // producing lane * 16 + its contact number
+      int cst_n;
+    };
+  };
   T efc_pos[PH_MAXEFC], efc_D[PH_MAXEFC], efc_aref[PH_MAXEFC], efc_bb[PH_MAXEFC];
   T efc_force[PH_MAXEFC], efc_jar[PH_MAXEFC], efc_Jp[PH_MAXEFC];
   int lim_count[PH_MAXJ];
@@ -532,18 +539,17 @@ __device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
     const int pi = base + l;
     bool keep = false;
     if (pi < m.npair) {
-      const int g1 = m.pair_g1[pi], g2 = m.pair_g2[pi];
-      const T r1 = m.geom_rbound[g1], r2 = m.geom_rbound[g2];
-      const T mg = fmax(m.geom_margin[g1], m.geom_margin[g2]);
+      const int g1 = m.pair_g1[pi], g2 = m.pair_g2[pi], kind = m.pair_kind[pi];
+      const T reach = m.pair_reach[pi];
       keep = true;
-      if (r1 > 0 && r2 > 0) {
+      if (reach >= 0) {
         T v[3] = {s.gpos[g1][0] - s.gpos[g2][0], s.gpos[g1][1] - s.gpos[g2][1], s.gpos[g1][2] - s.gpos[g2][2]};
-        keep = t_dot3(v, v) <= (r1 + r2 + mg) * (r1 + r2 + mg);
+        keep = t_dot3(v, v) <= reach * reach;
       }
       // convex (MPR) pairs also need overlapping oriented bounding boxes; plane pairs (no
       // bounding sphere on the plane side) need the other geom's box to reach the plane
-      if (keep && c_is_convex_pair(m, g1, g2)) keep = !c_convex_obb_disjoint(m, s, g1, g2, mg);
-      else if (keep && m.geom_type[g1] == 0 && m.geom_type[g2] != 0) keep = !c_plane_obb_clear(m, s, g1, g2, mg);
+      if (keep && kind == PH_PAIR_CONVEX) keep = !c_convex_obb_disjoint(m, s, g1, g2, m.pair_margin[pi]);
+      else if (keep && kind == PH_PAIR_PLANE) keep = !c_plane_obb_clear(m, s, g1, g2, m.pair_margin[pi]);
     }
     const uint64_t bal = __ballot(keep);
     const int pos = nlive + __popcll(bal & ((1ull << l) - 1));
@@ -551,33 +557,52 @@ __device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
     nlive += __popcll(bal);
   }
   wsync();
-  // narrowphase in two passes (count, then write at the scanned offset).  Contact order: the
-  // primitive pairs in pair order, then the convex (MPR) pairs in pair order — MPR runs in a loop
-  // of its own, so its portal state never shares a register allocation with the rest of the
-  // stage (a call or inlined MPR inside the main loop slowed the whole step by 17-20 %).
+  // narrowphase, one pass: every lane collides its pair once, its contacts go to a staging area
+  // through an LDS slot counter, then each lands at (contacts so far) + (exclusive scan of the
+  // per-lane counts) + (its number within the pair) -- the order a sequential loop over the live
+  // pairs produces.  If a chunk stages more than 64 contacts it falls back to a second collide
+  // pass writing at the scanned offsets.  Contact order: primitive pairs in pair order, then the
+  // convex (MPR) pairs in pair order (st_collision_convex).
   int ncon = 0, nconvex = 0;
   for (int base = 0; base < nlive; base += NT) {
     const int k = base + l;
-    LdsSink<T> cs{nullptr, 0};   // count only
     const int pair = k < nlive ? s.live[k] : 0;
     const bool cvx = k < nlive && c_is_convex_pair(m, m.pair_g1[pair], m.pair_g2[pair]);
     nconvex += __popcll(__ballot(cvx));
-    if (k < nlive && !cvx) collide_pair(m, s, pair, cs);
-    int incl = cs.n;
+    if (l == 0) s.cst_n = 0;
+    wsync();
+    StageSink<T> ss{&s.cst_n, s.cst_val, s.cst_key, l};
+    if (k < nlive && !cvx) collide_pair(m, s, pair, ss);
+    wsync();
+    const int staged = s.cst_n;
+    int incl = ss.n;
     for (int o = 1; o < 64; o <<= 1) {
       const int y = __shfl_up(incl, o);
       if (l >= o) incl += y;
     }
     const int total = __shfl(incl, 63);
-    const int off = ncon + incl - cs.n;
-    if (cs.n) {
+    const int off = ncon + incl - ss.n;
+    if (staged <= NT && !__ballot(ss.n >= 16)) {
+      const int key = l < staged ? s.cst_key[l] : 0;
+      const int src = key >> 4;
+      const int at = __shfl(off, src) + (key & 15);
+      const int sp = __shfl(pair, src);
+      if (l < staged && at < PH_MAXCON) {
+        Con<T>& c = s.con[at];
+        c.dist = s.cst_val[l][0];
+        for (int t = 0; t < 3; t++) c.pos[t] = s.cst_val[l][1 + t];
+        for (int t = 0; t < 9; t++) c.frame[t] = t < 3 ? s.cst_val[l][4 + t] : T(0);
+        c_params(m, c, m.pair_g1[sp], m.pair_g2[sp]);
+      }
+    } else if (ss.n) {
       LdsSink<T> ls{s.con + off, PH_MAXCON - off};
       if (ls.cap > 0) {
         collide_pair(m, s, pair, ls);
         const int g1 = m.pair_g1[pair], g2 = m.pair_g2[pair];
-        for (int c = 0; c < cs.n && c < ls.cap; c++) c_params(m, s.con[off + c], g1, g2);
+        for (int c = 0; c < ss.n && c < ls.cap; c++) c_params(m, s.con[off + c], g1, g2);
       }
     }
+    wsync();
     ncon += total;
   }
   if (l == 0) {
