@@ -128,7 +128,16 @@ struct StageClock {
 
 // ============================================================================ small helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
-__device__ __forceinline__ void wsync() { __syncthreads(); }
+// Lane hand-off through LDS inside the env's single wave.  The DS instructions of one wave execute
+// in issue order, so a store by one lane is seen by a later load of any lane of the same wave
+// without an s_waitcnt drain: a wavefront-scope fence (no instruction, a compiler ordering point)
+// is all a hand-off needs.  __syncthreads() would also drain every outstanding LDS load at each
+// of the step's ~60 hand-offs, serialising loads the scheduler could otherwise overlap.
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // ---- wave reductions on the DPP crossbar (no LDS round trips): butterfly inside each row of
 // 16 lanes (quad_perm 1032, quad_perm 2301, row_half_mirror, row_mirror), then the four row
@@ -496,24 +505,96 @@ __device__ void chol_solve_block(const T* Lb, int n, int ld, const int* idx, int
   }
 }
 
+// chol_block in registers for n <= N (same operation order, so the same factor): one lane,
+// packed lower triangle, no LDS round trip per multiply-add.  Rows >= n are identity padding.
+// A = M block (row stride n) + diag(h * damping) when damp != nullptr.
+template <typename T, int N>
+__device__ __forceinline__ void chol_reg(const T* A, int n, const T* damp, T h, T* L) {
+#pragma unroll
+  for (int i = 0; i < N; i++)
+#pragma unroll
+    for (int j = 0; j <= i; j++)
+      L[i * (i + 1) / 2 + j] = i < n ? A[i * n + j] + (i == j && damp ? h * damp[i] : T(0)) : T(i == j);
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    T d = L[j * (j + 1) / 2 + j];
+#pragma unroll
+    for (int k = 0; k < j; k++) d -= L[j * (j + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+    d = PM<T>::sqrt_(d > T(0) ? d : T(1e-30));
+    L[j * (j + 1) / 2 + j] = d;
+    const T inv = T(1) / d;
+#pragma unroll
+    for (int i = j + 1; i < N; i++) {
+      T v = L[i * (i + 1) / 2 + j];
+#pragma unroll
+      for (int k = 0; k < j; k++) v -= L[i * (i + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+      L[i * (i + 1) / 2 + j] = v * inv;
+    }
+  }
+}
+// x = (L L^T)^-1 b for a register factor (chol_solve_block's order); x, b at adr (may alias)
+template <typename T, int N>
+__device__ __forceinline__ void chol_solve_reg(const T* L, int n, T* x, const T* b) {
+  T y[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    T v = i < n ? b[i] : T(0);
+#pragma unroll
+    for (int k = 0; k < i; k++) v -= L[i * (i + 1) / 2 + k] * y[k];
+    y[i] = v / L[i * (i + 1) / 2 + i];
+  }
+#pragma unroll
+  for (int i = N - 1; i >= 0; i--) {
+    T v = y[i];
+#pragma unroll
+    for (int k = i + 1; k < N; k++) v -= L[k * (k + 1) / 2 + i] * y[k];
+    y[i] = v / L[i * (i + 1) / 2 + i];
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++)
+    if (i < n) x[i] = y[i];
+}
+
 template <typename T>
 __device__ void st_factor_M(const DevPhys<T>& m, Env<T>& s) {
   const int t = lane_id();
   if (t < m.ntree) {
     const int n = m.tree_dofnum[t], o = m.tree_moff[t];
-    chol_block(s.M + o, s.L + o, n, n);
+    if (n <= 9) {
+      T L[45];
+      chol_reg<T, 9>(s.M + o, n, (const T*)nullptr, T(0), L);
+#pragma unroll
+      for (int i = 0; i < 9; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++)
+          if (i < n) s.L[o + i * n + j] = L[i * (i + 1) / 2 + j];
+    } else {
+      chol_block(s.M + o, s.L + o, n, n);
+    }
   }
   wsync();
 }
 
+// x = M_t^-1 b on one tree block with the factor in s.L (registers for n <= 9)
+template <typename T, bool REG = true>
+__device__ __forceinline__ void tree_solve(const Env<T>& s, int o, int a, int n, T* x, const T* b) {
+  if (REG && n <= 9) {
+    T L[45];
+#pragma unroll
+    for (int i = 0; i < 9; i++)
+#pragma unroll
+      for (int j = 0; j <= i; j++) L[i * (i + 1) / 2 + j] = i < n ? s.L[o + i * n + j] : T(i == j);
+    chol_solve_reg<T, 9>(L, n, x + a, b + a);
+  } else {
+    chol_solve_block(s.L + o, n, n, (const int*)nullptr, a, x, b);
+  }
+}
+
 // x = M^-1 b (tree blocks, lane per tree); x and b may alias
-template <typename T>
+template <typename T, bool REG = true>
 __device__ void solve_M(const DevPhys<T>& m, Env<T>& s, T* x, const T* b) {
   const int t = lane_id();
-  if (t < m.ntree) {
-    const int n = m.tree_dofnum[t], o = m.tree_moff[t];
-    chol_solve_block(s.L + o, n, n, (const int*)nullptr, m.tree_dofadr[t], x, b);
-  }
+  if (t < m.ntree) tree_solve<T, REG>(s, m.tree_moff[t], m.tree_dofadr[t], m.tree_dofnum[t], x, b);
   wsync();
 }
 
@@ -1058,6 +1139,37 @@ __device__ __forceinline__ int row_slot_(const Env<T>& s, int t0, int t1, int tr
 }
 #define row_slot(m, t0, t1, tree, dof) row_slot_(s, t0, t1, tree, dof)
 
+// The slot of a lane's own dof (tree t, index li inside it) in row r, or -1.  Every load is
+// unconditional (LDS reads cannot fault; invalid slots are clamped to 0 and masked by the caller),
+// so consecutive rows' loads can be in flight together instead of one exec-masked branch and
+// drain per row.
+template <typename T>
+__device__ __forceinline__ int own_slot(const Env<T>& s, int r, int t, int li, int& off) {
+  const int a = s.efc_t0[r], b = s.efc_t1[r];
+  off = s.efc_off[r];
+  const int na = s.c_tree_dofnum[a];
+  return a == t ? li : (b == t ? na + li : -1);
+}
+// g + sum over island I's rows of (J(r, slot of the lane's dof) * f1[r]) * f2[r] (f2 may be null),
+// rows with an inactive flag skipped when act is set; same operation order as the plain loop
+template <typename T>
+__device__ __forceinline__ T dof_row_sum(T g, const Env<T>& s, int I, int t, int li, const T* f1, const T* f2,
+                                         bool only_active) {
+  const int e = s.isl_roff[I + 1];
+#pragma unroll 2
+  for (int rr = s.isl_roff[I]; rr < e; rr++) {
+    const int r = s.isl_row[rr];
+    int off;
+    const int k = own_slot(s, r, t, li, off);
+    const T jv = s.efc_Jv[off + (k >= 0 ? k : 0)];
+    T c = jv * f1[r];
+    if (f2) c = c * f2[r];
+    const bool use = k >= 0 && (!only_active || s.efc_act[r]);
+    g = use ? g + c : g;
+  }
+  return g;
+}
+
 // OR over the wave (DPP butterfly in each row of 16, then the four rows)
 __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
   v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
@@ -1356,14 +1468,8 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
     if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
     wsync();
     if (l < m.nv) {
-      T g = mulM_row(m, s, l, s.v1);
       const int t = m.dof_tree[l], I = s.tree_island[t];
-      for (int rr = s.isl_roff[I]; rr < s.isl_roff[I + 1]; rr++) {
-        const int r = s.isl_row[rr];
-        if (!s.efc_act[r]) continue;
-        const int k = row_slot(m, s.efc_t0[r], s.efc_t1[r], t, l);
-        if (k >= 0) g += EJ(r, k) * s.efc_D[r] * s.efc_jar[r];
-      }
+      const T g = dof_row_sum(mulM_row(m, s, l, s.v1), s, I, t, l - s.c_tree_dofadr[t], s.efc_D, s.efc_jar, true);
       s.grad[l] = g;
       s.v2[l] = g * g;
     }
@@ -1390,13 +1496,17 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
       const int i = s.isl_dof[I][a], j = s.isl_dof[I][b];
       const int ti = m.dof_tree[i], tj = m.dof_tree[j];
       T h = ti == tj ? s.M[mblk(m, i, j)] : T(0);
-      for (int rr = s.isl_roff[I]; rr < s.isl_roff[I + 1]; rr++) {
+      const int li = i - s.c_tree_dofadr[ti], lj = j - s.c_tree_dofadr[tj];
+      const int e1 = s.isl_roff[I + 1];
+#pragma unroll 2
+      for (int rr = s.isl_roff[I]; rr < e1; rr++) {   // unconditional loads (see own_slot)
         const int r = s.isl_row[rr];
-        if (!s.efc_act[r]) continue;
-        const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
-        const int ki = row_slot(m, t0, t1, ti, i);
-        const int kj = row_slot(m, t0, t1, tj, j);
-        if (ki >= 0 && kj >= 0) h += EJ(r, ki) * s.efc_D[r] * EJ(r, kj);
+        const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], off = s.efc_off[r];
+        const int n0 = s.c_tree_dofnum[t0];
+        const int ki = t0 == ti ? li : (t1 == ti ? n0 + li : -1);
+        const int kj = t0 == tj ? lj : (t1 == tj ? n0 + lj : -1);
+        const T c = s.efc_Jv[off + (ki >= 0 ? ki : 0)] * s.efc_D[r] * s.efc_Jv[off + (kj >= 0 ? kj : 0)];
+        h = ki >= 0 && kj >= 0 && s.efc_act[r] ? h + c : h;
       }
       s.H[i][j] = h;
       s.H[j][i] = h;
@@ -1490,12 +1600,7 @@ __device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
   // v = M^-1 J^T f over the dof's island rows
   if (l < m.nv) {
     const int t = m.dof_tree[l], I = s.tree_island[t];
-    T g = 0;
-    for (int rr = s.isl_roff[I]; rr < s.isl_roff[I + 1]; rr++) {
-      const int r = s.isl_row[rr];
-      const int k = row_slot(m, s.efc_t0[r], s.efc_t1[r], t, l);
-      if (k >= 0) g += EJ(r, k) * s.efc_force[r];
-    }
+    const T g = dof_row_sum(T(0), s, I, t, l - s.c_tree_dofadr[t], s.efc_force, (const T*)nullptr, false);
     s.v2[l] = g;
   }
   // Pair lists: islands are independent under Gauss-Seidel (block-diagonal M, rows inside one
@@ -1525,22 +1630,44 @@ __device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
   solve_M(m, s, s.v2, s.v2);
   const int glen = s.ns_len[grp];
   const int maxlen = max(max(s.ns_len[0], s.ns_len[1]), max(s.ns_len[2], s.ns_len[3]));
+  // One pair of opposing pyramid edges per group and step; sparse rows have <= 16 slots = one
+  // DPP row.  A pair's J, W, b and slot dofs are read-only here, so the next pair's are loaded
+  // while the current one is updated; only v2 and the forces (written by the previous update)
+  // are read after the hand-off.
+  struct NsPair {
+    int j, d;
+    bool act, on;
+    T J0, J1, W0, W1, b0, b1;
+  };
+  auto fetch = [&](int k) {
+    NsPair p;
+    p.act = k < glen;
+    p.j = p.act ? s.ns_list[grp][k] : 0;
+    const int t0 = s.efc_t0[p.j], t1 = s.efc_t1[p.j], w = row_width(m, t0, t1);
+    p.on = p.act && q < w;
+    const int qq = p.on ? q : 0;                 // unconditional, in-range loads; masked below
+    const int o0 = s.efc_off[p.j], o1 = s.efc_off[p.j + 1];
+    p.d = p.on ? slot_dof(m, t0, t1, qq) : 0;
+    const T J0 = s.efc_Jv[o0 + qq], J1 = s.efc_Jv[o1 + qq];
+    const T W0 = s.efc_Wv[o0 + qq], W1 = s.efc_Wv[o1 + qq];
+    p.J0 = p.on ? J0 : T(0);
+    p.J1 = p.on ? J1 : T(0);
+    p.W0 = p.on ? W0 : T(0);
+    p.W1 = p.on ? W1 : T(0);
+    p.b0 = s.efc_bb[p.j];
+    p.b1 = s.efc_bb[p.j + 1];
+    return p;
+  };
   for (int iter = 0; iter < m.noslip_iterations; iter++) {
+    NsPair cur = fetch(0);
     for (int k = 0; k < maxlen; k++) {
-      // one pair of opposing pyramid edges per group; sparse rows have <= 16 slots = one DPP row
-      const bool act = k < glen;
-      const int j = act ? s.ns_list[grp][k] : 0;
-      const int t0 = s.efc_t0[j], t1 = s.efc_t1[j], w = row_width(m, t0, t1);
-      const bool on = act && q < w;
-      const int d = on ? slot_dof(m, t0, t1, q) : 0;
-      const T J0 = on ? EJ(j, q) : T(0), J1 = on ? EJ(j + 1, q) : T(0);
-      const T W0 = on ? EW(j, q) : T(0), W1 = on ? EW(j + 1, q) : T(0);
-      const T vd = on ? s.v2[d] : T(0);
-      const T r0 = rowsum16(J0 * vd) + s.efc_bb[j];
-      const T r1 = rowsum16(J1 * vd) + s.efc_bb[j + 1];
-      const T a00 = rowsum16(J0 * W0), a01 = rowsum16(J0 * W1);
-      const T a10 = rowsum16(J1 * W0), a11 = rowsum16(J1 * W1);
-      const T f0 = s.efc_force[j], f1 = s.efc_force[j + 1];
+      const NsPair nxt = fetch(k + 1 < maxlen ? k + 1 : k);
+      const T vd = cur.on ? s.v2[cur.d] : T(0);
+      const T a00 = rowsum16(cur.J0 * cur.W0), a01 = rowsum16(cur.J0 * cur.W1);
+      const T a10 = rowsum16(cur.J1 * cur.W0), a11 = rowsum16(cur.J1 * cur.W1);
+      const T r0 = rowsum16(cur.J0 * vd) + cur.b0;
+      const T r1 = rowsum16(cur.J1 * vd) + cur.b1;
+      const T f0 = s.efc_force[cur.j], f1 = s.efc_force[cur.j + 1];
       const T bc0 = r0 - (a00 * f0 + a01 * f1), bc1 = r1 - (a10 * f0 + a11 * f1);
       const T mid = T(0.5) * (f0 + f1);
       const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;
@@ -1551,9 +1678,10 @@ __device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
         if (y < -mid) y = -mid; else if (y > mid) y = mid;
         n0 = mid + y; n1 = mid - y;
       }
-      if (on) s.v2[d] += W0 * (n0 - f0) + W1 * (n1 - f1);
-      if (act && q == 0) { s.efc_force[j] = n0; s.efc_force[j + 1] = n1; }
+      if (cur.on) s.v2[cur.d] += cur.W0 * (n0 - f0) + cur.W1 * (n1 - f1);
+      if (cur.act && q == 0) { s.efc_force[cur.j] = n0; s.efc_force[cur.j + 1] = n1; }
       wsync();
+      cur = nxt;
     }
   }
 }
@@ -1565,12 +1693,7 @@ __device__ void st_finish_accel(const DevPhys<T>& m, Env<T>& s) {
   if (l < m.nv) {
     // J^T f over the dof's island rows (the other rows do not touch it)
     const int t = m.dof_tree[l], I = s.tree_island[t];
-    T g = 0;
-    for (int rr = s.isl_roff[I]; rr < s.isl_roff[I + 1]; rr++) {
-      const int r = s.isl_row[rr];
-      const int k = row_slot(m, s.efc_t0[r], s.efc_t1[r], t, l);
-      if (k >= 0) g += EJ(r, k) * s.efc_force[r];
-    }
+    const T g = dof_row_sum(T(0), s, I, t, l - s.c_tree_dofadr[t], s.efc_force, (const T*)nullptr, false);
     s.v2[l] = s.qfrc_smooth[l] + g;
   }
   wsync();
@@ -1605,11 +1728,22 @@ __device__ void st_euler(const DevPhys<T>& m, Env<T>& s) {
   wsync();
   if (l < m.ntree) {
     const int n = m.tree_dofnum[l], o = m.tree_moff[l], a = m.tree_dofadr[l];
-    T* A = s.H[0];   // scratch: n x n
-    for (int i = 0; i < n; i++)
-      for (int j = 0; j < n; j++) A[o + i * n + j] = s.M[o + i * n + j] + (i == j ? h * m.dof_damping[a + i] : T(0));
-    chol_block(A + o, A + o, n, n);
-    chol_solve_block(A + o, n, n, (const int*)nullptr, a, s.v2, s.v1);
+    bool damped = false;
+    for (int i = 0; i < n; i++) damped |= m.dof_damping[a + i] != T(0);
+    if (!damped) {
+      // M + h*0 = M exactly: the factor from st_factor_M is this block's factor
+      tree_solve(s, o, a, n, s.v2, s.v1);
+    } else if (n <= 9) {
+      T L[45];
+      chol_reg<T, 9>(s.M + o, n, m.dof_damping + a, h, L);
+      chol_solve_reg<T, 9>(L, n, s.v2 + a, s.v1 + a);
+    } else {
+      T* A = s.H[0];   // scratch: n x n
+      for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) A[o + i * n + j] = s.M[o + i * n + j] + (i == j ? h * m.dof_damping[a + i] : T(0));
+      chol_block(A + o, A + o, n, n);
+      chol_solve_block(A + o, n, n, (const int*)nullptr, a, s.v2, s.v1);
+    }
   }
   wsync();
   if (l < m.nv) s.qvel[l] += h * s.v2[l];
