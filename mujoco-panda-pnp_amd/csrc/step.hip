@@ -272,6 +272,22 @@ __device__ __forceinline__ int mblk_(const Env<T>& s, int i, int j) {
 }
 #define slot_dof(m, t0, t1, k) slot_dof_(s, t0, t1, k)
 #define row_width(m, t0, t1) row_width_(s, t0, t1)
+
+// v + J_r . x in slot order (the order of the slot_dof loop it replaces), with the row's tree
+// table entries read once and every product's loads independent of the running sum
+template <typename T>
+__device__ __forceinline__ T row_dot(const Env<T>& s, int r, const T* x, T v) {
+  const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], off = s.efc_off[r];
+  const int n0 = s.c_tree_dofnum[t0], a0 = s.c_tree_dofadr[t0];
+  const int t1c = t1 >= 0 ? t1 : 0;
+  const int n1 = t1 >= 0 ? s.c_tree_dofnum[t1c] : 0, a1 = s.c_tree_dofadr[t1c];
+  const T* J = s.efc_Jv + off;
+#pragma unroll 3
+  for (int q = 0; q < n0; q++) v += J[q] * x[a0 + q];
+#pragma unroll 3
+  for (int q = 0; q < n1; q++) v += J[n0 + q] * x[a1 + q];
+  return v;
+}
 #define mblk(m, i, j) mblk_(s, i, j)
 
 // ============================================================================ position stage
@@ -1045,10 +1061,7 @@ __device__ void st_velocity(const DevPhys<T>& m, Env<T>& s) {
   }
   // reference acceleration of the rows: aref = -b (J qvel) - k imp (pos - margin)
   for (int r = l; r < s.nefc; r += NT) {
-    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
-    T v = 0;
-    for (int k = 0; k < w; k++) v += EJ(r, k) * s.qvel[slot_dof(m, t0, t1, k)];
-    s.efc_aref[r] -= s.efc_Jp[r] * v;
+    s.efc_aref[r] -= s.efc_Jp[r] * row_dot(s, r, s.qvel, T(0));
   }
   wsync();
 }
@@ -1076,10 +1089,7 @@ __device__ void st_actuation_smooth(const DevPhys<T>& m, Env<T>& s) {
   wsync();
   solve_M(m, s, s.qacc_smooth, s.qfrc_smooth);
   for (int r = l; r < s.nefc; r += NT) {
-    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
-    T v = -s.efc_aref[r];
-    for (int k = 0; k < w; k++) v += EJ(r, k) * s.qacc_smooth[slot_dof(m, t0, t1, k)];
-    s.efc_bb[r] = v;
+    s.efc_bb[r] = row_dot(s, r, s.qacc_smooth, -s.efc_aref[r]);
   }
   wsync();
 }
@@ -1120,9 +1130,7 @@ __device__ void eval_cost(const DevPhys<T>& m, Env<T>& s, const T* x, bool store
   wsync();
   if (l < m.nv) s.v2[l] = T(0.5) * s.v1[l] * mulM_row(m, s, l, s.v1);
   for (int r = l; r < s.nefc; r += NT) {
-    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
-    T v = -s.efc_aref[r];
-    for (int q = 0; q < w; q++) v += EJ(r, q) * x[slot_dof(m, t0, t1, q)];
+    const T v = row_dot(s, r, x, -s.efc_aref[r]);
     const int a = r < s.ne || v < 0;
     if (store) { s.efc_jar[r] = v; s.efc_act[r] = a; }
     s.ntmp[r] = a ? T(0.5) * s.efc_D[r] * v * v : T(0);
@@ -1363,10 +1371,7 @@ __device__ void line_search(const DevPhys<T>& m, Env<T>& s) {
   const int l = lane_id();
   if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
   for (int r = l; r < s.nefc; r += NT) {
-    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
-    T v = 0;
-    for (int q = 0; q < w; q++) v += EJ(r, q) * s.p[slot_dof(m, t0, t1, q)];
-    s.efc_Jp[r] = v;
+    s.efc_Jp[r] = row_dot(s, r, s.p, T(0));
   }
   wsync();
   if (l < m.nv) {
@@ -1383,13 +1388,39 @@ __device__ void line_search(const DevPhys<T>& m, Env<T>& s) {
     }
     const T A0 = group_sum(s, I, s.v2, (const T*)nullptr), B0 = group_sum(s, I, s.grad, (const T*)nullptr);
     const int r0 = s.isl_roff[I], r1 = s.isl_roff[I + 1];
+    // the lane's rows (rr = r0 + q + 16 k) are fixed over the iterations: islands of up to 64
+    // rows keep (Jp, jar, D, equality) in registers, larger ones read LDS each iteration
+    constexpr int RK = 4;
+    T rjp[RK], rjar[RK], rD[RK];
+    bool req[RK], rin[RK];
+#pragma unroll
+    for (int k = 0; k < RK; k++) {
+      const int rr = r0 + q + 16 * k;
+      rin[k] = rr < r1;
+      const int r = s.isl_row[rin[k] ? rr : r0];
+      rjp[k] = s.efc_Jp[r];
+      rjar[k] = s.efc_jar[r];
+      rD[k] = s.efc_D[r];
+      req[k] = r < s.ne;
+    }
+    const bool small = r1 - r0 <= 16 * RK;
     T lo = 0, hi = T(-1), a = 1;
     for (int it = 0; it < 60; it++) {
       T d1 = 0, d2 = 0;
-      for (int rr = r0 + q; rr < r1; rr += 16) {
-        const int r = s.isl_row[rr];
-        const T jp = s.efc_Jp[r], v = s.efc_jar[r] + a * jp;
-        if (r < s.ne || v < 0) { d1 += s.efc_D[r] * v * jp; d2 += s.efc_D[r] * jp * jp; }
+      if (small) {
+#pragma unroll
+        for (int k = 0; k < RK; k++) {
+          const T jp = rjp[k], v = rjar[k] + a * jp;
+          const bool on = rin[k] && (req[k] || v < 0);
+          d1 = on ? d1 + rD[k] * v * jp : d1;
+          d2 = on ? d2 + rD[k] * jp * jp : d2;
+        }
+      } else {
+        for (int rr = r0 + q; rr < r1; rr += 16) {
+          const int r = s.isl_row[rr];
+          const T jp = s.efc_Jp[r], v = s.efc_jar[r] + a * jp;
+          if (r < s.ne || v < 0) { d1 += s.efc_D[r] * v * jp; d2 += s.efc_D[r] * jp * jp; }
+        }
       }
       d1 = rowsum16(d1) + A0 * a + B0;
       d2 = rowsum16(d2) + A0;
@@ -1425,9 +1456,7 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
   wsync();
   if (l < m.nv) s.v2[l] = T(0.5) * s.v1[l] * mulM_row(m, s, l, s.v1);
   for (int r = l; r < s.nefc; r += NT) {
-    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
-    T v = -s.efc_aref[r];
-    for (int q = 0; q < w; q++) v += EJ(r, q) * s.qacc_ws[slot_dof(m, t0, t1, q)];
+    const T v = row_dot(s, r, s.qacc_ws, -s.efc_aref[r]);
     const T bs = s.efc_bb[r];
     s.efc_jar[r] = v;
     s.ntmp[r] = r < s.ne || v < 0 ? T(0.5) * s.efc_D[r] * v * v : T(0);
