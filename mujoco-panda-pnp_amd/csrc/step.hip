@@ -293,40 +293,56 @@ __device__ __forceinline__ T row_dot(const Env<T>& s, int r, const T* x, T v) {
 // ============================================================================ position stage
 template <typename T>
 __device__ void st_kinematics(const DevPhys<T>& m, Env<T>& s) {
+  // Level-synchronous tree pass (mj_kinematics order): a body's frame is its parent's composed
+  // with its own offset and joints, the parent's read from LDS one level earlier.  The per-body
+  // work that does not need the parent -- the model constants and a single hinge's rotation
+  // (sincos) -- is done by every lane at once before the levels, so each level costs one
+  // composition instead of each lane re-walking its whole root path.
   const int b = lane_id();
-  if (b < m.nbody) {
-    T p[3] = {0, 0, 0}, q[4] = {1, 0, 0, 0}, R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-    const int n = b ? m.body_pathlen[b] : 0;
-    for (int k = 0; k < n; k++) {
-      const int c = m.body_path[b][k];
-      const int ja = m.body_jntadr[c], jn = m.body_jntnum[c];
-      if (jn == 1 && m.jnt_type[ja] == 0) {
+  const bool mine = b > 0 && b < m.nbody;
+  const int bb = mine ? b : 1;
+  const int depth = mine ? m.body_pathlen[bb] : 0;
+  const int pid = m.body_parentid[bb], ja = m.body_jntadr[bb], jn = m.body_jntnum[bb];
+  const int jt = jn > 0 ? m.jnt_type[ja] : -1;
+  const int mid = m.body_mocapid[bb];
+  T bp[3], bq[4];
+  for (int t = 0; t < 3; t++) bp[t] = m.body_pos[bb][t];
+  for (int t = 0; t < 4; t++) bq[t] = m.body_quat[bb][t];
+  if (mid >= 0) {
+    for (int t = 0; t < 3; t++) bp[t] = s.mocap_pos[3 * mid + t];
+    for (int t = 0; t < 4; t++) bq[t] = s.mocap_quat[4 * mid + t];
+    t_normalize4(bq);
+  }
+  // single hinge: its local rotation up front
+  T qh[4] = {1, 0, 0, 0};
+  if (jn == 1 && jt == 3) {
+    const int qa = m.jnt_qposadr[ja];
+    const T ang = s.qpos[qa] - m.qpos0[qa];
+    if (ang != T(0)) {
+      T sn, cs;
+      d_sincos(ang * T(0.5), &sn, &cs);
+      qh[0] = cs; qh[1] = m.jnt_axis[ja][0] * sn; qh[2] = m.jnt_axis[ja][1] * sn; qh[3] = m.jnt_axis[ja][2] * sn;
+    }
+  }
+  for (int d = 1; __ballot(mine && depth >= d); d++) {
+    if (mine && depth == d) {
+      T p[3], q[4];
+      if (jn == 1 && jt == 0) {
         const T* qp = s.qpos + m.jnt_qposadr[ja];
         p[0] = qp[0]; p[1] = qp[1]; p[2] = qp[2];
         q[0] = qp[3]; q[1] = qp[4]; q[2] = qp[5]; q[3] = qp[6];
         t_normalize4(q);
-        if (c == b) {
-          for (int t = 0; t < 3; t++) { s.xanchor[ja][t] = p[t]; s.xaxis[ja][t] = m.jnt_axis[ja][t]; }
-        }
+        for (int t = 0; t < 3; t++) { s.xanchor[ja][t] = p[t]; s.xaxis[ja][t] = m.jnt_axis[ja][t]; }
       } else {
-        T bp[3], bq[4];
-        const int mid = m.body_mocapid[c];
-        if (mid >= 0) {
-          for (int t = 0; t < 3; t++) bp[t] = s.mocap_pos[3 * mid + t];
-          for (int t = 0; t < 4; t++) bq[t] = s.mocap_quat[4 * mid + t];
-          t_normalize4(bq);
-        } else {
-          for (int t = 0; t < 3; t++) bp[t] = m.body_pos[c][t];
-          for (int t = 0; t < 4; t++) bq[t] = m.body_quat[c][t];
-        }
-        if (k > 0) {
-          T d[3];
-          d_mulmatvec3(d, R, bp);
-          p[0] += d[0]; p[1] += d[1]; p[2] += d[2];
+        if (pid > 0) {
+          T dv[3];
+          d_mulmatvec3(dv, s.xmat[pid], bp);
+          for (int t = 0; t < 3; t++) p[t] = s.xpos[pid][t] + dv[t];
+          for (int t = 0; t < 4; t++) q[t] = s.xquat[pid][t];
           d_mulquat(q, q, bq);
         } else {
-          p[0] = bp[0]; p[1] = bp[1]; p[2] = bp[2];
-          q[0] = bq[0]; q[1] = bq[1]; q[2] = bq[2]; q[3] = bq[3];
+          for (int t = 0; t < 3; t++) p[t] = bp[t];
+          for (int t = 0; t < 4; t++) q[t] = bq[t];
         }
         for (int j = 0; j < jn; j++) {
           const int jid = ja + j, qa = m.jnt_qposadr[jid], ty = m.jnt_type[jid];
@@ -338,28 +354,36 @@ __device__ void st_kinematics(const DevPhys<T>& m, Env<T>& s) {
             const T dd = s.qpos[qa] - m.qpos0[qa];
             p[0] += ax[0] * dd; p[1] += ax[1] * dd; p[2] += ax[2] * dd;
           } else if (ty == 3) {
-            const T ang = s.qpos[qa] - m.qpos0[qa];
-            T ql[4] = {1, 0, 0, 0}, v[3];
-            if (ang != T(0)) {
-              T sn, cs;
-              d_sincos(ang * T(0.5), &sn, &cs);
-              ql[0] = cs; ql[1] = m.jnt_axis[jid][0] * sn; ql[2] = m.jnt_axis[jid][1] * sn; ql[3] = m.jnt_axis[jid][2] * sn;
+            T ql[4] = {qh[0], qh[1], qh[2], qh[3]}, v[3];
+            if (jn != 1) {
+              const T ang = s.qpos[qa] - m.qpos0[qa];
+              ql[0] = 1; ql[1] = ql[2] = ql[3] = 0;
+              if (ang != T(0)) {
+                T sn, cs;
+                d_sincos(ang * T(0.5), &sn, &cs);
+                ql[0] = cs; ql[1] = m.jnt_axis[jid][0] * sn; ql[2] = m.jnt_axis[jid][1] * sn; ql[3] = m.jnt_axis[jid][2] * sn;
+              }
             }
             d_mulquat(q, q, ql);
             t_rotvecquat_mj(v, m.jnt_pos[jid], q);
             p[0] = an[0] - v[0]; p[1] = an[1] - v[1]; p[2] = an[2] - v[2];
           }
-          if (c == b) {
-            for (int t = 0; t < 3; t++) { s.xanchor[jid][t] = an[t]; s.xaxis[jid][t] = ax[t]; }
-          }
+          for (int t = 0; t < 3; t++) { s.xanchor[jid][t] = an[t]; s.xaxis[jid][t] = ax[t]; }
         }
       }
       t_normalize4(q);
+      T R[9];
       d_quat2mat(R, q);
+      for (int t = 0; t < 3; t++) s.xpos[b][t] = p[t];
+      for (int t = 0; t < 4; t++) s.xquat[b][t] = q[t];
+      for (int t = 0; t < 9; t++) s.xmat[b][t] = R[t];
     }
-    for (int t = 0; t < 3; t++) s.xpos[b][t] = p[t];
-    for (int t = 0; t < 4; t++) s.xquat[b][t] = q[t];
-    for (int t = 0; t < 9; t++) s.xmat[b][t] = R[t];
+    wsync();
+  }
+  if (b == 0) {
+    for (int t = 0; t < 3; t++) s.xpos[0][t] = 0;
+    s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
+    for (int t = 0; t < 9; t++) s.xmat[0][t] = (t % 4 == 0) ? T(1) : T(0);
   }
   wsync();
   // inertial frames (bodies) and geom frames (collidable geoms)
