@@ -20,7 +20,7 @@ run() {  # name, timeout, cmd...
 }
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -x ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     prof)  cd /tmp && run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline; cd "$ROOT" ;;
