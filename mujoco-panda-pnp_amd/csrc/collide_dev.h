@@ -77,8 +77,9 @@ __device__ void c_plane_box(const T* p1, const T* R1, const T* p2, const T* R2, 
 }
 
 template <typename T, class S>
-__device__ void c_plane_mesh(const DevPhys<T>& m, const T* p1, const T* R1, const T* p2, const T* R2, int mesh, T margin,
+__device__ void c_plane_mesh(const DevPhys<T>& /*image: phys<T>()*/, const T* p1, const T* R1, const T* p2, const T* R2, int mesh, T margin,
                              S& out) {
+  const DevPhys<T>& m = phys<T>();
   const T n[3] = {R1[2], R1[5], R1[8]};
   const int a = m.mesh_vertadr[mesh], nv = m.mesh_vertnum[mesh];
   T best[4];
@@ -364,7 +365,8 @@ __device__ __forceinline__ T c_wave_max(T v) {
   return fmax(fmax(rdlane(v, 0), rdlane(v, 16)), fmax(rdlane(v, 32), rdlane(v, 48)));
 }
 template <typename T>
-__device__ void c_load_shape(const DevPhys<T>& m, CShape<T>& sh) {
+__device__ void c_load_shape(const DevPhys<T>& /*image: phys<T>()*/, CShape<T>& sh) {
+  const DevPhys<T>& m = phys<T>();
   const int l = threadIdx.x;
   sh.vadr = sh.type == 7 ? m.mesh_vertadr[sh.mesh] : 0;
   sh.nvert = sh.type == 7 ? m.mesh_vertnum[sh.mesh] : 0;
@@ -376,7 +378,8 @@ __device__ void c_load_shape(const DevPhys<T>& m, CShape<T>& sh) {
 }
 // first vertex within the tie band of the maximum (oracle/convex.c support), wave-cooperative
 template <typename T>
-__device__ int c_mesh_argmax(const DevPhys<T>& m, const CShape<T>& s, const T* ld) {
+__device__ int c_mesh_argmax(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& s, const T* ld) {
+  const DevPhys<T>& m = phys<T>();
   const int l = threadIdx.x, n = s.nvert;
   T dv[C_WV], bd = T(-1e30);
 #pragma unroll
@@ -408,7 +411,8 @@ __device__ int c_mesh_argmax(const DevPhys<T>& m, const CShape<T>& s, const T* l
   return 0;
 }
 template <typename T>
-__device__ void c_support(const DevPhys<T>& m, const CShape<T>& s, const T* d, T* out) {
+__device__ void c_support(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& s, const T* d, T* out) {
+  const DevPhys<T>& m = phys<T>();
   T ld[3];
   for (int k = 0; k < 3; k++) ld[k] = s.R[k] * d[0] + s.R[3 + k] * d[1] + s.R[6 + k] * d[2];
   T lp[3];
@@ -424,7 +428,8 @@ __device__ void c_support(const DevPhys<T>& m, const CShape<T>& s, const T* d, T
     out[k] = s.pos[k] + s.R[3 * k] * lp[0] + s.R[3 * k + 1] * lp[1] + s.R[3 * k + 2] * lp[2] + T(0.5) * s.margin * d[k];
 }
 template <typename T>
-__device__ __forceinline__ void c_mksupport(const DevPhys<T>& m, const CShape<T>& a, const CShape<T>& b, const T* d, SVert<T>& v) {
+__device__ __forceinline__ void c_mksupport(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& a, const CShape<T>& b, const T* d, SVert<T>& v) {
+  const DevPhys<T>& m = phys<T>();
   const T nd[3] = {-d[0], -d[1], -d[2]};
   c_support(m, a, d, v.v1);
   c_support(m, b, nd, v.v2);
@@ -509,7 +514,8 @@ __device__ T c_tri_dist2(const T* P, const T* x0, const T* B, const T* C, T* w) 
 
 // ccdMPRPenetration: true and (depth, dir, pos) on intersection
 template <typename T>
-__device__ bool c_mpr(const DevPhys<T>& m, const CShape<T>& A, const CShape<T>& Bs, T& depth, T* dir, T* pos) {
+__device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A, const CShape<T>& Bs, T& depth, T* dir, T* pos) {
+  const DevPhys<T>& m = phys<T>();
   const T tol = T(1e-6);   // mjOption mpr_tolerance
   SVert<T> p0, p1, p2, p3, v4;
   T d[3], va[3], vb[3], dot;
@@ -645,14 +651,16 @@ __device__ bool c_obb_disjoint(const T* p1, const T* R1, const T* h1, const T* p
 
 // convex pair: (sphere | box | mesh) x mesh (g1 has the lower type)
 template <typename T>
-__device__ __forceinline__ bool c_is_convex_pair(const DevPhys<T>& m, int g1, int g2) {
+__device__ __forceinline__ bool c_is_convex_pair(const DevPhys<T>& /*image: phys<T>()*/, int g1, int g2) {
+  const DevPhys<T>& m = phys<T>();
   return m.geom_type[g2] == 7 && m.geom_type[g1] != 0;
 }
 
 // oriented bounding boxes of a convex pair disjoint (broadphase: such pairs cannot touch, MPR
 // would find no contact)
 template <typename T>
-__device__ __forceinline__ bool c_convex_obb_disjoint(const DevPhys<T>& m, const Env<T>& s, int g1, int g2, T margin) {
+__device__ __forceinline__ bool c_convex_obb_disjoint(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int g1, int g2, T margin) {
+  const DevPhys<T>& m = phys<T>();
   T bp[2][3];
   const int gs[2] = {g1, g2};
 #pragma unroll
@@ -669,7 +677,8 @@ __device__ __forceinline__ bool c_convex_obb_disjoint(const DevPhys<T>& m, const
 // than the margin, plus 1 um of slack) -- no vertex / corner / surface point can reach it, so the
 // pair cannot produce a contact.  Exact cull: the contact set is unchanged.
 template <typename T>
-__device__ __forceinline__ bool c_plane_obb_clear(const DevPhys<T>& m, const Env<T>& s, int gp, int g, T margin) {
+__device__ __forceinline__ bool c_plane_obb_clear(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int gp, int g, T margin) {
+  const DevPhys<T>& m = phys<T>();
   const T* Rp = s.gmat[gp];
   const T n[3] = {Rp[2], Rp[5], Rp[8]};
   const T* R = s.gmat[g];
@@ -687,8 +696,9 @@ __device__ __forceinline__ bool c_plane_obb_clear(const DevPhys<T>& m, const Env
 // mjc_Convex by MPR (the OBB pre-test ran in the broadphase): at most one contact.  Wave-uniform
 // call: every lane passes the same pair and gets the same result.
 template <typename T>
-__device__ __forceinline__ bool c_convex(const DevPhys<T>& m, const Env<T>& s, int g1, int g2, T margin,
+__device__ __forceinline__ bool c_convex(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int g1, int g2, T margin,
                                                     T& dist, T* pos, T* nrm) {
+  const DevPhys<T>& m = phys<T>();
   CShape<T> sh[2];
   const int gs[2] = {g1, g2};
 #pragma unroll
@@ -722,7 +732,8 @@ __device__ void t_makeframe(T f[9]) {
 }
 
 template <typename T>
-__device__ void c_params(const DevPhys<T>& m, Con<T>& c, int g1, int g2) {
+__device__ void c_params(const DevPhys<T>& /*image: phys<T>()*/, Con<T>& c, int g1, int g2) {
+  const DevPhys<T>& m = phys<T>();
   t_makeframe(c.frame);
   c.g1 = g1;
   c.g2 = g2;
@@ -747,7 +758,8 @@ __device__ void c_params(const DevPhys<T>& m, Con<T>& c, int g1, int g2) {
 }
 
 template <typename T, class S>
-__device__ void collide_pair(const DevPhys<T>& m, const Env<T>& s, int pair, S& out) {
+__device__ void collide_pair(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int pair, S& out) {
+  const DevPhys<T>& m = phys<T>();
   const int g1 = m.pair_g1[pair], g2 = m.pair_g2[pair];
   const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
   const T *p1 = s.gpos[g1], *R1 = s.gmat[g1], *s1 = m.geom_size[g1];

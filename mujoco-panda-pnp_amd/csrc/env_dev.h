@@ -103,7 +103,8 @@ struct EnvOutT {
 
 // site frame from the body frames of the last st_kinematics (mj_kinematics site pass)
 template <typename T>
-__device__ void site_frame(const DevPhys<T>& m, const Env<T>& s, int site, T pos[3], T mat[9]) {
+__device__ void site_frame(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int site, T pos[3], T mat[9]) {
+  const DevPhys<T>& m = phys<T>();
   const int b = m.site_bodyid[site];
   T v[3], q[4];
   d_mulmatvec3(v, s.xmat[b], m.site_pos[site]);
@@ -114,7 +115,8 @@ __device__ void site_frame(const DevPhys<T>& m, const Env<T>& s, int site, T pos
 // mj_jacSite(site) * qvel (gymnasium_robotics get_site_xvelp / xvelr); needs st_compos_crb
 // (subtree COM, cdof); lane-uniform result
 template <typename T>
-__device__ void site_vel(const DevPhys<T>& m, Env<T>& s, int site, const T pt[3], T vp[3], T vr[3]) {
+__device__ void site_vel(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, int site, const T pt[3], T vp[3], T vr[3]) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   T jp[3] = {0, 0, 0}, jr[3] = {0, 0, 0};
   if (l < m.nv) jac_col(m, s, m.site_bodyid[site], l, pt, jp, jr);
@@ -127,7 +129,8 @@ __device__ void site_vel(const DevPhys<T>& m, Env<T>& s, int site, const T pt[3]
 
 // forward kinematics (+ comPos for Jacobians) at qk, keeping s.qpos: s.qpos_pre holds s.qpos
 template <typename T>
-__device__ void kin_at(const DevPhys<T>& m, Env<T>& s, const T* qk, bool jac) {
+__device__ void kin_at(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, const T* qk, bool jac) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (l < m.nq) { s.qpos_pre[l] = s.qpos[l]; s.qpos[l] = qk[l]; }
   wsync();
@@ -141,8 +144,9 @@ __device__ void kin_at(const DevPhys<T>& m, Env<T>& s, const T* qk, bool jac) {
 // _get_obs on the current kinematics (positions) and s.qvel; width = finger qpos sum of the
 // integrated state.  Writes obs / achieved / desired goal of env b; returns ee / object data.
 template <typename T>
-__device__ void env_observe(const DevPhys<T>& m, Env<T>& s, const pnp_env_params& prm, int task, const T goal[3],
+__device__ void env_observe(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, const pnp_env_params& prm, int task, const T goal[3],
                             const EnvOutT<T>& out, int b, T width, T ee_p[3], T ee_R[9], T ob_p[3]) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   const int ti = task < prm.n_tasks ? task : prm.n_tasks - 1;   // current_target_object
   T ob_R[9], ee_vp[3], ee_vr[3], ob_vp[3], ob_vr[3], eul[3];
@@ -173,7 +177,8 @@ __device__ void env_observe(const DevPhys<T>& m, Env<T>& s, const pnp_env_params
 }
 
 template <typename T>
-__device__ void store_controls(const DevPhys<T>& m, const Env<T>& s, const pnp_state_t<T>& st, int b) {
+__device__ void store_controls(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, const pnp_state_t<T>& st, int b) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (l < m.nu) st.ctrl[(size_t)b * m.nu + l] = s.ctrl[l];
   if (l < 3 * m.nmocap) st.mocap_pos[(size_t)b * 3 * m.nmocap + l] = s.mocap_pos[l];
@@ -186,7 +191,8 @@ __global__ void __launch_bounds__(NT) env_init_kernel(const DevPhys<T>* __restri
                                                       pnp_env_params prm, EnvSoA<T> es, int B) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
-  const DevPhys<T>& m = *mp;
+  const DevPhys<T>& m = phys<T>();
+  (void)mp;
   const int b = blockIdx.x;
   if (b >= B) return;
   const int l = lane_id();
@@ -235,7 +241,8 @@ __global__ void __launch_bounds__(NT) env_reset_kernel(const DevPhys<T>* __restr
                                                        const uint8_t* __restrict__ mask, EnvOutT<T> out, int B) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
-  const DevPhys<T>& m = *mp;
+  const DevPhys<T>& m = phys<T>();
+  (void)mp;
   const int b = blockIdx.x;
   if (b >= B || (mask && !mask[b])) return;
   const int l = lane_id();
@@ -292,7 +299,8 @@ __global__ void __launch_bounds__(NT) env_step_kernel(const DevPhys<T>* __restri
                                                       EnvOutT<T> out, int B) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
-  const DevPhys<T>& m = *mp;
+  const DevPhys<T>& m = phys<T>();
+  (void)mp;
   const int b = blockIdx.x;
   if (b >= B) return;
   const int l = lane_id();
@@ -430,7 +438,8 @@ static int32_t env_check(pnp_model* model, const void* st, const pnp_env_params*
 }
 
 template <typename T, typename K>
-static int32_t env_prep(pnp_model* model, const pnp_state_t<T>* st, K kernel, const DevPhys<T>** dm, const char* fn) {
+static int32_t env_prep(pnp_model* model, const pnp_state_t<T>* st, K kernel, const DevPhys<T>** dm, const char* fn,
+                        void* stream) {
   if (!st->qpos || !st->qvel || !st->ctrl || !st->mocap_pos || !st->mocap_quat || !st->qacc_warmstart || !st->time ||
       !st->warn) {
     pnp_set_error("%s: null state buffer", fn);
@@ -438,6 +447,7 @@ static int32_t env_prep(pnp_model* model, const pnp_state_t<T>* st, K kernel, co
   }
   *dm = phys_image<T>(model);
   if (!*dm) { pnp_set_error("%s: model has no physics image (%s)", fn, model->phys_err); return PNP_ERR_MODEL; }
+  if (const int32_t rc = phys_resident<T>(model, stream)) return rc;
   if (hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(Env<T>)) !=
       hipSuccess) {
     pnp_set_error("%s: LDS %zu B not available", fn, sizeof(Env<T>));
@@ -453,7 +463,7 @@ static int32_t launch_env_init(pnp_model* model, const pnp_state_t<T>* st, const
   if (rc || B == 0) return rc;
   const DevPhys<T>* dm;
   auto k = env_init_kernel<T>;
-  if ((rc = env_prep(model, st, k, &dm, "pnp_env_init"))) return rc;
+  if ((rc = env_prep(model, st, k, &dm, "pnp_env_init", stream))) return rc;
   hipLaunchKernelGGL(k, dim3(B), dim3(NT), sizeof(Env<T>), (hipStream_t)stream, dm, *st, *p, env_view<T>(e), B);
   return pnp_check_launch("env_init_kernel");
 }
@@ -465,7 +475,7 @@ static int32_t launch_env_reset(pnp_model* model, const pnp_state_t<T>* st, cons
   if (rc || B == 0) return rc;
   const DevPhys<T>* dm;
   auto k = env_reset_kernel<T>;
-  if ((rc = env_prep(model, st, k, &dm, "pnp_env_reset"))) return rc;
+  if ((rc = env_prep(model, st, k, &dm, "pnp_env_reset", stream))) return rc;
   hipLaunchKernelGGL(k, dim3(B), dim3(NT), sizeof(Env<T>), (hipStream_t)stream, dm, *st, *p, env_view<T>(e), mask,
                      out_view<T>(o), B);
   return pnp_check_launch("env_reset_kernel");
@@ -479,7 +489,7 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   if (!action) { pnp_set_error("pnp_env_step: null action"); return PNP_ERR_ARG; }
   const DevPhys<T>* dm;
   auto k = env_step_kernel<T>;
-  if ((rc = env_prep(model, st, k, &dm, "pnp_env_step"))) return rc;
+  if ((rc = env_prep(model, st, k, &dm, "pnp_env_step", stream))) return rc;
   hipLaunchKernelGGL(k, dim3(B), dim3(NT), sizeof(Env<T>), (hipStream_t)stream, dm, *st, *p, env_view<T>(e), action,
                      out_view<T>(o), B);
   return pnp_check_launch("env_step_kernel");

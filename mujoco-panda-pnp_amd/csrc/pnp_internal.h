@@ -77,6 +77,10 @@ template <typename T> const DevPhys<T>* phys_image(const pnp_model* m);
 template <> inline const DevPhys<float>* phys_image<float>(const pnp_model* m) { return m->p_f32; }
 template <> inline const DevPhys<double>* phys_image<double>(const pnp_model* m) { return m->p_f64; }
 template <typename T> int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen);
+// step.hip: make the model's physics image the device's resident one (stream-ordered copy into
+// the constant segment when another model was resident); forget a destroyed model
+template <typename T> int32_t phys_resident(const pnp_model* model, void* stream);
+void phys_forget(const pnp_model* model);
 
 // ---------------------------------------------------------------------------- error plumbing
 void pnp_set_error(const char* fmt, ...);

@@ -18,8 +18,23 @@
 //   pairs   : lane p runs broadphase + narrowphase of one candidate geom pair
 //   rows    : lane r (impedance, reference acceleration, J.x); rows are stored sparsely over
 //             the dofs of the <= 2 trees they touch (PH_ROWW slots)
+#include <atomic>
+
 #include "phys_model.h"
 #include "pnp_internal.h"
+
+// The physics image lives in the device's constant segment, one resident image per precision
+// and device (phys_resident below copies a model's image in, stream-ordered, when a launch uses
+// another model than the last one).  Every stage reads it through phys<T>(), a known global
+// address: wave-uniform reads become scalar loads and per-lane reads global loads off a scalar
+// base, in out-of-line stage functions as well.  Passed down by reference instead, the image
+// reached the out-of-line stages as a generic pointer and every model read was a flat load that
+// waits on the vector-memory and the LDS counters together.
+__constant__ DevPhys<float> g_phys_f32;
+__constant__ DevPhys<double> g_phys_f64;
+template <typename T> __device__ __forceinline__ const DevPhys<T>& phys();
+template <> __device__ __forceinline__ const DevPhys<float>& phys<float>() { return g_phys_f32; }
+template <> __device__ __forceinline__ const DevPhys<double>& phys<double>() { return g_phys_f64; }
 
 #define NT 64
 #define EJ(r, k) s.efc_Jv[s.efc_off[r] + (k)]
@@ -113,9 +128,11 @@ struct Env {
 };
 
 // stage timer (diagnostic instantiation only: TIMED = true); cycles accumulate in prof[stage]
+// Sub-stage timers (sub_start / sub_lap) run inside a parent stage without resetting its lap;
+// count() accumulates per-sub-step sizes (contacts, rows, iterations ...) into the count slots.
 struct StageClock {
   unsigned long long* prof;
-  unsigned long long t;
+  unsigned long long t, ts;
   __device__ void start() { if (prof) t = __builtin_amdgcn_s_memtime(); }
   __device__ void lap(int k) {
     if (!prof) return;
@@ -124,6 +141,26 @@ struct StageClock {
     if (threadIdx.x == 0) prof[k] += n - t;
     t = n;
   }
+  __device__ void sub_start() {
+    if (!prof) return;
+    __syncthreads();
+    ts = __builtin_amdgcn_s_memtime();
+  }
+  __device__ void sub_lap(int k) {
+    if (!prof) return;
+    __syncthreads();
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) prof[k] += n - ts;
+    ts = n;
+  }
+  __device__ void count(int k, int v) {
+    if (prof && threadIdx.x == 0) prof[k] += (unsigned long long)v;
+  }
+};
+// stage slots (include/pnp.h PNP_NSTAGE): sub-stages and per-step counts after the 16 stages
+enum {
+  SC_BROAD = 16, SC_NARROW, SC_CONVEX, SC_NS_W, SC_NS_LISTS,
+  SN_CON = 21, SN_EFC, SN_ITER, SN_CONVEX, SN_ISLAND, SN_NS_SWEEP, SN_LIVE
 };
 
 // ============================================================================ small helpers
@@ -292,7 +329,8 @@ __device__ __forceinline__ T row_dot(const Env<T>& s, int r, const T* x, T v) {
 
 // ============================================================================ position stage
 template <typename T>
-__device__ void st_kinematics(const DevPhys<T>& m, Env<T>& s) {
+__device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+  const DevPhys<T>& m = phys<T>();
   // Level-synchronous tree pass (mj_kinematics order): a body's frame is its parent's composed
   // with its own offset and joints, the parent's read from LDS one level earlier.  The per-body
   // work that does not need the parent -- the model constants and a single hinge's rotation
@@ -406,7 +444,8 @@ __device__ void st_kinematics(const DevPhys<T>& m, Env<T>& s) {
 }
 
 template <typename T>
-__device__ void st_compos_crb(const DevPhys<T>& m, Env<T>& s) {
+__device__ void st_compos_crb(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   // subtree COM of each root body (only roots are read: cinert and cdof are rooted there)
   if (l > 0 && l < m.nbody && m.body_rootid[l] == l) {
@@ -596,10 +635,11 @@ __device__ __forceinline__ void chol_solve_reg(const T* L, int n, T* x, const T*
 }
 
 template <typename T>
-__device__ void st_factor_M(const DevPhys<T>& m, Env<T>& s) {
+__device__ void st_factor_M(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+  const DevPhys<T>& m = phys<T>();
   const int t = lane_id();
   if (t < m.ntree) {
-    const int n = m.tree_dofnum[t], o = m.tree_moff[t];
+    const int n = s.c_tree_dofnum[t], o = s.c_tree_moff[t];
     if (n <= 9) {
       T L[45];
       chol_reg<T, 9>(s.M + o, n, (const T*)nullptr, T(0), L);
@@ -632,15 +672,16 @@ __device__ __forceinline__ void tree_solve(const Env<T>& s, int o, int a, int n,
 
 // x = M^-1 b (tree blocks, lane per tree); x and b may alias
 template <typename T, bool REG = true>
-__device__ void solve_M(const DevPhys<T>& m, Env<T>& s, T* x, const T* b) {
+__device__ void solve_M(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, T* x, const T* b) {
+  const DevPhys<T>& m = phys<T>();
   const int t = lane_id();
-  if (t < m.ntree) tree_solve<T, REG>(s, m.tree_moff[t], m.tree_dofadr[t], m.tree_dofnum[t], x, b);
+  if (t < m.ntree) tree_solve<T, REG>(s, s.c_tree_moff[t], s.c_tree_dofadr[t], s.c_tree_dofnum[t], x, b);
   wsync();
 }
 
 // r = M v (tree blocks, lane per dof)
 template <typename T>
-__device__ T mulM_row(const DevPhys<T>& m, const Env<T>& s, int i, const T* v) {
+__device__ T mulM_row(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int i, const T* v) {
   const int t = s.c_dof_tree[i];
   const int a = s.c_tree_dofadr[t], n = s.c_tree_dofnum[t], o = s.c_tree_moff[t] + (i - a) * n;
   T r = 0;
@@ -652,8 +693,10 @@ __device__ T mulM_row(const DevPhys<T>& m, const Env<T>& s, int i, const T* v) {
 #include "collide_dev.h"
 
 template <typename T>
-__device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
+__device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, StageClock& clk) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
+  clk.sub_start();
   // broadphase: bounding spheres (+ exact box tests, below); survivors compacted in pair order
   int nlive = 0;
   for (int base = 0; base < m.npair; base += NT) {
@@ -678,6 +721,7 @@ __device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
     nlive += __popcll(bal);
   }
   wsync();
+  clk.sub_lap(SC_BROAD);
   // narrowphase, one pass: every lane collides its pair once, its contacts go to a staging area
   // through an LDS slot counter, then each lands at (contacts so far) + (exclusive scan of the
   // per-lane counts) + (its number within the pair) -- the order a sequential loop over the live
@@ -734,6 +778,7 @@ __device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
     if (ncon > PH_MAXCON) s.warn |= 8u;
   }
   wsync();
+  clk.sub_lap(SC_NARROW);
 }
 
 // Convex (MPR) pairs of the live list, appended after the primitive contacts.  A stage of its
@@ -742,7 +787,8 @@ __device__ void st_collision(const DevPhys<T>& m, Env<T>& s) {
 // candidates pay neither its frame nor its callee-saved registers (inlined, or called
 // unconditionally, it slowed the whole step by 17-20 %).
 template <typename T>
-__device__ __attribute__((noinline)) void st_collision_convex(const DevPhys<T>& m, Env<T>& s) {
+__device__ __attribute__((noinline)) void st_collision_convex(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   const int nlive = s.nlive;
   int ncon = s.ncon_raw;
@@ -794,8 +840,9 @@ __device__ T impedance_(const T* si, T x) {
 // position part of the reference acceleration; the velocity part (-b J qvel) is added by
 // finish_rows once the row's Jacobian is complete (b parked in efc_Jp meanwhile)
 template <typename T>
-__device__ void row_imp(const DevPhys<T>& m, Env<T>& s, int r, T pos, T margin, T diag, const T* solref,
+__device__ void row_imp(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, int r, T pos, T margin, T diag, const T* solref,
                         const T* solimp) {
+  const DevPhys<T>& m = phys<T>();
   const T dmax = fmin(fmax(solimp[1], T(0.0001)), T(0.9999));
   T k, b;
   if (solref[0] > 0) {
@@ -815,7 +862,8 @@ __device__ void row_imp(const DevPhys<T>& m, Env<T>& s, int r, T pos, T margin, 
 
 // translational Jacobian column of world point pt on body b at dof d (0 if d does not move b)
 template <typename T>
-__device__ __forceinline__ void jac_col(const DevPhys<T>& m, const Env<T>& s, int b, int d, const T pt[3], T jp[3], T jr[3]) {
+__device__ __forceinline__ void jac_col(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int b, int d, const T pt[3], T jp[3], T jr[3]) {
+  const DevPhys<T>& m = phys<T>();
   if (d < 0 || !(m.body_dofmask[b] >> d & 1)) {
     jp[0] = jp[1] = jp[2] = 0;
     jr[0] = jr[1] = jr[2] = 0;
@@ -830,7 +878,8 @@ __device__ __forceinline__ void jac_col(const DevPhys<T>& m, const Env<T>& s, in
 }
 
 template <typename T>
-__device__ __forceinline__ void body_trees(const DevPhys<T>& m, int b1, int b2, int& t0, int& t1) {
+__device__ __forceinline__ void body_trees(const DevPhys<T>& /*image: phys<T>()*/, int b1, int b2, int& t0, int& t1) {
+  const DevPhys<T>& m = phys<T>();
   t0 = m.body_dofmask[b1] ? m.body_tree[b1] : -1;
   t1 = m.body_dofmask[b2] ? m.body_tree[b2] : -1;
   if (t0 < 0) { t0 = t1; t1 = -1; }
@@ -853,7 +902,8 @@ __device__ __forceinline__ int wscan(int n, int* tot) {
 // contact, pyramidal edges J_n +- mu_k J_tk).  Every row is stored packed over the dofs of the
 // <= 2 trees it touches (weld: arm 9; limits: 1 slot; cube-shelf: 6).
 template <typename T>
-__device__ void st_constraints(const DevPhys<T>& m, Env<T>& s) {
+__device__ void st_constraints(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   int nrow = 0, nslot = 0;
   // ---- weld
@@ -1018,7 +1068,8 @@ __device__ void st_constraints(const DevPhys<T>& m, Env<T>& s) {
 
 // ============================================================================ velocity stage
 template <typename T>
-__device__ void st_velocity(const DevPhys<T>& m, Env<T>& s) {
+__device__ void st_velocity(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   // cvel of bodies
   if (l < m.nbody) {
@@ -1092,7 +1143,8 @@ __device__ void st_velocity(const DevPhys<T>& m, Env<T>& s) {
 
 // ============================================================================ acceleration
 template <typename T>
-__device__ void st_actuation_smooth(const DevPhys<T>& m, Env<T>& s) {
+__device__ void st_actuation_smooth(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (l < m.nv) {
     T f = 0;
@@ -1148,7 +1200,8 @@ __device__ __forceinline__ void island_sums(Env<T>& s, const T* vd, const T* vr,
 
 // jar = J x - aref, active set (store), per-island cost -> out[I]
 template <typename T>
-__device__ void eval_cost(const DevPhys<T>& m, Env<T>& s, const T* x, bool store, T* out) {
+__device__ void eval_cost(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, const T* x, bool store, T* out) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (l < m.nv) s.v1[l] = x[l] - s.qacc_smooth[l];
   wsync();
@@ -1218,7 +1271,8 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
 // component, dofs keep increasing order inside an island (trees are contiguous dof ranges).
 // Then the rows of each island (CSR, wave ballots) and the island Hessian entry offsets.
 template <typename T>
-__device__ void build_islands(const DevPhys<T>& m, Env<T>& s) {
+__device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   uint64_t e = 0;
   if (l < s.ncon && s.con_rbase[l] >= 0 && s.con_t[l][1] >= 0) {
@@ -1391,7 +1445,8 @@ __device__ void island_newton_dir_lds(Env<T>& s, int I, int n) {
 // the row's 16 lanes and its bracket iterates independently of the other islands.  Islands with
 // isl_flag set (done) keep a = 0.  Leaves the step lengths in s.isl_alpha.
 template <typename T>
-__device__ void line_search(const DevPhys<T>& m, Env<T>& s) {
+__device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
   for (int r = l; r < s.nefc; r += NT) {
@@ -1463,7 +1518,8 @@ __device__ void line_search(const DevPhys<T>& m, Env<T>& s) {
 }
 
 template <typename T>
-__device__ void st_newton(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
+__device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, StageClock& clk) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (s.nefc == 0) {
     if (l < m.nv) s.qacc[l] = s.qacc_smooth[l];
@@ -1497,7 +1553,7 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
     s.isl_hvalid[l] = 0;
   }
   wsync();
-  if (l < m.nv) s.x[l] = s.isl_alpha[s.tree_island[m.dof_tree[l]]] != T(0) ? s.qacc_ws[l] : s.qacc_smooth[l];
+  if (l < m.nv) s.x[l] = s.isl_alpha[s.tree_island[s.c_dof_tree[l]]] != T(0) ? s.qacc_ws[l] : s.qacc_smooth[l];
   for (int r = l; r < s.nefc; r += NT) {
     const T v = s.isl_alpha[s.tree_island[s.efc_t0[r]]] != T(0) ? s.efc_jar[r] : s.efc_bb[r];
     s.efc_jar[r] = v;
@@ -1521,7 +1577,7 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
     if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
     wsync();
     if (l < m.nv) {
-      const int t = m.dof_tree[l], I = s.tree_island[t];
+      const int t = s.c_dof_tree[l], I = s.tree_island[t];
       const T g = dof_row_sum(mulM_row(m, s, l, s.v1), s, I, t, l - s.c_tree_dofadr[t], s.efc_D, s.efc_jar, true);
       s.grad[l] = g;
       s.v2[l] = g * g;
@@ -1547,7 +1603,7 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
       while ((a + 1) * (a + 2) / 2 <= le) a++;
       const int b = le - a * (a + 1) / 2;
       const int i = s.isl_dof[I][a], j = s.isl_dof[I][b];
-      const int ti = m.dof_tree[i], tj = m.dof_tree[j];
+      const int ti = s.c_dof_tree[i], tj = s.c_dof_tree[j];
       T h = ti == tj ? s.M[mblk(m, i, j)] : T(0);
       const int li = i - s.c_tree_dofadr[ti], lj = j - s.c_tree_dofadr[tj];
       const int e1 = s.isl_roff[I + 1];
@@ -1580,7 +1636,7 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
     clk.lap(10);
     line_search(m, s);
     clk.lap(11);
-    if (l < m.nv) s.x[l] += s.isl_alpha[s.tree_island[m.dof_tree[l]]] * s.p[l];
+    if (l < m.nv) s.x[l] += s.isl_alpha[s.tree_island[s.c_dof_tree[l]]] * s.p[l];
     // remember the active set the step was computed with
     for (int r = l; r < s.nefc; r += NT) s.efc_Jp[r] = (T)s.efc_act[r];
     wsync();
@@ -1624,9 +1680,11 @@ __device__ void st_newton(const DevPhys<T>& m, Env<T>& s, StageClock& clk) {
 
 // ============================================================================ no-slip
 template <typename T>
-__device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
+__device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, StageClock& clk) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (m.noslip_iterations <= 0 || s.nefc == 0) return;
+  clk.sub_start();
   // W_r = M^-1 J_r^T for contact rows (block-diagonal M: solve per tree of the row)
   for (int r = l; r < s.nefc; r += NT) {
     if (s.efc_type[r] != 6) continue;
@@ -1635,7 +1693,7 @@ __device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
     for (int h = 0; h < 2; h++) {
       const int t = h ? t1 : t0;
       if (t < 0) continue;
-      const int n = m.tree_dofnum[t], o = m.tree_moff[t];
+      const int n = s.c_tree_dofnum[t], o = s.c_tree_moff[t];
       T y[PH_MAXTDOF];
       for (int i = 0; i < n; i++) {
         T v = EJ(r, base + i);
@@ -1650,9 +1708,10 @@ __device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
       base += n;
     }
   }
+  clk.sub_lap(SC_NS_W);
   // v = M^-1 J^T f over the dof's island rows
   if (l < m.nv) {
-    const int t = m.dof_tree[l], I = s.tree_island[t];
+    const int t = s.c_dof_tree[l], I = s.tree_island[t];
     const T g = dof_row_sum(T(0), s, I, t, l - s.c_tree_dofadr[t], s.efc_force, (const T*)nullptr, false);
     s.v2[l] = g;
   }
@@ -1683,6 +1742,8 @@ __device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
   solve_M(m, s, s.v2, s.v2);
   const int glen = s.ns_len[grp];
   const int maxlen = max(max(s.ns_len[0], s.ns_len[1]), max(s.ns_len[2], s.ns_len[3]));
+  clk.sub_lap(SC_NS_LISTS);
+  clk.count(SN_NS_SWEEP, maxlen);
   // One pair of opposing pyramid edges per group and step; sparse rows have <= 16 slots = one
   // DPP row.  A pair's J, W, b and slot dofs are read-only here, so the next pair's are loaded
   // while the current one is updated; only v2 and the forces (written by the previous update)
@@ -1740,12 +1801,13 @@ __device__ void st_noslip(const DevPhys<T>& m, Env<T>& s) {
 }
 
 template <typename T>
-__device__ void st_finish_accel(const DevPhys<T>& m, Env<T>& s) {
+__device__ void st_finish_accel(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (s.nefc == 0) return;
   if (l < m.nv) {
     // J^T f over the dof's island rows (the other rows do not touch it)
-    const int t = m.dof_tree[l], I = s.tree_island[t];
+    const int t = s.c_dof_tree[l], I = s.tree_island[t];
     const T g = dof_row_sum(T(0), s, I, t, l - s.c_tree_dofadr[t], s.efc_force, (const T*)nullptr, false);
     s.v2[l] = s.qfrc_smooth[l] + g;
   }
@@ -1755,7 +1817,8 @@ __device__ void st_finish_accel(const DevPhys<T>& m, Env<T>& s) {
 
 // ============================================================================ reset / Euler
 template <typename T>
-__device__ void reset_state(const DevPhys<T>& m, Env<T>& s) {
+__device__ void reset_state(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (l < m.nq) s.qpos[l] = m.qpos0[l];
   if (l < m.nv) { s.qvel[l] = 0; s.qacc_ws[l] = 0; }
@@ -1773,14 +1836,15 @@ template <typename T>
 __device__ __forceinline__ bool is_bad(T x) { return !(fabs(x) <= T(1e10)); }
 
 template <typename T>
-__device__ void st_euler(const DevPhys<T>& m, Env<T>& s) {
+__device__ void st_euler(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   const T h = m.timestep;
   // qfrc = M qacc ; (M + h D) qacc_e = qfrc  (implicit joint damping)
   if (l < m.nv) s.v1[l] = mulM_row(m, s, l, s.qacc);
   wsync();
   if (l < m.ntree) {
-    const int n = m.tree_dofnum[l], o = m.tree_moff[l], a = m.tree_dofadr[l];
+    const int n = s.c_tree_dofnum[l], o = s.c_tree_moff[l], a = s.c_tree_dofadr[l];
     bool damped = false;
     for (int i = 0; i < n; i++) damped |= m.dof_damping[a + i] != T(0);
     if (!damped) {
@@ -1830,7 +1894,8 @@ __device__ void st_euler(const DevPhys<T>& m, Env<T>& s) {
 // debug record of the contacts (PNP_DBG_CON): written right after collision, because the contact
 // list shares storage with the solver's scratch
 template <typename T>
-__device__ void dump_contacts(const DevPhys<T>& m, const Env<T>& s, double* o) {
+__device__ void dump_contacts(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, double* o) {
+  const DevPhys<T>& m = phys<T>();
   for (int c = lane_id(); c < s.ncon; c += NT) {
     double* q = o + PNP_DBG_CON + c * PNP_DBG_CON_STRIDE;
     for (int t = 0; t < 3; t++) q[t] = s.con[c].pos[t];
@@ -1843,30 +1908,43 @@ __device__ void dump_contacts(const DevPhys<T>& m, const Env<T>& s, double* o) {
 }
 
 template <typename T>
-__device__ void forward(const DevPhys<T>& m, Env<T>& s, StageClock& clk, double* dbg = nullptr) {
+__device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, StageClock& clk, double* dbg = nullptr) {
+  const DevPhys<T>& m = phys<T>();
   st_kinematics(m, s);      clk.lap(1);
   st_compos_crb(m, s);      clk.lap(2);
   st_factor_M(m, s);        clk.lap(3);
-  st_collision(m, s);
-  if (s.nconvex) st_collision_convex(m, s);
+  st_collision(m, s, clk);
+  if (s.nconvex) {
+    clk.sub_start();
+    st_collision_convex(m, s);
+    clk.sub_lap(SC_CONVEX);
+  }
   clk.lap(4);
+  clk.count(SN_CON, s.ncon);
+  clk.count(SN_CONVEX, s.nconvex);
+  clk.count(SN_LIVE, s.nlive);
   if (dbg) dump_contacts(m, s, dbg);
   st_constraints(m, s);     clk.lap(5);
   st_velocity(m, s);        clk.lap(6);
   st_actuation_smooth(m, s); clk.lap(7);
   st_newton(m, s, clk);     // laps 8..12 inside
-  st_noslip(m, s);          clk.lap(13);
+  clk.count(SN_EFC, s.nefc);
+  clk.count(SN_ITER, s.solver_iter);
+  clk.count(SN_ISLAND, s.nefc ? s.nisland : 0);
+  st_noslip(m, s, clk);     clk.lap(13);
   st_finish_accel(m, s);    clk.lap(14);
 }
 
 template <typename T>
-__device__ void forward(const DevPhys<T>& m, Env<T>& s) {
+__device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+  const DevPhys<T>& m = phys<T>();
   StageClock clk{nullptr, 0};
   forward(m, s, clk);
 }
 
 template <typename T>
-__device__ void check_state(const DevPhys<T>& m, Env<T>& s) {
+__device__ void check_state(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   const bool bq = l < m.nq && is_bad(s.qpos[l]);
   const bool bv = l < m.nv && is_bad(s.qvel[l]);
@@ -1881,7 +1959,8 @@ __device__ void check_state(const DevPhys<T>& m, Env<T>& s) {
 // save_qpos (gym env, last sub-step): the qpos the forward ran at, i.e. where MuJoCo's
 // data.site_* / Jacobians stay after mj_step returns
 template <typename T>
-__device__ void mj_step_dev(const DevPhys<T>& m, Env<T>& s, StageClock& clk, T* save_qpos = nullptr) {
+__device__ void mj_step_dev(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, StageClock& clk, T* save_qpos = nullptr) {
+  const DevPhys<T>& m = phys<T>();
   clk.start();
   check_state(m, s);
   clk.lap(0);
@@ -1903,7 +1982,8 @@ __device__ void mj_step_dev(const DevPhys<T>& m, Env<T>& s, StageClock& clk, T* 
 }
 
 template <typename T>
-__device__ void load_env(const DevPhys<T>& m, Env<T>& s, const pnp_state_t<T>& st, int b) {
+__device__ void load_env(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, const pnp_state_t<T>& st, int b) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (l < PH_MAXT) {
     s.c_tree_dofadr[l] = m.tree_dofadr[l];
@@ -1921,7 +2001,8 @@ __device__ void load_env(const DevPhys<T>& m, Env<T>& s, const pnp_state_t<T>& s
 }
 
 template <typename T>
-__device__ void store_env(const DevPhys<T>& m, const Env<T>& s, const pnp_state_t<T>& st, int b) {
+__device__ void store_env(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, const pnp_state_t<T>& st, int b) {
+  const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (l < m.nq) st.qpos[(size_t)b * m.nq + l] = s.qpos[l];
   if (l < m.nv) { st.qvel[(size_t)b * m.nv + l] = s.qvel[l]; st.qacc_warmstart[(size_t)b * m.nv + l] = s.qacc_ws[l]; }
@@ -1933,7 +2014,8 @@ __global__ void __launch_bounds__(NT) step_kernel(const DevPhys<T>* __restrict__
                                                  unsigned long long* __restrict__ prof) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
-  const DevPhys<T>& m = *mp;
+  const DevPhys<T>& m = phys<T>();
+  (void)mp;
   const int b = blockIdx.x;
   if (b >= B) return;
   StageClock clk{TIMED ? prof + (size_t)b * PNP_NSTAGE : nullptr, 0};
@@ -1948,7 +2030,8 @@ __global__ void __launch_bounds__(NT) forward_debug_kernel(const DevPhys<T>* __r
                                                           double* __restrict__ dbg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
-  const DevPhys<T>& m = *mp;
+  const DevPhys<T>& m = phys<T>();
+  (void)mp;
   const int b = blockIdx.x;
   if (b >= B) return;
   load_env(m, s, st, b);
@@ -1988,6 +2071,35 @@ __global__ void __launch_bounds__(NT) forward_debug_kernel(const DevPhys<T>* __r
 }
 
 // ============================================================================ host launchers
+// Resident-image bookkeeping: the model whose image each device's constant segment holds.
+static std::atomic<const pnp_model*> g_resident[2][64];
+
+template <typename T>
+int32_t phys_resident(const pnp_model* model, void* stream) {
+  const DevPhys<T>* src = phys_image<T>(model);
+  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { pnp_set_error("phys_resident: bad device"); return PNP_ERR_HIP; }
+  std::atomic<const pnp_model*>& slot = g_resident[sizeof(T) == 8][dev];
+  if (slot.load() == model) return PNP_OK;
+  const void* sym = sizeof(T) == 8 ? (const void*)&g_phys_f64 : (const void*)&g_phys_f32;
+  const hipError_t e = hipMemcpyToSymbolAsync(sym, src, sizeof(DevPhys<T>), 0, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+  if (e != hipSuccess) { pnp_set_error("phys_resident: %s", hipGetErrorString(e)); return PNP_ERR_HIP; }
+  slot.store(model);
+  return PNP_OK;
+}
+template int32_t phys_resident<float>(const pnp_model*, void*);
+template int32_t phys_resident<double>(const pnp_model*, void*);
+
+// a destroyed model is no longer resident anywhere (a new model may reuse its address)
+void phys_forget(const pnp_model* model) {
+  for (auto& row : g_resident)
+    for (auto& slot : row) {
+      const pnp_model* cur = model;
+      slot.compare_exchange_strong(cur, nullptr);
+    }
+}
+
 template <typename T>
 static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B, int32_t nsub, void* stream,
                            double* dbg, unsigned long long* prof = nullptr) {
@@ -2000,6 +2112,7 @@ static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B
   }
   const DevPhys<T>* dm = phys_image<T>(model);
   if (!dm) { pnp_set_error("pnp_step: model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  if (const int32_t rc = phys_resident<T>(model, stream)) return rc;
   const size_t lds = sizeof(Env<T>);
   if (dbg) {
     auto k = forward_debug_kernel<T>;

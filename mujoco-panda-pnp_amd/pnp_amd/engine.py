@@ -139,10 +139,16 @@ class Engine:
 
     STAGES = ("check", "kinematics", "compos_crb", "factor_M", "collision", "constraints", "velocity_rne",
               "actuation_smooth", "newton_setup", "newton_grad_hess", "newton_dir", "newton_linesearch",
-              "newton_update", "noslip", "finish_accel", "euler")
+              "newton_update", "noslip", "finish_accel", "euler",
+              # sub-stages (also inside their parent's cycles)
+              "col_broadphase", "col_primitive", "col_convex", "noslip_W", "noslip_lists",
+              # per-sub-step counts (summed over sub-steps), not cycles
+              "n_con", "n_efc", "n_newton_iter", "n_convex", "n_island", "n_noslip_sweep", "n_live")
+    N_STAGE_CYCLES = 21
 
     def step_profile(self, st, nsub=1):
-        """Diagnostic timed instantiation of pnp_step: per-stage shader cycles [B, 12] (uint64)."""
+        """Diagnostic timed instantiation of pnp_step: per-stage shader cycles and per-step counts
+        [B, len(STAGES)] (int64, summed over the nsub sub-steps; see include/pnp.h)."""
         S, B, dt = self._state_struct(st)
         if dt != torch.float32:
             raise TypeError("step_profile times the fp32 product kernel")
