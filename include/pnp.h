@@ -252,11 +252,12 @@ int32_t pnp_forward_debug_f64(pnp_model* model, const pnp_state_f64* state, int3
  * (islands, warm start), Newton gradient+Hessian, Newton direction (island Cholesky), Newton line
  * search, Newton update+convergence, noslip, finish accel, Euler; then sub-stages (cycles
  * also counted in their parent): broadphase, primitive narrowphase, convex (MPR) pairs, noslip
- * W = M^-1 J^T, noslip pair lists; then per-sub-step counts summed over the sub-steps (not
+ * W = M^-1 J^T, noslip pair lists, kinematics per-body prologue, kinematics tree levels,
+ * kinematics inertial/geom frames, Newton gradient, Newton convergence test, Newton Hessian; then per-sub-step counts summed over the sub-steps (not
  * cycles): ncon, nefc, Newton iterations, live convex pairs, islands, noslip sweep length,
  * broadphase survivors.  Separate instantiation: the product kernel carries no timers. */
-#define PNP_NSTAGE 28
-#define PNP_NSTAGE_CYCLES 21
+#define PNP_NSTAGE 34
+#define PNP_NSTAGE_CYCLES 27
 int32_t pnp_step_profile(pnp_model* model, const pnp_state* state, int32_t B, int32_t nsub,
                          unsigned long long* stage_cycles, void* stream);
 /* LDS bytes one env occupies in the step kernel (fp64 != 0: the debug instantiation). */

@@ -189,8 +189,8 @@ __device__ void store_controls(const DevPhys<T>& /*image: phys<T>()*/, const Env
 template <typename T>
 __global__ void __launch_bounds__(NT) env_init_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
                                                       pnp_env_params prm, EnvSoA<T> es, int B) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
+  __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
+  Env<T>& s = s_env;
   const DevPhys<T>& m = phys<T>();
   (void)mp;
   const int b = blockIdx.x;
@@ -215,7 +215,7 @@ __global__ void __launch_bounds__(NT) env_init_kernel(const DevPhys<T>* __restri
   }
   wsync();
   // _mujoco_step(): 10 x mj_step(nstep = n_substeps)
-  StageClock clk{nullptr, 0};
+  NoClock clk;
   const int nsub = prm.n_substeps * prm.n_calls;
   for (int k = 0; k < nsub; k++) mj_step_dev(m, s, clk, k == nsub - 1 ? s.qpos_pre : nullptr);
   store_env(m, s, st, b);
@@ -239,8 +239,8 @@ template <typename T>
 __global__ void __launch_bounds__(NT) env_reset_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
                                                        pnp_env_params prm, EnvSoA<T> es,
                                                        const uint8_t* __restrict__ mask, EnvOutT<T> out, int B) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
+  __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
+  Env<T>& s = s_env;
   const DevPhys<T>& m = phys<T>();
   (void)mp;
   const int b = blockIdx.x;
@@ -297,8 +297,8 @@ template <typename T>
 __global__ void __launch_bounds__(NT) env_step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
                                                       pnp_env_params prm, EnvSoA<T> es, const T* __restrict__ action,
                                                       EnvOutT<T> out, int B) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
+  __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
+  Env<T>& s = s_env;
   const DevPhys<T>& m = phys<T>();
   (void)mp;
   const int b = blockIdx.x;
@@ -332,7 +332,7 @@ __global__ void __launch_bounds__(NT) env_step_kernel(const DevPhys<T>* __restri
   }
   wsync();
   // ---- _mujoco_step: n_calls x mj_step(nstep = n_substeps)
-  StageClock clk{nullptr, 0};
+  NoClock clk;
   const int nsub = prm.n_substeps * prm.n_calls;
   for (int k = 0; k < nsub; k++) mj_step_dev(m, s, clk, k == nsub - 1 ? s.qpos_pre : nullptr);
   store_env(m, s, st, b);
@@ -448,11 +448,7 @@ static int32_t env_prep(pnp_model* model, const pnp_state_t<T>* st, K kernel, co
   *dm = phys_image<T>(model);
   if (!*dm) { pnp_set_error("%s: model has no physics image (%s)", fn, model->phys_err); return PNP_ERR_MODEL; }
   if (const int32_t rc = phys_resident<T>(model, stream)) return rc;
-  if (hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(Env<T>)) !=
-      hipSuccess) {
-    pnp_set_error("%s: LDS %zu B not available", fn, sizeof(Env<T>));
-    return PNP_ERR_HIP;
-  }
+  (void)kernel;
   return PNP_OK;
 }
 
@@ -464,7 +460,7 @@ static int32_t launch_env_init(pnp_model* model, const pnp_state_t<T>* st, const
   const DevPhys<T>* dm;
   auto k = env_init_kernel<T>;
   if ((rc = env_prep(model, st, k, &dm, "pnp_env_init", stream))) return rc;
-  hipLaunchKernelGGL(k, dim3(B), dim3(NT), sizeof(Env<T>), (hipStream_t)stream, dm, *st, *p, env_view<T>(e), B);
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), B);
   return pnp_check_launch("env_init_kernel");
 }
 template <typename T>
@@ -476,7 +472,7 @@ static int32_t launch_env_reset(pnp_model* model, const pnp_state_t<T>* st, cons
   const DevPhys<T>* dm;
   auto k = env_reset_kernel<T>;
   if ((rc = env_prep(model, st, k, &dm, "pnp_env_reset", stream))) return rc;
-  hipLaunchKernelGGL(k, dim3(B), dim3(NT), sizeof(Env<T>), (hipStream_t)stream, dm, *st, *p, env_view<T>(e), mask,
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), mask,
                      out_view<T>(o), B);
   return pnp_check_launch("env_reset_kernel");
 }
@@ -490,7 +486,7 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   const DevPhys<T>* dm;
   auto k = env_step_kernel<T>;
   if ((rc = env_prep(model, st, k, &dm, "pnp_env_step", stream))) return rc;
-  hipLaunchKernelGGL(k, dim3(B), dim3(NT), sizeof(Env<T>), (hipStream_t)stream, dm, *st, *p, env_view<T>(e), action,
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), action,
                      out_view<T>(o), B);
   return pnp_check_launch("env_step_kernel");
 }

@@ -56,6 +56,11 @@ struct Con {
   int dim, g1, g2;
 };
 
+// env_lds_note: every kernel declares its Env as a static __shared__ variable and hands stage
+// functions a reference to it.  The stages then address LDS off that pointer (ds_* with a VGPR
+// base).  With a dynamic `extern __shared__` buffer instead, out-of-line stages reached the
+// buffer through the per-kernel dynamic-LDS offset table: an s_load + lgkmcnt(0) drain that
+// the compiler re-issued after every wave fence (once per no-slip pair update, for example).
 template <typename T>
 struct Env {
   // ---- small model tables read in every inner loop (copied from the global model image once
@@ -157,10 +162,19 @@ struct StageClock {
     if (prof && threadIdx.x == 0) prof[k] += (unsigned long long)v;
   }
 };
+// the product kernels' clock: every call compiles to nothing (no prof pointer to test at run time)
+struct NoClock {
+  __device__ __forceinline__ void start() {}
+  __device__ __forceinline__ void lap(int) {}
+  __device__ __forceinline__ void sub_start() {}
+  __device__ __forceinline__ void sub_lap(int) {}
+  __device__ __forceinline__ void count(int, int) {}
+};
 // stage slots (include/pnp.h PNP_NSTAGE): sub-stages and per-step counts after the 16 stages
 enum {
-  SC_BROAD = 16, SC_NARROW, SC_CONVEX, SC_NS_W, SC_NS_LISTS,
-  SN_CON = 21, SN_EFC, SN_ITER, SN_CONVEX, SN_ISLAND, SN_NS_SWEEP, SN_LIVE
+  SC_BROAD = 16, SC_NARROW, SC_CONVEX, SC_NS_W, SC_NS_LISTS, SC_K_PRE, SC_K_LEVELS, SC_K_FRAMES, SC_N_GRAD,
+  SC_N_CONV, SC_N_HESS,
+  SN_CON = 27, SN_EFC, SN_ITER, SN_CONVEX, SN_ISLAND, SN_NS_SWEEP, SN_LIVE
 };
 
 // ============================================================================ small helpers
@@ -328,9 +342,10 @@ __device__ __forceinline__ T row_dot(const Env<T>& s, int r, const T* x, T v) {
 #define mblk(m, i, j) mblk_(s, i, j)
 
 // ============================================================================ position stage
-template <typename T>
-__device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+template <typename T, class CLK>
+__device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
+  clk.sub_start();
   // Level-synchronous tree pass (mj_kinematics order): a body's frame is its parent's composed
   // with its own offset and joints, the parent's read from LDS one level earlier.  The per-body
   // work that does not need the parent -- the model constants and a single hinge's rotation
@@ -351,62 +366,84 @@ __device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s)
     for (int t = 0; t < 4; t++) bq[t] = s.mocap_quat[4 * mid + t];
     t_normalize4(bq);
   }
-  // single hinge: its local rotation up front
-  T qh[4] = {1, 0, 0, 0};
-  if (jn == 1 && jt == 3) {
-    const int qa = m.jnt_qposadr[ja];
-    const T ang = s.qpos[qa] - m.qpos0[qa];
-    if (ang != T(0)) {
-      T sn, cs;
-      d_sincos(ang * T(0.5), &sn, &cs);
-      qh[0] = cs; qh[1] = m.jnt_axis[ja][0] * sn; qh[2] = m.jnt_axis[ja][1] * sn; qh[3] = m.jnt_axis[ja][2] * sn;
-    }
+  // the body's own joint, loaded up front (bodies here carry at most one joint; a body with more
+  // takes the generic loop): constants, its qpos, and a single hinge's local rotation (sincos)
+  const bool one = jn == 1;
+  const int qa1 = one ? m.jnt_qposadr[ja] : 0;
+  T jax[3] = {0, 0, 0}, jpos[3] = {0, 0, 0}, fq[7] = {0, 0, 0, 1, 0, 0, 0}, sl = 0;
+  if (one) {
+    for (int t = 0; t < 3; t++) { jax[t] = m.jnt_axis[ja][t]; jpos[t] = m.jnt_pos[ja][t]; }
+    if (jt == 0)
+      for (int t = 0; t < 7; t++) fq[t] = s.qpos[qa1 + t];
+    else
+      sl = s.qpos[qa1] - m.qpos0[qa1];
   }
+  T qh[4] = {1, 0, 0, 0};
+  if (one && jt == 3 && sl != T(0)) {
+    T sn, cs;
+    d_sincos(sl * T(0.5), &sn, &cs);
+    qh[0] = cs; qh[1] = jax[0] * sn; qh[2] = jax[1] * sn; qh[3] = jax[2] * sn;
+  }
+  clk.sub_lap(SC_K_PRE);
   for (int d = 1; __ballot(mine && depth >= d); d++) {
     if (mine && depth == d) {
       T p[3], q[4];
-      if (jn == 1 && jt == 0) {
-        const T* qp = s.qpos + m.jnt_qposadr[ja];
-        p[0] = qp[0]; p[1] = qp[1]; p[2] = qp[2];
-        q[0] = qp[3]; q[1] = qp[4]; q[2] = qp[5]; q[3] = qp[6];
+      if (one && jt == 0) {
+        p[0] = fq[0]; p[1] = fq[1]; p[2] = fq[2];
+        q[0] = fq[3]; q[1] = fq[4]; q[2] = fq[5]; q[3] = fq[6];
         t_normalize4(q);
-        for (int t = 0; t < 3; t++) { s.xanchor[ja][t] = p[t]; s.xaxis[ja][t] = m.jnt_axis[ja][t]; }
+        for (int t = 0; t < 3; t++) { s.xanchor[ja][t] = p[t]; s.xaxis[ja][t] = jax[t]; }
       } else {
         if (pid > 0) {
-          T dv[3];
-          d_mulmatvec3(dv, s.xmat[pid], bp);
-          for (int t = 0; t < 3; t++) p[t] = s.xpos[pid][t] + dv[t];
+          T pm[9], pp[3], dv[3];
+          for (int t = 0; t < 9; t++) pm[t] = s.xmat[pid][t];
+          for (int t = 0; t < 3; t++) pp[t] = s.xpos[pid][t];
           for (int t = 0; t < 4; t++) q[t] = s.xquat[pid][t];
+          d_mulmatvec3(dv, pm, bp);
+          for (int t = 0; t < 3; t++) p[t] = pp[t] + dv[t];
           d_mulquat(q, q, bq);
         } else {
           for (int t = 0; t < 3; t++) p[t] = bp[t];
           for (int t = 0; t < 4; t++) q[t] = bq[t];
         }
-        for (int j = 0; j < jn; j++) {
-          const int jid = ja + j, qa = m.jnt_qposadr[jid], ty = m.jnt_type[jid];
+        if (one) {
           T ax[3], an[3];
-          t_rotvecquat_mj(ax, m.jnt_axis[jid], q);
-          t_rotvecquat_mj(an, m.jnt_pos[jid], q);
+          t_rotvecquat_mj(ax, jax, q);
+          t_rotvecquat_mj(an, jpos, q);
           an[0] += p[0]; an[1] += p[1]; an[2] += p[2];
-          if (ty == 2) {
-            const T dd = s.qpos[qa] - m.qpos0[qa];
-            p[0] += ax[0] * dd; p[1] += ax[1] * dd; p[2] += ax[2] * dd;
-          } else if (ty == 3) {
-            T ql[4] = {qh[0], qh[1], qh[2], qh[3]}, v[3];
-            if (jn != 1) {
+          if (jt == 2) {
+            p[0] += ax[0] * sl; p[1] += ax[1] * sl; p[2] += ax[2] * sl;
+          } else if (jt == 3) {
+            T v[3];
+            d_mulquat(q, q, qh);
+            t_rotvecquat_mj(v, jpos, q);
+            p[0] = an[0] - v[0]; p[1] = an[1] - v[1]; p[2] = an[2] - v[2];
+          }
+          for (int t = 0; t < 3; t++) { s.xanchor[ja][t] = an[t]; s.xaxis[ja][t] = ax[t]; }
+        } else {
+          for (int j = 0; j < jn; j++) {
+            const int jid = ja + j, qa = m.jnt_qposadr[jid], ty = m.jnt_type[jid];
+            T ax[3], an[3];
+            t_rotvecquat_mj(ax, m.jnt_axis[jid], q);
+            t_rotvecquat_mj(an, m.jnt_pos[jid], q);
+            an[0] += p[0]; an[1] += p[1]; an[2] += p[2];
+            if (ty == 2) {
+              const T dd = s.qpos[qa] - m.qpos0[qa];
+              p[0] += ax[0] * dd; p[1] += ax[1] * dd; p[2] += ax[2] * dd;
+            } else if (ty == 3) {
               const T ang = s.qpos[qa] - m.qpos0[qa];
-              ql[0] = 1; ql[1] = ql[2] = ql[3] = 0;
+              T ql[4] = {1, 0, 0, 0}, v[3];
               if (ang != T(0)) {
                 T sn, cs;
                 d_sincos(ang * T(0.5), &sn, &cs);
                 ql[0] = cs; ql[1] = m.jnt_axis[jid][0] * sn; ql[2] = m.jnt_axis[jid][1] * sn; ql[3] = m.jnt_axis[jid][2] * sn;
               }
+              d_mulquat(q, q, ql);
+              t_rotvecquat_mj(v, m.jnt_pos[jid], q);
+              p[0] = an[0] - v[0]; p[1] = an[1] - v[1]; p[2] = an[2] - v[2];
             }
-            d_mulquat(q, q, ql);
-            t_rotvecquat_mj(v, m.jnt_pos[jid], q);
-            p[0] = an[0] - v[0]; p[1] = an[1] - v[1]; p[2] = an[2] - v[2];
+            for (int t = 0; t < 3; t++) { s.xanchor[jid][t] = an[t]; s.xaxis[jid][t] = ax[t]; }
           }
-          for (int t = 0; t < 3; t++) { s.xanchor[jid][t] = an[t]; s.xaxis[jid][t] = ax[t]; }
         }
       }
       t_normalize4(q);
@@ -424,6 +461,7 @@ __device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s)
     for (int t = 0; t < 9; t++) s.xmat[0][t] = (t % 4 == 0) ? T(1) : T(0);
   }
   wsync();
+  clk.sub_lap(SC_K_LEVELS);
   // inertial frames (bodies) and geom frames (collidable geoms)
   for (int i = lane_id(); i < m.nbody + m.ngeom; i += NT) {
     if (i < m.nbody) {
@@ -441,6 +479,12 @@ __device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s)
     }
   }
   wsync();
+  clk.sub_lap(SC_K_FRAMES);
+}
+template <typename T>
+__device__ void st_kinematics(const DevPhys<T>& m, Env<T>& s) {
+  NoClock clk;
+  st_kinematics(m, s, clk);
 }
 
 template <typename T>
@@ -692,8 +736,8 @@ __device__ T mulM_row(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, i
 // ============================================================================ collision
 #include "collide_dev.h"
 
-template <typename T>
-__device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, StageClock& clk) {
+template <typename T, class CLK>
+__device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   clk.sub_start();
@@ -1517,8 +1561,8 @@ __device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
   wsync();
 }
 
-template <typename T>
-__device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, StageClock& clk) {
+template <typename T, class CLK>
+__device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (s.nefc == 0) {
@@ -1573,6 +1617,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, Sta
   int it = 0;
   const int nent = s.isl_eoff[s.nisland];
   for (; it < m.iterations; it++) {
+    clk.sub_start();
     // gradient g = M (x - x_smooth) + J^T (D jar) over the dof's island rows
     if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
     wsync();
@@ -1583,6 +1628,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, Sta
       s.v2[l] = g * g;
     }
     wsync();
+    clk.sub_lap(SC_N_GRAD);
     // an island whose last step kept its active set is at that quadratic's minimiser up to the
     // rounding of one Cholesky solve (cond(H) eps): done once its gradient is at the floor,
     // otherwise it takes one more (refining) Newton step
@@ -1590,6 +1636,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, Sta
     if (!done && unchanged >= 1 && PM<T>::sqrt_(s.isl_val[l]) * gscale < gtol) done = true;
     if (l < PH_MAXT) s.isl_flag[l] = done;
     wsync();
+    clk.sub_lap(SC_N_CONV);
     if (!__ballot(!done)) { clk.lap(9); break; }
     // Hessian island blocks (lower triangle, lane per entry): M + sum_active D J J^T; blocks of
     // islands whose active set is unchanged since their last assembly are reused as they are
@@ -1621,6 +1668,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, Sta
       s.H[j][i] = h;
     }
     wsync();
+    clk.sub_lap(SC_N_HESS);
     clk.lap(9);
     // Newton direction per island (lane per island); the register path leaves H intact, the
     // in-place LDS path (merged islands > 9 dofs) consumes it
@@ -1679,8 +1727,8 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, Sta
 }
 
 // ============================================================================ no-slip
-template <typename T>
-__device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, StageClock& clk) {
+template <typename T, class CLK>
+__device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (m.noslip_iterations <= 0 || s.nefc == 0) return;
@@ -1772,6 +1820,57 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, Sta
     p.b1 = s.efc_bb[p.j + 1];
     return p;
   };
+  // Short sweeps (every group's list <= NSR pairs, the common case: an island of a box resting on
+  // a board has 8) keep the whole sweep in registers: each pair's J / W slots, its 2 x 2 Delassus
+  // block (fixed over the iterations), b and its two forces (only this pair writes them).  An
+  // update is then one LDS read of v at the slot's dof, two row sums, the 2 x 2 projection and
+  // the write back of v; the forces return to LDS once, after the last iteration.  Same
+  // arithmetic in the same order as the streaming path below.
+  constexpr int NSR = 8;
+  if (maxlen <= NSR) {
+    NsPair P[NSR];
+    T A00[NSR], A01[NSR], A10[NSR], A11[NSR], F0[NSR], F1[NSR];
+#pragma unroll
+    for (int k = 0; k < NSR; k++) {
+      P[k] = fetch(k < maxlen ? k : 0);
+      P[k].act = P[k].act && k < maxlen;
+      P[k].on = P[k].on && k < maxlen;
+      A00[k] = rowsum16(P[k].J0 * P[k].W0); A01[k] = rowsum16(P[k].J0 * P[k].W1);
+      A10[k] = rowsum16(P[k].J1 * P[k].W0); A11[k] = rowsum16(P[k].J1 * P[k].W1);
+      F0[k] = s.efc_force[P[k].j];
+      F1[k] = s.efc_force[P[k].j + 1];
+    }
+    for (int iter = 0; iter < m.noslip_iterations; iter++) {
+#pragma unroll
+      for (int k = 0; k < NSR; k++) {
+        if (k >= maxlen) break;
+        const NsPair& cur = P[k];
+        const T vd = cur.on ? s.v2[cur.d] : T(0);
+        const T r0 = rowsum16(cur.J0 * vd) + cur.b0;
+        const T r1 = rowsum16(cur.J1 * vd) + cur.b1;
+        const T f0 = F0[k], f1 = F1[k];
+        const T a00 = A00[k], a01 = A01[k], a10 = A10[k], a11 = A11[k];
+        const T bc0 = r0 - (a00 * f0 + a01 * f1), bc1 = r1 - (a10 * f0 + a11 * f1);
+        const T mid = T(0.5) * (f0 + f1);
+        const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;
+        T n0, n1;
+        if (K1 < T(1e-15)) { n0 = n1 = mid; }
+        else {
+          T y = -K0 / K1;
+          if (y < -mid) y = -mid; else if (y > mid) y = mid;
+          n0 = mid + y; n1 = mid - y;
+        }
+        if (cur.on) s.v2[cur.d] = vd + (cur.W0 * (n0 - f0) + cur.W1 * (n1 - f1));
+        if (cur.act) { F0[k] = n0; F1[k] = n1; }
+        wsync();
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NSR; k++)
+      if (P[k].act && q == 0) { s.efc_force[P[k].j] = F0[k]; s.efc_force[P[k].j + 1] = F1[k]; }
+    wsync();
+    return;
+  }
   for (int iter = 0; iter < m.noslip_iterations; iter++) {
     NsPair cur = fetch(0);
     for (int k = 0; k < maxlen; k++) {
@@ -1907,10 +2006,10 @@ __device__ void dump_contacts(const DevPhys<T>& /*image: phys<T>()*/, const Env<
   }
 }
 
-template <typename T>
-__device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, StageClock& clk, double* dbg = nullptr) {
+template <typename T, class CLK>
+__device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk, double* dbg = nullptr) {
   const DevPhys<T>& m = phys<T>();
-  st_kinematics(m, s);      clk.lap(1);
+  st_kinematics(m, s, clk); clk.lap(1);
   st_compos_crb(m, s);      clk.lap(2);
   st_factor_M(m, s);        clk.lap(3);
   st_collision(m, s, clk);
@@ -1938,7 +2037,7 @@ __device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, Stage
 template <typename T>
 __device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
   const DevPhys<T>& m = phys<T>();
-  StageClock clk{nullptr, 0};
+  NoClock clk;
   forward(m, s, clk);
 }
 
@@ -1958,8 +2057,8 @@ __device__ void check_state(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
 
 // save_qpos (gym env, last sub-step): the qpos the forward ran at, i.e. where MuJoCo's
 // data.site_* / Jacobians stay after mj_step returns
-template <typename T>
-__device__ void mj_step_dev(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, StageClock& clk, T* save_qpos = nullptr) {
+template <typename T, class CLK>
+__device__ void mj_step_dev(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk, T* save_qpos = nullptr) {
   const DevPhys<T>& m = phys<T>();
   clk.start();
   check_state(m, s);
@@ -2012,15 +2111,20 @@ __device__ void store_env(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& 
 template <typename T, bool TIMED>
 __global__ void __launch_bounds__(NT) step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st, int B, int nsub,
                                                  unsigned long long* __restrict__ prof) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
+  __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
+  Env<T>& s = s_env;
   const DevPhys<T>& m = phys<T>();
   (void)mp;
   const int b = blockIdx.x;
   if (b >= B) return;
-  StageClock clk{TIMED ? prof + (size_t)b * PNP_NSTAGE : nullptr, 0};
   load_env(m, s, st, b);
-  for (int k = 0; k < nsub; k++) mj_step_dev(m, s, clk);
+  if constexpr (TIMED) {
+    StageClock clk{prof + (size_t)b * PNP_NSTAGE, 0, 0};
+    for (int k = 0; k < nsub; k++) mj_step_dev(m, s, clk);
+  } else {
+    NoClock clk;
+    for (int k = 0; k < nsub; k++) mj_step_dev(m, s, clk);
+  }
   store_env(m, s, st, b);
 }
 
@@ -2028,15 +2132,15 @@ __global__ void __launch_bounds__(NT) step_kernel(const DevPhys<T>* __restrict__
 template <typename T>
 __global__ void __launch_bounds__(NT) forward_debug_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st, int B,
                                                           double* __restrict__ dbg) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  Env<T>& s = *reinterpret_cast<Env<T>*>(smem);
+  __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
+  Env<T>& s = s_env;
   const DevPhys<T>& m = phys<T>();
   (void)mp;
   const int b = blockIdx.x;
   if (b >= B) return;
   load_env(m, s, st, b);
   double* o = dbg + (size_t)b * PNP_DBG_SIZE;
-  StageClock clk{nullptr, 0};
+  NoClock clk;
   forward(m, s, clk, o);
   const int l = lane_id();
   const int nv = m.nv;
@@ -2113,22 +2217,13 @@ static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B
   const DevPhys<T>* dm = phys_image<T>(model);
   if (!dm) { pnp_set_error("pnp_step: model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
   if (const int32_t rc = phys_resident<T>(model, stream)) return rc;
-  const size_t lds = sizeof(Env<T>);
   if (dbg) {
     auto k = forward_debug_kernel<T>;
-    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
-      pnp_set_error("pnp_forward_debug: LDS %zu B not available", lds);
-      return PNP_ERR_HIP;
-    }
-    hipLaunchKernelGGL(k, dim3(B), dim3(NT), lds, (hipStream_t)stream, dm, *st, B, dbg);
+    hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, dbg);
     return pnp_check_launch("forward_debug_kernel");
   }
   auto k = prof ? step_kernel<T, true> : step_kernel<T, false>;
-  if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
-    pnp_set_error("pnp_step: LDS %zu B not available", lds);
-    return PNP_ERR_HIP;
-  }
-  hipLaunchKernelGGL(k, dim3(B), dim3(NT), lds, (hipStream_t)stream, dm, *st, B, nsub, prof);
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, nsub, prof);
   return pnp_check_launch("step_kernel");
 }
 

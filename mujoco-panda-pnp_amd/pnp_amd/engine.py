@@ -142,9 +142,10 @@ class Engine:
               "newton_update", "noslip", "finish_accel", "euler",
               # sub-stages (also inside their parent's cycles)
               "col_broadphase", "col_primitive", "col_convex", "noslip_W", "noslip_lists",
+              "kin_prologue", "kin_levels", "kin_frames", "newton_gradient", "newton_converge", "newton_hessian",
               # per-sub-step counts (summed over sub-steps), not cycles
               "n_con", "n_efc", "n_newton_iter", "n_convex", "n_island", "n_noslip_sweep", "n_live")
-    N_STAGE_CYCLES = 21
+    N_STAGE_CYCLES = 27
 
     def step_profile(self, st, nsub=1):
         """Diagnostic timed instantiation of pnp_step: per-stage shader cycles and per-step counts
