@@ -231,6 +231,65 @@ int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
     }
   }
   d->npair = np;
+  // ---- body-pair pre-cull (result-neutral: a body sphere contains its geoms' spheres)
+  {
+    const double slack = 1e-5;
+    for (int b = 0; b < s->nbody; b++) {
+      double c[3] = {0, 0, 0}, lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+      int cnt = 0, plane = 0;
+      for (int g = 0; g < s->ngeom; g++) {
+        if (map[g] < 0 || s->geom_bodyid[g] != b) continue;
+        if (!(s->geom_rbound[g] > 0)) { plane = 1; continue; }
+        for (int k = 0; k < 3; k++) {
+          const double v = s->geom_pos[3 * g + k];
+          lo[k] = v - s->geom_rbound[g] < lo[k] ? v - s->geom_rbound[g] : lo[k];
+          hi[k] = v + s->geom_rbound[g] > hi[k] ? v + s->geom_rbound[g] : hi[k];
+        }
+        cnt++;
+      }
+      double r = 0;
+      if (cnt) {
+        for (int k = 0; k < 3; k++) c[k] = 0.5 * (lo[k] + hi[k]);
+        for (int g = 0; g < s->ngeom; g++) {
+          if (map[g] < 0 || s->geom_bodyid[g] != b || !(s->geom_rbound[g] > 0)) continue;
+          double dd = 0;
+          for (int k = 0; k < 3; k++) dd += (s->geom_pos[3 * g + k] - c[k]) * (s->geom_pos[3 * g + k] - c[k]);
+          const double rr = __builtin_sqrt(dd) + s->geom_rbound[g];
+          r = rr > r ? rr : r;
+        }
+      }
+      for (int k = 0; k < 3; k++) d->body_bcen[b][k] = (T)c[k];
+      d->body_brad[b] = plane ? (T)-1 : (T)(r * (1 + slack) + slack);
+    }
+    int nbp = 0;
+    static thread_local int grp[PH_MAXPAIR];
+    for (int p = 0; p < np; p++) grp[p] = -1;
+    for (int p = 0; p < np; p++) {
+      if (grp[p] >= 0) continue;
+      if (nbp >= PH_MAXBP) { snprintf(err, errlen, "too many collision body pairs"); return -1; }
+      const int g1 = d->geom_id[d->pair_g1[p]], g2 = d->geom_id[d->pair_g2[p]];
+      int b1 = s->geom_bodyid[g1], b2 = s->geom_bodyid[g2];
+      if (b1 > b2) { const int t = b1; b1 = b2; b2 = t; }
+      d->bp_b1[nbp] = (short)b1;
+      d->bp_b2[nbp] = (short)b2;
+      double mg = 0;
+      for (int q = p; q < np; q++) {
+        const int h1 = d->geom_id[d->pair_g1[q]], h2 = d->geom_id[d->pair_g2[q]];
+        int c1 = s->geom_bodyid[h1], c2 = s->geom_bodyid[h2];
+        if (c1 > c2) { const int t = c1; c1 = c2; c2 = t; }
+        if (c1 != b1 || c2 != b2) continue;
+        grp[q] = nbp;
+        mg = (double)d->pair_margin[q] > mg ? (double)d->pair_margin[q] : mg;
+      }
+      const double r1 = (double)d->body_brad[b1], r2 = (double)d->body_brad[b2];
+      d->bp_reach[nbp] = (T)(r1 < 0 || r2 < 0 ? -1.0 : (r1 + r2 + mg) * (1 + slack) + slack);
+      nbp++;
+    }
+    d->nbpair = nbp;
+    for (int p = 0; p < np; p++)
+      d->pair_pack[p] = (uint32_t)d->pair_g1[p] | (uint32_t)d->pair_g2[p] << 8 |
+                        (uint32_t)d->pair_kind[p] << 16 | (uint32_t)grp[p] << 24;
+  }
   for (int k = 0; k < s->nmesh; k++) {
     d->mesh_vertadr[k] = s->mesh_vertadr[k];
     d->mesh_vertnum[k] = s->mesh_vertnum[k];

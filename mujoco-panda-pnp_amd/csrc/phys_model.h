@@ -29,6 +29,7 @@
 #define PH_PAIR_PRIM 0     // primitive collider, sphere test only
 #define PH_PAIR_CONVEX 1   // MPR pair: + oriented bounding boxes overlap
 #define PH_PAIR_PLANE 2    // plane vs geom: + the geom's box reaches the plane
+#define PH_MAXBP 256        // body pairs with at least one candidate geom pair
 #define PH_MAXMESHV 1400
 #define PH_MAXMESH 16
 #define PH_MAXCON 48      // contacts per env (lane per contact: <= 64)
@@ -79,6 +80,16 @@ struct DevPhys {
   // i.e. a plane), the pair margin, and the exact box test the pair gets (PH_PAIR_*)
   T pair_reach[PH_MAXPAIR], pair_margin[PH_MAXPAIR];
   unsigned char pair_kind[PH_MAXPAIR];
+  // the broadphase's per-pair word: g1 | g2 << 8 | kind << 16 | body pair << 24 (one load per lane)
+  uint32_t pair_pack[PH_MAXPAIR];
+  // body-pair pre-cull: the candidate geom pairs grouped by their (body, body) pair; a body's
+  // bounding sphere (body-frame centre body_bcen, radius body_brad covering every collidable geom's
+  // bounding sphere) and the group reach R1 + R2 + max margin (< 0: a body with a plane, always
+  // tested).  Result-neutral: a body pair out of reach has every geom pair out of reach.
+  int nbpair;
+  short bp_b1[PH_MAXBP], bp_b2[PH_MAXBP];
+  T bp_reach[PH_MAXBP];
+  T body_bcen[PH_MAXB][3], body_brad[PH_MAXB];
   // meshes (convex hulls)
   int mesh_vertadr[PH_MAXMESH], mesh_vertnum[PH_MAXMESH];
   T mesh_vert[PH_MAXMESHV][3];

@@ -137,7 +137,7 @@ struct Env {
 // count() accumulates per-sub-step sizes (contacts, rows, iterations ...) into the count slots.
 struct StageClock {
   unsigned long long* prof;
-  unsigned long long t, ts;
+  unsigned long long t, ts, ta;
   __device__ void start() { if (prof) t = __builtin_amdgcn_s_memtime(); }
   __device__ void lap(int k) {
     if (!prof) return;
@@ -161,6 +161,19 @@ struct StageClock {
   __device__ void count(int k, int v) {
     if (prof && threadIdx.x == 0) prof[k] += (unsigned long long)v;
   }
+  // ad-hoc timers (SC_AUX0 ..): a third clock, independent of the stage and sub-stage laps
+  __device__ void aux_start() {
+    if (!prof) return;
+    __syncthreads();
+    ta = __builtin_amdgcn_s_memtime();
+  }
+  __device__ void aux_lap(int k) {
+    if (!prof) return;
+    __syncthreads();
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) prof[k] += n - ta;
+    ta = n;
+  }
 };
 // the product kernels' clock: every call compiles to nothing (no prof pointer to test at run time)
 struct NoClock {
@@ -169,12 +182,15 @@ struct NoClock {
   __device__ __forceinline__ void sub_start() {}
   __device__ __forceinline__ void sub_lap(int) {}
   __device__ __forceinline__ void count(int, int) {}
+  __device__ __forceinline__ void aux_start() {}
+  __device__ __forceinline__ void aux_lap(int) {}
 };
 // stage slots (include/pnp.h PNP_NSTAGE): sub-stages and per-step counts after the 16 stages
 enum {
   SC_BROAD = 16, SC_NARROW, SC_CONVEX, SC_NS_W, SC_NS_LISTS, SC_K_PRE, SC_K_LEVELS, SC_K_FRAMES, SC_N_GRAD,
   SC_N_CONV, SC_N_HESS,
-  SN_CON = 27, SN_EFC, SN_ITER, SN_CONVEX, SN_ISLAND, SN_NS_SWEEP, SN_LIVE
+  SN_CON = 27, SN_EFC, SN_ITER, SN_CONVEX, SN_ISLAND, SN_NS_SWEEP, SN_LIVE,
+  SC_AUX0 = 34   // 8 ad-hoc sub-stage timers, SC_AUX0 .. SC_AUX0 + 7
 };
 
 // ============================================================================ small helpers
@@ -741,30 +757,80 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   clk.sub_start();
-  // broadphase: bounding spheres (+ exact box tests, below); survivors compacted in pair order
+  clk.aux_start();
+  // broadphase, three passes, survivors compacted in pair order throughout.
+  // (1) body pairs: bounding spheres over each body's collidable geoms (bit per body pair, kept
+  //     wave-uniform in four 64-bit words); (2) geom pairs of live body pairs: bounding spheres;
+  //     (3) the exact box tests (convex: oriented boxes overlap; plane: the box reaches the plane)
+  //     over the pass-(2) survivors only -- a compact list, so the divergent box tests occupy
+  //     one or two lane chunks instead of one in every chunk of the pair table.
+  uint64_t bpm[PH_MAXBP / 64];
+#pragma unroll
+  for (int w = 0; w < PH_MAXBP / 64; w++) {
+    const int bp = w * NT + l;
+    bool alive = false;
+    if (w * NT < m.nbpair && bp < m.nbpair) {
+      const T reach = m.bp_reach[bp];
+      alive = true;
+      if (reach >= 0) {
+        const int b1 = m.bp_b1[bp], b2 = m.bp_b2[bp];
+        T v[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+          v[k] = s.xpos[b1][k] + s.xmat[b1][3 * k] * m.body_bcen[b1][0] + s.xmat[b1][3 * k + 1] * m.body_bcen[b1][1] +
+                 s.xmat[b1][3 * k + 2] * m.body_bcen[b1][2] - s.xpos[b2][k] - s.xmat[b2][3 * k] * m.body_bcen[b2][0] -
+                 s.xmat[b2][3 * k + 1] * m.body_bcen[b2][1] - s.xmat[b2][3 * k + 2] * m.body_bcen[b2][2];
+        alive = t_dot3(v, v) <= reach * reach;
+      }
+    }
+    bpm[w] = __ballot(alive);
+  }
+  clk.aux_lap(SC_AUX0);   // aux0: broadphase body-pair pass
   int nlive = 0;
   for (int base = 0; base < m.npair; base += NT) {
     const int pi = base + l;
     bool keep = false;
     if (pi < m.npair) {
-      const int g1 = m.pair_g1[pi], g2 = m.pair_g2[pi], kind = m.pair_kind[pi];
+      const uint32_t pk = m.pair_pack[pi];
+      const int bp = pk >> 24;
+      const uint64_t word = bp < 64 ? bpm[0] : bp < 128 ? bpm[1] : bp < 192 ? bpm[2] : bpm[3];
+      keep = (word >> (bp & 63)) & 1;
       const T reach = m.pair_reach[pi];
-      keep = true;
-      if (reach >= 0) {
+      if (keep && reach >= 0) {
+        const int g1 = pk & 255, g2 = (pk >> 8) & 255;
         T v[3] = {s.gpos[g1][0] - s.gpos[g2][0], s.gpos[g1][1] - s.gpos[g2][1], s.gpos[g1][2] - s.gpos[g2][2]};
         keep = t_dot3(v, v) <= reach * reach;
       }
-      // convex (MPR) pairs also need overlapping oriented bounding boxes; plane pairs (no
-      // bounding sphere on the plane side) need the other geom's box to reach the plane
-      if (keep && kind == PH_PAIR_CONVEX) keep = !c_convex_obb_disjoint(m, s, g1, g2, m.pair_margin[pi]);
-      else if (keep && kind == PH_PAIR_PLANE) keep = !c_plane_obb_clear(m, s, g1, g2, m.pair_margin[pi]);
     }
     const uint64_t bal = __ballot(keep);
-    const int pos = nlive + __popcll(bal & ((1ull << l) - 1));
-    if (keep) s.live[pos] = (short)pi;
+    if (keep) s.live[nlive + __popcll(bal & ((1ull << l) - 1))] = (short)pi;
     nlive += __popcll(bal);
   }
   wsync();
+  clk.aux_lap(SC_AUX0 + 1);   // aux1: broadphase geom-pair sphere pass
+  // exact box tests over the sphere survivors, compacted in place (a chunk reads its entries into
+  // registers before any lane writes, and writes land at or below the read positions)
+  const int nsph = nlive;
+  nlive = 0;
+  for (int base = 0; base < nsph; base += NT) {
+    const int k = base + l;
+    bool keep = false;
+    int pi = 0;
+    if (k < nsph) {
+      pi = s.live[k];
+      const uint32_t pk = m.pair_pack[pi];
+      const int g1 = pk & 255, g2 = (pk >> 8) & 255, kind = (pk >> 16) & 255;
+      keep = true;
+      if (kind == PH_PAIR_CONVEX) keep = !c_convex_obb_disjoint(m, s, g1, g2, m.pair_margin[pi]);
+      else if (kind == PH_PAIR_PLANE) keep = !c_plane_obb_clear(m, s, g1, g2, m.pair_margin[pi]);
+    }
+    const uint64_t bal = __ballot(keep);
+    wsync();
+    if (keep) s.live[nlive + __popcll(bal & ((1ull << l) - 1))] = (short)pi;
+    nlive += __popcll(bal);
+  }
+  wsync();
+  clk.aux_lap(SC_AUX0 + 2);   // aux2: broadphase exact box tests
   clk.sub_lap(SC_BROAD);
   // narrowphase, one pass: every lane collides its pair once, its contacts go to a staging area
   // through an LDS slot counter, then each lands at (contacts so far) + (exclusive scan of the

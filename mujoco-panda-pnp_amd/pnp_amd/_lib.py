@@ -9,7 +9,7 @@ from .model import PnpIKParams, PnpModelDesc
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpnp.so")
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # every symbol include/pnp.h declares (tests check the library exports all of them)
 EXPORTS = [

@@ -144,7 +144,9 @@ class Engine:
               "col_broadphase", "col_primitive", "col_convex", "noslip_W", "noslip_lists",
               "kin_prologue", "kin_levels", "kin_frames", "newton_gradient", "newton_converge", "newton_hessian",
               # per-sub-step counts (summed over sub-steps), not cycles
-              "n_con", "n_efc", "n_newton_iter", "n_convex", "n_island", "n_noslip_sweep", "n_live")
+              "n_con", "n_efc", "n_newton_iter", "n_convex", "n_island", "n_noslip_sweep", "n_live",
+              # ad-hoc sub-stage timers (cycles; see the sub_lap calls in csrc/step.hip)
+              "aux0", "aux1", "aux2", "aux3", "aux4", "aux5", "aux6", "aux7")
     N_STAGE_CYCLES = 27
 
     def step_profile(self, st, nsub=1):

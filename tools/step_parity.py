@@ -128,7 +128,9 @@ def profile_stages(B=4096, nsub=10, bench_inputs=False):
               f"implied resident waves {B * nsub * tot / nsub / t / 2.4e9:.0f} (at 2.4 GHz)")
     print(f"per env per sub-step: {tot / nsub:.0f} cycles")
     for k, name in enumerate(eng.STAGES):
-        if k < nc:
+        if k < nc or name.startswith("aux"):
+            if name.startswith("aux") and not prof[:, k].any():
+                continue
             print(f"  {name:18s} {prof[:, k].mean() / nsub:10.0f} cycles  {100 * prof[:, k].mean() / tot:5.1f}%")
         else:
             print(f"  {name:18s} {prof[:, k].mean() / nsub:10.2f} per env-sub-step (max {prof[:, k].max() / nsub:.2f})")
