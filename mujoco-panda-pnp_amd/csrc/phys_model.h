@@ -35,6 +35,7 @@
 #define PH_MAXCON 48      // contacts per env (lane per contact: <= 64)
 #define PH_MAXEFC 208     // 6 weld + 9 limit + 4 x 48 contact rows
 #define PH_MAXJSLOT 2048  // packed constraint-Jacobian slots (sum of row widths)
+#define PH_JTCAP 1536    // dense island Jacobian entries (sum over islands of rows x dofs; larger: slot path)
 #define PH_ROWW 16        // sparse row width: dofs of <= 2 trees (arm 9 + cube 6)
 #define PH_MAXMENTRY 160  // (i, j in ancestors(i)) entries of M
 #define PH_MAXMBLK 256    // sum over trees of tree_dofnum^2

@@ -88,14 +88,25 @@ struct Env {
       short live[PH_MAXPAIR];   // broadphase survivors: every candidate pair fits
       Con<T> con[PH_MAXCON];
     };
-    struct {                   // Newton: island Hessian blocks + per-row scratch
-      T H[PH_MAXV][PH_MAXV];
-      T ntmp[PH_MAXEFC];
-    };
-    struct {                   // no-slip: W = M^-1 J^T and the per-group pair lists
-      T efc_Wv[PH_MAXJSLOT];
-      short ns_list[4][PH_MAXEFC / 2];
-      int ns_len[4];
+    struct {
+      // solver stages: the constraint Jacobian once more, as dense island blocks (rows of island I
+      // in island row order x its dofs in island order, row-major at isl_joff[I]; zeros where a
+      // row does not touch a dof).  The dof-side sums (gradient, Hessian, J^T f) then stream
+      // contiguous rows with no per-row slot lookup.  Built by build_islands when it fits (jt_ok).
+      T jt[PH_JTCAP];
+      union {
+        struct {               // Newton: island Hessian blocks + per-row scratch
+          T H[PH_MAXV][PH_MAXV];
+          T ntmp[PH_MAXEFC];
+          T rr_f[PH_MAXEFC], rr_d[PH_MAXEFC];   // island row order: D jar, D (active rows; else 0)
+        };
+        struct {               // no-slip: W = M^-1 J^T and the per-group pair lists
+          T efc_Wv[PH_MAXJSLOT];
+          short ns_list[4][PH_MAXEFC / 2];
+          int ns_len[4];
+          T rr_g[PH_MAXEFC];   // island row order: forces
+        };
+      };
     };
   };
   T M[PH_MAXMBLK];    // per-tree dense blocks
@@ -123,6 +134,8 @@ struct Env {
   int tree_island[PH_MAXT], isl_n[PH_MAXT];
   unsigned char isl_dof[PH_MAXT][PH_MAXV];
   int isl_eoff[PH_MAXT + 1], isl_roff[PH_MAXT + 1];
+  int isl_joff[PH_MAXT + 1], tree_ipos[PH_MAXT], jt_ok;   // dense island Jacobian blocks (jt)
+  unsigned char dof_ipos[PH_MAXV];                         // a dof's position in its island
   short isl_row[PH_MAXEFC];
   T isl_alpha[PH_MAXT];        // per-island line-search step (also the warm-start choice)
   T isl_cost[PH_MAXT], isl_val[PH_MAXT];   // per-island reductions (cost, |grad|^2 ...)
@@ -1427,6 +1440,14 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s)
     for (int u = 0; u < t; u++)
       if (comp >> u & 1u) pos += s.c_tree_dofnum[u];
     s.isl_dof[island_of(t)][pos] = (unsigned char)l;
+    s.dof_ipos[l] = (unsigned char)pos;
+  }
+  if (l < nt) {
+    const uint32_t comp = (uint32_t)(R >> (8 * l)) & 0xFFu;
+    int pos = 0;
+    for (int u = 0; u < l; u++)
+      if (comp >> u & 1u) pos += s.c_tree_dofnum[u];
+    s.tree_ipos[l] = pos;
   }
   if (l < nis) {
     int n = 0;
@@ -1456,8 +1477,51 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s)
       off += __popcll(bal);
     }
   }
-  if (l == 0) s.isl_roff[nis] = off;
+  if (l == 0) {
+    s.isl_roff[nis] = off;
+    int jo = 0;
+    for (int I = 0; I < nis; I++) {
+      s.isl_joff[I] = jo;
+      jo += (s.isl_roff[I + 1] - s.isl_roff[I]) * s.isl_n[I];
+    }
+    s.isl_joff[nis] = jo;
+    s.jt_ok = jo <= PH_JTCAP;
+  }
   wsync();
+  // dense island Jacobian blocks: zero, then lane per row scatters its packed slots (tree t's
+  // slots are contiguous columns from tree_ipos[t] in the island's dof order)
+  if (s.jt_ok) {
+    const int tot = s.isl_joff[nis];
+    for (int e = l; e < tot; e += NT) s.jt[e] = T(0);
+    wsync();
+    for (int rr = l; rr < s.nefc; rr += NT) {
+      const int r = s.isl_row[rr];
+      const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], off = s.efc_off[r];
+      const int I = s.tree_island[t0], n = s.isl_n[I];
+      T* row = s.jt + s.isl_joff[I] + (rr - s.isl_roff[I]) * n;
+      const int n0 = s.c_tree_dofnum[t0], w = row_width(m, t0, t1);
+      const int p0 = s.tree_ipos[t0], p1 = t1 >= 0 ? s.tree_ipos[t1] - n0 : 0;
+      for (int k = 0; k < w; k++) row[k < n0 ? p0 + k : p1 + k] = s.efc_Jv[off + k];
+    }
+    wsync();
+  }
+}
+
+// g + sum over island I's rows (island row order) of jt(row, a) * f[row] with the dense blocks:
+// a = the dof's island position, f in island row order (zero for rows that do not count)
+template <typename T>
+__device__ __forceinline__ T jt_dof_sum(const Env<T>& s, int I, int a, T g, const T* f) {
+  const int n = s.isl_n[I], r0 = s.isl_roff[I], nr = s.isl_roff[I + 1] - r0;
+  const T* col = s.jt + s.isl_joff[I] + a;
+  const T* fr = f + r0;
+#pragma unroll 4
+  for (int k = 0; k < nr; k++) g += col[k * n] * fr[k];
+  return g;
+}
+// out[rr] = v[isl_row[rr]] (island row order)
+template <typename T>
+__device__ __forceinline__ void gather_rows(const Env<T>& s, const T* v, T* out) {
+  for (int rr = lane_id(); rr < s.nefc; rr += NT) out[rr] = v[s.isl_row[rr]];
 }
 
 // Cholesky + solve of one island's Hessian block held in registers (n <= N), lane-private.
@@ -1682,14 +1746,25 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   const T gtol = T(100) * PM<T>::eps();
   int it = 0;
   const int nent = s.isl_eoff[s.nisland];
+  const bool jt = s.jt_ok;
   for (; it < m.iterations; it++) {
     clk.sub_start();
     // gradient g = M (x - x_smooth) + J^T (D jar) over the dof's island rows
     if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
+    if (jt)
+      for (int rr = l; rr < s.nefc; rr += NT) {
+        const int r = s.isl_row[rr];
+        const bool a = s.efc_act[r];
+        const T d = s.efc_D[r];
+        s.rr_f[rr] = a ? d * s.efc_jar[r] : T(0);
+        s.rr_d[rr] = a ? d : T(0);
+      }
     wsync();
     if (l < m.nv) {
       const int t = s.c_dof_tree[l], I = s.tree_island[t];
-      const T g = dof_row_sum(mulM_row(m, s, l, s.v1), s, I, t, l - s.c_tree_dofadr[t], s.efc_D, s.efc_jar, true);
+      const T mv = mulM_row(m, s, l, s.v1);
+      const T g = jt ? jt_dof_sum(s, I, s.dof_ipos[l], mv, s.rr_f)
+                     : dof_row_sum(mv, s, I, t, l - s.c_tree_dofadr[t], s.efc_D, s.efc_jar, true);
       s.grad[l] = g;
       s.v2[l] = g * g;
     }
@@ -1720,6 +1795,14 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       T h = ti == tj ? s.M[mblk(m, i, j)] : T(0);
       const int li = i - s.c_tree_dofadr[ti], lj = j - s.c_tree_dofadr[tj];
       const int e1 = s.isl_roff[I + 1];
+      if (jt) {
+        const int n = s.isl_n[I], r0 = s.isl_roff[I];
+        const T* ja = s.jt + s.isl_joff[I] + a;
+        const T* jb = s.jt + s.isl_joff[I] + b;
+        const T* dr = s.rr_d + r0;
+#pragma unroll 4
+        for (int k = 0; k < e1 - r0; k++) h += ja[k * n] * dr[k] * jb[k * n];
+      } else
 #pragma unroll 2
       for (int rr = s.isl_roff[I]; rr < e1; rr++) {   // unconditional loads (see own_slot)
         const int r = s.isl_row[rr];
@@ -1824,9 +1907,15 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   }
   clk.sub_lap(SC_NS_W);
   // v = M^-1 J^T f over the dof's island rows
+  const bool jt = s.jt_ok;
+  if (jt) {
+    gather_rows(s, s.efc_force, s.rr_g);
+    wsync();
+  }
   if (l < m.nv) {
     const int t = s.c_dof_tree[l], I = s.tree_island[t];
-    const T g = dof_row_sum(T(0), s, I, t, l - s.c_tree_dofadr[t], s.efc_force, (const T*)nullptr, false);
+    const T g = jt ? jt_dof_sum(s, I, s.dof_ipos[l], T(0), s.rr_g)
+                   : dof_row_sum(T(0), s, I, t, l - s.c_tree_dofadr[t], s.efc_force, (const T*)nullptr, false);
     s.v2[l] = g;
   }
   // Pair lists: islands are independent under Gauss-Seidel (block-diagonal M, rows inside one
@@ -1970,10 +2059,16 @@ __device__ void st_finish_accel(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& 
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (s.nefc == 0) return;
+  const bool jt = s.jt_ok;
+  if (jt) {
+    gather_rows(s, s.efc_force, s.rr_g);
+    wsync();
+  }
   if (l < m.nv) {
     // J^T f over the dof's island rows (the other rows do not touch it)
     const int t = s.c_dof_tree[l], I = s.tree_island[t];
-    const T g = dof_row_sum(T(0), s, I, t, l - s.c_tree_dofadr[t], s.efc_force, (const T*)nullptr, false);
+    const T g = jt ? jt_dof_sum(s, I, s.dof_ipos[l], T(0), s.rr_g)
+                   : dof_row_sum(T(0), s, I, t, l - s.c_tree_dofadr[t], s.efc_force, (const T*)nullptr, false);
     s.v2[l] = s.qfrc_smooth[l] + g;
   }
   wsync();
