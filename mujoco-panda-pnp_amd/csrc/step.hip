@@ -99,6 +99,7 @@ struct Env {
           T H[PH_MAXV][PH_MAXV];
           T ntmp[PH_MAXEFC];
           T rr_f[PH_MAXEFC], rr_d[PH_MAXEFC];   // island row order: D jar, D (active rows; else 0)
+          T NL[7][9][9];       // island Hessian factors of the group-parallel path (GCH_*), kept while isl_hvalid
         };
         struct {               // no-slip: W = M^-1 J^T and the per-group pair lists
           T efc_Wv[PH_MAXJSLOT];
@@ -707,10 +708,75 @@ __device__ __forceinline__ void chol_solve_reg(const T* L, int n, T* x, const T*
     if (i < n) x[i] = y[i];
 }
 
+// ---- wave-parallel Cholesky of up to 7 blocks of n <= 9 at once.  Block g lives on the 9-lane
+// group 9g .. 9g+8 (lane 63 idle), lane row r = l - 9g holds row r of the block in registers;
+// rows >= n are identity padding.  Same operation order as chol_reg / chol_solve_reg (hence the
+// same factor and solution), but the 9 rows of a column step run on 9 lanes: a column step is
+// j ds_bpermute reads of the pivot row (independent), j multiply-adds and one pivot broadcast,
+// instead of one lane running the whole unrolled 9 x 9 factorisation (~1.5k instructions).
+#define GCH_N 9
+#define GCH_GROUPS 7
+__device__ __forceinline__ int gch_group(int l) { return l / GCH_N; }
+// in: Lrow = the lane's row of A (entries j <= r used); out: the lane's row of L (j <= r)
+template <typename T>
+__device__ __forceinline__ void gch_factor(T Lrow[GCH_N], int r, int base) {
+#pragma unroll
+  for (int j = 0; j < GCH_N; j++) {
+    T t = Lrow[j];
+#pragma unroll
+    for (int k = 0; k < j; k++) t -= Lrow[k] * __shfl(Lrow[k], base + j);
+    const T tj = __shfl(t, base + j);
+    const T d = PM<T>::sqrt_(tj > T(0) ? tj : T(1e-30));
+    const T inv = T(1) / d;
+    if (r == j) Lrow[j] = d;
+    else if (r > j) Lrow[j] = t * inv;
+  }
+}
+// x_r of (L L^T) x = b: Lrow = the lane's row of L, Lcol[k] = L[k][r] (k > r; zero for padding
+// rows), b = b_r (zero for padding rows); returns x_r
+template <typename T>
+__device__ __forceinline__ T gch_solve(const T Lrow[GCH_N], const T Lcol[GCH_N], int r, int base, T b) {
+  T y[GCH_N];
+#pragma unroll
+  for (int i = 0; i < GCH_N; i++) {
+    T v = b;
+#pragma unroll
+    for (int k = 0; k < i; k++) v -= Lrow[k] * y[k];
+    y[i] = __shfl(v / Lrow[i], base + i);
+  }
+  T x = 0;
+#pragma unroll
+  for (int i = GCH_N - 1; i >= 0; i--) {
+    T v = y[i];
+#pragma unroll
+    for (int k = i + 1; k < GCH_N; k++) v -= Lcol[k] * y[k];
+    const T xi = __shfl(v / Lrow[i], base + i);
+    y[i] = xi;
+    if (r == i) x = xi;
+  }
+  return x;
+}
+
 template <typename T>
 __device__ void st_factor_M(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
   const DevPhys<T>& m = phys<T>();
   const int t = lane_id();
+  if (m.ntree <= GCH_GROUPS && !__ballot(t < m.ntree && s.c_tree_dofnum[t] > GCH_N)) {
+    // every tree block on its own 9-lane group
+    const int g = gch_group(t), r = t - GCH_N * g;
+    const bool on = g < m.ntree;
+    const int n = on ? s.c_tree_dofnum[g] : 0, o = on ? s.c_tree_moff[g] : 0;
+    T Lrow[GCH_N];
+#pragma unroll
+    for (int j = 0; j < GCH_N; j++) Lrow[j] = r < n && j <= r ? s.M[o + r * n + j] : T(r == j);
+    gch_factor(Lrow, r, GCH_N * g);
+    if (r < n)
+#pragma unroll
+      for (int j = 0; j < GCH_N; j++)
+        if (j <= r) s.L[o + r * n + j] = Lrow[j];
+    wsync();
+    return;
+  }
   if (t < m.ntree) {
     const int n = s.c_tree_dofnum[t], o = s.c_tree_moff[t];
     if (n <= 9) {
@@ -1747,6 +1813,8 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   int it = 0;
   const int nent = s.isl_eoff[s.nisland];
   const bool jt = s.jt_ok;
+  // group-parallel island factorisation when every island fits a 9-lane group
+  const bool gch = s.nisland <= GCH_GROUPS && !__ballot(l < s.nisland && s.isl_n[l] > GCH_N);
   for (; it < m.iterations; it++) {
     clk.sub_start();
     // gradient g = M (x - x_smooth) + J^T (D jar) over the dof's island rows
@@ -1821,7 +1889,38 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     clk.lap(9);
     // Newton direction per island (lane per island); the register path leaves H intact, the
     // in-place LDS path (merged islands > 9 dofs) consumes it
-    if (!done) {
+    if (gch) {
+      // every island on its own 9-lane group; the Jacobi-scaled factor is kept in NL while the
+      // island's H block stays valid (isl_hvalid), so a refining step only solves
+      const int g = gch_group(l), r = l - GCH_N * g, base = GCH_N * g;
+      const bool on = g < s.nisland && !s.isl_flag[g];
+      const int n = on ? s.isl_n[g] : 0;
+      const int id = r < n ? s.isl_dof[g][r] : 0;
+      const T hd = s.H[id][id];
+      const T sc = r < n && hd > T(0) ? T(1) / PM<T>::sqrt_(hd) : T(1);
+      T Lrow[GCH_N], Lcol[GCH_N];
+      T* Ls = &s.NL[0][0][0];
+      const bool fac = on && !s.isl_hvalid[g];
+#pragma unroll
+      for (int j = 0; j < GCH_N; j++) {
+        const T scj = __shfl(sc, base + j);
+        const int idj = s.isl_dof[g][j < n ? j : 0];
+        Lrow[j] = fac && r < n && j <= r ? s.H[id][idj] * sc * scj : T(r == j);
+      }
+      if (__ballot(fac)) gch_factor(Lrow, r, base);
+      if (fac)
+#pragma unroll
+        for (int j = 0; j < GCH_N; j++) Ls[(base + r) * GCH_N + j] = Lrow[j];
+      wsync();
+#pragma unroll
+      for (int j = 0; j < GCH_N; j++) Lrow[j] = Ls[(base + r) * GCH_N + j];
+#pragma unroll
+      for (int k = 0; k < GCH_N; k++) Lcol[k] = k > r && k < n ? Ls[(base + k) * GCH_N + r] : T(0);
+      const T x = gch_solve(Lrow, Lcol, r, base, r < n ? s.grad[id] * sc : T(0));
+      if (on && r < n) s.p[id] = -x * sc;
+      wsync();
+      if (l < s.nisland && !done) s.isl_hvalid[l] = 1;
+    } else if (!done) {
       // one unrolled register variant (islands of <= 9 dofs padded with identity): lanes holding
       // 6- and 9-dof islands run the same code instead of two divergent copies
       const int n = s.isl_n[l];
@@ -2103,7 +2202,26 @@ __device__ void st_euler(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
   // qfrc = M qacc ; (M + h D) qacc_e = qfrc  (implicit joint damping)
   if (l < m.nv) s.v1[l] = mulM_row(m, s, l, s.qacc);
   wsync();
-  if (l < m.ntree) {
+  if (m.ntree <= GCH_GROUPS && !__ballot(l < m.ntree && s.c_tree_dofnum[l] > GCH_N)) {
+    // every tree's M + h D on its own 9-lane group (undamped trees: M + h 0 = M, the same factor
+    // st_factor_M made); rows through the dead solver scratch for the column reads
+    const int g = gch_group(l), r = l - GCH_N * g, base = GCH_N * g;
+    const bool on = g < m.ntree;
+    const int n = on ? s.c_tree_dofnum[g] : 0, o = on ? s.c_tree_moff[g] : 0, a = on ? s.c_tree_dofadr[g] : 0;
+    T Lrow[GCH_N], Lcol[GCH_N];
+#pragma unroll
+    for (int j = 0; j < GCH_N; j++)
+      Lrow[j] = r < n && j <= r ? s.M[o + r * n + j] + (j == r ? h * m.dof_damping[a + r] : T(0)) : T(r == j);
+    gch_factor(Lrow, r, base);
+    T* Ls = &s.NL[0][0][0];
+#pragma unroll
+    for (int j = 0; j < GCH_N; j++) Ls[(base + r) * GCH_N + j] = Lrow[j];
+    wsync();
+#pragma unroll
+    for (int k = 0; k < GCH_N; k++) Lcol[k] = k > r && k < n ? Ls[(base + k) * GCH_N + r] : T(0);
+    const T x = gch_solve(Lrow, Lcol, r, base, r < n ? s.v1[a + r] : T(0));
+    if (r < n) s.v2[a + r] = x;
+  } else if (l < m.ntree) {
     const int n = s.c_tree_dofnum[l], o = s.c_tree_moff[l], a = s.c_tree_dofadr[l];
     bool damped = false;
     for (int i = 0; i < n; i++) damped |= m.dof_damping[a + i] != T(0);
