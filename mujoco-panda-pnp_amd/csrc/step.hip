@@ -709,52 +709,35 @@ __device__ __forceinline__ void chol_solve_reg(const T* L, int n, T* x, const T*
 }
 
 // ---- wave-parallel Cholesky of up to 7 blocks of n <= 9 at once.  Block g lives on the 9-lane
-// group 9g .. 9g+8 (lane 63 idle), lane row r = l - 9g holds row r of the block in registers;
-// rows >= n are identity padding.  Same operation order as chol_reg / chol_solve_reg (hence the
-// same factor and solution), but the 9 rows of a column step run on 9 lanes: a column step is
-// j ds_bpermute reads of the pivot row (independent), j multiply-adds and one pivot broadcast,
-// instead of one lane running the whole unrolled 9 x 9 factorisation (~1.5k instructions).
+// group 9g .. 9g+8 (lane 63 idle); lane row r = l - 9g computes row r of the factor, and every
+// finished column is broadcast (ds_bpermute) so that each lane of the group ends up holding the
+// whole factor in registers (packed lower triangle P).  Column step j: every lane forms the pivot
+// L[j][j] itself from the broadcast row j (the pivot lane's own arithmetic, so the same bits),
+// its own L[r][j], then the column's broadcast, whose latency overlaps the next step's pivot row
+// terms.  Same operation order as chol_reg (hence the same factor); the solves then run
+// redundantly in every lane (chol_solve_reg on P) with no further cross-lane traffic.  Rows >= n
+// are identity padding.
 #define GCH_N 9
 #define GCH_GROUPS 7
 __device__ __forceinline__ int gch_group(int l) { return l / GCH_N; }
-// in: Lrow = the lane's row of A (entries j <= r used); out: the lane's row of L (j <= r)
+// in: Lrow = the lane's row of A (entries j <= r used), Ad[j] = A[j][j]; out: P (every lane)
 template <typename T>
-__device__ __forceinline__ void gch_factor(T Lrow[GCH_N], int r, int base) {
+__device__ __forceinline__ void gch_factor(T Lrow[GCH_N], const T Ad[GCH_N], int r, int base, T P[45]) {
 #pragma unroll
   for (int j = 0; j < GCH_N; j++) {
+    T td = Ad[j];
+#pragma unroll
+    for (int k = 0; k < j; k++) td -= P[j * (j + 1) / 2 + k] * P[j * (j + 1) / 2 + k];
+    const T d = PM<T>::sqrt_(td > T(0) ? td : T(1e-30));
+    const T inv = T(1) / d;
     T t = Lrow[j];
 #pragma unroll
-    for (int k = 0; k < j; k++) t -= Lrow[k] * __shfl(Lrow[k], base + j);
-    const T tj = __shfl(t, base + j);
-    const T d = PM<T>::sqrt_(tj > T(0) ? tj : T(1e-30));
-    const T inv = T(1) / d;
-    if (r == j) Lrow[j] = d;
-    else if (r > j) Lrow[j] = t * inv;
+    for (int k = 0; k < j; k++) t -= Lrow[k] * P[j * (j + 1) / 2 + k];
+    Lrow[j] = r == j ? d : (r > j ? t * inv : Lrow[j]);
+    P[j * (j + 1) / 2 + j] = d;
+#pragma unroll
+    for (int i = j + 1; i < GCH_N; i++) P[i * (i + 1) / 2 + j] = __shfl(Lrow[j], base + i);
   }
-}
-// x_r of (L L^T) x = b: Lrow = the lane's row of L, Lcol[k] = L[k][r] (k > r; zero for padding
-// rows), b = b_r (zero for padding rows); returns x_r
-template <typename T>
-__device__ __forceinline__ T gch_solve(const T Lrow[GCH_N], const T Lcol[GCH_N], int r, int base, T b) {
-  T y[GCH_N];
-#pragma unroll
-  for (int i = 0; i < GCH_N; i++) {
-    T v = b;
-#pragma unroll
-    for (int k = 0; k < i; k++) v -= Lrow[k] * y[k];
-    y[i] = __shfl(v / Lrow[i], base + i);
-  }
-  T x = 0;
-#pragma unroll
-  for (int i = GCH_N - 1; i >= 0; i--) {
-    T v = y[i];
-#pragma unroll
-    for (int k = i + 1; k < GCH_N; k++) v -= Lcol[k] * y[k];
-    const T xi = __shfl(v / Lrow[i], base + i);
-    y[i] = xi;
-    if (r == i) x = xi;
-  }
-  return x;
 }
 
 template <typename T>
@@ -766,10 +749,13 @@ __device__ void st_factor_M(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
     const int g = gch_group(t), r = t - GCH_N * g;
     const bool on = g < m.ntree;
     const int n = on ? s.c_tree_dofnum[g] : 0, o = on ? s.c_tree_moff[g] : 0;
-    T Lrow[GCH_N];
+    T Lrow[GCH_N], Ad[GCH_N], P[45];
 #pragma unroll
-    for (int j = 0; j < GCH_N; j++) Lrow[j] = r < n && j <= r ? s.M[o + r * n + j] : T(r == j);
-    gch_factor(Lrow, r, GCH_N * g);
+    for (int j = 0; j < GCH_N; j++) {
+      Lrow[j] = r < n && j <= r ? s.M[o + r * n + j] : T(r == j);
+      Ad[j] = j < n ? s.M[o + j * n + j] : T(1);
+    }
+    gch_factor(Lrow, Ad, r, GCH_N * g, P);
     if (r < n)
 #pragma unroll
       for (int j = 0; j < GCH_N; j++)
@@ -1898,25 +1884,34 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       const int id = r < n ? s.isl_dof[g][r] : 0;
       const T hd = s.H[id][id];
       const T sc = r < n && hd > T(0) ? T(1) / PM<T>::sqrt_(hd) : T(1);
-      T Lrow[GCH_N], Lcol[GCH_N];
+      T Lrow[GCH_N], Ad[GCH_N], scv[GCH_N], P[45], y[GCH_N];
+#pragma unroll
+      for (int i = 0; i < GCH_N; i++)
+#pragma unroll
+        for (int k = 0; k <= i; k++) P[i * (i + 1) / 2 + k] = T(i == k);
       T* Ls = &s.NL[0][0][0];
       const bool fac = on && !s.isl_hvalid[g];
 #pragma unroll
       for (int j = 0; j < GCH_N; j++) {
-        const T scj = __shfl(sc, base + j);
+        scv[j] = __shfl(sc, base + j);
         const int idj = s.isl_dof[g][j < n ? j : 0];
-        Lrow[j] = fac && r < n && j <= r ? s.H[id][idj] * sc * scj : T(r == j);
+        Lrow[j] = fac && r < n && j <= r ? s.H[id][idj] * sc * scv[j] : T(r == j);
+        Ad[j] = j < n ? s.H[idj][idj] * scv[j] * scv[j] : T(1);
+        y[j] = j < n ? s.grad[idj] * scv[j] : T(0);
       }
-      if (__ballot(fac)) gch_factor(Lrow, r, base);
+      if (__ballot(fac)) gch_factor(Lrow, Ad, r, base, P);
       if (fac)
 #pragma unroll
         for (int j = 0; j < GCH_N; j++) Ls[(base + r) * GCH_N + j] = Lrow[j];
-      wsync();
+      if (on && !fac)   // H block unchanged since its factorisation: the kept factor
 #pragma unroll
-      for (int j = 0; j < GCH_N; j++) Lrow[j] = Ls[(base + r) * GCH_N + j];
+        for (int i = 0; i < GCH_N; i++)
 #pragma unroll
-      for (int k = 0; k < GCH_N; k++) Lcol[k] = k > r && k < n ? Ls[(base + k) * GCH_N + r] : T(0);
-      const T x = gch_solve(Lrow, Lcol, r, base, r < n ? s.grad[id] * sc : T(0));
+          for (int k = 0; k <= i; k++) P[i * (i + 1) / 2 + k] = i < n ? Ls[(base + i) * GCH_N + k] : T(i == k);
+      chol_solve_reg<T, GCH_N>(P, GCH_N, y, y);
+      T x = 0;
+#pragma unroll
+      for (int i = 0; i < GCH_N; i++) x = r == i ? y[i] : x;
       if (on && r < n) s.p[id] = -x * sc;
       wsync();
       if (l < s.nisland && !done) s.isl_hvalid[l] = 1;
@@ -2208,18 +2203,18 @@ __device__ void st_euler(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
     const int g = gch_group(l), r = l - GCH_N * g, base = GCH_N * g;
     const bool on = g < m.ntree;
     const int n = on ? s.c_tree_dofnum[g] : 0, o = on ? s.c_tree_moff[g] : 0, a = on ? s.c_tree_dofadr[g] : 0;
-    T Lrow[GCH_N], Lcol[GCH_N];
+    T Lrow[GCH_N], Ad[GCH_N], P[45], y[GCH_N];
 #pragma unroll
-    for (int j = 0; j < GCH_N; j++)
+    for (int j = 0; j < GCH_N; j++) {
+      y[j] = T(0);
       Lrow[j] = r < n && j <= r ? s.M[o + r * n + j] + (j == r ? h * m.dof_damping[a + r] : T(0)) : T(r == j);
-    gch_factor(Lrow, r, base);
-    T* Ls = &s.NL[0][0][0];
+      Ad[j] = j < n ? s.M[o + j * n + j] + h * m.dof_damping[a + j] : T(1);
+    }
+    gch_factor(Lrow, Ad, r, base, P);
+    chol_solve_reg<T, GCH_N>(P, n, y, s.v1 + a);
+    T x = 0;
 #pragma unroll
-    for (int j = 0; j < GCH_N; j++) Ls[(base + r) * GCH_N + j] = Lrow[j];
-    wsync();
-#pragma unroll
-    for (int k = 0; k < GCH_N; k++) Lcol[k] = k > r && k < n ? Ls[(base + k) * GCH_N + r] : T(0);
-    const T x = gch_solve(Lrow, Lcol, r, base, r < n ? s.v1[a + r] : T(0));
+    for (int i = 0; i < GCH_N; i++) x = r == i ? y[i] : x;
     if (r < n) s.v2[a + r] = x;
   } else if (l < m.ntree) {
     const int n = s.c_tree_dofnum[l], o = s.c_tree_moff[l], a = s.c_tree_dofadr[l];
