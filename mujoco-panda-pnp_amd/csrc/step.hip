@@ -1349,26 +1349,35 @@ __device__ void st_actuation_smooth(const DevPhys<T>& /*image: phys<T>()*/, Env<
 // Island reductions.  The cost separates over islands (block-diagonal M, every row inside one
 // island), so the solver runs per island: a single global cost would hide the 1e-10
 // improvements of the 4 mg dummy island under the arm's cost in fp32, and a single global step
-// length would tie every island to the arm's line search.  Island I is reduced on DPP row
-// (I & 3): 16 lanes sum its dofs / rows, rowsum16 finishes; the four rows run concurrently.
+// length would tie every island to the arm's line search.  Island I is reduced on the 8-lane
+// group I (lanes 8I .. 8I+7; <= PH_MAXT = 8 islands, so every island in one pass): the group sums
+// its dofs / rows, rowsum8 (three DPP steps) finishes; the groups run concurrently.
+template <typename T>
+__device__ __forceinline__ T rowsum8(T v) {
+  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);   // row_half_mirror: the other quad of the 8
+  return v;
+}
 template <typename T>
 __device__ __forceinline__ T group_sum(const Env<T>& s, int I, const T* vd, const T* vr) {
-  const int q = lane_id() & 15;
+  const int q = lane_id() & 7;
   T acc = 0;
   const int n = s.isl_n[I];
   if (vd)
-    for (int c = q; c < n; c += 16) acc += vd[s.isl_dof[I][c]];
+    for (int c = q; c < n; c += 8) acc += vd[s.isl_dof[I][c]];
   if (vr)
-    for (int rr = s.isl_roff[I] + q; rr < s.isl_roff[I + 1]; rr += 16) acc += vr[s.isl_row[rr]];
-  return rowsum16(acc);
+    for (int rr = s.isl_roff[I] + q; rr < s.isl_roff[I + 1]; rr += 8) acc += vr[s.isl_row[rr]];
+  return rowsum8(acc);
 }
 // out[I] = group_sum for every island (vd / vr in LDS)
 template <typename T>
 __device__ __forceinline__ void island_sums(Env<T>& s, const T* vd, const T* vr, T* out) {
   const int l = lane_id();
-  for (int I = l >> 4; I < s.nisland; I += 4) {
+  const int I = l >> 3;
+  if (I < s.nisland) {
     const T c = group_sum(s, I, vd, vr);
-    if ((l & 15) == 0) out[I] = c;
+    if ((l & 7) == 0) out[I] = c;
   }
   wsync();
 }
@@ -1445,8 +1454,8 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
 // (three boolean squarings) gives the components; island ids follow the lowest tree of each
 // component, dofs keep increasing order inside an island (trees are contiguous dof ranges).
 // Then the rows of each island (CSR, wave ballots) and the island Hessian entry offsets.
-template <typename T>
-__device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+template <typename T, class CLK>
+__device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   uint64_t e = 0;
@@ -1458,21 +1467,22 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s)
     const int a = s.efc_t0[r], b = s.efc_t1[r];
     if (a >= 0 && b >= 0) e |= (1ull << (8 * a + b)) | (1ull << (8 * b + a));
   }
-  uint64_t R = ((uint64_t)wave_or((uint32_t)(e >> 32)) << 32) | wave_or((uint32_t)e);
-  R |= 0x8040201008040201ull;
+  const uint64_t E = ((uint64_t)wave_or((uint32_t)(e >> 32)) << 32) | wave_or((uint32_t)e);
+  // transitive closure (Warshall on bit rows): lane t < 8 holds row t; step k ORs row k into
+  // every row that reaches k.  The rows are then gathered back into the 8 x 8 matrix R.
+  uint32_t row = l < 8 ? (uint32_t)(E >> (8 * l)) & 0xFFu : 0u;
+  row |= l < 8 ? 1u << l : 0u;
 #pragma unroll
-  for (int k = 0; k < 3; k++) {
-    uint64_t R2 = 0;
+  for (int k = 0; k < 8; k++) {
+    const uint32_t rk = (uint32_t)__builtin_amdgcn_readlane((int)row, k);
+    row = (row >> k & 1u) ? row | rk : row;
+  }
+  uint64_t R = 0;
 #pragma unroll
-    for (int t = 0; t < 8; t++) {
-      const uint32_t row = (uint32_t)(R >> (8 * t)) & 0xFFu;
-      uint64_t acc = 0;
+  for (int b = 0; b < 8; b++) {
+    const uint64_t bits = __ballot(row >> b & 1u) & 0xFFull;   // bit t = row t has bit b
 #pragma unroll
-      for (int j = 0; j < 8; j++)
-        if (row >> j & 1u) acc |= (R >> (8 * j)) & 0xFFull;
-      R2 |= acc << (8 * t);
-    }
-    R = R2;
+    for (int t = 0; t < 8; t++) R |= ((bits >> t) & 1ull) << (8 * t + b);
   }
   const int nt = m.ntree;
   uint32_t roots = 0;
@@ -1540,6 +1550,7 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s)
     s.jt_ok = jo <= PH_JTCAP;
   }
   wsync();
+  clk.aux_lap(SC_AUX0 + 3);   // aux3: islands (closure, dof lists, row lists)
   // dense island Jacobian blocks: zero, then lane per row scatters its packed slots (tree t's
   // slots are contiguous columns from tree_ipos[t] in the island's dof order)
   if (s.jt_ok) {
@@ -1557,6 +1568,7 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s)
     }
     wsync();
   }
+  clk.aux_lap(SC_AUX0 + 4);   // aux4: dense island Jacobian blocks
 }
 
 // g + sum over island I's rows (island row order) of jt(row, a) * f[row] with the dense blocks:
@@ -1670,8 +1682,8 @@ __device__ void island_newton_dir_lds(Env<T>& s, int I, int n) {
 // (semi-smooth Newton on phi', bracketed), island I on DPP row (I & 3): its rows are summed by
 // the row's 16 lanes and its bracket iterates independently of the other islands.  Islands with
 // isl_flag set (done) keep a = 0.  Leaves the step lengths in s.isl_alpha.
-template <typename T>
-__device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+template <typename T, class CLK>
+__device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
@@ -1685,22 +1697,25 @@ __device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
     s.grad[l] = mp * s.v1[l];   // the gradient is no longer needed this iteration
   }
   wsync();
-  const int q = l & 15;
-  for (int I = l >> 4; I < s.nisland; I += 4) {
+  clk.aux_lap(SC_AUX0 + 5);   // aux5: line search J p, M p
+  const int q = l & 7;
+  {
+    const int I = l >> 3;
+    if (I >= s.nisland) goto ls_done;
     if (s.isl_flag[I]) {
       if (q == 0) s.isl_alpha[I] = 0;
-      continue;
+      goto ls_done;
     }
     const T A0 = group_sum(s, I, s.v2, (const T*)nullptr), B0 = group_sum(s, I, s.grad, (const T*)nullptr);
     const int r0 = s.isl_roff[I], r1 = s.isl_roff[I + 1];
-    // the lane's rows (rr = r0 + q + 16 k) are fixed over the iterations: islands of up to 64
+    // the lane's rows (rr = r0 + q + 8 k) are fixed over the iterations: islands of up to 32
     // rows keep (Jp, jar, D, equality) in registers, larger ones read LDS each iteration
     constexpr int RK = 4;
     T rjp[RK], rjar[RK], rD[RK];
     bool req[RK], rin[RK];
 #pragma unroll
     for (int k = 0; k < RK; k++) {
-      const int rr = r0 + q + 16 * k;
+      const int rr = r0 + q + 8 * k;
       rin[k] = rr < r1;
       const int r = s.isl_row[rin[k] ? rr : r0];
       rjp[k] = s.efc_Jp[r];
@@ -1708,7 +1723,7 @@ __device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
       rD[k] = s.efc_D[r];
       req[k] = r < s.ne;
     }
-    const bool small = r1 - r0 <= 16 * RK;
+    const bool small = r1 - r0 <= 8 * RK;
     T lo = 0, hi = T(-1), a = 1;
     for (int it = 0; it < 60; it++) {
       T d1 = 0, d2 = 0;
@@ -1721,14 +1736,14 @@ __device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
           d2 = on ? d2 + rD[k] * jp * jp : d2;
         }
       } else {
-        for (int rr = r0 + q; rr < r1; rr += 16) {
+        for (int rr = r0 + q; rr < r1; rr += 8) {
           const int r = s.isl_row[rr];
           const T jp = s.efc_Jp[r], v = s.efc_jar[r] + a * jp;
           if (r < s.ne || v < 0) { d1 += s.efc_D[r] * v * jp; d2 += s.efc_D[r] * jp * jp; }
         }
       }
-      d1 = rowsum16(d1) + A0 * a + B0;
-      d2 = rowsum16(d2) + A0;
+      d1 = rowsum8(d1) + A0 * a + B0;
+      d2 = rowsum8(d2) + A0;
       if (!(d2 > T(0))) { a = 0; break; }
       if (d1 == T(0)) break;
       if (d1 > 0) hi = a; else lo = a;
@@ -1740,7 +1755,9 @@ __device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
     }
     if (q == 0) s.isl_alpha[I] = a;
   }
+ls_done:
   wsync();
+  clk.aux_lap(SC_AUX0 + 6);   // aux6: line search bracketing per island
 }
 
 template <typename T, class CLK>
@@ -1753,7 +1770,8 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     wsync();
     return;
   }
-  build_islands(m, s);
+  clk.aux_start();
+  build_islands(m, s, clk);
   // warm start per island: the better of qacc_warmstart and qacc_smooth (MuJoCo chooses for the
   // whole problem; per island the minimiser is the same and the start is better).  One pass:
   // cost(qacc_smooth) has no dof term and its jar is efc_bb (= J qacc_smooth - aref, same
@@ -1925,7 +1943,8 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     }
     wsync();
     clk.lap(10);
-    line_search(m, s);
+    clk.aux_start();
+    line_search(m, s, clk);
     clk.lap(11);
     if (l < m.nv) s.x[l] += s.isl_alpha[s.tree_island[s.c_dof_tree[l]]] * s.p[l];
     // remember the active set the step was computed with
@@ -1934,16 +1953,15 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     eval_cost(m, s, s.x, true, s.isl_cost);
     // active-set change per island (rows of island I on DPP row I & 3)
     {
-      const int q = l & 15;
-      for (int I = l >> 4; I < s.nisland; I += 4) {
-        bool ch = false;
-        for (int rr = s.isl_roff[I] + q; rr < s.isl_roff[I + 1]; rr += 16) {
+      const int q = l & 7, I = l >> 3;
+      bool ch = false;
+      if (I < s.nisland)
+        for (int rr = s.isl_roff[I] + q; rr < s.isl_roff[I + 1]; rr += 8) {
           const int r = s.isl_row[rr];
           ch |= (T)s.efc_act[r] != s.efc_Jp[r];
         }
-        const bool any = ((__ballot(ch) >> (l & 48)) & 0xFFFFull) != 0;
-        if (q == 0) s.isl_val[I] = any ? T(1) : T(0);
-      }
+      const bool any = ((__ballot(ch) >> (l & 56)) & 0xFFull) != 0;
+      if (I < s.nisland && q == 0) s.isl_val[I] = any ? T(1) : T(0);
     }
     wsync();
     // island converged: two consecutive steps kept its active set (then its piecewise quadratic
