@@ -102,7 +102,7 @@ struct Env {
           T NL[7][9][9];       // island Hessian factors of the group-parallel path (GCH_*), kept while isl_hvalid
         };
         struct {               // no-slip: W = M^-1 J^T and the per-group pair lists
-          T efc_Wv[PH_MAXJSLOT];
+          T efc_Wv[PH_MAXJSLOT + 8];   // + 8: unmasked 8-slot reads past the last row (zeroed)
           short ns_list[4][PH_MAXEFC / 2];
           int ns_len[4];
           T rr_g[PH_MAXEFC];   // island row order: forces
@@ -120,7 +120,7 @@ struct Env {
   unsigned char efc_id[PH_MAXEFC], efc_act[PH_MAXEFC];
   int efc_off[PH_MAXEFC + 1];   // packed rows: slots [efc_off[r], efc_off[r+1])
   union {
-    T efc_Jv[PH_MAXJSLOT];
+    T efc_Jv[PH_MAXJSLOT + 8];   // + 8: room for unmasked 8-slot reads past the last row
     struct {                   // collision: single-pass contact staging (rows are rebuilt after it)
       T cst_val[NT][7];        // dist, pos[3], normal[3]
       unsigned short cst_key[NT];   // producing lane * 16 + its contact number
@@ -244,6 +244,11 @@ __device__ __forceinline__ double rdlane(double v, int l) {
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+// lane K of each row of 16 to the whole row (gfx90a+ DPP row_newbcast)
+template <int K>
+__device__ __forceinline__ float rowbcast(float v) { return dpp_f<0x150 + K>(v); }
+template <int K>
+__device__ __forceinline__ double rowbcast(double v) { return dpp_f<0x150 + K>(v); }
 // sum over each row of 16 lanes, result in every lane of the row
 template <typename T>
 __device__ __forceinline__ T rowsum16(T v) {
@@ -850,7 +855,6 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
     }
     bpm[w] = __ballot(alive);
   }
-  clk.aux_lap(SC_AUX0);   // aux0: broadphase body-pair pass
   int nlive = 0;
   for (int base = 0; base < m.npair; base += NT) {
     const int pi = base + l;
@@ -872,7 +876,6 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
     nlive += __popcll(bal);
   }
   wsync();
-  clk.aux_lap(SC_AUX0 + 1);   // aux1: broadphase geom-pair sphere pass
   // exact box tests over the sphere survivors, compacted in place (a chunk reads its entries into
   // registers before any lane writes, and writes land at or below the read positions)
   const int nsph = nlive;
@@ -895,7 +898,6 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
     nlive += __popcll(bal);
   }
   wsync();
-  clk.aux_lap(SC_AUX0 + 2);   // aux2: broadphase exact box tests
   clk.sub_lap(SC_BROAD);
   // narrowphase, one pass: every lane collides its pair once, its contacts go to a staging area
   // through an LDS slot counter, then each lands at (contacts so far) + (exclusive scan of the
@@ -1994,6 +1996,11 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   const int l = lane_id();
   if (m.noslip_iterations <= 0 || s.nefc == 0) return;
   clk.sub_start();
+  {   // zero the 8 slots past the last row: the tail of the force-space setup's unmasked reads
+    const int rl = s.nefc - 1;
+    const int end = s.efc_off[rl] + row_width(m, s.efc_t0[rl], s.efc_t1[rl]);
+    if (l < 8) s.efc_Wv[end + l] = T(0);
+  }
   // W_r = M^-1 J_r^T for contact rows (block-diagonal M: solve per tree of the row)
   for (int r = l; r < s.nefc; r += NT) {
     if (s.efc_type[r] != 6) continue;
@@ -2094,6 +2101,112 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   // the write back of v; the forces return to LDS once, after the last iteration.  Same
   // arithmetic in the same order as the streaming path below.
   constexpr int NSR = 8;
+  // Force space (the common case: every group's pairs act on the same trees, so their packed
+  // slots address the same dofs): lane q of a group owns pair-row q (pair q / 2, edge q & 1) of
+  // the group's list and keeps its residual r_q = J_q v + b_q and its row of the Delassus block
+  // A_qj = J_q W_j (j over the group's pair rows) in registers.  A pair update reads its two
+  // residuals and A entries by DPP row broadcasts, projects as below, and adds A(:, pair) df to
+  // every lane's residual -- r = J (v0 + W df) + b without the v round trip through LDS and
+  // the two row sums per update.  Same projection arithmetic; residuals differ from the
+  // v-space sweep by rounding only.
+  {
+    bool uni = true;
+    int jr = 0, off = 0, w = 0;
+    const bool mine = q < 2 * glen && q < 2 * NSR;
+    if (mine) {
+      jr = s.ns_list[grp][q >> 1] + (q & 1);
+      const int j0 = s.ns_list[grp][0];
+      uni = s.efc_t0[jr] == s.efc_t0[j0] && s.efc_t1[jr] == s.efc_t1[j0];
+      off = s.efc_off[jr];
+      w = row_width(m, s.efc_t0[jr], s.efc_t1[jr]);
+    }
+    if (maxlen <= NSR && !__ballot(!uni)) {
+      clk.aux_start();
+      T r = 0, A[2 * NSR];
+      if (!__ballot(mine && w > 8)) {
+        // rows of <= 8 slots (a free body against the world): fully unrolled, every load of a
+        // row issued back to back
+        const int t0 = s.efc_t0[jr], t1 = s.efc_t1[jr];
+        const int n0 = s.c_tree_dofnum[t0], d0 = s.c_tree_dofadr[t0];
+        const int d1 = t1 >= 0 ? s.c_tree_dofadr[t1] - n0 : 0;
+        // 8 slots read per row with no masking of the loads: Jq is zero past the row's width and
+        // the W slots past a contact row are the next contact row's or the zeroed tail
+        T Jq[8];
+        r = mine ? s.efc_bb[jr] : T(0);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const T jv = s.efc_Jv[off + k];
+          const T vd = s.v2[k < n0 ? d0 + k : (d1 + k < PH_MAXV ? d1 + k : 0)];
+          Jq[k] = mine && k < w ? jv : T(0);
+          r += Jq[k] * vd;
+        }
+#pragma unroll
+        for (int j = 0; j < 2 * NSR; j++) {
+          const int oj = s.efc_off[s.ns_list[grp][j < 2 * glen ? j >> 1 : 0] + (j & 1)];
+          const T* W = s.efc_Wv + oj;
+          T a = 0;
+#pragma unroll
+          for (int k = 0; k < 8; k++) a += Jq[k] * W[k];
+          A[j] = j < 2 * glen ? a : T(0);
+        }
+      } else {
+        if (mine) {
+          const int t0 = s.efc_t0[jr], t1 = s.efc_t1[jr];
+          r = s.efc_bb[jr];
+          for (int k = 0; k < w; k++) r += s.efc_Jv[off + k] * s.v2[slot_dof(m, t0, t1, k)];
+        }
+#pragma unroll
+        for (int j = 0; j < 2 * NSR; j++) {
+          T a = 0;
+          if (mine && j < 2 * glen) {
+            const int oj = s.efc_off[s.ns_list[grp][j >> 1] + (j & 1)];
+            for (int k = 0; k < w; k++) a += s.efc_Jv[off + k] * s.efc_Wv[oj + k];
+          }
+          A[j] = a;
+        }
+      }
+      T F0[NSR], F1[NSR], A00[NSR], A01[NSR], A10[NSR], A11[NSR];
+#pragma unroll
+      for (int k = 0; k < NSR; k++) {
+        const int jk = k < glen ? s.ns_list[grp][k] : 0;
+        F0[k] = s.efc_force[jk];
+        F1[k] = s.efc_force[jk + 1];
+      }
+#define NS_BC(K)                                                                          \
+      A00[K] = rowbcast<2 * K>(A[2 * K]); A01[K] = rowbcast<2 * K>(A[2 * K + 1]);         \
+      A10[K] = rowbcast<2 * K + 1>(A[2 * K]); A11[K] = rowbcast<2 * K + 1>(A[2 * K + 1]);
+      NS_BC(0) NS_BC(1) NS_BC(2) NS_BC(3) NS_BC(4) NS_BC(5) NS_BC(6) NS_BC(7)
+#undef NS_BC
+      clk.aux_lap(SC_AUX0);       // aux0: force-space no-slip setup (residuals, Delassus rows)
+      for (int iter = 0; iter < m.noslip_iterations; iter++) {
+#define NS_UPD(K)                                                                          \
+        if (K < maxlen) {                                                                 \
+          const T r0 = rowbcast<2 * K>(r), r1 = rowbcast<2 * K + 1>(r);                  \
+          const T f0 = F0[K], f1 = F1[K];                                                 \
+          const T a00 = A00[K], a01 = A01[K], a10 = A10[K], a11 = A11[K];                 \
+          const T bc0 = r0 - (a00 * f0 + a01 * f1), bc1 = r1 - (a10 * f0 + a11 * f1);     \
+          const T mid = T(0.5) * (f0 + f1);                                               \
+          const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;         \
+          T y = -K0 / K1;                                                                 \
+          y = y < -mid ? -mid : (y > mid ? mid : y);                                      \
+          const bool flat = K1 < T(1e-15);                                                \
+          const T n0 = flat ? mid : mid + y, n1 = flat ? mid : mid - y;                   \
+          const bool act = K < glen;                                                      \
+          const T d0 = act ? n0 - f0 : T(0), d1 = act ? n1 - f1 : T(0);                   \
+          r += A[2 * K] * d0 + A[2 * K + 1] * d1;                                         \
+          if (act) { F0[K] = n0; F1[K] = n1; }                                            \
+        }
+        NS_UPD(0) NS_UPD(1) NS_UPD(2) NS_UPD(3) NS_UPD(4) NS_UPD(5) NS_UPD(6) NS_UPD(7)
+#undef NS_UPD
+      }
+      clk.aux_lap(SC_AUX0 + 1);   // aux1: force-space no-slip sweeps
+#pragma unroll
+      for (int k = 0; k < NSR; k++)
+        if (k < glen && q == 0) { s.efc_force[s.ns_list[grp][k]] = F0[k]; s.efc_force[s.ns_list[grp][k] + 1] = F1[k]; }
+      wsync();
+      return;
+    }
+  }
   if (maxlen <= NSR) {
     NsPair P[NSR];
     T A00[NSR], A01[NSR], A10[NSR], A11[NSR], F0[NSR], F1[NSR];
