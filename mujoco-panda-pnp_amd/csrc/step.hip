@@ -1762,6 +1762,53 @@ ls_done:
   clk.aux_lap(SC_AUX0 + 6);   // aux6: line search bracketing per island
 }
 
+// Newton direction of every island on its own 9-lane group (see st_newton); out of line so that
+// its ~80 live factor / solve registers do not raise the register pressure of the whole solver
+// (callee-saved spills of every st_newton call)
+template <typename T>
+__device__ __attribute__((noinline)) void newton_dir_groups(Env<T>& s, bool done) {
+  const int l = lane_id();
+  // every island on its own 9-lane group; the Jacobi-scaled factor is kept in NL while the
+  // island's H block stays valid (isl_hvalid), so a refining step only solves
+  const int g = gch_group(l), r = l - GCH_N * g, base = GCH_N * g;
+  const bool on = g < s.nisland && !s.isl_flag[g];
+  const int n = on ? s.isl_n[g] : 0;
+  const int id = r < n ? s.isl_dof[g][r] : 0;
+  const T hd = s.H[id][id];
+  const T sc = r < n && hd > T(0) ? T(1) / PM<T>::sqrt_(hd) : T(1);
+  T Lrow[GCH_N], Ad[GCH_N], scv[GCH_N], P[45], y[GCH_N];
+#pragma unroll
+  for (int i = 0; i < GCH_N; i++)
+#pragma unroll
+    for (int k = 0; k <= i; k++) P[i * (i + 1) / 2 + k] = T(i == k);
+  T* Ls = &s.NL[0][0][0];
+  const bool fac = on && !s.isl_hvalid[g];
+#pragma unroll
+  for (int j = 0; j < GCH_N; j++) {
+    scv[j] = __shfl(sc, base + j);
+    const int idj = s.isl_dof[g][j < n ? j : 0];
+    Lrow[j] = fac && r < n && j <= r ? s.H[id][idj] * sc * scv[j] : T(r == j);
+    Ad[j] = j < n ? s.H[idj][idj] * scv[j] * scv[j] : T(1);
+    y[j] = j < n ? s.grad[idj] * scv[j] : T(0);
+  }
+  if (__ballot(fac)) gch_factor(Lrow, Ad, r, base, P);
+  if (fac)
+#pragma unroll
+    for (int j = 0; j < GCH_N; j++) Ls[(base + r) * GCH_N + j] = Lrow[j];
+  if (on && !fac)   // H block unchanged since its factorisation: the kept factor
+#pragma unroll
+    for (int i = 0; i < GCH_N; i++)
+#pragma unroll
+      for (int k = 0; k <= i; k++) P[i * (i + 1) / 2 + k] = i < n ? Ls[(base + i) * GCH_N + k] : T(i == k);
+  chol_solve_reg<T, GCH_N>(P, GCH_N, y, y);
+  T x = 0;
+#pragma unroll
+  for (int i = 0; i < GCH_N; i++) x = r == i ? y[i] : x;
+  if (on && r < n) s.p[id] = -x * sc;
+  wsync();
+  if (l < s.nisland && !done) s.isl_hvalid[l] = 1;
+}
+
 template <typename T, class CLK>
 __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
@@ -1896,45 +1943,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     // Newton direction per island (lane per island); the register path leaves H intact, the
     // in-place LDS path (merged islands > 9 dofs) consumes it
     if (gch) {
-      // every island on its own 9-lane group; the Jacobi-scaled factor is kept in NL while the
-      // island's H block stays valid (isl_hvalid), so a refining step only solves
-      const int g = gch_group(l), r = l - GCH_N * g, base = GCH_N * g;
-      const bool on = g < s.nisland && !s.isl_flag[g];
-      const int n = on ? s.isl_n[g] : 0;
-      const int id = r < n ? s.isl_dof[g][r] : 0;
-      const T hd = s.H[id][id];
-      const T sc = r < n && hd > T(0) ? T(1) / PM<T>::sqrt_(hd) : T(1);
-      T Lrow[GCH_N], Ad[GCH_N], scv[GCH_N], P[45], y[GCH_N];
-#pragma unroll
-      for (int i = 0; i < GCH_N; i++)
-#pragma unroll
-        for (int k = 0; k <= i; k++) P[i * (i + 1) / 2 + k] = T(i == k);
-      T* Ls = &s.NL[0][0][0];
-      const bool fac = on && !s.isl_hvalid[g];
-#pragma unroll
-      for (int j = 0; j < GCH_N; j++) {
-        scv[j] = __shfl(sc, base + j);
-        const int idj = s.isl_dof[g][j < n ? j : 0];
-        Lrow[j] = fac && r < n && j <= r ? s.H[id][idj] * sc * scv[j] : T(r == j);
-        Ad[j] = j < n ? s.H[idj][idj] * scv[j] * scv[j] : T(1);
-        y[j] = j < n ? s.grad[idj] * scv[j] : T(0);
-      }
-      if (__ballot(fac)) gch_factor(Lrow, Ad, r, base, P);
-      if (fac)
-#pragma unroll
-        for (int j = 0; j < GCH_N; j++) Ls[(base + r) * GCH_N + j] = Lrow[j];
-      if (on && !fac)   // H block unchanged since its factorisation: the kept factor
-#pragma unroll
-        for (int i = 0; i < GCH_N; i++)
-#pragma unroll
-          for (int k = 0; k <= i; k++) P[i * (i + 1) / 2 + k] = i < n ? Ls[(base + i) * GCH_N + k] : T(i == k);
-      chol_solve_reg<T, GCH_N>(P, GCH_N, y, y);
-      T x = 0;
-#pragma unroll
-      for (int i = 0; i < GCH_N; i++) x = r == i ? y[i] : x;
-      if (on && r < n) s.p[id] = -x * sc;
-      wsync();
-      if (l < s.nisland && !done) s.isl_hvalid[l] = 1;
+      newton_dir_groups(s, done);
     } else if (!done) {
       // one unrolled register variant (islands of <= 9 dofs padded with identity): lanes holding
       // 6- and 9-dof islands run the same code instead of two divergent copies
