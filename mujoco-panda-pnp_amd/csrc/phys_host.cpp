@@ -226,7 +226,9 @@ int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
       d->pair_reach[np] = (T)(ra > 0 && rb > 0 ? ra + rb + mg : -1.0);
       d->pair_margin[np] = (T)mg;
       const int ta = s->geom_type[a], tb = s->geom_type[b];
-      d->pair_kind[np] = tb == 7 && ta != 0 ? PH_PAIR_CONVEX : (ta == 0 && tb != 0 ? PH_PAIR_PLANE : PH_PAIR_PRIM);
+      d->pair_kind[np] = tb == 7 && ta != 0 ? PH_PAIR_CONVEX
+                         : ta == 0 && tb != 0 ? PH_PAIR_PLANE
+                         : ta == 6 && tb == 6 ? PH_PAIR_BOX : PH_PAIR_PRIM;
       np++;
     }
   }

@@ -29,6 +29,7 @@
 #define PH_PAIR_PRIM 0     // primitive collider, sphere test only
 #define PH_PAIR_CONVEX 1   // MPR pair: + oriented bounding boxes overlap
 #define PH_PAIR_PLANE 2    // plane vs geom: + the geom's box reaches the plane
+#define PH_PAIR_BOX 3      // box vs box: + the boxes (inflated by margin + 1 um) overlap
 #define PH_MAXBP 256        // body pairs with at least one candidate geom pair
 #define PH_MAXMESHV 1400
 #define PH_MAXMESH 16

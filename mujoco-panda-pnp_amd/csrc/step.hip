@@ -889,7 +889,11 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
       const uint32_t pk = m.pair_pack[pi];
       const int g1 = pk & 255, g2 = (pk >> 8) & 255, kind = (pk >> 16) & 255;
       keep = true;
-      if (kind == PH_PAIR_CONVEX) keep = !c_convex_obb_disjoint(m, s, g1, g2, m.pair_margin[pi]);
+      // convex and box-box pairs share one oriented-box separating-axis test (box-box: the
+      // boxes themselves, inflated by margin + 1 um, so that a pair the box-box collider's own
+      // SAT would keep is never culled)
+      if (kind == PH_PAIR_CONVEX || kind == PH_PAIR_BOX)
+        keep = !c_convex_obb_disjoint(m, s, g1, g2, m.pair_margin[pi] + (kind == PH_PAIR_BOX ? T(1e-6) : T(0)));
       else if (kind == PH_PAIR_PLANE) keep = !c_plane_obb_clear(m, s, g1, g2, m.pair_margin[pi]);
     }
     const uint64_t bal = __ballot(keep);
@@ -914,8 +918,10 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
     if (l == 0) s.cst_n = 0;
     wsync();
     StageSink<T> ss{&s.cst_n, s.cst_val, s.cst_key, l};
+    clk.aux_start();
     if (k < nlive && !cvx) collide_pair(m, s, pair, ss);
     wsync();
+    clk.aux_lap(SC_AUX0);   // aux0: narrowphase colliders
     const int staged = s.cst_n;
     int incl = ss.n;
     for (int o = 1; o < 64; o <<= 1) {
@@ -929,6 +935,7 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
       const int src = key >> 4;
       const int at = __shfl(off, src) + (key & 15);
       const int sp = __shfl(pair, src);
+      clk.aux_lap(SC_AUX0 + 1);   // aux1: narrowphase staging scan
       if (l < staged && at < PH_MAXCON) {
         Con<T>& c = s.con[at];
         c.dist = s.cst_val[l][0];
@@ -936,6 +943,7 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
         for (int t = 0; t < 9; t++) c.frame[t] = t < 3 ? s.cst_val[l][4 + t] : T(0);
         c_params(m, c, m.pair_g1[sp], m.pair_g2[sp]);
       }
+      clk.aux_lap(SC_AUX0 + 2);   // aux2: contact parameters
     } else if (ss.n) {
       LdsSink<T> ls{s.con + off, PH_MAXCON - off};
       if (ls.cap > 0) {
@@ -1701,6 +1709,7 @@ __device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, C
   wsync();
   clk.aux_lap(SC_AUX0 + 5);   // aux5: line search J p, M p
   const int q = l & 7;
+  int itc = 0;   // bracketing iterations of the lane's island (stage profile count)
   {
     const int I = l >> 3;
     if (I >= s.nisland) goto ls_done;
@@ -1728,6 +1737,7 @@ __device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, C
     const bool small = r1 - r0 <= 8 * RK;
     T lo = 0, hi = T(-1), a = 1;
     for (int it = 0; it < 60; it++) {
+      itc++;
       T d1 = 0, d2 = 0;
       if (small) {
 #pragma unroll
@@ -1760,6 +1770,12 @@ __device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, C
 ls_done:
   wsync();
   clk.aux_lap(SC_AUX0 + 6);   // aux6: line search bracketing per island
+  {
+    int mx = 0;
+#pragma unroll
+    for (int g = 0; g < 8; g++) mx = max(mx, __builtin_amdgcn_readlane(itc, 8 * g));
+    clk.count(SC_AUX0 + 7, mx);   // aux7: line-search bracketing iterations (max over islands)
+  }
 }
 
 // Newton direction of every island on its own 9-lane group (see st_newton); out of line so that
@@ -2130,7 +2146,6 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       w = row_width(m, s.efc_t0[jr], s.efc_t1[jr]);
     }
     if (maxlen <= NSR && !__ballot(!uni)) {
-      clk.aux_start();
       T r = 0, A[2 * NSR];
       if (!__ballot(mine && w > 8)) {
         // rows of <= 8 slots (a free body against the world): fully unrolled, every load of a
@@ -2186,7 +2201,6 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       A10[K] = rowbcast<2 * K + 1>(A[2 * K]); A11[K] = rowbcast<2 * K + 1>(A[2 * K + 1]);
       NS_BC(0) NS_BC(1) NS_BC(2) NS_BC(3) NS_BC(4) NS_BC(5) NS_BC(6) NS_BC(7)
 #undef NS_BC
-      clk.aux_lap(SC_AUX0);       // aux0: force-space no-slip setup (residuals, Delassus rows)
       for (int iter = 0; iter < m.noslip_iterations; iter++) {
 #define NS_UPD(K)                                                                          \
         if (K < maxlen) {                                                                 \
@@ -2208,7 +2222,6 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
         NS_UPD(0) NS_UPD(1) NS_UPD(2) NS_UPD(3) NS_UPD(4) NS_UPD(5) NS_UPD(6) NS_UPD(7)
 #undef NS_UPD
       }
-      clk.aux_lap(SC_AUX0 + 1);   // aux1: force-space no-slip sweeps
 #pragma unroll
       for (int k = 0; k < NSR; k++)
         if (k < glen && q == 0) { s.efc_force[s.ns_list[grp][k]] = F0[k]; s.efc_force[s.ns_list[grp][k] + 1] = F1[k]; }

@@ -10,7 +10,7 @@ TAG="${TAG:-quick}"
 TESTS="${TESTS:-tests}"
 timeout -k 10 600 python -u -m pytest $TESTS -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/${TAG}_pytest.log" 2>&1
 rc=$?; tail -3 "$OUT/${TAG}_pytest.log"; [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit $rc; }
-timeout -k 10 300 python -u tools/step_parity.py 4096 prof bench > "$OUT/${TAG}_stageprof.log" 2>&1
+timeout -k 10 300 python -u tools/step_parity.py 4096 prof > "$OUT/${TAG}_stageprof.log" 2>&1
 rc=$?; head -4 "$OUT/${TAG}_stageprof.log"; [ $rc -eq 0 ] || { echo "prof rc=$rc"; exit $rc; }
 timeout -k 10 300 python -u bench.py --no-cpu-baseline > "$OUT/${TAG}_bench.log" 2>&1
 rc=$?; tail -1 "$OUT/${TAG}_bench.log" | cut -c1-400; exit $rc
