@@ -187,7 +187,7 @@ __device__ void store_controls(const DevPhys<T>& /*image: phys<T>()*/, const Env
 
 // ---------------------------------------------------------------- init (_env_setup)
 template <typename T>
-__global__ void __launch_bounds__(NT) env_init_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
+__global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_init_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
                                                       pnp_env_params prm, EnvSoA<T> es, int B) {
   __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
   Env<T>& s = s_env;
@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(NT) env_init_kernel(const DevPhys<T>* __restri
 
 // ---------------------------------------------------------------- reset (_reset_sim + _get_obs)
 template <typename T>
-__global__ void __launch_bounds__(NT) env_reset_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
+__global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_reset_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
                                                        pnp_env_params prm, EnvSoA<T> es,
                                                        const uint8_t* __restrict__ mask, EnvOutT<T> out, int B) {
   __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
@@ -294,7 +294,7 @@ __global__ void __launch_bounds__(NT) env_reset_kernel(const DevPhys<T>* __restr
 
 // ---------------------------------------------------------------- step (FrankaEnv.step)
 template <typename T>
-__global__ void __launch_bounds__(NT) env_step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
+__global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
                                                       pnp_env_params prm, EnvSoA<T> es, const T* __restrict__ action,
                                                       EnvOutT<T> out, int B) {
   __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note

@@ -33,10 +33,18 @@
 #define PH_MAXBP 256        // body pairs with at least one candidate geom pair
 #define PH_MAXMESHV 1400
 #define PH_MAXMESH 16
+#ifndef PH_MAXCON
 #define PH_MAXCON 48      // contacts per env (lane per contact: <= 64)
+#endif
+#ifndef PH_MAXEFC
 #define PH_MAXEFC 208     // 6 weld + 9 limit + 4 x 48 contact rows
+#endif
+#ifndef PH_MAXJSLOT
 #define PH_MAXJSLOT 2048  // packed constraint-Jacobian slots (sum of row widths)
+#endif
+#ifndef PH_JTCAP
 #define PH_JTCAP 1536    // dense island Jacobian entries (sum over islands of rows x dofs; larger: slot path)
+#endif
 #define PH_ROWW 16        // sparse row width: dofs of <= 2 trees (arm 9 + cube 6)
 #define PH_MAXMENTRY 160  // (i, j in ancestors(i)) entries of M
 #define PH_MAXMBLK 256    // sum over trees of tree_dofnum^2

@@ -81,6 +81,11 @@ template <typename T> int build_phys(const pnp_model_desc* s, DevPhys<T>* d, cha
 // the constant segment when another model was resident); forget a destroyed model
 template <typename T> int32_t phys_resident(const pnp_model* model, void* stream);
 void phys_forget(const pnp_model* model);
+// step_compact.hip: the compact-capacity fp32 step kernel (see the top of step.hip)
+int32_t launch_step_compact(const pnp_model* model, const pnp_state_t<float>* st, int32_t B, int32_t nsub,
+                            void* stream, unsigned long long* prof);
+void phys_forget_compact(const pnp_model* model);
+int32_t step_compact_lds_bytes();
 
 // ---------------------------------------------------------------------------- error plumbing
 void pnp_set_error(const char* fmt, ...);

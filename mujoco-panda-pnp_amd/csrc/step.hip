@@ -23,6 +23,22 @@
 #include "phys_model.h"
 #include "pnp_internal.h"
 
+// Two builds of this file.  step.hip itself: the full-capacity kernels (namespace pnp_full) and
+// the C ABI.  step_compact.hip: the same device code with smaller contact / row / Jacobian
+// capacities (namespace pnp_compact, fp32 step kernel only), so that the per-env LDS working set
+// fits 6 envs per CU instead of 4.  A compact sub-step that would overflow a compact capacity is
+// abandoned before it changes the state and re-run from that sub-step by the full kernel (resume
+// protocol: PNP_RESUME_* below), so results are those of the full kernel, bit for bit.
+#ifndef PNP_COMPACT
+#define PNP_COMPACT 0
+#endif
+#if PNP_COMPACT
+#define PNP_NS pnp_compact
+#else
+#define PNP_NS pnp_full
+#endif
+namespace PNP_NS {
+
 // The physics image lives in the device's constant segment, one resident image per precision
 // and device (phys_resident below copies a model's image in, stream-ordered, when a launch uses
 // another model than the last one).  Every stage reads it through phys<T>(), a known global
@@ -85,7 +101,6 @@ struct Env {
       T cinert[PH_MAXB][10], crb[PH_MAXB][10], cdof[PH_MAXV][6], cvel[PH_MAXB][6], cdofdot[PH_MAXV][6];
       T scr6[PH_MAXB > PH_MAXV ? PH_MAXB : PH_MAXV][6];   // per-body / per-dof 6-vector scratch
       T scr6b[PH_MAXB][6];
-      short live[PH_MAXPAIR];   // broadphase survivors: every candidate pair fits
       Con<T> con[PH_MAXCON];
     };
     struct {
@@ -125,6 +140,7 @@ struct Env {
       T cst_val[NT][7];        // dist, pos[3], normal[3]
       unsigned short cst_key[NT];   // producing lane * 16 + its contact number
       int cst_n;
+      short live[PH_MAXPAIR];  // broadphase survivors: every candidate pair fits
     };
   };
   T efc_pos[PH_MAXEFC], efc_D[PH_MAXEFC], efc_aref[PH_MAXEFC], efc_bb[PH_MAXEFC];
@@ -144,7 +160,24 @@ struct Env {
   int isl_hvalid[PH_MAXT];     // per-island: H block is current for the island's active set
   T qpos_pre[PH_MAXQ];         // gym env: qpos of the last forward (pre-integration)
   T red[8];
+  int ovf;                     // compact build: a capacity overflowed in this sub-step
 };
+static_assert(sizeof(((Env<float>*)0)->efc_Jv) >= 7 * 4 * NT + 2 * NT + 4 + 2 * PH_MAXPAIR,
+              "collision staging + broadphase survivors must fit the efc_Jv union");
+
+// capacity overflow.  Full build: MuJoCo's behaviour (a warning bit, the list truncated).
+// Compact build: flag the env; the stages return at the next check and the kernel hands the
+// sub-step to the full kernel (mj_step_dev, step_kernel).
+#if PNP_COMPACT
+#define CAP_FULL(bit) (s.ovf = 1)
+#else
+#define CAP_FULL(bit) (s.warn |= (bit))
+#endif
+// resume protocol between the compact kernel and the full kernel's resume pass: the env's warn
+// word carries the flag and the sub-step to resume from (bits 16..30; the warning bits are 0..4)
+#define PNP_RESUME_FLAG 0x80000000u
+#define PNP_RESUME_SHIFT 16
+#define PNP_RESUME_MAXSUB 0x7FFF
 
 // stage timer (diagnostic instantiation only: TIMED = true); cycles accumulate in prof[stage]
 // Sub-stage timers (sub_start / sub_lap) run inside a parent stage without resetting its lap;
@@ -960,7 +993,7 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
     s.ncon_raw = ncon;
     s.nconvex = nconvex;
     s.ncon = min(ncon, PH_MAXCON);
-    if (ncon > PH_MAXCON) s.warn |= 8u;
+    if (ncon > PH_MAXCON) CAP_FULL(8u);
   }
   wsync();
   clk.sub_lap(SC_NARROW);
@@ -997,7 +1030,7 @@ __device__ __attribute__((noinline)) void st_collision_convex(const DevPhys<T>& 
     }
   }
   if (l == 0) {
-    if (ncon > PH_MAXCON) s.warn |= 8u;
+    if (ncon > PH_MAXCON) CAP_FULL(8u);
     s.ncon = min(ncon, PH_MAXCON);
   }
   wsync();
@@ -1099,7 +1132,7 @@ __device__ void st_constraints(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s
     int t0, t1;
     body_trees(m, id0, id1, t0, t1);
     const int w = row_width(m, t0, t1);
-    if (nrow + 6 > PH_MAXEFC || nslot + 6 * w > PH_MAXJSLOT) { if (l == 0) s.warn |= 16u; break; }
+    if (nrow + 6 > PH_MAXEFC || nslot + 6 * w > PH_MAXJSLOT) { if (l == 0) CAP_FULL(16u); break; }
     T pos0[3], pos1[3], q[4], q1[4], q2[4];
     d_mulmatvec3(pos0, s.xmat[id0], data + 3);
     d_mulmatvec3(pos1, s.xmat[id1], data);
@@ -1168,7 +1201,7 @@ __device__ void st_constraints(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s
     }
   }
   if (nrow + nlim > PH_MAXEFC || nslot + nlslot > PH_MAXJSLOT) {
-    if (l == 0) s.warn |= 16u;
+    if (l == 0) CAP_FULL(16u);
     nlim = 0;   // (rows past capacity were not written; drop the limits block entirely)
     nlslot = 0;
   }
@@ -1195,7 +1228,7 @@ __device__ void st_constraints(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s
     s.con_t[l][1] = t1c;
     s.con_dim[l] = (unsigned char)s.con[l].dim;
   }
-  if (__ballot(l < nc && !fits) && l == 0) s.warn |= 16u;
+  if (__ballot(l < nc && !fits) && l == 0) CAP_FULL(16u);
   wsync();
   int kept_rows = nrow;
   {
@@ -1558,6 +1591,7 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
     }
     s.isl_joff[nis] = jo;
     s.jt_ok = jo <= PH_JTCAP;
+    if (PNP_COMPACT && !s.jt_ok) s.ovf = 1;   // the full build's larger jt decides dense vs slot path
   }
   wsync();
   clk.aux_lap(SC_AUX0 + 3);   // aux3: islands (closure, dof lists, row lists)
@@ -1837,6 +1871,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   }
   clk.aux_start();
   build_islands(m, s, clk);
+  if (PNP_COMPACT && s.ovf) return;
   // warm start per island: the better of qacc_warmstart and qacc_smooth (MuJoCo chooses for the
   // whole problem; per island the minimiser is the same and the start is better).  One pass:
   // cost(qacc_smooth) has no dof term and its jar is efc_bb (= J qacc_smooth - aref, same
@@ -2449,11 +2484,14 @@ __device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& 
   clk.count(SN_CON, s.ncon);
   clk.count(SN_CONVEX, s.nconvex);
   clk.count(SN_LIVE, s.nlive);
+  if (PNP_COMPACT && s.ovf) return;
   if (dbg) dump_contacts(m, s, dbg);
   st_constraints(m, s);     clk.lap(5);
+  if (PNP_COMPACT && s.ovf) return;
   st_velocity(m, s);        clk.lap(6);
   st_actuation_smooth(m, s); clk.lap(7);
   st_newton(m, s, clk);     // laps 8..12 inside
+  if (PNP_COMPACT && s.ovf) return;
   clk.count(SN_EFC, s.nefc);
   clk.count(SN_ITER, s.solver_iter);
   clk.count(SN_ISLAND, s.nefc ? s.nisland : 0);
@@ -2491,6 +2529,7 @@ __device__ void mj_step_dev(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, C
   check_state(m, s);
   clk.lap(0);
   forward(m, s, clk);
+  if (PNP_COMPACT && s.ovf) return;   // state unchanged so far (check_state's reset is idempotent)
   const int l = lane_id();
   const uint64_t bad = __ballot(l < m.nv && is_bad(s.qacc[l]));
   if (bad) {
@@ -2498,6 +2537,7 @@ __device__ void mj_step_dev(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, C
     wsync();
     reset_state(m, s);
     forward(m, s, clk);
+    if (PNP_COMPACT && s.ovf) return;
   }
   if (save_qpos) {
     if (l < m.nq) save_qpos[l] = s.qpos[l];
@@ -2522,7 +2562,7 @@ __device__ void load_env(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, cons
   if (l < m.nu) s.ctrl[l] = st.ctrl[(size_t)b * m.nu + l];
   if (l < 3 * m.nmocap) s.mocap_pos[l] = st.mocap_pos[(size_t)b * 3 * m.nmocap + l];
   if (l < 4 * m.nmocap) s.mocap_quat[l] = st.mocap_quat[(size_t)b * 4 * m.nmocap + l];
-  if (l == 0) { s.time = st.time[b]; s.warn = st.warn[b]; }
+  if (l == 0) { s.time = st.time[b]; s.warn = st.warn[b] & ~(PNP_RESUME_FLAG | (PNP_RESUME_MAXSUB << PNP_RESUME_SHIFT)); s.ovf = 0; }
   wsync();
 }
 
@@ -2535,29 +2575,45 @@ __device__ void store_env(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& 
   if (l == 0) { st.time[b] = s.time; st.warn[b] = s.warn; }   // ctrl / mocap are inputs only
 }
 
+// PNP_STEP_WAVES: minimum waves per SIMD the step kernel's registers are budgeted for (2 caps a
+// wave at 256 VGPR+AGPR; only useful once the Env fits more than 4 envs per CU)
+#ifndef PNP_STEP_WAVES
+#define PNP_STEP_WAVES 1
+#endif
 template <typename T, bool TIMED>
-__global__ void __launch_bounds__(NT) step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st, int B, int nsub,
-                                                 unsigned long long* __restrict__ prof) {
+__global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st, int B, int nsub,
+                                                 unsigned long long* __restrict__ prof, int resume) {
   __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
   Env<T>& s = s_env;
   const DevPhys<T>& m = phys<T>();
   (void)mp;
   const int b = blockIdx.x;
   if (b >= B) return;
+  // full kernel, resume pass: only the envs the compact kernel handed over, from their sub-step
+  int k0 = 0;
+  if (!PNP_COMPACT && resume) {
+    const uint32_t w = st.warn[b];
+    if (!(w & PNP_RESUME_FLAG)) return;
+    k0 = (int)((w >> PNP_RESUME_SHIFT) & PNP_RESUME_MAXSUB);
+  }
   load_env(m, s, st, b);
+  int k = k0;
   if constexpr (TIMED) {
     StageClock clk{prof + (size_t)b * PNP_NSTAGE, 0, 0};
-    for (int k = 0; k < nsub; k++) mj_step_dev(m, s, clk);
+    for (; k < nsub && !s.ovf; k++) mj_step_dev(m, s, clk);
   } else {
     NoClock clk;
-    for (int k = 0; k < nsub; k++) mj_step_dev(m, s, clk);
+    for (; k < nsub && !s.ovf; k++) mj_step_dev(m, s, clk);
   }
+  // compact kernel: sub-step k - 1 overflowed a capacity before changing the state
+  if (PNP_COMPACT && s.ovf && lane_id() == 0) s.warn |= PNP_RESUME_FLAG | ((uint32_t)(k - 1) << PNP_RESUME_SHIFT);
+  wsync();
   store_env(m, s, st, b);
 }
 
 // debug: one forward, dump intermediates (layout PNP_DBG_* in include/pnp.h)
 template <typename T>
-__global__ void __launch_bounds__(NT) forward_debug_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st, int B,
+__global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) forward_debug_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st, int B,
                                                           double* __restrict__ dbg) {
   __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
   Env<T>& s = s_env;
@@ -2601,9 +2657,46 @@ __global__ void __launch_bounds__(NT) forward_debug_kernel(const DevPhys<T>* __r
   }
 }
 
+}  // namespace PNP_NS
+using namespace PNP_NS;
+
 // ============================================================================ host launchers
-// Resident-image bookkeeping: the model whose image each device's constant segment holds.
+// Resident-image bookkeeping: the model whose image each device's constant segment holds (per
+// build: the compact build has its own constant-segment images).
 static std::atomic<const pnp_model*> g_resident[2][64];
+
+#if PNP_COMPACT
+int32_t phys_resident_compact(const pnp_model* model, void* stream) {
+  const DevPhys<float>* src = phys_image<float>(model);
+  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { pnp_set_error("phys_resident: bad device"); return PNP_ERR_HIP; }
+  std::atomic<const pnp_model*>& slot = g_resident[0][dev];
+  if (slot.load() == model) return PNP_OK;
+  const hipError_t e = hipMemcpyToSymbolAsync(g_phys_f32, src, sizeof(DevPhys<float>), 0, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+  if (e != hipSuccess) { pnp_set_error("phys_resident: %s", hipGetErrorString(e)); return PNP_ERR_HIP; }
+  slot.store(model);
+  return PNP_OK;
+}
+
+void phys_forget_compact(const pnp_model* model) {
+  for (auto& row : g_resident)
+    for (auto& slot : row) {
+      const pnp_model* cur = model;
+      slot.compare_exchange_strong(cur, nullptr);
+    }
+}
+
+int32_t launch_step_compact(const pnp_model* model, const pnp_state_t<float>* st, int32_t B, int32_t nsub,
+                            void* stream, unsigned long long* prof) {
+  if (const int32_t rc = phys_resident_compact(model, stream)) return rc;
+  auto k = prof ? step_kernel<float, true> : step_kernel<float, false>;
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, phys_image<float>(model), *st, B, nsub, prof, 0);
+  return pnp_check_launch("step_kernel (compact)");
+}
+
+int32_t step_compact_lds_bytes() { return (int32_t)sizeof(Env<float>); }
+#else
 
 template <typename T>
 int32_t phys_resident(const pnp_model* model, void* stream) {
@@ -2629,6 +2722,13 @@ void phys_forget(const pnp_model* model) {
       const pnp_model* cur = model;
       slot.compare_exchange_strong(cur, nullptr);
     }
+  phys_forget_compact(model);
+}
+
+// the compact fp32 path is on unless PNP_STEP_COMPACT=0 (A/B runs and the equivalence tests)
+static bool compact_enabled() {
+  const char* e = getenv("PNP_STEP_COMPACT");
+  return !(e && e[0] == '0');
 }
 
 template <typename T>
@@ -2650,7 +2750,16 @@ static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B
     return pnp_check_launch("forward_debug_kernel");
   }
   auto k = prof ? step_kernel<T, true> : step_kernel<T, false>;
-  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, nsub, prof);
+  if (sizeof(T) == 4 && nsub <= PNP_RESUME_MAXSUB && compact_enabled()) {
+    // compact kernel over every env, then the full kernel resumes the envs it handed over (an
+    // env not handed over costs the resume pass one load of its warn word)
+    if (const int32_t rc = launch_step_compact(model, reinterpret_cast<const pnp_state_t<float>*>(st), B, nsub,
+                                               stream, prof))
+      return rc;
+    hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, nsub, prof, 1);
+    return pnp_check_launch("step_kernel (resume)");
+  }
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, nsub, prof, 0);
   return pnp_check_launch("step_kernel");
 }
 
@@ -2682,3 +2791,4 @@ extern "C" int32_t pnp_step_lds_bytes(int32_t fp64) {
 
 // ============================================================================ gym env (fused)
 #include "env_dev.h"
+#endif  // !PNP_COMPACT

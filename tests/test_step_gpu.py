@@ -287,6 +287,40 @@ def test_mesh_contacts_step_f64(engine, model, mesh_scene):
     assert np.array_equal(g["warn"], ref["warn"])
 
 
+def _step_f32(engine, st, nsub, compact):
+    import os
+    old = os.environ.get("PNP_STEP_COMPACT")
+    os.environ["PNP_STEP_COMPACT"] = "1" if compact else "0"
+    try:
+        g = engine.step(_dev(st, torch.float32), nsub)
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            del os.environ["PNP_STEP_COMPACT"]
+        else:
+            os.environ["PNP_STEP_COMPACT"] = old
+    return g
+
+
+def test_compact_kernel_hand_over_is_exact(engine, model, scene, mesh_scene):
+    """The fp32 step runs the compact-capacity kernel (20 contacts, 6 envs per CU) and hands any
+    env whose sub-step would overflow it to the full kernel from that sub-step (step.hip, resume
+    protocol).  Results must be the full kernel's, bit for bit — on envs that stay within the
+    compact capacities and on mesh-contact envs that exceed them (up to 40 contacts), with the
+    hand-over at the first or at a later sub-step — and the resume bits must not leak into warn."""
+    from pnp_amd import _lib
+    D = _lib.DBG
+    st = {k: np.concatenate([scene[k], mesh_scene[k]]) for k in scene}
+    ncon = engine.forward_debug(_dev(st, torch.float64)).cpu().numpy()[:, D["COUNTS"]]
+    assert (ncon > 20).any() and (ncon <= 20).any(), ncon
+    for nsub in (1, 7):
+        a = _step_f32(engine, st, nsub, compact=True)
+        b = _step_f32(engine, st, nsub, compact=False)
+        for k in a:
+            assert torch.equal(a[k], b[k]), (nsub, k)
+        assert int(a["warn"].max()) < (1 << 16)
+
+
 def test_mesh_contacts_f32(engine, model, mesh_scene):
     ref = PS.copy_state(mesh_scene)
     O.step(ref, nsub=1, nthreads=8, model=model)
