@@ -181,7 +181,8 @@ def run_step(args, engine, model, rank, world, dist):
         },
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": src,
-                     "kernel": "step_kernel<float, false>", "kernel_avg_ms": kern_ms,
+                     "kernel": "pnp_compact::step_kernel<float, false> + pnp_full::step_kernel resume pass (one pnp_step)",
+                     "kernel_avg_ms": kern_ms,
                      "algorithmic_bytes_per_launch": STEP_BYTES_PER_ENV * B},
         "state_ok": {"max_warn": warn, "finite": finite},
         "host_cores": len(os.sched_getaffinity(0)),
