@@ -218,10 +218,17 @@ typedef struct pnp_state_f64 {
 #define PNP_WARN_BADQACC 4u
 #define PNP_WARN_CONTACTFULL 8u
 #define PNP_WARN_CNSTRFULL 16u
+/* bits 16..31 are reserved: inside one pnp_step / pnp_env_step call they carry the compact
+ * kernel's hand-over to the full kernel (flag + sub-step); they are clear when a call returns
+ * and are ignored on input */
 
 /* nsub x mj_step on every env, in place (reference envs/panda_env.py:355-358 calls this with
  * nsub = 25, ten times; skills/base.py:43 and scripts/execute_pnp.py:103 with nsub = 1).
- * ctrl and mocap are held constant over the nsub sub-steps, as in the reference. */
+ * ctrl and mocap are held constant over the nsub sub-steps, as in the reference.
+ * fp32: a compact-capacity kernel (6 envs per CU) runs first and hands any env whose sub-step
+ * would overflow its capacities to the full-capacity kernel from that sub-step; results equal
+ * the full kernel's bit for bit.  Environment variable PNP_STEP_COMPACT=0 runs the full kernel
+ * alone (2: the compact kernel alone, a test diagnostic that leaves handed-over envs mid-call). */
 int32_t pnp_step(pnp_model* model, const pnp_state* state, int32_t B, int32_t nsub, void* stream);
 int32_t pnp_step_f64(pnp_model* model, const pnp_state_f64* state, int32_t B, int32_t nsub, void* stream);
 

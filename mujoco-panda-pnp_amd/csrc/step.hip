@@ -169,15 +169,20 @@ static_assert(sizeof(((Env<float>*)0)->efc_Jv) >= 7 * 4 * NT + 2 * NT + 4 + 2 * 
 // Compact build: flag the env; the stages return at the next check and the kernel hands the
 // sub-step to the full kernel (mj_step_dev, step_kernel).
 #if PNP_COMPACT
-#define CAP_FULL(bit) (s.ovf = 1)
+#define CAP_FULL(bit) (s.ovf |= (bit) == 8u ? PNP_OVF_CONTACTS : PNP_OVF_ROWS)
 #else
 #define CAP_FULL(bit) (s.warn |= (bit))
 #endif
 // resume protocol between the compact kernel and the full kernel's resume pass: the env's warn
-// word carries the flag and the sub-step to resume from (bits 16..30; the warning bits are 0..4)
+// word carries the flag (bit 31), the capacity that overflowed (bits 28..30, diagnostic) and the
+// sub-step to resume from (bits 16..27); the warning bits are 0..4
 #define PNP_RESUME_FLAG 0x80000000u
 #define PNP_RESUME_SHIFT 16
-#define PNP_RESUME_MAXSUB 0x7FFF
+#define PNP_RESUME_MAXSUB 0xFFF
+#define PNP_RESUME_WHY_SHIFT 28
+#define PNP_OVF_CONTACTS 1   // > PH_MAXCON contacts
+#define PNP_OVF_ROWS 2       // > PH_MAXEFC rows or > PH_MAXJSLOT Jacobian slots
+#define PNP_OVF_JT 4         // dense island Jacobian blocks > PH_JTCAP
 
 // stage timer (diagnostic instantiation only: TIMED = true); cycles accumulate in prof[stage]
 // Sub-stage timers (sub_start / sub_lap) run inside a parent stage without resetting its lap;
@@ -1591,7 +1596,7 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
     }
     s.isl_joff[nis] = jo;
     s.jt_ok = jo <= PH_JTCAP;
-    if (PNP_COMPACT && !s.jt_ok) s.ovf = 1;   // the full build's larger jt decides dense vs slot path
+    if (PNP_COMPACT && !s.jt_ok) s.ovf |= PNP_OVF_JT;   // the full build's larger jt decides dense vs slot path
   }
   wsync();
   clk.aux_lap(SC_AUX0 + 3);   // aux3: islands (closure, dof lists, row lists)
@@ -2562,7 +2567,7 @@ __device__ void load_env(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, cons
   if (l < m.nu) s.ctrl[l] = st.ctrl[(size_t)b * m.nu + l];
   if (l < 3 * m.nmocap) s.mocap_pos[l] = st.mocap_pos[(size_t)b * 3 * m.nmocap + l];
   if (l < 4 * m.nmocap) s.mocap_quat[l] = st.mocap_quat[(size_t)b * 4 * m.nmocap + l];
-  if (l == 0) { s.time = st.time[b]; s.warn = st.warn[b] & ~(PNP_RESUME_FLAG | (PNP_RESUME_MAXSUB << PNP_RESUME_SHIFT)); s.ovf = 0; }
+  if (l == 0) { s.time = st.time[b]; s.warn = st.warn[b] & 0xFFFFu; s.ovf = 0; }
   wsync();
 }
 
@@ -2606,7 +2611,8 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) step_
     for (; k < nsub && !s.ovf; k++) mj_step_dev(m, s, clk);
   }
   // compact kernel: sub-step k - 1 overflowed a capacity before changing the state
-  if (PNP_COMPACT && s.ovf && lane_id() == 0) s.warn |= PNP_RESUME_FLAG | ((uint32_t)(k - 1) << PNP_RESUME_SHIFT);
+  if (PNP_COMPACT && s.ovf && lane_id() == 0)
+    s.warn |= PNP_RESUME_FLAG | ((uint32_t)s.ovf << PNP_RESUME_WHY_SHIFT) | ((uint32_t)(k - 1) << PNP_RESUME_SHIFT);
   wsync();
   store_env(m, s, st, b);
 }
@@ -2657,6 +2663,8 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) forwa
   }
 }
 
+// ============================================================================ gym env (fused)
+#include "env_dev.h"
 }  // namespace PNP_NS
 using namespace PNP_NS;
 
@@ -2696,6 +2704,16 @@ int32_t launch_step_compact(const pnp_model* model, const pnp_state_t<float>* st
 }
 
 int32_t step_compact_lds_bytes() { return (int32_t)sizeof(Env<float>); }
+
+int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
+                                const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
+                                void* stream, int phase, int k_begin, int k_end) {
+  if (const int32_t rc = phys_resident_compact(model, stream)) return rc;
+  auto k = env_step_kernel<float>;
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, phys_image<float>(model), *st, *p,
+                     env_view<float>(e), action, out_view<float>(o), B, 0, phase, k_begin, k_end);
+  return pnp_check_launch("env_step_kernel (compact)");
+}
 #else
 
 template <typename T>
@@ -2725,11 +2743,15 @@ void phys_forget(const pnp_model* model) {
   phys_forget_compact(model);
 }
 
-// the compact fp32 path is on unless PNP_STEP_COMPACT=0 (A/B runs and the equivalence tests)
-static bool compact_enabled() {
+// PNP_STEP_COMPACT: unset / 1 = compact kernel + resume pass (default), 0 = the full kernel alone
+// (A/B runs, equivalence tests), 2 = the compact kernel alone — diagnostic only: handed-over envs
+// are left at their hand-over sub-step with the resume bits set in warn, so that tests can see
+// where hand-overs happen
+static int compact_mode() {
   const char* e = getenv("PNP_STEP_COMPACT");
-  return !(e && e[0] == '0');
+  return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
 }
+static bool compact_enabled() { return compact_mode() != 0; }
 
 template <typename T>
 static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B, int32_t nsub, void* stream,
@@ -2756,6 +2778,7 @@ static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B
     if (const int32_t rc = launch_step_compact(model, reinterpret_cast<const pnp_state_t<float>*>(st), B, nsub,
                                                stream, prof))
       return rc;
+    if (compact_mode() == 2) return PNP_OK;
     hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, nsub, prof, 1);
     return pnp_check_launch("step_kernel (resume)");
   }
@@ -2790,5 +2813,5 @@ extern "C" int32_t pnp_step_lds_bytes(int32_t fp64) {
 }
 
 // ============================================================================ gym env (fused)
-#include "env_dev.h"
+#include "env_host.h"
 #endif  // !PNP_COMPACT

@@ -321,6 +321,56 @@ def test_compact_kernel_hand_over_is_exact(engine, model, scene, mesh_scene):
         assert int(a["warn"].max()) < (1 << 16)
 
 
+def _reset_workload(engine, model, B):
+    """The bench's C3 envs straight after reset (before its settle phase): cubes landing on their
+    boards, i.e. contact / row counts that rise during a launch."""
+    from pnp_amd import workloads
+    q = torch.as_tensor(np.tile(model.qpos0, (1, 1)), dtype=torch.float64, device=engine.device)
+    q[:, :9] = torch.as_tensor(workloads.NEUTRAL, dtype=torch.float64)
+    sx, sm = engine.site_kinematics(q.contiguous())
+    host = workloads.c3_reset(model, np.arange(B), sx[0].cpu().numpy(), sm[0].cpu().numpy())
+    return {k: (v.astype(np.int32) if k == "warn" else v) for k, v in host.items()}
+
+
+def test_compact_hand_over_mid_launch(engine, model):
+    """Envs handed over at a later sub-step of a launch (the compact kernel alone, mode 2, leaves
+    the resume bits in warn: flag + sub-step) and the whole settle phase stepped both ways,
+    bit for bit."""
+    st = _reset_workload(engine, model, 1024)
+    probe = _step_f32_mode(engine, st, 25, "2")
+    w = probe["warn"].cpu().numpy().astype(np.uint32)
+    flag = (w >> 31) & 1 == 1
+    sub = (w >> 16) & 0xFFF
+    assert flag.any() and (sub[flag] > 0).any(), (flag.sum(), np.unique(sub[flag]))
+    a = _dev(st, torch.float32)
+    b = _dev(st, torch.float32)
+    for _ in range(4):
+        _run_mode(engine, a, 25, "1")
+        _run_mode(engine, b, 25, "0")
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
+    assert int(a["warn"].max()) < (1 << 16)
+
+
+def _run_mode(engine, g, nsub, mode):
+    import os
+    old = os.environ.get("PNP_STEP_COMPACT")
+    os.environ["PNP_STEP_COMPACT"] = mode
+    try:
+        engine.step(g, nsub)
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            del os.environ["PNP_STEP_COMPACT"]
+        else:
+            os.environ["PNP_STEP_COMPACT"] = old
+    return g
+
+
+def _step_f32_mode(engine, st, nsub, mode):
+    return _run_mode(engine, _dev(st, torch.float32), nsub, mode)
+
+
 def test_mesh_contacts_f32(engine, model, mesh_scene):
     ref = PS.copy_state(mesh_scene)
     O.step(ref, nsub=1, nthreads=8, model=model)
