@@ -1542,60 +1542,97 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
     const int low = __builtin_ctz((uint32_t)(R >> (8 * t)) & 0xFFu);
     return __builtin_popcount(roots & ((1u << low) - 1u));
   };
+  // Island bookkeeping in registers: the tree sizes are read once, island sizes and every
+  // per-island offset (Hessian / row / dense-block) are prefix sums over <= 8 islands that each
+  // lane forms from readlane broadcasts, and the island row order comes from per-island ballots
+  // (a counting sort) instead of one LDS pass over the rows per island.
+  int tdn[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) tdn[u] = u < nt ? s.c_tree_dofnum[u] : 0;
   if (l < nt) s.tree_island[l] = island_of(l);
   if (l < m.nv) {
     const int t = s.c_dof_tree[l];
     const uint32_t comp = (uint32_t)(R >> (8 * t)) & 0xFFu;
     int pos = l - s.c_tree_dofadr[t];
-    for (int u = 0; u < t; u++)
-      if (comp >> u & 1u) pos += s.c_tree_dofnum[u];
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (u < t && (comp >> u & 1u)) pos += tdn[u];
     s.isl_dof[island_of(t)][pos] = (unsigned char)l;
     s.dof_ipos[l] = (unsigned char)pos;
   }
   if (l < nt) {
     const uint32_t comp = (uint32_t)(R >> (8 * l)) & 0xFFu;
     int pos = 0;
-    for (int u = 0; u < l; u++)
-      if (comp >> u & 1u) pos += s.c_tree_dofnum[u];
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (u < l && (comp >> u & 1u)) pos += tdn[u];
     s.tree_ipos[l] = pos;
   }
+  // island sizes: lane I sums its trees; isz[J] = readlane broadcast (uniform)
+  int nI = 0;
+#pragma unroll
+  for (int t = 0; t < 8; t++)
+    if (t < nt && island_of(t) == l) nI += tdn[t];
+  int isz[8];
+#pragma unroll
+  for (int J = 0; J < 8; J++) isz[J] = __builtin_amdgcn_readlane(nI, J);
+  // rows by island: per-island counts over the row chunks, then positions
+  int rcnt[8];
+#pragma unroll
+  for (int J = 0; J < 8; J++) rcnt[J] = 0;
+  const int nefc = s.nefc;
+  for (int base = 0; base < nefc; base += NT) {
+    const int r = base + l;
+    const int I = r < nefc ? island_of(s.efc_t0[r]) : -1;
+#pragma unroll
+    for (int J = 0; J < 8; J++) rcnt[J] += J < nis ? __popcll(__ballot(I == J)) : 0;
+  }
+  int roff[9], eoff[9], joff[9];
+  roff[0] = eoff[0] = joff[0] = 0;
+#pragma unroll
+  for (int J = 0; J < 8; J++) {
+    const bool in = J < nis;
+    roff[J + 1] = roff[J] + (in ? rcnt[J] : 0);
+    eoff[J + 1] = eoff[J] + (in ? isz[J] * (isz[J] + 1) / 2 : 0);
+    joff[J + 1] = joff[J] + (in ? rcnt[J] * isz[J] : 0);
+  }
+  int run[8];
+#pragma unroll
+  for (int J = 0; J < 8; J++) run[J] = roff[J];
+  for (int base = 0; base < nefc; base += NT) {
+    const int r = base + l;
+    const int I = r < nefc ? island_of(s.efc_t0[r]) : -1;
+    const uint64_t below = (1ull << l) - 1;
+#pragma unroll
+    for (int J = 0; J < 8; J++) {
+      if (J >= nis) break;
+      const uint64_t bal = __ballot(I == J);
+      if (I == J) s.isl_row[run[J] + __popcll(bal & below)] = (short)r;
+      run[J] += __popcll(bal);
+    }
+  }
+  // per-island tables: lane I writes its entries (and lane 0 the end markers)
   if (l < nis) {
-    int n = 0;
-    for (int t = 0; t < nt; t++)
-      if (island_of(t) == l) n += s.c_tree_dofnum[t];
-    s.isl_n[l] = n;
+    int ro = 0, eo = 0, jo = 0;
+#pragma unroll
+    for (int J = 0; J < 8; J++)
+      if (J == l) { ro = roff[J]; eo = eoff[J]; jo = joff[J]; }
+    s.isl_n[l] = nI;
+    s.isl_roff[l] = ro;
+    s.isl_eoff[l] = eo;
+    s.isl_joff[l] = jo;
   }
-  if (l == 0) s.nisland = nis;
-  wsync();
+  int rtot = 0, etot = 0, jtot = 0;
+#pragma unroll
+  for (int J = 0; J < 8; J++)
+    if (J == nis) { rtot = roff[J]; etot = eoff[J]; jtot = joff[J]; }
+  if (nis == 8) { rtot = roff[8]; etot = eoff[8]; jtot = joff[8]; }
   if (l == 0) {
-    int eo = 0;
-    for (int I = 0; I < nis; I++) {
-      s.isl_eoff[I] = eo;
-      eo += s.isl_n[I] * (s.isl_n[I] + 1) / 2;
-    }
-    s.isl_eoff[nis] = eo;
-  }
-  // rows grouped by island (stable, row order kept inside an island)
-  int off = 0;
-  for (int I = 0; I < nis; I++) {
-    if (l == 0) s.isl_roff[I] = off;
-    for (int base = 0; base < s.nefc; base += NT) {
-      const int r = base + l;
-      const bool in = r < s.nefc && s.tree_island[s.efc_t0[r]] == I;
-      const uint64_t bal = __ballot(in);
-      if (in) s.isl_row[off + __popcll(bal & ((1ull << l) - 1))] = (short)r;
-      off += __popcll(bal);
-    }
-  }
-  if (l == 0) {
-    s.isl_roff[nis] = off;
-    int jo = 0;
-    for (int I = 0; I < nis; I++) {
-      s.isl_joff[I] = jo;
-      jo += (s.isl_roff[I + 1] - s.isl_roff[I]) * s.isl_n[I];
-    }
-    s.isl_joff[nis] = jo;
-    s.jt_ok = jo <= PH_JTCAP;
+    s.nisland = nis;
+    s.isl_roff[nis] = rtot;
+    s.isl_eoff[nis] = etot;
+    s.isl_joff[nis] = jtot;
+    s.jt_ok = jtot <= PH_JTCAP;
     if (PNP_COMPACT && !s.jt_ok) s.ovf |= PNP_OVF_JT;   // the full build's larger jt decides dense vs slot path
   }
   wsync();
