@@ -673,6 +673,27 @@ __device__ __forceinline__ bool c_convex_obb_disjoint(const DevPhys<T>& /*image:
   return c_obb_disjoint(bp[0], s.gmat[g1], m.geom_aabb[g1] + 3, bp[1], s.gmat[g2], m.geom_aabb[g2] + 3, margin);
 }
 
+// broadphase pre-test: geom gs's bounding sphere (centre gpos, radius rbound -- MuJoCo's) does not
+// reach geom gb's bounding box (geom_aabb in gb's frame) inflated by the margin.  Exact cull:
+// every point of gs lies in its sphere and every point of gb in its box, so a pair culled here
+// has no two points within the margin.
+template <typename T>
+__device__ __forceinline__ bool c_sphere_obb_disjoint(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int gs, int gb, T margin) {
+  const DevPhys<T>& m = phys<T>();
+  const T* R = s.gmat[gb];
+  const T* c = m.geom_aabb[gb];
+  const T d[3] = {s.gpos[gs][0] - s.gpos[gb][0], s.gpos[gs][1] - s.gpos[gb][1], s.gpos[gs][2] - s.gpos[gb][2]};
+  T q = 0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const T loc = R[k] * d[0] + R[3 + k] * d[1] + R[6 + k] * d[2] - c[k];   // (R^T d)_k - centre_k
+    const T out = fmax(fabs(loc) - c[3 + k], T(0));
+    q += out * out;
+  }
+  const T r = m.geom_rbound[gs] + margin;
+  return q > r * r;
+}
+
 // plane pairs: the other geom's oriented bounding box lies entirely beyond the plane (by more
 // than the margin, plus 1 um of slack) -- no vertex / corner / surface point can reach it, so the
 // pair cannot produce a contact.  Exact cull: the contact set is unchanged.

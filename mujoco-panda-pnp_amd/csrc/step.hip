@@ -893,6 +893,7 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
     }
     bpm[w] = __ballot(alive);
   }
+  clk.aux_lap(SC_AUX0);       // aux0: broadphase pass 1 (body pairs)
   int nlive = 0;
   for (int base = 0; base < m.npair; base += NT) {
     const int pi = base + l;
@@ -914,9 +915,39 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
     nlive += __popcll(bal);
   }
   wsync();
-  // exact box tests over the sphere survivors, compacted in place (a chunk reads its entries into
-  // registers before any lane writes, and writes land at or below the read positions)
-  const int nsph = nlive;
+  clk.aux_lap(SC_AUX0 + 1);   // aux1: broadphase pass 2 (geom-pair spheres)
+  clk.count(SC_AUX0 + 2, nlive);   // aux2: sphere survivors (count)
+  // cheap exact pre-test over the sphere survivors (~180 per sub-step here: the shelf boards'
+  // bounding spheres are large): each geom's bounding sphere against the other's bounding box,
+  // both ways, and the plane test; compacted in place (a chunk reads its entries into registers
+  // before any lane writes, and writes land at or below the read positions), so that the
+  // separating-axis tests below run over one chunk of survivors instead of every chunk
+  int nsph = nlive;
+  nlive = 0;
+  for (int base = 0; base < nsph; base += NT) {
+    const int k = base + l;
+    bool keep = false;
+    int pi = 0;
+    if (k < nsph) {
+      pi = s.live[k];
+      const uint32_t pk = m.pair_pack[pi];
+      const int g1 = pk & 255, g2 = (pk >> 8) & 255, kind = (pk >> 16) & 255;
+      keep = true;
+      if (kind == PH_PAIR_CONVEX || kind == PH_PAIR_BOX) {
+        const T mg = m.pair_margin[pi] + T(1e-6);
+        keep = !c_sphere_obb_disjoint(m, s, g1, g2, mg) && !c_sphere_obb_disjoint(m, s, g2, g1, mg);
+      } else if (kind == PH_PAIR_PLANE) {
+        keep = !c_plane_obb_clear(m, s, g1, g2, m.pair_margin[pi]);
+      }
+    }
+    const uint64_t bal = __ballot(keep);
+    wsync();
+    if (keep) s.live[nlive + __popcll(bal & ((1ull << l) - 1))] = (short)pi;
+    nlive += __popcll(bal);
+  }
+  wsync();
+  // exact oriented-box tests over the pre-test survivors, compacted in place likewise
+  nsph = nlive;
   nlive = 0;
   for (int base = 0; base < nsph; base += NT) {
     const int k = base + l;
@@ -932,7 +963,6 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
       // SAT would keep is never culled)
       if (kind == PH_PAIR_CONVEX || kind == PH_PAIR_BOX)
         keep = !c_convex_obb_disjoint(m, s, g1, g2, m.pair_margin[pi] + (kind == PH_PAIR_BOX ? T(1e-6) : T(0)));
-      else if (kind == PH_PAIR_PLANE) keep = !c_plane_obb_clear(m, s, g1, g2, m.pair_margin[pi]);
     }
     const uint64_t bal = __ballot(keep);
     wsync();
@@ -956,10 +986,8 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
     if (l == 0) s.cst_n = 0;
     wsync();
     StageSink<T> ss{&s.cst_n, s.cst_val, s.cst_key, l};
-    clk.aux_start();
     if (k < nlive && !cvx) collide_pair(m, s, pair, ss);
     wsync();
-    clk.aux_lap(SC_AUX0);   // aux0: narrowphase colliders
     const int staged = s.cst_n;
     int incl = ss.n;
     for (int o = 1; o < 64; o <<= 1) {
@@ -973,7 +1001,6 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
       const int src = key >> 4;
       const int at = __shfl(off, src) + (key & 15);
       const int sp = __shfl(pair, src);
-      clk.aux_lap(SC_AUX0 + 1);   // aux1: narrowphase staging scan
       if (l < staged && at < PH_MAXCON) {
         Con<T>& c = s.con[at];
         c.dist = s.cst_val[l][0];
@@ -981,7 +1008,6 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
         for (int t = 0; t < 9; t++) c.frame[t] = t < 3 ? s.cst_val[l][4 + t] : T(0);
         c_params(m, c, m.pair_g1[sp], m.pair_g2[sp]);
       }
-      clk.aux_lap(SC_AUX0 + 2);   // aux2: contact parameters
     } else if (ss.n) {
       LdsSink<T> ls{s.con + off, PH_MAXCON - off};
       if (ls.cap > 0) {
