@@ -293,17 +293,10 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_r
 }
 
 // ---------------------------------------------------------------- step (FrankaEnv.step)
-// Phases (env_host.h: launch_env_step): ENV_ALL runs the whole gym step in one launch (fp64, and
-// fp32 with PNP_STEP_COMPACT=0).  The fp32 path launches ENV_PRO (_set_action: controls stored),
-// then one ENV_PHYS launch per mj_step call (sub-steps [k_begin, k_end), each followed by the
-// full kernel's resume pass, so that a hand-over costs at most the rest of one call), then
-// ENV_EPI (observation, reward, task sequencing from the stored state and qpos_kin).
-enum { ENV_ALL = 0, ENV_PRO = 1, ENV_PHYS = 2, ENV_EPI = 3 };
 template <typename T>
 __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
                                                       pnp_env_params prm, EnvSoA<T> es, const T* __restrict__ action,
-                                                      EnvOutT<T> out, int B, int resume, int phase, int k_begin,
-                                                      int k_end) {
+                                                      EnvOutT<T> out, int B) {
   __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
   Env<T>& s = s_env;
   const DevPhys<T>& m = phys<T>();
@@ -311,19 +304,10 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
   const int b = blockIdx.x;
   if (b >= B) return;
   const int l = lane_id();
-  // full kernel, resume pass (step.hip: PNP_RESUME_*): only the envs the compact kernel handed
-  // over, from their sub-step; their action is already applied (ctrl / mocap stored with them)
-  int k0 = phase == ENV_PHYS ? k_begin : 0;
-  if (!PNP_COMPACT && resume) {
-    const uint32_t w = st.warn[b];
-    if (!(w & PNP_RESUME_FLAG)) return;
-    k0 = (int)((w >> PNP_RESUME_SHIFT) & PNP_RESUME_MAXSUB);
-  }
   load_env(m, s, st, b);
-  T ee_p[3], ee_R[9], ee_q[4];
-  if (!resume && (phase == ENV_ALL || phase == ENV_PRO)) {
   // ---- _set_action: ee pose from the last forward's site frame
   kin_at(m, s, es.qpos_kin + (size_t)b * m.nq, false);
+  T ee_p[3], ee_R[9], ee_q[4];
   site_frame(m, s, prm.ee_site, ee_p, ee_R);
   g_mat2quat(ee_R, ee_q);
   if (l == 0) {
@@ -347,39 +331,14 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
     for (int t = 0; t < 4; t++) s.mocap_quat[t] = tq[t];
   }
   wsync();
-  if (phase == ENV_PRO) {
-    store_controls(m, s, st, b);
-    return;
-  }
-  }
+  // ---- _mujoco_step: n_calls x mj_step(nstep = n_substeps)
+  NoClock clk;
   const int nsub = prm.n_substeps * prm.n_calls;
-  if (phase != ENV_EPI) {
-    // ---- _mujoco_step: n_calls x mj_step(nstep = n_substeps)
-    NoClock clk;
-    const int kend = phase == ENV_PHYS ? k_end : nsub;
-    int k = k0;
-    for (; k < kend && !s.ovf; k++) mj_step_dev(m, s, clk, k == nsub - 1 ? s.qpos_pre : nullptr);
-    if (PNP_COMPACT && s.ovf) {
-      // hand over: the state as of sub-step k - 1, with this step's controls, to the resume pass
-      if (l == 0) s.warn |= PNP_RESUME_FLAG | ((uint32_t)s.ovf << PNP_RESUME_WHY_SHIFT) | ((uint32_t)(k - 1) << PNP_RESUME_SHIFT);
-      wsync();
-      store_env(m, s, st, b);
-      store_controls(m, s, st, b);
-      return;
-    }
-    store_env(m, s, st, b);
-    if (phase == ENV_PHYS) {
-      if (kend == nsub && l < m.nq) es.qpos_kin[(size_t)b * m.nq + l] = s.qpos_pre[l];
-      return;
-    }
-    store_controls(m, s, st, b);
-    if (l < m.nq) es.qpos_kin[(size_t)b * m.nq + l] = s.qpos_pre[l];
-  } else {
-    // the state after the last sub-step; its pre-integration qpos was stored in qpos_kin
-    if (l < m.nq) s.qpos_pre[l] = es.qpos_kin[(size_t)b * m.nq + l];
-    wsync();
-  }
+  for (int k = 0; k < nsub; k++) mj_step_dev(m, s, clk, k == nsub - 1 ? s.qpos_pre : nullptr);
+  store_env(m, s, st, b);
+  store_controls(m, s, st, b);
   const T width = s.qpos[prm.finger_qadr[0]] + s.qpos[prm.finger_qadr[1]];
+  if (l < m.nq) es.qpos_kin[(size_t)b * m.nq + l] = s.qpos_pre[l];
   // ---- _get_obs at data.site_* (kinematics of qpos_pre) with the integrated qvel
   if (l < m.nq) { const T t = s.qpos[l]; s.qpos[l] = s.qpos_pre[l]; s.qpos_pre[l] = t; }
   wsync();
@@ -442,7 +401,7 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
   }
 }
 
-// ---------------------------------------------------------------- launch views
+// ---------------------------------------------------------------- host launchers
 template <typename T>
 static EnvSoA<T> env_view(const pnp_env_state* e) {
   return EnvSoA<T>{(T*)e->goal, e->task, e->elapsed, (T*)e->qpos_kin, (T*)e->obj_height0, (T*)e->init_mocap,
@@ -455,3 +414,110 @@ static EnvOutT<T> out_view(const pnp_env_out* o) {
                     o->terminated, o->truncated};
 }
 
+static int32_t env_check(pnp_model* model, const void* st, const pnp_env_params* p, const pnp_env_state* e,
+                         int32_t B, const char* fn) {
+  if (!model || !st || !p || !e || B < 0) { pnp_set_error("%s: bad argument", fn); return PNP_ERR_ARG; }
+  const DevModel<double>& h = model->h;
+  bool ok = p->n_tasks >= 1 && p->n_tasks <= PNP_MAX_TASKS && p->n_substeps >= 1 && p->n_calls >= 1 &&
+            p->ee_site >= 0 && p->ee_site < h.nsite && h.nmocap == 1 && model->nu >= 2 &&
+            p->arm_ctrl_n >= 0 && p->arm_ctrl_n <= model->nu;
+  for (int k = 0; k < p->n_tasks && ok; k++)
+    ok = p->obj_site[k] >= 0 && p->obj_site[k] < h.nsite && p->target_site[k] >= 0 && p->target_site[k] < h.nsite &&
+         p->obj_qadr[k] >= 0 && p->obj_qadr[k] + 7 <= h.nq;
+  for (int k = 0; k < 9 && ok; k++) ok = p->neutral_qadr[k] >= 0 && p->neutral_qadr[k] < h.nq;
+  ok = ok && p->finger_qadr[0] >= 0 && p->finger_qadr[0] < h.nq && p->finger_qadr[1] >= 0 &&
+       p->finger_qadr[1] < h.nq && p->height_qadr >= 0 && p->height_qadr + 3 <= h.nq;
+  if (!ok) { pnp_set_error("%s: env params do not fit the model", fn); return PNP_ERR_ARG; }
+  if (B == 0) return PNP_OK;
+  if (!e->goal || !e->task || !e->elapsed || !e->qpos_kin || !e->obj_height0 || !e->init_mocap || !e->init_qvel ||
+      !e->init_time || !e->episode || !e->env_index) {
+    pnp_set_error("%s: null env state buffer", fn);
+    return PNP_ERR_ARG;
+  }
+  return PNP_OK;
+}
+
+template <typename T, typename K>
+static int32_t env_prep(pnp_model* model, const pnp_state_t<T>* st, K kernel, const DevPhys<T>** dm, const char* fn,
+                        void* stream) {
+  if (!st->qpos || !st->qvel || !st->ctrl || !st->mocap_pos || !st->mocap_quat || !st->qacc_warmstart || !st->time ||
+      !st->warn) {
+    pnp_set_error("%s: null state buffer", fn);
+    return PNP_ERR_ARG;
+  }
+  *dm = phys_image<T>(model);
+  if (!*dm) { pnp_set_error("%s: model has no physics image (%s)", fn, model->phys_err); return PNP_ERR_MODEL; }
+  if (const int32_t rc = phys_resident<T>(model, stream)) return rc;
+  (void)kernel;
+  return PNP_OK;
+}
+
+template <typename T>
+static int32_t launch_env_init(pnp_model* model, const pnp_state_t<T>* st, const pnp_env_params* p,
+                               const pnp_env_state* e, int32_t B, void* stream) {
+  int32_t rc = env_check(model, st, p, e, B, "pnp_env_init");
+  if (rc || B == 0) return rc;
+  const DevPhys<T>* dm;
+  auto k = env_init_kernel<T>;
+  if ((rc = env_prep(model, st, k, &dm, "pnp_env_init", stream))) return rc;
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), B);
+  return pnp_check_launch("env_init_kernel");
+}
+template <typename T>
+static int32_t launch_env_reset(pnp_model* model, const pnp_state_t<T>* st, const pnp_env_params* p,
+                                const pnp_env_state* e, const uint8_t* mask, const pnp_env_out* o, int32_t B,
+                                void* stream) {
+  int32_t rc = env_check(model, st, p, e, B, "pnp_env_reset");
+  if (rc || B == 0) return rc;
+  const DevPhys<T>* dm;
+  auto k = env_reset_kernel<T>;
+  if ((rc = env_prep(model, st, k, &dm, "pnp_env_reset", stream))) return rc;
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), mask,
+                     out_view<T>(o), B);
+  return pnp_check_launch("env_reset_kernel");
+}
+template <typename T>
+static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const pnp_env_params* p,
+                               const pnp_env_state* e, const T* action, const pnp_env_out* o, int32_t B,
+                               void* stream) {
+  int32_t rc = env_check(model, st, p, e, B, "pnp_env_step");
+  if (rc || B == 0) return rc;
+  if (!action) { pnp_set_error("pnp_env_step: null action"); return PNP_ERR_ARG; }
+  const DevPhys<T>* dm;
+  auto k = env_step_kernel<T>;
+  if ((rc = env_prep(model, st, k, &dm, "pnp_env_step", stream))) return rc;
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), action,
+                     out_view<T>(o), B);
+  return pnp_check_launch("env_step_kernel");
+}
+
+extern "C" int32_t pnp_env_params_size(void) { return (int32_t)sizeof(pnp_env_params); }
+
+extern "C" int32_t pnp_env_init(pnp_model* model, const pnp_state* st, const pnp_env_params* p,
+                                const pnp_env_state* e, int32_t B, void* stream) {
+  return launch_env_init<float>(model, reinterpret_cast<const pnp_state_t<float>*>(st), p, e, B, stream);
+}
+extern "C" int32_t pnp_env_init_f64(pnp_model* model, const pnp_state_f64* st, const pnp_env_params* p,
+                                    const pnp_env_state* e, int32_t B, void* stream) {
+  return launch_env_init<double>(model, reinterpret_cast<const pnp_state_t<double>*>(st), p, e, B, stream);
+}
+extern "C" int32_t pnp_env_reset(pnp_model* model, const pnp_state* st, const pnp_env_params* p,
+                                 const pnp_env_state* e, const uint8_t* mask, const pnp_env_out* o, int32_t B,
+                                 void* stream) {
+  return launch_env_reset<float>(model, reinterpret_cast<const pnp_state_t<float>*>(st), p, e, mask, o, B, stream);
+}
+extern "C" int32_t pnp_env_reset_f64(pnp_model* model, const pnp_state_f64* st, const pnp_env_params* p,
+                                     const pnp_env_state* e, const uint8_t* mask, const pnp_env_out* o, int32_t B,
+                                     void* stream) {
+  return launch_env_reset<double>(model, reinterpret_cast<const pnp_state_t<double>*>(st), p, e, mask, o, B, stream);
+}
+extern "C" int32_t pnp_env_step(pnp_model* model, const pnp_state* st, const pnp_env_params* p,
+                                const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
+                                void* stream) {
+  return launch_env_step<float>(model, reinterpret_cast<const pnp_state_t<float>*>(st), p, e, action, o, B, stream);
+}
+extern "C" int32_t pnp_env_step_f64(pnp_model* model, const pnp_state_f64* st, const pnp_env_params* p,
+                                    const pnp_env_state* e, const double* action, const pnp_env_out* o, int32_t B,
+                                    void* stream) {
+  return launch_env_step<double>(model, reinterpret_cast<const pnp_state_t<double>*>(st), p, e, action, o, B, stream);
+}

@@ -86,9 +86,6 @@ int32_t launch_step_compact(const pnp_model* model, const pnp_state_t<float>* st
                             void* stream, unsigned long long* prof);
 void phys_forget_compact(const pnp_model* model);
 int32_t step_compact_lds_bytes();
-int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
-                                const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
-                                void* stream, int phase, int k_begin, int k_end);
 
 // ---------------------------------------------------------------------------- error plumbing
 void pnp_set_error(const char* fmt, ...);

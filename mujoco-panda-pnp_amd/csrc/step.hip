@@ -1594,37 +1594,39 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
       if (u < l && (comp >> u & 1u)) pos += tdn[u];
     s.tree_ipos[l] = pos;
   }
-  // island sizes: lane I sums its trees; isz[J] = readlane broadcast (uniform)
+  // island sizes: lane I sums its trees
   int nI = 0;
 #pragma unroll
   for (int t = 0; t < 8; t++)
     if (t < nt && island_of(t) == l) nI += tdn[t];
-  int isz[8];
-#pragma unroll
-  for (int J = 0; J < 8; J++) isz[J] = __builtin_amdgcn_readlane(nI, J);
-  // rows by island: per-island counts over the row chunks, then positions
-  int rcnt[8];
-#pragma unroll
-  for (int J = 0; J < 8; J++) rcnt[J] = 0;
+  // rows by island (counting sort): lane J counts island J's rows over the row chunks ...
+  int rc = 0;
   const int nefc = s.nefc;
   for (int base = 0; base < nefc; base += NT) {
     const int r = base + l;
     const int I = r < nefc ? island_of(s.efc_t0[r]) : -1;
 #pragma unroll
-    for (int J = 0; J < 8; J++) rcnt[J] += J < nis ? __popcll(__ballot(I == J)) : 0;
+    for (int J = 0; J < 8; J++) {
+      if (J >= nis) break;
+      const int c = __popcll(__ballot(I == J));
+      if (l == J) rc += c;
+    }
   }
-  int roff[9], eoff[9], joff[9];
-  roff[0] = eoff[0] = joff[0] = 0;
+  // ... exclusive prefix sums over the island lanes (row, Hessian and dense-block offsets) ...
+  const bool isl = l < nis;
+  int ro = isl ? rc : 0, eo = isl ? nI * (nI + 1) / 2 : 0, jo = isl ? rc * nI : 0;
 #pragma unroll
-  for (int J = 0; J < 8; J++) {
-    const bool in = J < nis;
-    roff[J + 1] = roff[J] + (in ? rcnt[J] : 0);
-    eoff[J + 1] = eoff[J] + (in ? isz[J] * (isz[J] + 1) / 2 : 0);
-    joff[J + 1] = joff[J] + (in ? rcnt[J] * isz[J] : 0);
+  for (int o = 1; o < 8; o <<= 1) {
+    const int a = __shfl_up(ro, o), e = __shfl_up(eo, o), j = __shfl_up(jo, o);
+    if (l >= o) { ro += a; eo += e; jo += j; }
   }
-  int run[8];
-#pragma unroll
-  for (int J = 0; J < 8; J++) run[J] = roff[J];
+  const int rtot = __builtin_amdgcn_readlane(ro, 7), etot = __builtin_amdgcn_readlane(eo, 7),
+            jtot = __builtin_amdgcn_readlane(jo, 7);
+  ro -= isl ? rc : 0;
+  eo -= isl ? nI * (nI + 1) / 2 : 0;
+  jo -= isl ? rc * nI : 0;
+  // ... then every row lands at its island's offset + its rank among the island's earlier rows
+  int run = ro;
   for (int base = 0; base < nefc; base += NT) {
     const int r = base + l;
     const int I = r < nefc ? island_of(s.efc_t0[r]) : -1;
@@ -1633,26 +1635,18 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
     for (int J = 0; J < 8; J++) {
       if (J >= nis) break;
       const uint64_t bal = __ballot(I == J);
-      if (I == J) s.isl_row[run[J] + __popcll(bal & below)] = (short)r;
-      run[J] += __popcll(bal);
+      const int at = __builtin_amdgcn_readlane(run, J);
+      if (I == J) s.isl_row[at + __popcll(bal & below)] = (short)r;
+      if (l == J) run += __popcll(bal);
     }
   }
-  // per-island tables: lane I writes its entries (and lane 0 the end markers)
-  if (l < nis) {
-    int ro = 0, eo = 0, jo = 0;
-#pragma unroll
-    for (int J = 0; J < 8; J++)
-      if (J == l) { ro = roff[J]; eo = eoff[J]; jo = joff[J]; }
+  // per-island tables: lane I writes its entries, lane 0 the end markers
+  if (isl) {
     s.isl_n[l] = nI;
     s.isl_roff[l] = ro;
     s.isl_eoff[l] = eo;
     s.isl_joff[l] = jo;
   }
-  int rtot = 0, etot = 0, jtot = 0;
-#pragma unroll
-  for (int J = 0; J < 8; J++)
-    if (J == nis) { rtot = roff[J]; etot = eoff[J]; jtot = joff[J]; }
-  if (nis == 8) { rtot = roff[8]; etot = eoff[8]; jtot = joff[8]; }
   if (l == 0) {
     s.nisland = nis;
     s.isl_roff[nis] = rtot;
@@ -2726,8 +2720,6 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) forwa
   }
 }
 
-// ============================================================================ gym env (fused)
-#include "env_dev.h"
 }  // namespace PNP_NS
 using namespace PNP_NS;
 
@@ -2768,15 +2760,6 @@ int32_t launch_step_compact(const pnp_model* model, const pnp_state_t<float>* st
 
 int32_t step_compact_lds_bytes() { return (int32_t)sizeof(Env<float>); }
 
-int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
-                                const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
-                                void* stream, int phase, int k_begin, int k_end) {
-  if (const int32_t rc = phys_resident_compact(model, stream)) return rc;
-  auto k = env_step_kernel<float>;
-  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, phys_image<float>(model), *st, *p,
-                     env_view<float>(e), action, out_view<float>(o), B, 0, phase, k_begin, k_end);
-  return pnp_check_launch("env_step_kernel (compact)");
-}
 #else
 
 template <typename T>
@@ -2876,5 +2859,11 @@ extern "C" int32_t pnp_step_lds_bytes(int32_t fp64) {
 }
 
 // ============================================================================ gym env (fused)
-#include "env_host.h"
+// (full build only: the gym step runs the full-capacity kernel.  A compact gym path -- set_action,
+// compact physics launches with resume passes, observation -- was built and measured at eadc013:
+// bit-exact, but random-action workloads keep > 20 contacts in about a third of the envs (closed
+// finger pads), so it ran slower than one full launch (275 vs 304-337 ms per 4096-env gym step),
+// and compiling the gym kernels into the compact build grew the compact step kernel's call
+// frames (scratch 384 -> 464 B per lane, 5x the HBM write-back traffic).)
+#include "env_dev.h"
 #endif  // !PNP_COMPACT

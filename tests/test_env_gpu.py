@@ -192,51 +192,6 @@ def test_truncation_autoreset_and_mask(model):
     assert not torch.equal(g.state["qpos"][1], before[1])
 
 
-def _gym_steps(mode, nsteps, B=256, **cfg):
-    import os
-    old = os.environ.get("PNP_STEP_COMPACT")
-    os.environ["PNP_STEP_COMPACT"] = mode
-    os.environ["PNP_GYM_COMPACT"] = "1"
-    try:
-        g = _env(torch.float32, B=B, **cfg)
-        g.reset()
-        outs = []
-        for k in range(nsteps):
-            a = torch.as_tensor(_actions(B, 40 + k), dtype=torch.float32, device=g.device)
-            obs, r, term, trunc, info = g.step(a)
-            outs.append((obs["observation"].clone(), r.clone(), term.clone(), trunc.clone()))
-        torch.cuda.synchronize()
-    finally:
-        del os.environ["PNP_GYM_COMPACT"]
-        if old is None:
-            del os.environ["PNP_STEP_COMPACT"]
-        else:
-            os.environ["PNP_STEP_COMPACT"] = old
-    return g, outs
-
-
-def test_compact_gym_step_is_exact():
-    """The opt-in compact gym path (PNP_GYM_COMPACT=1) runs the fp32 gym step as compact-capacity phases (set_action, one launch per mj_step call,
-    observation / reward) with the full kernel's resume pass after each call (step.hip, resume
-    protocol): observations, rewards, flags and the whole state equal the single full-kernel
-    launch's bit for bit, through the first steps after reset, where hand-overs do happen (the
-    closed finger pads: > 20 contacts; the compact kernel alone over one 250-sub-step call leaves
-    their resume bits in warn)."""
-    probe, _ = _gym_steps("2", 1, n_substeps=250, n_calls=1)
-    w = probe.state["warn"].cpu().numpy().astype(np.uint32)
-    assert ((w >> 31) & 1).any()
-    a, oa = _gym_steps("1", 3)
-    b, ob = _gym_steps("0", 3)
-    for x, y in zip(oa, ob):
-        for u, v in zip(x, y):
-            assert torch.equal(u, v)
-    for k in a.state:
-        assert torch.equal(a.state[k], b.state[k]), k
-    for k in a.env:
-        assert torch.equal(a.env[k], b.env[k]), k
-    assert int(a.state["warn"].max()) < (1 << 16)
-
-
 def test_shard_invariant_resets():
     """Envs [2, 4) of a 4-env batch == a 2-env batch with env_offset 2 (Philox by global index)."""
     from pnp_amd.envs import BatchedFrankaShelfPNPEnv
