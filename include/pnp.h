@@ -218,7 +218,7 @@ typedef struct pnp_state_f64 {
 #define PNP_WARN_BADQACC 4u
 #define PNP_WARN_CONTACTFULL 8u
 #define PNP_WARN_CNSTRFULL 16u
-/* bits 16..31 are reserved: inside one pnp_step / pnp_env_step call they carry the compact
+/* bits 16..31 are reserved: inside one fp32 pnp_step call they carry the compact
  * kernel's hand-over to the full kernel (flag + sub-step); they are clear when a call returns
  * and are ignored on input */
 
