@@ -458,6 +458,75 @@ __device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
     qh[0] = cs; qh[1] = jax[0] * sn; qh[2] = jax[1] * sn; qh[3] = jax[2] * sn;
   }
   clk.sub_lap(SC_K_PRE);
+  if (!__ballot(mine && jn > 1)) {
+    // Pointer jumping: every body's frame relative to its parent (offset, then its one joint) is
+    // formed by all lanes at once, then each lane composes with its ancestor's accumulated
+    // transform and jumps to that ancestor's ancestor -- ceil(log2(depth)) = 4 register
+    // exchanges (ds_bpermute) for the arm's 11 levels instead of one LDS round trip per level.
+    // Rigid transforms compose associatively, so the frames are MuJoCo's up to rounding (the
+    // order of the compositions differs).  Free-joint and mocap bodies hang off the world.
+    T p[3] = {0, 0, 0}, q[4] = {1, 0, 0, 0};
+    int anc = 0;
+    if (mine) {
+      if (one && jt == 0) {
+        p[0] = fq[0]; p[1] = fq[1]; p[2] = fq[2];
+        q[0] = fq[3]; q[1] = fq[4]; q[2] = fq[5]; q[3] = fq[6];
+        t_normalize4(q);
+      } else {
+        for (int t = 0; t < 3; t++) p[t] = bp[t];
+        for (int t = 0; t < 4; t++) q[t] = bq[t];
+        if (one && jt == 2) {
+          T ax[3];
+          t_rotvecquat_mj(ax, jax, bq);
+          for (int t = 0; t < 3; t++) p[t] += ax[t] * sl;
+        } else if (one && jt == 3) {
+          // rotation qh about the axis through jpos: p += R(bq) (jpos - R(qh) jpos), q = bq qh
+          T v[3], w[3], u[3];
+          t_rotvecquat_mj(v, jpos, qh);
+          for (int t = 0; t < 3; t++) w[t] = jpos[t] - v[t];
+          t_rotvecquat_mj(u, w, bq);
+          for (int t = 0; t < 3; t++) p[t] += u[t];
+          d_mulquat(q, bq, qh);
+        }
+        anc = pid;
+      }
+    }
+    while (__ballot(anc > 0)) {
+      const int a = anc > 0 ? anc : 0;
+      T pa[3], qa[4];
+      for (int t = 0; t < 3; t++) pa[t] = __shfl(p[t], a);
+      for (int t = 0; t < 4; t++) qa[t] = __shfl(q[t], a);
+      const int a2 = __shfl(anc, a);
+      if (anc > 0) {
+        T r[3];
+        t_rotvecquat_mj(r, p, qa);
+        for (int t = 0; t < 3; t++) p[t] = pa[t] + r[t];
+        d_mulquat(q, qa, q);
+        anc = a2;
+      }
+    }
+    if (mine) {
+      t_normalize4(q);
+      T R[9];
+      d_quat2mat(R, q);
+      for (int t = 0; t < 3; t++) s.xpos[b][t] = p[t];
+      for (int t = 0; t < 4; t++) s.xquat[b][t] = q[t];
+      for (int t = 0; t < 9; t++) s.xmat[b][t] = R[t];
+      if (one && jt == 0) {
+        for (int t = 0; t < 3; t++) { s.xanchor[ja][t] = p[t]; s.xaxis[ja][t] = jax[t]; }
+      } else if (one) {
+        // the joint's axis and anchor in the body's final frame: a hinge leaves its axis and the
+        // point jpos fixed; a slide moved the frame by axis * sl
+        T ax[3], an[3];
+        t_rotvecquat_mj(ax, jax, q);
+        t_rotvecquat_mj(an, jpos, q);
+        for (int t = 0; t < 3; t++) {
+          s.xanchor[ja][t] = an[t] + p[t] - (jt == 2 ? ax[t] * sl : T(0));
+          s.xaxis[ja][t] = ax[t];
+        }
+      }
+    }
+  } else
   for (int d = 1; __ballot(mine && depth >= d); d++) {
     if (mine && depth == d) {
       T p[3], q[4];
