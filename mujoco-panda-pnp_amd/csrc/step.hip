@@ -2181,6 +2181,31 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
 }
 
 // ============================================================================ no-slip
+// x = (L L^T)^-1 j for one dense tree block of compile-time size N (L row-major, N x N): the
+// substitutions fully unrolled, y / x in registers -- the block's loads are independent of the
+// substitution chain and issue together (a runtime-n loop kept y in private memory and waited on
+// each L load in turn).  Same operations in the same order as the generic loop below.
+template <int N, typename T>
+__device__ __forceinline__ void tree_solve_fixed(const T* L, const T* j, T* x_out) {
+  T y[N], x[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    T v = j[i];
+#pragma unroll
+    for (int k = 0; k < i; k++) v -= L[i * N + k] * y[k];
+    y[i] = v / L[i * N + i];
+  }
+#pragma unroll
+  for (int i = N - 1; i >= 0; i--) {
+    T v = y[i];
+#pragma unroll
+    for (int k = i + 1; k < N; k++) v -= L[k * N + i] * x[k];
+    x[i] = v / L[i * N + i];
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) x_out[i] = x[i];
+}
+
 template <typename T, class CLK>
 __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
@@ -2201,6 +2226,14 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       const int t = h ? t1 : t0;
       if (t < 0) continue;
       const int n = s.c_tree_dofnum[t], o = s.c_tree_moff[t];
+      if (n == 9 || n == 6) {
+        const T* Jr = s.efc_Jv + s.efc_off[r] + base;
+        T* Wr = s.efc_Wv + s.efc_off[r] + base;
+        if (n == 9) tree_solve_fixed<9>(s.L + o, Jr, Wr);
+        else tree_solve_fixed<6>(s.L + o, Jr, Wr);
+        base += n;
+        continue;
+      }
       T y[PH_MAXTDOF];
       for (int i = 0; i < n; i++) {
         T v = EJ(r, base + i);
