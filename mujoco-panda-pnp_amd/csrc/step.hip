@@ -922,7 +922,16 @@ __device__ T mulM_row(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, i
   const int t = s.c_dof_tree[i];
   const int a = s.c_tree_dofadr[t], n = s.c_tree_dofnum[t], o = s.c_tree_moff[t] + (i - a) * n;
   T r = 0;
-  for (int k = 0; k < n; k++) r += s.M[o + k] * v[a + k];
+  // the scene's block sizes fully unrolled (all loads issue before the sum), same order
+  if (n == 9) {
+#pragma unroll
+    for (int k = 0; k < 9; k++) r += s.M[o + k] * v[a + k];
+  } else if (n == 6) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) r += s.M[o + k] * v[a + k];
+  } else {
+    for (int k = 0; k < n; k++) r += s.M[o + k] * v[a + k];
+  }
   return r;
 }
 
@@ -2050,6 +2059,16 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   const bool jt = s.jt_ok;
   // group-parallel island factorisation when every island fits a 9-lane group
   const bool gch = s.nisland <= GCH_GROUPS && !__ballot(l < s.nisland && s.isl_n[l] > GCH_N);
+  // the island tables the Hessian assembly indexes per entry, held in registers for the whole
+  // solve (an entry's island by comparisons instead of a loop of LDS loads)
+  int h_eoff[PH_MAXT + 1], h_n[PH_MAXT], h_roff[PH_MAXT + 1], h_joff[PH_MAXT];
+#pragma unroll
+  for (int J = 0; J <= PH_MAXT; J++) {
+    const bool in = J <= s.nisland;
+    h_eoff[J] = in ? s.isl_eoff[J] : 0x7FFFFFFF;
+    h_roff[J] = in ? s.isl_roff[J] : 0;
+    if (J < PH_MAXT) { h_n[J] = J < s.nisland ? s.isl_n[J] : 0; h_joff[J] = J < s.nisland ? s.isl_joff[J] : 0; }
+  }
   for (; it < m.iterations; it++) {
     clk.sub_start();
     // gradient g = M (x - x_smooth) + J^T (D jar) over the dof's island rows
@@ -2086,9 +2105,14 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     // islands whose active set is unchanged since their last assembly are reused as they are
     for (int e = l; e < nent; e += NT) {
       int I = 0;
-      while (e >= s.isl_eoff[I + 1]) I++;
+#pragma unroll
+      for (int J = 1; J <= PH_MAXT; J++) I += e >= h_eoff[J] ? 1 : 0;
+      int eI = 0, nI = 0, r0I = 0, e1I = 0, joI = 0;
+#pragma unroll
+      for (int J = 0; J < PH_MAXT; J++)
+        if (I == J) { eI = h_eoff[J]; nI = h_n[J]; r0I = h_roff[J]; e1I = h_roff[J + 1]; joI = h_joff[J]; }
       if (s.isl_flag[I] || s.isl_hvalid[I]) continue;
-      const int le = e - s.isl_eoff[I];
+      const int le = e - eI;
       int a = (int)((PM<float>::sqrt_(8.0f * le + 1.0f) - 1.0f) * 0.5f);
       while (a * (a + 1) / 2 > le) a--;
       while ((a + 1) * (a + 2) / 2 <= le) a++;
@@ -2097,17 +2121,17 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       const int ti = s.c_dof_tree[i], tj = s.c_dof_tree[j];
       T h = ti == tj ? s.M[mblk(m, i, j)] : T(0);
       const int li = i - s.c_tree_dofadr[ti], lj = j - s.c_tree_dofadr[tj];
-      const int e1 = s.isl_roff[I + 1];
+      const int e1 = e1I;
       if (jt) {
-        const int n = s.isl_n[I], r0 = s.isl_roff[I];
-        const T* ja = s.jt + s.isl_joff[I] + a;
-        const T* jb = s.jt + s.isl_joff[I] + b;
+        const int n = nI, r0 = r0I;
+        const T* ja = s.jt + joI + a;
+        const T* jb = s.jt + joI + b;
         const T* dr = s.rr_d + r0;
 #pragma unroll 4
         for (int k = 0; k < e1 - r0; k++) h += ja[k * n] * dr[k] * jb[k * n];
       } else
 #pragma unroll 2
-      for (int rr = s.isl_roff[I]; rr < e1; rr++) {   // unconditional loads (see own_slot)
+      for (int rr = r0I; rr < e1; rr++) {   // unconditional loads (see own_slot)
         const int r = s.isl_row[rr];
         const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], off = s.efc_off[r];
         const int n0 = s.c_tree_dofnum[t0];
