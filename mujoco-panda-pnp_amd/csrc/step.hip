@@ -419,11 +419,11 @@ template <typename T, class CLK>
 __device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
   clk.sub_start();
-  // Level-synchronous tree pass (mj_kinematics order): a body's frame is its parent's composed
-  // with its own offset and joints, the parent's read from LDS one level earlier.  The per-body
-  // work that does not need the parent -- the model constants and a single hinge's rotation
-  // (sincos) -- is done by every lane at once before the levels, so each level costs one
-  // composition instead of each lane re-walking its whole root path.
+  // Bodies with at most one joint (this scene): pointer jumping over parent-relative transforms
+  // (below).  Otherwise a level-synchronous tree pass (mj_kinematics order): a body's frame is
+  // its parent's composed with its own offset and joints, the parent's read from LDS one level
+  // earlier.  Either way the per-body work that does not need the parent -- the model constants
+  // and a single hinge's rotation (sincos) -- is done by every lane at once up front.
   const int b = lane_id();
   const bool mine = b > 0 && b < m.nbody;
   const int bb = mine ? b : 1;
@@ -2059,16 +2059,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   const bool jt = s.jt_ok;
   // group-parallel island factorisation when every island fits a 9-lane group
   const bool gch = s.nisland <= GCH_GROUPS && !__ballot(l < s.nisland && s.isl_n[l] > GCH_N);
-  // the island tables the Hessian assembly indexes per entry, held in registers for the whole
-  // solve (an entry's island by comparisons instead of a loop of LDS loads)
-  int h_eoff[PH_MAXT + 1], h_n[PH_MAXT], h_roff[PH_MAXT + 1], h_joff[PH_MAXT];
-#pragma unroll
-  for (int J = 0; J <= PH_MAXT; J++) {
-    const bool in = J <= s.nisland;
-    h_eoff[J] = in ? s.isl_eoff[J] : 0x7FFFFFFF;
-    h_roff[J] = in ? s.isl_roff[J] : 0;
-    if (J < PH_MAXT) { h_n[J] = J < s.nisland ? s.isl_n[J] : 0; h_joff[J] = J < s.nisland ? s.isl_joff[J] : 0; }
-  }
+  const int nisl = s.nisland;
   for (; it < m.iterations; it++) {
     clk.sub_start();
     // gradient g = M (x - x_smooth) + J^T (D jar) over the dof's island rows
@@ -2104,13 +2095,13 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     // Hessian island blocks (lower triangle, lane per entry): M + sum_active D J J^T; blocks of
     // islands whose active set is unchanged since their last assembly are reused as they are
     for (int e = l; e < nent; e += NT) {
+      // the entry's island: comparisons against the offsets (independent LDS loads issued
+      // together) instead of a loop that waits on one load per island
       int I = 0;
 #pragma unroll
-      for (int J = 1; J <= PH_MAXT; J++) I += e >= h_eoff[J] ? 1 : 0;
-      int eI = 0, nI = 0, r0I = 0, e1I = 0, joI = 0;
-#pragma unroll
-      for (int J = 0; J < PH_MAXT; J++)
-        if (I == J) { eI = h_eoff[J]; nI = h_n[J]; r0I = h_roff[J]; e1I = h_roff[J + 1]; joI = h_joff[J]; }
+      for (int J = 1; J <= PH_MAXT; J++) I += J < nisl && e >= s.isl_eoff[J] ? 1 : 0;
+      const int eI = s.isl_eoff[I], nI = s.isl_n[I], r0I = s.isl_roff[I], e1I = s.isl_roff[I + 1],
+                joI = s.isl_joff[I];
       if (s.isl_flag[I] || s.isl_hvalid[I]) continue;
       const int le = e - eI;
       int a = (int)((PM<float>::sqrt_(8.0f * le + 1.0f) - 1.0f) * 0.5f);
