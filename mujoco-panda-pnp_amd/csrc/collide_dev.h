@@ -627,26 +627,53 @@ __device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A
   }
 }
 
-// oriented-box separating-axis test (15 axes), boxes inflated by margin
+// oriented-box separating-axis test (15 axes), boxes inflated by margin.  The classic form: the
+// 9 direction cosines R = A^T B and the centre offset in both frames are formed once, then every
+// axis is a few products of them -- all 15 evaluated branch-free (no per-axis early exit, so
+// the wave's lanes stay converged).  Face axes: |t_i| > h1_i + sum_j h2_j |R_ij| + margin (and
+// the same from B); edge axes A_i x B_j (skipped when parallel) compare the projections over
+// |A_i x B_j| = sqrt(1 - R_ij^2), the margin scaled by it as before.
 template <typename T>
 __device__ bool c_obb_disjoint(const T* p1, const T* R1, const T* h1, const T* p2, const T* R2, const T* h2, T margin) {
   T A[3][3], B[3][3], Tv[3];
+#pragma unroll
   for (int i = 0; i < 3; i++)
+#pragma unroll
     for (int k = 0; k < 3; k++) { A[i][k] = R1[3 * k + i]; B[i][k] = R2[3 * k + i]; }
   cs3(Tv, p2, p1);
+  T R[3][3], aR[3][3], ta[3], tb[3];
 #pragma unroll
-  for (int a = 0; a < 15; a++) {
-    T L[3];
-    if (a < 3) { L[0] = A[a][0]; L[1] = A[a][1]; L[2] = A[a][2]; }
-    else if (a < 6) { L[0] = B[a - 3][0]; L[1] = B[a - 3][1]; L[2] = B[a - 3][2]; }
-    else cc3(L, A[(a - 6) / 3], B[(a - 6) % 3]);
-    const T len2 = cd3(L, L);
-    if (len2 < T(1e-12)) continue;
-    T ra = 0, rb = 0;
-    for (int k = 0; k < 3; k++) { ra += h1[k] * fabs(cd3(A[k], L)); rb += h2[k] * fabs(cd3(B[k], L)); }
-    if (fabs(cd3(Tv, L)) > ra + rb + margin * PM<T>::sqrt_(len2)) return true;
+  for (int i = 0; i < 3; i++) {
+    ta[i] = cd3(Tv, A[i]);
+    tb[i] = cd3(Tv, B[i]);
+#pragma unroll
+    for (int j = 0; j < 3; j++) { R[i][j] = cd3(A[i], B[j]); aR[i][j] = fabs(R[i][j]); }
   }
-  return false;
+  bool sep = false;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const T rb = h2[0] * aR[i][0] + h2[1] * aR[i][1] + h2[2] * aR[i][2];
+    sep |= fabs(ta[i]) > h1[i] + rb + margin;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    const T ra = h1[0] * aR[0][j] + h1[1] * aR[1][j] + h1[2] * aR[2][j];
+    sep |= fabs(tb[j]) > ra + h2[j] + margin;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      const T len2 = T(1) - R[i][j] * R[i][j];
+      const T d = fabs(ta[i2] * R[i1][j] - ta[i1] * R[i2][j]);
+      const T ra = h1[i1] * aR[i2][j] + h1[i2] * aR[i1][j];
+      const T rb = h2[j1] * aR[i][j2] + h2[j2] * aR[i][j1];
+      sep |= len2 >= T(1e-12) && d > ra + rb + margin * PM<T>::sqrt_(len2 > T(0) ? len2 : T(0));
+    }
+  }
+  return sep;
 }
 
 // convex pair: (sphere | box | mesh) x mesh (g1 has the lower type)
