@@ -265,23 +265,39 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
     if (sep > margin) return;
     if (sep > best + T(C_BB_TOL)) { best = sep; btype = 1; bj = j; for (int k = 0; k < 3; k++) bestn[k] = tl >= 0 ? Bm[j][k] : -Bm[j][k]; }
   }
-  for (int i = 0; i < 3; i++)
+  // edge axes A_i x B_j in closed form from the direction cosines AB and the centre offset in
+  // A's frame (Tv . (A_i x B_j) = ta_i2 AB_i1j - ta_i1 AB_i2j, |A_k . L|, |B_k . L| likewise); the
+  // winning axis vector is formed once below
+  T tA[3];
+  for (int i = 0; i < 3; i++) tA[i] = t_dot3(Tv, A[i]);
+  T btl = 0;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+#pragma unroll
     for (int j = 0; j < 3; j++) {
-      T L[3];
-      t_cross(L, A[i], Bm[j]);
-      const T len = PM<T>::sqrt_(t_dot3(L, L));
+      const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      // |A_i x B_j|^2 = AB_i1j^2 + AB_i2j^2 (A orthonormal): no cancellation for near-parallel
+      // edges, unlike 1 - AB_ij^2 in fp32
+      const T len = PM<T>::sqrt_(AB[i1][j] * AB[i1][j] + AB[i2][j] * AB[i2][j]);
       if (len < T(1e-6)) continue;
-      for (int k = 0; k < 3; k++) L[k] /= len;
-      const T tl = t_dot3(Tv, L);
-      const T ra = s1[0] * fabs(t_dot3(A[0], L)) + s1[1] * fabs(t_dot3(A[1], L)) + s1[2] * fabs(t_dot3(A[2], L));
-      const T rb = s2[0] * fabs(t_dot3(Bm[0], L)) + s2[1] * fabs(t_dot3(Bm[1], L)) + s2[2] * fabs(t_dot3(Bm[2], L));
+      const T inv = T(1) / len;
+      const T tl = (tA[i2] * AB[i1][j] - tA[i1] * AB[i2][j]) * inv;
+      const T ra = (s1[i1] * fabs(AB[i2][j]) + s1[i2] * fabs(AB[i1][j])) * inv;
+      const T rb = (s2[j1] * fabs(AB[i][j2]) + s2[j2] * fabs(AB[i][j1])) * inv;
       const T sep = fabs(tl) - ra - rb;
       if (sep > margin) return;
       if (T(1.05) * sep > best + T(1e-12)) {
-        best = sep; btype = 2; bi = i; bj = j;
-        for (int k = 0; k < 3; k++) bestn[k] = tl >= 0 ? L[k] : -L[k];
+        best = sep; btype = 2; bi = i; bj = j; btl = tl;
       }
     }
+  }
+  if (btype == 2) {
+    T L[3];
+    t_cross(L, A[bi], Bm[bj]);
+    const T len = PM<T>::sqrt_(t_dot3(L, L));
+    for (int k = 0; k < 3; k++) bestn[k] = btl >= 0 ? L[k] / len : -L[k] / len;
+  }
   if (btype == 0) { c_box_face(p1, R1, s1, bi, bestn, p2, R2, s2, bestn, margin, out); return; }
   if (btype == 1) {
     const T nr[3] = {-bestn[0], -bestn[1], -bestn[2]};
@@ -632,7 +648,7 @@ __device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A
 // axis is a few products of them -- all 15 evaluated branch-free (no per-axis early exit, so
 // the wave's lanes stay converged).  Face axes: |t_i| > h1_i + sum_j h2_j |R_ij| + margin (and
 // the same from B); edge axes A_i x B_j (skipped when parallel) compare the projections over
-// |A_i x B_j| = sqrt(1 - R_ij^2), the margin scaled by it as before.
+// |A_i x B_j| = sqrt(R_i1j^2 + R_i2j^2), the margin scaled by it as before.
 template <typename T>
 __device__ bool c_obb_disjoint(const T* p1, const T* R1, const T* h1, const T* p2, const T* R2, const T* h2, T margin) {
   T A[3][3], B[3][3], Tv[3];
@@ -666,7 +682,7 @@ __device__ bool c_obb_disjoint(const T* p1, const T* R1, const T* h1, const T* p
 #pragma unroll
     for (int j = 0; j < 3; j++) {
       const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
-      const T len2 = T(1) - R[i][j] * R[i][j];
+      const T len2 = R[i1][j] * R[i1][j] + R[i2][j] * R[i2][j];   // |A_i x B_j|^2, cancellation-free
       const T d = fabs(ta[i2] * R[i1][j] - ta[i1] * R[i2][j]);
       const T ra = h1[i1] * aR[i2][j] + h1[i2] * aR[i1][j];
       const T rb = h2[j1] * aR[i][j2] + h2[j2] * aR[i][j1];
