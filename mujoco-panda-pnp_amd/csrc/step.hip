@@ -1935,7 +1935,9 @@ __device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, C
       if (d1 > 0) hi = a; else lo = a;
       T an = a - d1 / d2;
       if (!(an > lo) || (hi >= T(0) && !(an < hi))) an = hi >= T(0) ? T(0.5) * (lo + hi) : T(2) * a;
-      const bool fin = an == a || (hi >= T(0) && hi - lo <= PM<T>::eps() * hi);
+      // converged once the Newton step is at the rounding level of a (waiting for an == a bit
+      // for bit cost extra rounds of last-bit oscillation), or the bracket has collapsed
+      const bool fin = fabs(an - a) <= T(4) * PM<T>::eps() * fabs(a) || (hi >= T(0) && hi - lo <= PM<T>::eps() * hi);
       a = an;
       if (fin) break;
     }
