@@ -439,7 +439,7 @@ static int32_t env_check(pnp_model* model, const void* st, const pnp_env_params*
 
 template <typename T, typename K>
 static int32_t env_prep(pnp_model* model, const pnp_state_t<T>* st, K kernel, const DevPhys<T>** dm, const char* fn,
-                        void* stream) {
+                        void* stream, ResidentLease& lease) {
   if (!st->qpos || !st->qvel || !st->ctrl || !st->mocap_pos || !st->mocap_quat || !st->qacc_warmstart || !st->time ||
       !st->warn) {
     pnp_set_error("%s: null state buffer", fn);
@@ -447,7 +447,7 @@ static int32_t env_prep(pnp_model* model, const pnp_state_t<T>* st, K kernel, co
   }
   *dm = phys_image<T>(model);
   if (!*dm) { pnp_set_error("%s: model has no physics image (%s)", fn, model->phys_err); return PNP_ERR_MODEL; }
-  if (const int32_t rc = phys_resident<T>(model, stream)) return rc;
+  if (const int32_t rc = phys_resident<T>(model, stream, lease)) return rc;
   (void)kernel;
   return PNP_OK;
 }
@@ -458,10 +458,12 @@ static int32_t launch_env_init(pnp_model* model, const pnp_state_t<T>* st, const
   int32_t rc = env_check(model, st, p, e, B, "pnp_env_init");
   if (rc || B == 0) return rc;
   const DevPhys<T>* dm;
+  ResidentLease lease;
   auto k = env_init_kernel<T>;
-  if ((rc = env_prep(model, st, k, &dm, "pnp_env_init", stream))) return rc;
+  if ((rc = env_prep(model, st, k, &dm, "pnp_env_init", stream, lease))) return rc;
   hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), B);
-  return pnp_check_launch("env_init_kernel");
+  if ((rc = pnp_check_launch("env_init_kernel"))) return rc;
+  return lease.launched();
 }
 template <typename T>
 static int32_t launch_env_reset(pnp_model* model, const pnp_state_t<T>* st, const pnp_env_params* p,
@@ -470,11 +472,13 @@ static int32_t launch_env_reset(pnp_model* model, const pnp_state_t<T>* st, cons
   int32_t rc = env_check(model, st, p, e, B, "pnp_env_reset");
   if (rc || B == 0) return rc;
   const DevPhys<T>* dm;
+  ResidentLease lease;
   auto k = env_reset_kernel<T>;
-  if ((rc = env_prep(model, st, k, &dm, "pnp_env_reset", stream))) return rc;
+  if ((rc = env_prep(model, st, k, &dm, "pnp_env_reset", stream, lease))) return rc;
   hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), mask,
                      out_view<T>(o), B);
-  return pnp_check_launch("env_reset_kernel");
+  if ((rc = pnp_check_launch("env_reset_kernel"))) return rc;
+  return lease.launched();
 }
 template <typename T>
 static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const pnp_env_params* p,
@@ -484,11 +488,13 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   if (rc || B == 0) return rc;
   if (!action) { pnp_set_error("pnp_env_step: null action"); return PNP_ERR_ARG; }
   const DevPhys<T>* dm;
+  ResidentLease lease;
   auto k = env_step_kernel<T>;
-  if ((rc = env_prep(model, st, k, &dm, "pnp_env_step", stream))) return rc;
+  if ((rc = env_prep(model, st, k, &dm, "pnp_env_step", stream, lease))) return rc;
   hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), action,
                      out_view<T>(o), B);
-  return pnp_check_launch("env_step_kernel");
+  if ((rc = pnp_check_launch("env_step_kernel"))) return rc;
+  return lease.launched();
 }
 
 extern "C" int32_t pnp_env_params_size(void) { return (int32_t)sizeof(pnp_env_params); }

@@ -140,7 +140,7 @@ extern "C" int32_t pnp_model_create(const pnp_model_desc* desc, pnp_model** out)
 
 extern "C" int32_t pnp_model_destroy(pnp_model* model) {
   if (!model) return PNP_OK;
-  phys_forget(model);
+  resident_forget(model);
   (void)hipFree(model->d_f32);
   (void)hipFree(model->d_f64);
   if (model->p_f32) (void)hipFree(model->p_f32);

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "../../include/pnp.h"
 
 #define PNP_MAXBODY 24
@@ -77,14 +79,32 @@ template <typename T> const DevPhys<T>* phys_image(const pnp_model* m);
 template <> inline const DevPhys<float>* phys_image<float>(const pnp_model* m) { return m->p_f32; }
 template <> inline const DevPhys<double>* phys_image<double>(const pnp_model* m) { return m->p_f64; }
 template <typename T> int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen);
-// step.hip: make the model's physics image the device's resident one (stream-ordered copy into
-// the constant segment when another model was resident); forget a destroyed model
-template <typename T> int32_t phys_resident(const pnp_model* model, void* stream);
-void phys_forget(const pnp_model* model);
+// resident.cpp: stream-ordered residency of a physics image in a device's constant segment.
+// acquire() makes `model`'s image the one the symbol holds for launches on `stream` (copying it
+// in, after every earlier reader of the old image, when another model was resident) and holds
+// the slot until launched() has recorded the launch that reads it; see the top of resident.cpp.
+enum ResidentImage { RES_FULL_F32 = 0, RES_FULL_F64, RES_COMPACT_F32, RES_NKIND };
+class ResidentLease {
+ public:
+  ResidentLease() = default;
+  ResidentLease(const ResidentLease&) = delete;
+  ResidentLease& operator=(const ResidentLease&) = delete;
+  ~ResidentLease();
+  int32_t acquire(ResidentImage kind, const pnp_model* model, const void* symbol, const void* src, size_t bytes,
+                  void* stream);
+  int32_t launched();  // call once the kernels reading the image are enqueued on the stream
+ private:
+  void release();
+  void* slot_ = nullptr;
+  void* stream_ = nullptr;
+  std::unique_lock<std::mutex> lock_;
+};
+void resident_forget(const pnp_model* model);
+// step.hip: acquire the model's full-build physics image for a launch on `stream`
+template <typename T> int32_t phys_resident(const pnp_model* model, void* stream, ResidentLease& lease);
 // step_compact.hip: the compact-capacity fp32 step kernel (see the top of step.hip)
 int32_t launch_step_compact(const pnp_model* model, const pnp_state_t<float>* st, int32_t B, int32_t nsub,
                             void* stream, unsigned long long* prof);
-void phys_forget_compact(const pnp_model* model);
 int32_t step_compact_lds_bytes();
 
 // ---------------------------------------------------------------------------- error plumbing

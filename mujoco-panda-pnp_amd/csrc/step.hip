@@ -40,8 +40,8 @@
 namespace PNP_NS {
 
 // The physics image lives in the device's constant segment, one resident image per precision
-// and device (phys_resident below copies a model's image in, stream-ordered, when a launch uses
-// another model than the last one).  Every stage reads it through phys<T>(), a known global
+// and device (ResidentLease, resident.cpp, copies a model's image in, stream-ordered, when a
+// launch uses another model than the last one).  Every stage reads it through phys<T>(), a known global
 // address: wave-uniform reads become scalar loads and per-lane reads global loads off a scalar
 // base, in out-of-line stage functions as well.  Passed down by reference instead, the image
 // reached the out-of-line stages as a generic pointer and every model read was a flat load that
@@ -1863,9 +1863,11 @@ __device__ void island_newton_dir_lds(Env<T>& s, int I, int n) {
 }
 
 // Exact minimiser of each island's convex piecewise quadratic phi_I(a) = cost_I(x + a p)
-// (semi-smooth Newton on phi', bracketed), island I on DPP row (I & 3): its rows are summed by
-// the row's 16 lanes and its bracket iterates independently of the other islands.  Islands with
-// isl_flag set (done) keep a = 0.  Leaves the step lengths in s.isl_alpha.
+// (semi-smooth Newton on phi', bracketed).  Island I runs on the 8-lane group I = lane >> 3: its
+// rows are summed by the group's lanes with rowsum8 (three DPP steps), so all 8 islands bracket
+// at once, each independently of the others.  An island stops once its Newton step is at the
+// rounding level of the step length (|a_new - a| <= 4 eps |a|) or its bracket has collapsed.
+// Islands with isl_flag set (done) keep a = 0.  Leaves the step lengths in s.isl_alpha.
 template <typename T, class CLK>
 __device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
@@ -2843,38 +2845,22 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) forwa
 using namespace PNP_NS;
 
 // ============================================================================ host launchers
-// Resident-image bookkeeping: the model whose image each device's constant segment holds (per
-// build: the compact build has its own constant-segment images).
-static std::atomic<const pnp_model*> g_resident[2][64];
-
+// The constant-segment images are made resident through ResidentLease (resident.cpp): stream-
+// ordered copies, readers on other streams ordered after the copy, model switches after the
+// readers of the old image.
 #if PNP_COMPACT
-int32_t phys_resident_compact(const pnp_model* model, void* stream) {
-  const DevPhys<float>* src = phys_image<float>(model);
-  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { pnp_set_error("phys_resident: bad device"); return PNP_ERR_HIP; }
-  std::atomic<const pnp_model*>& slot = g_resident[0][dev];
-  if (slot.load() == model) return PNP_OK;
-  const hipError_t e = hipMemcpyToSymbolAsync(g_phys_f32, src, sizeof(DevPhys<float>), 0, hipMemcpyDeviceToDevice, (hipStream_t)stream);
-  if (e != hipSuccess) { pnp_set_error("phys_resident: %s", hipGetErrorString(e)); return PNP_ERR_HIP; }
-  slot.store(model);
-  return PNP_OK;
-}
-
-void phys_forget_compact(const pnp_model* model) {
-  for (auto& row : g_resident)
-    for (auto& slot : row) {
-      const pnp_model* cur = model;
-      slot.compare_exchange_strong(cur, nullptr);
-    }
-}
-
 int32_t launch_step_compact(const pnp_model* model, const pnp_state_t<float>* st, int32_t B, int32_t nsub,
                             void* stream, unsigned long long* prof) {
-  if (const int32_t rc = phys_resident_compact(model, stream)) return rc;
+  const DevPhys<float>* src = phys_image<float>(model);
+  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  ResidentLease lease;
+  if (const int32_t rc = lease.acquire(RES_COMPACT_F32, model, (const void*)&g_phys_f32, src, sizeof(DevPhys<float>),
+                                       stream))
+    return rc;
   auto k = prof ? step_kernel<float, true> : step_kernel<float, false>;
-  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, phys_image<float>(model), *st, B, nsub, prof, 0);
-  return pnp_check_launch("step_kernel (compact)");
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, B, nsub, prof, 0);
+  if (const int32_t rc = pnp_check_launch("step_kernel (compact)")) return rc;
+  return lease.launched();
 }
 
 int32_t step_compact_lds_bytes() { return (int32_t)sizeof(Env<float>); }
@@ -2882,31 +2868,14 @@ int32_t step_compact_lds_bytes() { return (int32_t)sizeof(Env<float>); }
 #else
 
 template <typename T>
-int32_t phys_resident(const pnp_model* model, void* stream) {
+int32_t phys_resident(const pnp_model* model, void* stream, ResidentLease& lease) {
   const DevPhys<T>* src = phys_image<T>(model);
   if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { pnp_set_error("phys_resident: bad device"); return PNP_ERR_HIP; }
-  std::atomic<const pnp_model*>& slot = g_resident[sizeof(T) == 8][dev];
-  if (slot.load() == model) return PNP_OK;
   const void* sym = sizeof(T) == 8 ? (const void*)&g_phys_f64 : (const void*)&g_phys_f32;
-  const hipError_t e = hipMemcpyToSymbolAsync(sym, src, sizeof(DevPhys<T>), 0, hipMemcpyDeviceToDevice, (hipStream_t)stream);
-  if (e != hipSuccess) { pnp_set_error("phys_resident: %s", hipGetErrorString(e)); return PNP_ERR_HIP; }
-  slot.store(model);
-  return PNP_OK;
+  return lease.acquire(sizeof(T) == 8 ? RES_FULL_F64 : RES_FULL_F32, model, sym, src, sizeof(DevPhys<T>), stream);
 }
-template int32_t phys_resident<float>(const pnp_model*, void*);
-template int32_t phys_resident<double>(const pnp_model*, void*);
-
-// a destroyed model is no longer resident anywhere (a new model may reuse its address)
-void phys_forget(const pnp_model* model) {
-  for (auto& row : g_resident)
-    for (auto& slot : row) {
-      const pnp_model* cur = model;
-      slot.compare_exchange_strong(cur, nullptr);
-    }
-  phys_forget_compact(model);
-}
+template int32_t phys_resident<float>(const pnp_model*, void*, ResidentLease&);
+template int32_t phys_resident<double>(const pnp_model*, void*, ResidentLease&);
 
 // PNP_STEP_COMPACT: unset / 1 = compact kernel + resume pass (default), 0 = the full kernel alone
 // (A/B runs, equivalence tests), 2 = the compact kernel alone — diagnostic only: handed-over envs
@@ -2930,11 +2899,13 @@ static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B
   }
   const DevPhys<T>* dm = phys_image<T>(model);
   if (!dm) { pnp_set_error("pnp_step: model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
-  if (const int32_t rc = phys_resident<T>(model, stream)) return rc;
+  ResidentLease lease;
+  if (const int32_t rc = phys_resident<T>(model, stream, lease)) return rc;
   if (dbg) {
     auto k = forward_debug_kernel<T>;
     hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, dbg);
-    return pnp_check_launch("forward_debug_kernel");
+    if (const int32_t rc = pnp_check_launch("forward_debug_kernel")) return rc;
+    return lease.launched();
   }
   auto k = prof ? step_kernel<T, true> : step_kernel<T, false>;
   if (sizeof(T) == 4 && nsub <= PNP_RESUME_MAXSUB && compact_enabled()) {
@@ -2945,10 +2916,12 @@ static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B
       return rc;
     if (compact_mode() == 2) return PNP_OK;
     hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, nsub, prof, 1);
-    return pnp_check_launch("step_kernel (resume)");
+    if (const int32_t rc = pnp_check_launch("step_kernel (resume)")) return rc;
+    return lease.launched();
   }
   hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, nsub, prof, 0);
-  return pnp_check_launch("step_kernel");
+  if (const int32_t rc = pnp_check_launch("step_kernel")) return rc;
+  return lease.launched();
 }
 
 extern "C" int32_t pnp_step(pnp_model* model, const pnp_state* st, int32_t B, int32_t nsub, void* stream) {

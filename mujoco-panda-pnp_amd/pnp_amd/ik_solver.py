@@ -14,8 +14,25 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
-from .engine import get_engine
+from .engine import Engine, get_engine
 from .model import load_model
+
+
+_MODEL_ENGINES = {}
+
+
+def _engine_for(model, device):
+    """The engine whose device image is `model`: site ids and joint limits are looked up in the
+    model the caller passed, so the kinematics solved must be that model's too."""
+    eng = get_engine(device)
+    if model is eng.model:
+        return eng
+    key = (id(model), eng.device.type, eng.device.index)
+    hit = _MODEL_ENGINES.get(key)
+    if hit is None or hit[0] is not model:
+        hit = (model, Engine(model=model, device=eng.device))
+        _MODEL_ENGINES[key] = hit
+    return hit[1]
 
 
 @dataclass
@@ -47,7 +64,7 @@ class JacobianIKController:
         self.lower = np.asarray(self.model.jnt_range)[:7, 0].copy()
         self.upper = np.asarray(self.model.jnt_range)[:7, 1].copy()
         self.dtype = dtype
-        self.engine = get_engine(device)
+        self.engine = _engine_for(self.model, device)
 
     def solve(self, target_pos: np.ndarray, q_init: np.ndarray, max_iters: int = 100,
               pos_thresh: float = 1e-3, damping: float = 1e-2, step_limit: float = 0.1) -> IKResult:
@@ -69,8 +86,8 @@ class BatchedIK:
     """B independent solves per launch (device tensors in, device tensors out)."""
 
     def __init__(self, site_name: str = "ee_center_site", device=None, model=None):
-        self.engine = get_engine(device)
-        self.model = model or self.engine.model
+        self.engine = get_engine(device) if model is None else _engine_for(model, device)
+        self.model = self.engine.model
         self.site_id = self.model.site_id(site_name)
 
     def solve(self, target_pos: torch.Tensor, q_init: torch.Tensor, **params):

@@ -238,3 +238,25 @@ def test_dropin_controller_matches_golden(golden, model):
     assert r.iterations == golden["iterations"][i] and r.converged and r.success
     np.testing.assert_allclose(r.q, golden["q"][i], atol=1e-9)
     np.testing.assert_allclose(Data.qpos[:7], r.q)
+
+
+def test_controller_solves_on_the_model_it_was_given(golden, model, engine):
+    """JacobianIKController looks up the site and joint limits in the model it is given, so it must
+    also solve that model's kinematics: a model whose link1 sits 1 cm higher gets its own device
+    image (reference skills/ik_solver.py:27-33 reads everything from the model passed in)."""
+    from pnp_amd.ik_solver import JacobianIKController
+    from pnp_amd.model import PandaModel
+    m2 = PandaModel()
+    m2.body_pos = m2.body_pos.copy()
+    m2.body_pos[m2.body_id("link1"), 2] += 0.01
+    ctl = JacobianIKController(m2)
+    assert ctl.engine is not engine and ctl.engine.model is m2
+    assert JacobianIKController(model).engine is engine
+    i = list(golden["tag"]).index("ik_test")
+    r = ctl.solve(golden["target"][i], golden["q_init"][i], max_iters=100, pos_thresh=1e-4, damping=0.05)
+    qf = np.tile(m2.qpos0, (1, 1))
+    qf[0, :7] = r.q
+    sx, _ = ctl.engine.site_kinematics(torch.as_tensor(qf, dtype=torch.float64, device="cuda"), want_xmat=False)
+    np.testing.assert_allclose(sx[0, ctl.site_id].cpu().numpy(), r.final_pos, atol=1e-12)
+    sx0, _ = engine.site_kinematics(torch.as_tensor(qf, dtype=torch.float64, device="cuda"), want_xmat=False)
+    assert abs(float(sx[0, ctl.site_id, 2] - sx0[0, ctl.site_id, 2]) - 0.01) < 1e-9
