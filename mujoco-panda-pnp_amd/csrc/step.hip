@@ -77,6 +77,27 @@ struct Con {
 // base).  With a dynamic `extern __shared__` buffer instead, out-of-line stages reached the
 // buffer through the per-kernel dynamic-LDS offset table: an s_load + lgkmcnt(0) drain that
 // the compiler re-issued after every wave fence (once per no-slip pair update, for example).
+// Per-env LDS working set, budgeted by lifetime (the compact build must fit 8 envs per CU:
+// sizeof(Env<float>) <= 20 KB).  Stage order: kinematics -> comPos / CRB -> factor M ->
+// collision -> constraint rows -> velocity / RNE -> actuation -> Newton -> noslip -> Euler.
+//   * pos.*  : kinematics through RNE.  Frames, subtree COM, cdof and cinert persist through the
+//              velocity stage; the kinematics -> CRB scratch (inertial frames, joint axes, crb)
+//              is dead once M is built and makes room for the contact list (collision ->
+//              constraint rows); geom frames die with the collision stage, the contact list with
+//              the constraint rows, and the velocity stage's RNE vectors reuse both.
+//   * sol.*  : Newton and noslip (dense island Jacobian blocks + either the packed island
+//              Hessians and factors, or the noslip W = M^-1 J^T and pair lists).  The two
+//              members of the outer union never live at the same time: the solver starts once the
+//              rows and qacc_smooth exist.
+// (The full build keeps the generalised forces of the velocity / actuation stages and the row
+// positions outside the unions: its debug kernel dumps them after the whole forward.)
+#ifndef PH_HCAP
+#define PH_HCAP (PH_MAXV * (PH_MAXV + 1) / 2)   // packed island Hessian entries (sum over islands of n (n + 1) / 2)
+#endif
+#ifndef PH_MAXLIVE
+#define PH_MAXLIVE PH_MAXPAIR   // broadphase survivors (the full build: every candidate pair)
+#endif
+static_assert(PH_HCAP >= PH_MAXMBLK, "the Euler stage's generic damped-block scratch lives in the Hessian store");
 template <typename T>
 struct Env {
   // ---- small model tables read in every inner loop (copied from the global model image once
@@ -89,19 +110,31 @@ struct Env {
   int ncon, nefc, ne, nisland, solver_iter;
   int nlive, ncon_raw;     // collision: broadphase survivors, contacts before the capacity cap
   int nconvex;             // collision: live convex (MPR) pairs
-  // ---- position / velocity-stage working set (kinematics -> collision -> constraints -> RNE).
-  // Dead once the solver starts, so it shares storage with the Newton Hessian H and the no-slip
-  // W = M^-1 J^T (those two lifetimes do not overlap either).
   union {
     struct {
-      T xpos[PH_MAXB][3], xquat[PH_MAXB][4], xmat[PH_MAXB][9], xipos[PH_MAXB][3];
-      T xanchor[PH_MAXJ][3], xaxis[PH_MAXJ][3];
-      T gpos[PH_MAXG][3], gmat[PH_MAXG][9];
-      T subcom[PH_MAXB][3];
-      T cinert[PH_MAXB][10], crb[PH_MAXB][10], cdof[PH_MAXV][6], cvel[PH_MAXB][6], cdofdot[PH_MAXV][6];
-      T scr6[PH_MAXB > PH_MAXV ? PH_MAXB : PH_MAXV][6];   // per-body / per-dof 6-vector scratch
-      T scr6b[PH_MAXB][6];
-      Con<T> con[PH_MAXCON];
+      // kinematics -> velocity stage (and the gym epilogue's site frames / Jacobians)
+      T xpos[PH_MAXB][3], xquat[PH_MAXB][4], xmat[PH_MAXB][9];
+      T subcom[PH_MAXB][3], cdof[PH_MAXV][6], cinert[PH_MAXB][10];
+      union {
+        struct {
+          T gpos[PH_MAXG][3], gmat[PH_MAXG][9];   // kinematics -> collision
+          union {
+            struct {                              // kinematics -> CRB
+              T xipos[PH_MAXB][3], xanchor[PH_MAXJ][3], xaxis[PH_MAXJ][3];
+              T crb[PH_MAXB][10], scr6a[PH_MAXV][6];
+            };
+            Con<T> con[PH_MAXCON];                // collision -> constraint rows
+          };
+        };
+        struct {                                  // velocity stage -> actuation
+          T cvel[PH_MAXB][6], cdofdot[PH_MAXV][6];
+          T scr6[PH_MAXB > PH_MAXV ? PH_MAXB : PH_MAXV][6];   // per-body / per-dof 6-vector scratch
+          T scr6b[PH_MAXB][6];
+#if PNP_COMPACT
+          T qfrc_bias[PH_MAXV], qfrc_passive[PH_MAXV], qfrc_act[PH_MAXV];
+#endif
+        };
+      };
     };
     struct {
       // solver stages: the constraint Jacobian once more, as dense island blocks (rows of island I
@@ -110,8 +143,10 @@ struct Env {
       // contiguous rows with no per-row slot lookup.  Built by build_islands when it fits (jt_ok).
       T jt[PH_JTCAP];
       union {
-        struct {               // Newton: island Hessian blocks + per-row scratch
-          T H[PH_MAXV][PH_MAXV];
+        struct {               // Newton: packed island Hessian blocks + per-row scratch
+          // island I's block, lower triangle in island dof order: entry (a, b), a >= b, at
+          // isl_eoff[I] + a (a + 1) / 2 + b (HI below)
+          T Hp[PH_HCAP];
           T ntmp[PH_MAXEFC];
           T rr_f[PH_MAXEFC], rr_d[PH_MAXEFC];   // island row order: D jar, D (active rows; else 0)
           T NL[7][9][9];       // island Hessian factors of the group-parallel path (GCH_*), kept while isl_hvalid
@@ -128,7 +163,10 @@ struct Env {
   T M[PH_MAXMBLK];    // per-tree dense blocks
   T L[PH_MAXMBLK];    // Cholesky factors of the blocks
   // ---- vectors
-  T qfrc_bias[PH_MAXV], qfrc_passive[PH_MAXV], qfrc_act[PH_MAXV], qfrc_smooth[PH_MAXV];
+#if !PNP_COMPACT
+  T qfrc_bias[PH_MAXV], qfrc_passive[PH_MAXV], qfrc_act[PH_MAXV];
+#endif
+  T qfrc_smooth[PH_MAXV];
   T qacc_smooth[PH_MAXV], qacc[PH_MAXV], x[PH_MAXV], grad[PH_MAXV], p[PH_MAXV], v1[PH_MAXV], v2[PH_MAXV];
   // ---- constraints (sparse rows over <= 2 trees; t1 = -1 for single-tree rows)
   signed char efc_t0[PH_MAXEFC], efc_t1[PH_MAXEFC], efc_type[PH_MAXEFC];
@@ -140,12 +178,14 @@ struct Env {
       T cst_val[NT][7];        // dist, pos[3], normal[3]
       unsigned short cst_key[NT];   // producing lane * 16 + its contact number
       int cst_n;
-      short live[PH_MAXPAIR];  // broadphase survivors: every candidate pair fits
+      short live[PH_MAXLIVE];  // broadphase survivors
     };
   };
-  T efc_pos[PH_MAXEFC], efc_D[PH_MAXEFC], efc_aref[PH_MAXEFC], efc_bb[PH_MAXEFC];
+#if !PNP_COMPACT
+  T efc_pos[PH_MAXEFC];        // debug record only
+#endif
+  T efc_D[PH_MAXEFC], efc_aref[PH_MAXEFC], efc_bb[PH_MAXEFC];
   T efc_force[PH_MAXEFC], efc_jar[PH_MAXEFC], efc_Jp[PH_MAXEFC];
-  int lim_count[PH_MAXJ];
   int con_rbase[PH_MAXCON], con_sbase[PH_MAXCON], con_t[PH_MAXCON][2];
   unsigned char con_dim[PH_MAXCON];
   int tree_island[PH_MAXT], isl_n[PH_MAXT];
@@ -158,12 +198,15 @@ struct Env {
   T isl_cost[PH_MAXT], isl_val[PH_MAXT];   // per-island reductions (cost, |grad|^2 ...)
   int isl_flag[PH_MAXT];       // per-island: done (Newton), active set changed
   int isl_hvalid[PH_MAXT];     // per-island: H block is current for the island's active set
+#if !PNP_COMPACT
   T qpos_pre[PH_MAXQ];         // gym env: qpos of the last forward (pre-integration)
-  T red[8];
+#endif
   int ovf;                     // compact build: a capacity overflowed in this sub-step
 };
-static_assert(sizeof(((Env<float>*)0)->efc_Jv) >= 7 * 4 * NT + 2 * NT + 4 + 2 * PH_MAXPAIR,
+static_assert(sizeof(((Env<float>*)0)->efc_Jv) >= 7 * 4 * NT + 2 * NT + 4 + 2 * PH_MAXLIVE,
               "collision staging + broadphase survivors must fit the efc_Jv union");
+// island I's packed Hessian entry (a, b), a >= b (island dof positions)
+#define HI(I, a, b) s.Hp[s.isl_eoff[I] + (a) * ((a) + 1) / 2 + (b)]
 
 // capacity overflow.  Full build: MuJoCo's behaviour (a warning bit, the list truncated).
 // Compact build: flag the env; the stages return at the next check and the kernel hands the
@@ -180,9 +223,9 @@ static_assert(sizeof(((Env<float>*)0)->efc_Jv) >= 7 * 4 * NT + 2 * NT + 4 + 2 * 
 #define PNP_RESUME_SHIFT 16
 #define PNP_RESUME_MAXSUB 0xFFF
 #define PNP_RESUME_WHY_SHIFT 28
-#define PNP_OVF_CONTACTS 1   // > PH_MAXCON contacts
+#define PNP_OVF_CONTACTS 1   // collision: > PH_MAXCON contacts or > PH_MAXLIVE broadphase survivors
 #define PNP_OVF_ROWS 2       // > PH_MAXEFC rows or > PH_MAXJSLOT Jacobian slots
-#define PNP_OVF_JT 4         // dense island Jacobian blocks > PH_JTCAP
+#define PNP_OVF_JT 4         // dense island blocks: Jacobian > PH_JTCAP or Hessian > PH_HCAP
 
 // stage timer (diagnostic instantiation only: TIMED = true); cycles accumulate in prof[stage]
 // Sub-stage timers (sub_start / sub_lap) run inside a parent stage without resetting its lap;
@@ -722,14 +765,14 @@ __device__ void st_compos_crb(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s)
   if (l < m.nv) {
     T r[6];
     t_mulinertvec(r, s.crb[m.dof_bodyid[l]], s.cdof[l]);
-    for (int t = 0; t < 6; t++) s.scr6[l][t] = r[t];
+    for (int t = 0; t < 6; t++) s.scr6a[l][t] = r[t];
   }
   for (int i = l; i < m.nmblock; i += NT) s.M[i] = 0;
   wsync();
   for (int e = l; e < m.nmentry; e += NT) {
     const int i = m.mentry_i[e], j = m.mentry_j[e];
     T v = 0;
-    for (int t = 0; t < 6; t++) v += s.cdof[j][t] * s.scr6[i][t];
+    for (int t = 0; t < 6; t++) v += s.cdof[j][t] * s.scr6a[i][t];
     if (i == j) v += m.dof_armature[i];
     s.M[mblk(m, i, j)] = v;
     s.M[mblk(m, j, i)] = v;
@@ -989,10 +1032,16 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
       }
     }
     const uint64_t bal = __ballot(keep);
-    if (keep) s.live[nlive + __popcll(bal & ((1ull << l) - 1))] = (short)pi;
+    const int at = nlive + __popcll(bal & ((1ull << l) - 1));
+    if (keep && at < PH_MAXLIVE) s.live[at] = (short)pi;
     nlive += __popcll(bal);
   }
   wsync();
+  if (PNP_COMPACT && nlive > PH_MAXLIVE) {   // (the full build's list holds every candidate pair)
+    if (l == 0) { s.ovf |= PNP_OVF_CONTACTS; s.nlive = 0; s.ncon_raw = 0; s.nconvex = 0; s.ncon = 0; }
+    wsync();
+    return;
+  }
   clk.aux_lap(SC_AUX0 + 1);   // aux1: broadphase pass 2 (geom-pair spheres)
   clk.count(SC_AUX0 + 2, nlive);   // aux2: sphere survivors (count)
   // cheap exact pre-test over the sphere survivors (~180 per sub-step here: the shelf boards'
@@ -1181,7 +1230,9 @@ __device__ void row_imp(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, int r
     b = -solref[1] / dmax;
   }
   const T imp = impedance_(solimp, pos - margin);
+#if !PNP_COMPACT
   s.efc_pos[r] = pos;
+#endif
   s.efc_D[r] = T(1) / fmax(T(1e-15), (1 - imp) * diag / imp);
   s.efc_aref[r] = -k * imp * (pos - margin);
   s.efc_Jp[r] = b;
@@ -1731,7 +1782,9 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
     s.isl_eoff[nis] = etot;
     s.isl_joff[nis] = jtot;
     s.jt_ok = jtot <= PH_JTCAP;
-    if (PNP_COMPACT && !s.jt_ok) s.ovf |= PNP_OVF_JT;   // the full build's larger jt decides dense vs slot path
+    // the full build's larger jt decides dense vs slot path; its Hessian store fits every island
+    // partition of PH_MAXV dofs, the compact build's the common ones
+    if (PNP_COMPACT && (!s.jt_ok || etot > PH_HCAP)) s.ovf |= PNP_OVF_JT;
   }
   wsync();
   clk.aux_lap(SC_AUX0 + 3);   // aux3: islands (closure, dof lists, row lists)
@@ -1785,14 +1838,14 @@ __device__ void island_newton_dir_reg(Env<T>& s, int I, int n) {
   T sc[N];
 #pragma unroll
   for (int a = 0; a < N; a++) {
-    const T h = a < n ? s.H[id[a]][id[a]] : T(1);
+    const T h = a < n ? HI(I, a, a) : T(1);
     sc[a] = h > T(0) ? T(1) / PM<T>::sqrt_(h) : T(1);
   }
   T L[N * (N + 1) / 2];
 #pragma unroll
   for (int a = 0; a < N; a++)
 #pragma unroll
-    for (int b = 0; b <= a; b++) L[a * (a + 1) / 2 + b] = a < n ? s.H[id[a]][id[b]] * sc[a] * sc[b] : T(a == b);
+    for (int b = 0; b <= a; b++) L[a * (a + 1) / 2 + b] = a < n ? HI(I, a, b) * sc[a] * sc[b] : T(a == b);
 #pragma unroll
   for (int j = 0; j < N; j++) {
     T d = L[j * (j + 1) / 2 + j];
@@ -1829,35 +1882,33 @@ __device__ void island_newton_dir_reg(Env<T>& s, int I, int n) {
     if (i < n) s.p[id[i]] = -y[i] * sc[i];
 }
 
-// generic (merged islands of any size): in-place Cholesky through the dof list, LDS resident
+// generic (merged islands of any size): in-place Cholesky of the packed island block, LDS resident
 template <typename T>
 __device__ void island_newton_dir_lds(Env<T>& s, int I, int n) {
   const unsigned char* idx = s.isl_dof[I];
   for (int jj = 0; jj < n; jj++) {
-    const int j = idx[jj];
-    T sjj = s.H[j][j];
-    for (int kk = 0; kk < jj; kk++) sjj -= s.H[j][idx[kk]] * s.H[j][idx[kk]];
+    T sjj = HI(I, jj, jj);
+    for (int kk = 0; kk < jj; kk++) sjj -= HI(I, jj, kk) * HI(I, jj, kk);
     sjj = PM<T>::sqrt_(sjj > T(0) ? sjj : T(1e-30));
-    s.H[j][j] = sjj;
+    HI(I, jj, jj) = sjj;
     const T inv = T(1) / sjj;
     for (int ii = jj + 1; ii < n; ii++) {
-      const int i = idx[ii];
-      T t = s.H[i][j];
-      for (int kk = 0; kk < jj; kk++) t -= s.H[i][idx[kk]] * s.H[j][idx[kk]];
-      s.H[i][j] = t * inv;
+      T t = HI(I, ii, jj);
+      for (int kk = 0; kk < jj; kk++) t -= HI(I, ii, kk) * HI(I, jj, kk);
+      HI(I, ii, jj) = t * inv;
     }
   }
   for (int ii = 0; ii < n; ii++) {
     const int i = idx[ii];
     T v = s.grad[i];
-    for (int kk = 0; kk < ii; kk++) v -= s.H[i][idx[kk]] * s.p[idx[kk]];
-    s.p[i] = v / s.H[i][i];
+    for (int kk = 0; kk < ii; kk++) v -= HI(I, ii, kk) * s.p[idx[kk]];
+    s.p[i] = v / HI(I, ii, ii);
   }
   for (int ii = n - 1; ii >= 0; ii--) {
     const int i = idx[ii];
     T v = s.p[i];
-    for (int kk = ii + 1; kk < n; kk++) v -= s.H[idx[kk]][i] * s.p[idx[kk]];
-    s.p[i] = v / s.H[i][i];
+    for (int kk = ii + 1; kk < n; kk++) v -= HI(I, kk, ii) * s.p[idx[kk]];
+    s.p[i] = v / HI(I, ii, ii);
   }
   for (int ii = 0; ii < n; ii++) s.p[idx[ii]] = -s.p[idx[ii]];
 }
@@ -1967,8 +2018,11 @@ __device__ __attribute__((noinline)) void newton_dir_groups(Env<T>& s, bool done
   const int g = gch_group(l), r = l - GCH_N * g, base = GCH_N * g;
   const bool on = g < s.nisland && !s.isl_flag[g];
   const int n = on ? s.isl_n[g] : 0;
-  const int id = r < n ? s.isl_dof[g][r] : 0;
-  const T hd = s.H[id][id];
+  const int rc = r < n ? r : 0;
+  const int id = s.isl_dof[g][rc];
+  const int e0 = on ? s.isl_eoff[g] : 0;
+  const T* Hg = s.Hp + e0;   // the island's packed block (entry (a, b) at a (a + 1) / 2 + b)
+  const T hd = Hg[rc * (rc + 1) / 2 + rc];
   const T sc = r < n && hd > T(0) ? T(1) / PM<T>::sqrt_(hd) : T(1);
   T Lrow[GCH_N], Ad[GCH_N], scv[GCH_N], P[45], y[GCH_N];
 #pragma unroll
@@ -1980,9 +2034,10 @@ __device__ __attribute__((noinline)) void newton_dir_groups(Env<T>& s, bool done
 #pragma unroll
   for (int j = 0; j < GCH_N; j++) {
     scv[j] = __shfl(sc, base + j);
-    const int idj = s.isl_dof[g][j < n ? j : 0];
-    Lrow[j] = fac && r < n && j <= r ? s.H[id][idj] * sc * scv[j] : T(r == j);
-    Ad[j] = j < n ? s.H[idj][idj] * scv[j] * scv[j] : T(1);
+    const int jc = j < n ? j : 0;
+    const int idj = s.isl_dof[g][jc];
+    Lrow[j] = fac && r < n && j <= r ? Hg[rc * (rc + 1) / 2 + (j <= rc ? j : 0)] * sc * scv[j] : T(r == j);
+    Ad[j] = j < n ? Hg[jc * (jc + 1) / 2 + jc] * scv[j] * scv[j] : T(1);
     y[j] = j < n ? s.grad[idj] * scv[j] : T(0);
   }
   if (__ballot(fac)) gch_factor(Lrow, Ad, r, base, P);
@@ -2135,8 +2190,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
         const T c = s.efc_Jv[off + (ki >= 0 ? ki : 0)] * s.efc_D[r] * s.efc_Jv[off + (kj >= 0 ? kj : 0)];
         h = ki >= 0 && kj >= 0 && s.efc_act[r] ? h + c : h;
       }
-      s.H[i][j] = h;
-      s.H[j][i] = h;
+      s.Hp[e] = h;   // = HI(I, a, b)
     }
     wsync();
     clk.sub_lap(SC_N_HESS);
@@ -2599,7 +2653,7 @@ __device__ void st_euler(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
       chol_reg<T, 9>(s.M + o, n, m.dof_damping + a, h, L);
       chol_solve_reg<T, 9>(L, n, s.v2 + a, s.v1 + a);
     } else {
-      T* A = s.H[0];   // scratch: n x n
+      T* A = s.Hp;   // scratch (dead solver storage): the tree blocks' layout, nmblock <= PH_HCAP
       for (int i = 0; i < n; i++)
         for (int j = 0; j < n; j++) A[o + i * n + j] = s.M[o + i * n + j] + (i == j ? h * m.dof_damping[a + i] : T(0));
       chol_block(A + o, A + o, n, n);
