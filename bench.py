@@ -12,8 +12,9 @@ Inputs: the reference's reset distribution (Philox, seed 20250808, counter = glo
 rank r owns envs [r*B, (r+1)*B)), settled by 250 untimed sub-steps like _env_setup.
 
 --workload ik = configs[1] "C2": one batched JacobianIKController.solve over 4096 envs per step.
-The step workload also times C2 briefly ("ik") and the fused gym step of C5's env side ("gym":
-FrankaEnv.step = set_action + 250 sub-steps + obs / reward, one launch).
+The step workload also times C2 briefly ("ik"), the fused gym step of C5's env side ("gym":
+FrankaEnv.step = set_action + 250 sub-steps + obs / reward, one launch) and C5's whole TQC loop
+("tqc": 8192 envs per GPU, a gym step + a gradient step per step, pnp_amd/tqc.py).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload step|ik]
     torchrun --nproc-per-node N bench.py --gpus N ...    (one process per GPU)
@@ -194,6 +195,8 @@ def run_step(args, engine, model, rank, world, dist):
     }
     if not args.no_gym:
         rec["gym"] = run_gym(engine, B, rank, world, dist)
+    if not args.no_tqc:
+        rec["tqc"] = run_tqc(engine, args.tqc_envs, rank, world, dist)
     if not args.no_ik:
         ik = run_ik(args, engine, model, rank, world, dist, steps=50, warmup=5, baseline=False)
         rec["ik"] = {k: ik[k] for k in ("value", "unit", "ms_per_step")}
@@ -217,6 +220,37 @@ def run_gym(engine, B, rank, world, dist, steps=3, warmup=1):
     return {"gym_steps_per_s": B * world * steps / elapsed, "env_steps_per_s": B * world * steps * sub / elapsed,
             "ms_per_gym_step": elapsed / steps * 1e3, "kernel_avg_ms": kern_ms, "sub_steps_per_gym_step": sub,
             "kernel": "env_step_kernel<float>", "workload": f"{B} FrankaShelfPNPDense envs per GPU, random actions"}
+
+
+# ----------------------------------------------------------------------------- C5 TQC training loop
+def run_tqc(engine, B, rank, world, dist, steps=3, warmup=2, learner_reps=20):
+    """C5: scripts/train.py's TQC loop over B batched envs per GPU (pnp_amd.tqc, train.py
+    hyper-parameters): one step = one fused gym step of every env (policy actions, auto-reset,
+    replay insert, obs statistics) + one gradient step (batch 512; gradients all-reduced over
+    ranks when N > 1).  Also times the gradient step alone."""
+    from pnp_amd.envs import BatchedFrankaShelfPNPEnv
+    from pnp_amd.tqc import TQC, TQCConfig
+    env = BatchedFrankaShelfPNPEnv(B, engine=engine, env_offset=rank * B)
+    agent = TQC(env, TQCConfig())
+    agent.total_timesteps = 2_000_000
+    agent.reset()
+
+    def fn(i):
+        agent.collect_step()
+        agent.train()
+
+    elapsed, kern_ms = _timed(fn, steps, warmup, dist)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(learner_reps):
+        agent.train()
+    torch.cuda.synchronize()
+    learner_ms = (time.perf_counter() - t0) / learner_reps * 1e3
+    sub = env.cfg.n_substeps * env.cfg.n_calls
+    return {"gym_steps_per_s": B * world * steps / elapsed, "env_steps_per_s": B * world * steps * sub / elapsed,
+            "ms_per_step": elapsed / steps * 1e3, "learner_ms_per_update": learner_ms,
+            "workload": f"C5: TQC (train.py hyper-parameters) on {B} FrankaShelfPNPDense envs per GPU, "
+                        f"one gym step + one gradient step per step"}
 
 
 # ----------------------------------------------------------------------------- C2 IK
@@ -303,6 +337,8 @@ def main():
     ap.add_argument("--params", default="default", choices=sorted(workloads.IK_PARAMS))
     ap.add_argument("--no-ik", action="store_true", help="step workload: skip the secondary C2 timing")
     ap.add_argument("--no-gym", action="store_true", help="step workload: skip the secondary fused gym-step timing")
+    ap.add_argument("--no-tqc", action="store_true", help="step workload: skip the secondary C5 TQC-loop timing")
+    ap.add_argument("--tqc-envs", type=int, default=8192, help="C5 envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()

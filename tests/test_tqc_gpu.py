@@ -1,0 +1,73 @@
+"""C5 on the device: the TQC learner (pnp_amd/tqc.py, reference scripts/train.py) driving the fused
+gym env (libpnp.so pnp_env_step through pnp_amd.envs).
+
+* reward / success parity vs the CPU reference env: the learner's own rollout (its actions, its
+  auto-reset handling, its replay rows) is replayed through the env oracle (oracle/env_oracle.py:
+  the reference's FrankaEnv logic over the fp64 physics oracle) on the short-physics configuration
+  of tests/test_env_gpu.py (inside the scene's divergence horizon): rewards and observations within
+  1e-9 (fp64 env), success / termination flags identical, replay rows = the env's outputs.
+* the full C5 configuration (fp32, 250 sub-steps per gym step): rollout + gradient steps stay
+  finite, and the replay buffer holds exactly what the env returned.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.env_oracle import EnvConfig as OCfg, EnvOracle
+
+pytestmark = pytest.mark.gpu
+
+SHORT = dict(n_substeps=2, n_calls=2)
+
+
+def test_learner_rollout_matches_oracle_env(model):
+    from pnp_amd.envs import BatchedFrankaShelfPNPEnv, EnvConfig
+    from pnp_amd.tqc import TQC, TQCConfig, flat_obs
+    B = 4
+    env = BatchedFrankaShelfPNPEnv(B, dtype=torch.float64, config=EnvConfig(**SHORT))
+    o = EnvOracle(B, cfg=OCfg(**SHORT), model=model)
+    agent = TQC(env, TQCConfig(net_arch=(64, 64), batch_size=8, learning_starts=8, buffer_size=B * 16))
+    agent.total_timesteps = 10 ** 6
+    agent.reset()
+    ref = o.reset()
+    ref_flat = np.stack([np.concatenate([ref[b]["achieved_goal"], ref[b]["desired_goal"], ref[b]["observation"]])
+                         for b in range(B)])
+    np.testing.assert_allclose(flat_obs(agent._last_raw).double().cpu().numpy(), ref_flat, atol=1e-6)
+    for k in range(8):
+        reward, done, info = agent.collect_step()
+        act = agent.buffer.actions[k].double().cpu().numpy()      # what the learner sent
+        res = o.step(act)
+        for b in range(B):
+            assert abs(float(reward[b]) - res[b]["reward"]) < 1e-9
+            assert float(info["is_success"][b]) == res[b]["is_success"]
+            assert bool(done[b]) == (res[b]["terminated"] or res[b]["truncated"])
+            want = np.concatenate([res[b]["obs"]["achieved_goal"], res[b]["obs"]["desired_goal"],
+                                   res[b]["obs"]["observation"]])
+            np.testing.assert_allclose(agent.buffer.next_obs[k, b].double().cpu().numpy(), want, atol=1e-6)
+            assert float(agent.buffer.rewards[k, b]) == pytest.approx(res[b]["reward"], abs=1e-6)
+            assert float(agent.buffer.dones[k, b]) == float(res[b]["terminated"])
+        if agent.num_timesteps > agent.cfg.learning_starts:
+            logs = agent.train()
+            assert all(math.isfinite(v) for v in logs.values())
+
+
+def test_c5_full_physics_learner_steps():
+    from pnp_amd.envs import BatchedFrankaShelfPNPEnv
+    from pnp_amd.tqc import TQC, TQCConfig, flat_obs
+    B = 256
+    env = BatchedFrankaShelfPNPEnv(B)
+    agent = TQC(env, TQCConfig(learning_starts=0))
+    agent.total_timesteps = 10 ** 6
+    agent.reset()
+    for k in range(3):
+        reward, done, info = agent.collect_step()
+        assert torch.equal(agent.buffer.rewards[k], reward)
+        assert torch.equal(agent.buffer.next_obs[k][~done], flat_obs(env._obs())[~done])
+        logs = agent.train()
+        assert all(math.isfinite(v) for v in logs.values()), logs
+    assert bool(torch.isfinite(agent.buffer.next_obs[:3]).all())
+    assert int((env.state["warn"] & 7).max()) == 0          # no bad-state resets
+    for p in list(agent.actor.parameters()) + list(agent.critic.parameters()):
+        assert bool(torch.isfinite(p).all())

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 cd /tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/${TAG}_$c" -o run -- \
-    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-gym --no-ik > "$OUT/${TAG}_$c.log" 2>&1
+    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-gym --no-ik --no-tqc > "$OUT/${TAG}_$c.log" 2>&1
   rc=$?; echo "$c rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 cd "$ROOT"

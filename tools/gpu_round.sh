@@ -23,9 +23,10 @@ for s in $STEPS; do
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
-    prof)  cd /tmp && run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline; cd "$ROOT" ;;
-    pmc)   cd /tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline && \
-           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline; cd "$ROOT" ;;
+    tqc)   run pytest_tqc 300 python -u -m pytest tests/test_tqc_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    prof)  cd /tmp && run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --no-tqc; cd "$ROOT" ;;
+    pmc)   cd /tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-tqc && \
+           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-tqc; cd "$ROOT" ;;
   esac
 done
 echo "all steps done"
