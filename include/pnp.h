@@ -218,17 +218,21 @@ typedef struct pnp_state_f64 {
 #define PNP_WARN_BADQACC 4u
 #define PNP_WARN_CONTACTFULL 8u
 #define PNP_WARN_CNSTRFULL 16u
-/* bits 16..31 are reserved: inside one fp32 pnp_step call they carry the compact
- * kernel's hand-over to the full kernel (flag + sub-step); they are clear when a call returns
- * and are ignored on input */
+/* bits 16..31 are reserved: inside one fp32 pnp_step / pnp_env_step call they carry a
+ * capacity tier's hand-over to the next tier (flag + sub-step); they are clear when a call
+ * returns and are ignored on input */
 
 /* nsub x mj_step on every env, in place (reference envs/panda_env.py:355-358 calls this with
  * nsub = 25, ten times; skills/base.py:43 and scripts/execute_pnp.py:103 with nsub = 1).
  * ctrl and mocap are held constant over the nsub sub-steps, as in the reference.
- * fp32: a compact-capacity kernel (6 envs per CU) runs first and hands any env whose sub-step
- * would overflow its capacities to the full-capacity kernel from that sub-step; results equal
- * the full kernel's bit for bit.  Environment variable PNP_STEP_COMPACT=0 runs the full kernel
- * alone (2: the compact kernel alone, a test diagnostic that leaves handed-over envs mid-call). */
+ * fp32: three capacity tiers of one kernel source -- compact (20 contacts, 8 envs per CU), full
+ * (48 contacts, 4 per CU), wide (96 contacts, 2 per CU).  Each runs the envs the previous tier
+ * handed over, from the sub-step that would have overflowed its capacities, so results equal the
+ * wide kernel's bit for bit; only the wide tier truncates (PNP_WARN_CONTACTFULL / CNSTRFULL).
+ * fp64 (debugging instantiation): the full kernel alone, truncating at 48 contacts.
+ * Environment variables (A/B runs and tests): PNP_STEP_COMPACT=0 starts at the full tier,
+ * 3 runs the wide kernel alone, 2 the compact kernel alone (a test diagnostic that leaves
+ * handed-over envs mid-call); PNP_STEP_WIDE=0 drops the wide tier (the full kernel truncates). */
 int32_t pnp_step(pnp_model* model, const pnp_state* state, int32_t B, int32_t nsub, void* stream);
 int32_t pnp_step_f64(pnp_model* model, const pnp_state_f64* state, int32_t B, int32_t nsub, void* stream);
 
@@ -351,7 +355,9 @@ int32_t pnp_env_reset(pnp_model* model, const pnp_state* state, const pnp_env_pa
 int32_t pnp_env_reset_f64(pnp_model* model, const pnp_state_f64* state, const pnp_env_params* params,
                           const pnp_env_state* env, const uint8_t* mask, const pnp_env_out* out, int32_t B,
                           void* stream);
-/* action[B*7] (same dtype as the state), clipped to [-1, 1] like the action space. */
+/* action[B*7] (same dtype as the state), clipped to [-1, 1] like the action space.
+ * fp32: the full-capacity kernel runs the gym step; an env whose physics sub-step outgrows it is
+ * finished (remaining sub-steps + observation / reward) by the wide tier's resume pass. */
 int32_t pnp_env_step(pnp_model* model, const pnp_state* state, const pnp_env_params* params,
                      const pnp_env_state* env, const float* action, const pnp_env_out* out, int32_t B,
                      void* stream);

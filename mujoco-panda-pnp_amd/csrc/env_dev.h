@@ -11,6 +11,10 @@
 // are restated from their published definitions (third-party, absent here).
 #pragma once
 
+// Device code in the tier's namespace (step.hip PNP_NS): the full and the wide build both compile
+// these kernels, with different Env layouts, so they must not share symbol names.
+namespace PNP_NS {
+
 #define PNP_RESET_STREAM 0x40000000u   // Philox stream word of the reset draws: | episode
 
 // ---------------------------------------------------------------- Philox4x32-10 (pnp_amd/rng.py)
@@ -293,10 +297,14 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_r
 }
 
 // ---------------------------------------------------------------- step (FrankaEnv.step)
+// Tiers (step.hip): the full build runs the whole gym step; with hand = 1 a physics sub-step that
+// would overflow its capacity stops the env before that sub-step changes the state (controls and
+// state stored, resume bits in warn, no epilogue), and the wide build's resume pass (resume = 1)
+// finishes the physics from that sub-step and runs the epilogue.
 template <typename T>
 __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
                                                       pnp_env_params prm, EnvSoA<T> es, const T* __restrict__ action,
-                                                      EnvOutT<T> out, int B) {
+                                                      EnvOutT<T> out, int B, int resume, int hand) {
   __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
   Env<T>& s = s_env;
   const DevPhys<T>& m = phys<T>();
@@ -304,10 +312,17 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
   const int b = blockIdx.x;
   if (b >= B) return;
   const int l = lane_id();
-  load_env(m, s, st, b);
+  int k0 = 0;
+  if (resume) {
+    const uint32_t w = st.warn[b];
+    if (!(w & PNP_RESUME_FLAG)) return;
+    k0 = (int)((w >> PNP_RESUME_SHIFT) & PNP_RESUME_MAXSUB);
+  }
+  load_env(m, s, st, b, hand);
+  T ee_p[3], ee_R[9], ee_q[4];
+  if (!resume) {
   // ---- _set_action: ee pose from the last forward's site frame
   kin_at(m, s, es.qpos_kin + (size_t)b * m.nq, false);
-  T ee_p[3], ee_R[9], ee_q[4];
   site_frame(m, s, prm.ee_site, ee_p, ee_R);
   g_mat2quat(ee_R, ee_q);
   if (l == 0) {
@@ -331,10 +346,20 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
     for (int t = 0; t < 4; t++) s.mocap_quat[t] = tq[t];
   }
   wsync();
+  }
   // ---- _mujoco_step: n_calls x mj_step(nstep = n_substeps)
   NoClock clk;
   const int nsub = prm.n_substeps * prm.n_calls;
-  for (int k = 0; k < nsub; k++) mj_step_dev(m, s, clk, k == nsub - 1 ? s.qpos_pre : nullptr);
+  int k = k0;
+  for (; k < nsub && !(PNP_HANDS && s.ovf); k++) mj_step_dev(m, s, clk, k == nsub - 1 ? s.qpos_pre : nullptr);
+  if (PNP_HANDS && s.ovf) {   // sub-step k - 1 overflowed before changing the state: hand over
+    if (l == 0)
+      s.warn |= PNP_RESUME_FLAG | ((uint32_t)s.ovf << PNP_RESUME_WHY_SHIFT) | ((uint32_t)(k - 1) << PNP_RESUME_SHIFT);
+    wsync();
+    store_env(m, s, st, b);
+    store_controls(m, s, st, b);
+    return;
+  }
   store_env(m, s, st, b);
   store_controls(m, s, st, b);
   const T width = s.qpos[prm.finger_qadr[0]] + s.qpos[prm.finger_qadr[1]];
@@ -401,6 +426,8 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
   }
 }
 
+}  // namespace PNP_NS
+
 // ---------------------------------------------------------------- host launchers
 template <typename T>
 static EnvSoA<T> env_view(const pnp_env_state* e) {
@@ -414,6 +441,24 @@ static EnvOutT<T> out_view(const pnp_env_out* o) {
                     o->terminated, o->truncated};
 }
 
+#if PNP_WIDE
+// wide tier: resume pass of the gym step over the envs the full kernel handed over (launched by
+// the full build's launch_env_step, which holds the full image's lease)
+int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
+                             const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
+                             void* stream) {
+  const DevPhys<float>* src = phys_image<float>(model);
+  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  ResidentLease lease;
+  if (const int32_t rc = lease.acquire(RES_WIDE_F32, model, (const void*)&g_phys_f32, src, sizeof(DevPhys<float>),
+                                       stream))
+    return rc;
+  hipLaunchKernelGGL(env_step_kernel<float>, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, *p,
+                     env_view<float>(e), action, out_view<float>(o), B, 1, 0);
+  if (const int32_t rc = pnp_check_launch("env_step_kernel (wide resume)")) return rc;
+  return lease.launched();
+}
+#else
 static int32_t env_check(pnp_model* model, const void* st, const pnp_env_params* p, const pnp_env_state* e,
                          int32_t B, const char* fn) {
   if (!model || !st || !p || !e || B < 0) { pnp_set_error("%s: bad argument", fn); return PNP_ERR_ARG; }
@@ -491,9 +536,14 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   ResidentLease lease;
   auto k = env_step_kernel<T>;
   if ((rc = env_prep(model, st, k, &dm, "pnp_env_step", stream, lease))) return rc;
+  // fp32: the wide tier finishes the envs whose physics outgrew the full kernel's capacities
+  const int wide = sizeof(T) == 4 && wide_enabled() && p->n_substeps * p->n_calls <= PNP_RESUME_MAXSUB;
   hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), action,
-                     out_view<T>(o), B);
+                     out_view<T>(o), B, 0, wide);
   if ((rc = pnp_check_launch("env_step_kernel"))) return rc;
+  if (wide && (rc = launch_env_step_wide(model, reinterpret_cast<const pnp_state_t<float>*>(st), p, e,
+                                         reinterpret_cast<const float*>(action), o, B, stream)))
+    return rc;
   return lease.launched();
 }
 
@@ -527,3 +577,4 @@ extern "C" int32_t pnp_env_step_f64(pnp_model* model, const pnp_state_f64* st, c
                                     void* stream) {
   return launch_env_step<double>(model, reinterpret_cast<const pnp_state_t<double>*>(st), p, e, action, o, B, stream);
 }
+#endif  // PNP_WIDE

@@ -83,7 +83,7 @@ template <typename T> int build_phys(const pnp_model_desc* s, DevPhys<T>* d, cha
 // acquire() makes `model`'s image the one the symbol holds for launches on `stream` (copying it
 // in, after every earlier reader of the old image, when another model was resident) and holds
 // the slot until launched() has recorded the launch that reads it; see the top of resident.cpp.
-enum ResidentImage { RES_FULL_F32 = 0, RES_FULL_F64, RES_COMPACT_F32, RES_NKIND };
+enum ResidentImage { RES_FULL_F32 = 0, RES_FULL_F64, RES_COMPACT_F32, RES_WIDE_F32, RES_NKIND };
 class ResidentLease {
  public:
   ResidentLease() = default;
@@ -106,6 +106,13 @@ template <typename T> int32_t phys_resident(const pnp_model* model, void* stream
 int32_t launch_step_compact(const pnp_model* model, const pnp_state_t<float>* st, int32_t B, int32_t nsub,
                             void* stream, unsigned long long* prof);
 int32_t step_compact_lds_bytes();
+// step_wide.hip: the wide-capacity fp32 tier (resume passes of pnp_step and pnp_env_step)
+int32_t launch_step_wide(const pnp_model* model, const pnp_state_t<float>* st, int32_t B, int32_t nsub,
+                         void* stream, unsigned long long* prof, int resume);
+int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
+                             const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
+                             void* stream);
+int32_t step_wide_lds_bytes();
 
 // ---------------------------------------------------------------------------- error plumbing
 void pnp_set_error(const char* fmt, ...);

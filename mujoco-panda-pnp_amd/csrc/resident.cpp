@@ -11,8 +11,8 @@
 //     on another stream never sees its image overwritten;
 //   * the slot mutex is held from the residency check until the launch has been enqueued and its
 //     use recorded (ResidentLease), so two host threads cannot interleave check, copy and launch.
-// Lock order: a launch that holds two leases (pnp_step: full image, then compact image) always
-// takes them in the order of ResidentImage.
+// Lock order: a launch that holds two leases (pnp_step: the full image, then the compact or the
+// wide image, one at a time) always takes them in the order of ResidentImage.
 #include <hip/hip_runtime.h>
 
 #include <mutex>

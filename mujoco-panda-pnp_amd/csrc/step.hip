@@ -23,20 +23,34 @@
 #include "phys_model.h"
 #include "pnp_internal.h"
 
-// Two builds of this file.  step.hip itself: the full-capacity kernels (namespace pnp_full) and
-// the C ABI.  step_compact.hip: the same device code with smaller contact / row / Jacobian
-// capacities (namespace pnp_compact, fp32 step kernel only), so that the per-env LDS working set
-// fits 6 envs per CU instead of 4.  A compact sub-step that would overflow a compact capacity is
-// abandoned before it changes the state and re-run from that sub-step by the full kernel (resume
-// protocol: PNP_RESUME_* below), so results are those of the full kernel, bit for bit.
+// Three builds of this file, three capacity tiers of the same device code (fp32):
+//   step_compact.hip  pnp_compact  20 contacts / 96 rows: 20 KB of LDS per env, 8 envs per CU
+//   step.hip          pnp_full     48 contacts / 208 rows: 38 KB, 4 envs per CU; also the fp64
+//                                  debugging instantiation, the debug kernels and the C ABI
+//   step_wide.hip     pnp_wide     96 contacts / 400 rows: 2 envs per CU
+// A sub-step that would overflow a tier's capacity is abandoned before it changes the state and
+// re-run from that sub-step by the next tier's resume pass (protocol: PNP_RESUME_* below), so an
+// fp32 result is that of the widest tier, bit for bit, whichever tier finished each sub-step.  The
+// widest tier, and the full tier when it runs alone (fp64, diagnostics), truncate like MuJoCo at a
+// full buffer (warning bits CONTACTFULL / CNSTRFULL).  Closed fingers pressed together make 50-100
+// contacts (box-box pad pairs, mesh-pad pairs), so the gym workload needs the wide tier.
 #ifndef PNP_COMPACT
 #define PNP_COMPACT 0
 #endif
+#ifndef PNP_WIDE
+#define PNP_WIDE 0
+#endif
 #if PNP_COMPACT
 #define PNP_NS pnp_compact
+#elif PNP_WIDE
+#define PNP_NS pnp_wide
 #else
 #define PNP_NS pnp_full
 #endif
+// PNP_HANDS: this build can hand an overflowing sub-step to the next tier (the full build only
+// when its kernel is launched with hand = 1); PNP_LEAN: no debug-only fields outside the unions
+#define PNP_HANDS (!PNP_WIDE)
+#define PNP_LEAN (PNP_COMPACT || PNP_WIDE)
 namespace PNP_NS {
 
 // The physics image lives in the device's constant segment, one resident image per precision
@@ -130,7 +144,7 @@ struct Env {
           T cvel[PH_MAXB][6], cdofdot[PH_MAXV][6];
           T scr6[PH_MAXB > PH_MAXV ? PH_MAXB : PH_MAXV][6];   // per-body / per-dof 6-vector scratch
           T scr6b[PH_MAXB][6];
-#if PNP_COMPACT
+#if PNP_LEAN
           T qfrc_bias[PH_MAXV], qfrc_passive[PH_MAXV], qfrc_act[PH_MAXV];
 #endif
         };
@@ -163,7 +177,7 @@ struct Env {
   T M[PH_MAXMBLK];    // per-tree dense blocks
   T L[PH_MAXMBLK];    // Cholesky factors of the blocks
   // ---- vectors
-#if !PNP_COMPACT
+#if !PNP_LEAN
   T qfrc_bias[PH_MAXV], qfrc_passive[PH_MAXV], qfrc_act[PH_MAXV];
 #endif
   T qfrc_smooth[PH_MAXV];
@@ -181,7 +195,7 @@ struct Env {
       short live[PH_MAXLIVE];  // broadphase survivors
     };
   };
-#if !PNP_COMPACT
+#if !PNP_LEAN
   T efc_pos[PH_MAXEFC];        // debug record only
 #endif
   T efc_D[PH_MAXEFC], efc_aref[PH_MAXEFC], efc_bb[PH_MAXEFC];
@@ -201,22 +215,27 @@ struct Env {
 #if !PNP_COMPACT
   T qpos_pre[PH_MAXQ];         // gym env: qpos of the last forward (pre-integration)
 #endif
-  int ovf;                     // compact build: a capacity overflowed in this sub-step
+  int ovf;                     // a capacity overflowed in this sub-step (hand-over builds)
+  int hand;                    // full build: overflows hand over (1) or truncate with a warning (0)
 };
 static_assert(sizeof(((Env<float>*)0)->efc_Jv) >= 7 * 4 * NT + 2 * NT + 4 + 2 * PH_MAXLIVE,
               "collision staging + broadphase survivors must fit the efc_Jv union");
 // island I's packed Hessian entry (a, b), a >= b (island dof positions)
 #define HI(I, a, b) s.Hp[s.isl_eoff[I] + (a) * ((a) + 1) / 2 + (b)]
 
-// capacity overflow.  Full build: MuJoCo's behaviour (a warning bit, the list truncated).
-// Compact build: flag the env; the stages return at the next check and the kernel hands the
-// sub-step to the full kernel (mj_step_dev, step_kernel).
+// capacity overflow.  Wide build (and the full build launched with hand = 0): MuJoCo's behaviour
+// (a warning bit, the list truncated).  Compact build (and full with hand = 1): flag the env; the
+// stages return at the next check and the kernel hands the sub-step to the next tier
+// (mj_step_dev, step_kernel).
 #if PNP_COMPACT
 #define CAP_FULL(bit) (s.ovf |= (bit) == 8u ? PNP_OVF_CONTACTS : PNP_OVF_ROWS)
-#else
+#elif PNP_WIDE
 #define CAP_FULL(bit) (s.warn |= (bit))
+#else
+#define CAP_FULL(bit) \
+  (s.hand ? (void)(s.ovf |= (bit) == 8u ? PNP_OVF_CONTACTS : PNP_OVF_ROWS) : (void)(s.warn |= (bit)))
 #endif
-// resume protocol between the compact kernel and the full kernel's resume pass: the env's warn
+// resume protocol between a tier's kernel and the next tier's resume pass: the env's warn
 // word carries the flag (bit 31), the capacity that overflowed (bits 28..30, diagnostic) and the
 // sub-step to resume from (bits 16..27); the warning bits are 0..4
 #define PNP_RESUME_FLAG 0x80000000u
@@ -1230,7 +1249,7 @@ __device__ void row_imp(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, int r
     b = -solref[1] / dmax;
   }
   const T imp = impedance_(solimp, pos - margin);
-#if !PNP_COMPACT
+#if !PNP_LEAN
   s.efc_pos[r] = pos;
 #endif
   s.efc_D[r] = T(1) / fmax(T(1e-15), (1 - imp) * diag / imp);
@@ -1368,35 +1387,41 @@ __device__ void st_constraints(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s
   nrow += nlim;
   nslot += nlslot;
   wsync();
-  // ---- contacts: per-contact row/slot bases by scan, then lanes over (contact, slot)
+  // ---- contacts: per-contact row/slot bases by scan (64 contacts per pass), then lanes over
+  // (contact, slot)
   const int nc = s.ncon;
-  int my_rows = 0, my_slots = 0, t0c = -1, t1c = -1;
-  if (l < nc) {
-    const Con<T>& con = s.con[l];
-    body_trees(m, m.geom_bodyid[con.g1], m.geom_bodyid[con.g2], t0c, t1c);
-    my_rows = 2 * (con.dim - 1);
-    my_slots = my_rows * row_width(m, t0c, t1c);
-  }
-  int trows, tslots;
-  const int rbase = nrow + wscan(my_rows, &trows);
-  const int sbase = nslot + wscan(my_slots, &tslots);
-  const bool fits = l < nc && rbase + my_rows <= PH_MAXEFC && sbase + my_slots <= PH_MAXJSLOT;
-  if (l < nc) {
-    s.con_rbase[l] = fits ? rbase : -1;
-    s.con_sbase[l] = sbase;
-    s.con_t[l][0] = t0c;
-    s.con_t[l][1] = t1c;
-    s.con_dim[l] = (unsigned char)s.con[l].dim;
-  }
-  if (__ballot(l < nc && !fits) && l == 0) CAP_FULL(16u);
-  wsync();
   int kept_rows = nrow;
-  {
+  bool spill = false;
+  for (int cb = 0, rb = nrow, sb = nslot; cb < nc; cb += NT) {
+    const int c = cb + l;
+    int my_rows = 0, my_slots = 0, t0c = -1, t1c = -1;
+    if (c < nc) {
+      const Con<T>& con = s.con[c];
+      body_trees(m, m.geom_bodyid[con.g1], m.geom_bodyid[con.g2], t0c, t1c);
+      my_rows = 2 * (con.dim - 1);
+      my_slots = my_rows * row_width(m, t0c, t1c);
+    }
+    int trows, tslots;
+    const int rbase = rb + wscan(my_rows, &trows);
+    const int sbase = sb + wscan(my_slots, &tslots);
+    const bool fits = c < nc && rbase + my_rows <= PH_MAXEFC && sbase + my_slots <= PH_MAXJSLOT;
+    if (c < nc) {
+      s.con_rbase[c] = fits ? rbase : -1;
+      s.con_sbase[c] = sbase;
+      s.con_t[c][0] = t0c;
+      s.con_t[c][1] = t1c;
+      s.con_dim[c] = (unsigned char)s.con[c].dim;
+    }
+    spill |= __ballot(c < nc && !fits) != 0;
     // last contact that fits bounds the row count (contacts are added in order)
-    int lastrow = (l < nc && fits) ? rbase + my_rows : 0;
+    int lastrow = (c < nc && fits) ? rbase + my_rows : 0;
     for (int o = 32; o > 0; o >>= 1) lastrow = max(lastrow, __shfl_xor(lastrow, o));
-    kept_rows = max(nrow, lastrow);
+    kept_rows = max(kept_rows, lastrow);
+    rb += trows;
+    sb += tslots;
   }
+  if (spill && l == 0) CAP_FULL(16u);
+  wsync();
   // jacobian slots
   for (int base = 0; base < nc * PH_ROWW; base += NT) {
     const int idx = base + l;
@@ -1662,9 +1687,11 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   uint64_t e = 0;
-  if (l < s.ncon && s.con_rbase[l] >= 0 && s.con_t[l][1] >= 0) {
-    const int a = s.con_t[l][0], b = s.con_t[l][1];
-    e = (1ull << (8 * a + b)) | (1ull << (8 * b + a));
+  for (int c = l; c < s.ncon; c += NT) {
+    if (s.con_rbase[c] >= 0 && s.con_t[c][1] >= 0) {
+      const int a = s.con_t[c][0], b = s.con_t[c][1];
+      e |= (1ull << (8 * a + b)) | (1ull << (8 * b + a));
+    }
   }
   for (int r = l; r < s.ne; r += NT) {
     const int a = s.efc_t0[r], b = s.efc_t1[r];
@@ -1782,9 +1809,10 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
     s.isl_eoff[nis] = etot;
     s.isl_joff[nis] = jtot;
     s.jt_ok = jtot <= PH_JTCAP;
-    // the full build's larger jt decides dense vs slot path; its Hessian store fits every island
-    // partition of PH_MAXV dofs, the compact build's the common ones
-    if (PNP_COMPACT && (!s.jt_ok || etot > PH_HCAP)) s.ovf |= PNP_OVF_JT;
+    // the widest tier's jt decides dense vs slot path (a tier that can hand over does so when its
+    // jt is too small); the full / wide Hessian stores fit every island partition of PH_MAXV
+    // dofs, the compact build's the common ones
+    if ((PNP_COMPACT || (PNP_HANDS && s.hand)) && (!s.jt_ok || etot > PH_HCAP)) s.ovf |= PNP_OVF_JT;
   }
   wsync();
   clk.aux_lap(SC_AUX0 + 3);   // aux3: islands (closure, dof lists, row lists)
@@ -2070,7 +2098,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   }
   clk.aux_start();
   build_islands(m, s, clk);
-  if (PNP_COMPACT && s.ovf) return;
+  if (PNP_HANDS && s.ovf) return;
   // warm start per island: the better of qacc_warmstart and qacc_smooth (MuJoCo chooses for the
   // whole problem; per island the minimiser is the same and the start is better).  One pass:
   // cost(qacc_smooth) has no dof term and its jar is efc_bb (= J qacc_smooth - aref, same
@@ -2721,14 +2749,14 @@ __device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& 
   clk.count(SN_CON, s.ncon);
   clk.count(SN_CONVEX, s.nconvex);
   clk.count(SN_LIVE, s.nlive);
-  if (PNP_COMPACT && s.ovf) return;
+  if (PNP_HANDS && s.ovf) return;
   if (dbg) dump_contacts(m, s, dbg);
   st_constraints(m, s);     clk.lap(5);
-  if (PNP_COMPACT && s.ovf) return;
+  if (PNP_HANDS && s.ovf) return;
   st_velocity(m, s);        clk.lap(6);
   st_actuation_smooth(m, s); clk.lap(7);
   st_newton(m, s, clk);     // laps 8..12 inside
-  if (PNP_COMPACT && s.ovf) return;
+  if (PNP_HANDS && s.ovf) return;
   clk.count(SN_EFC, s.nefc);
   clk.count(SN_ITER, s.solver_iter);
   clk.count(SN_ISLAND, s.nefc ? s.nisland : 0);
@@ -2766,7 +2794,7 @@ __device__ void mj_step_dev(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, C
   check_state(m, s);
   clk.lap(0);
   forward(m, s, clk);
-  if (PNP_COMPACT && s.ovf) return;   // state unchanged so far (check_state's reset is idempotent)
+  if (PNP_HANDS && s.ovf) return;   // state unchanged so far (check_state's reset is idempotent)
   const int l = lane_id();
   const uint64_t bad = __ballot(l < m.nv && is_bad(s.qacc[l]));
   if (bad) {
@@ -2774,7 +2802,7 @@ __device__ void mj_step_dev(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, C
     wsync();
     reset_state(m, s);
     forward(m, s, clk);
-    if (PNP_COMPACT && s.ovf) return;
+    if (PNP_HANDS && s.ovf) return;
   }
   if (save_qpos) {
     if (l < m.nq) save_qpos[l] = s.qpos[l];
@@ -2785,7 +2813,8 @@ __device__ void mj_step_dev(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, C
 }
 
 template <typename T>
-__device__ void load_env(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, const pnp_state_t<T>& st, int b) {
+__device__ void load_env(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, const pnp_state_t<T>& st, int b,
+                         int hand = 0) {
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (l < PH_MAXT) {
@@ -2799,7 +2828,7 @@ __device__ void load_env(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, cons
   if (l < m.nu) s.ctrl[l] = st.ctrl[(size_t)b * m.nu + l];
   if (l < 3 * m.nmocap) s.mocap_pos[l] = st.mocap_pos[(size_t)b * 3 * m.nmocap + l];
   if (l < 4 * m.nmocap) s.mocap_quat[l] = st.mocap_quat[(size_t)b * 4 * m.nmocap + l];
-  if (l == 0) { s.time = st.time[b]; s.warn = st.warn[b] & 0xFFFFu; s.ovf = 0; }
+  if (l == 0) { s.time = st.time[b]; s.warn = st.warn[b] & 0xFFFFu; s.ovf = 0; s.hand = hand; }
   wsync();
 }
 
@@ -2819,21 +2848,22 @@ __device__ void store_env(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& 
 #endif
 template <typename T, bool TIMED>
 __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st, int B, int nsub,
-                                                 unsigned long long* __restrict__ prof, int resume) {
+                                                 unsigned long long* __restrict__ prof, int resume, int hand) {
   __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
   Env<T>& s = s_env;
   const DevPhys<T>& m = phys<T>();
   (void)mp;
   const int b = blockIdx.x;
   if (b >= B) return;
-  // full kernel, resume pass: only the envs the compact kernel handed over, from their sub-step
+  // resume pass: only the envs the previous tier handed over, from their sub-step; hand (full
+  // build): hand overflowing sub-steps to the wide tier instead of truncating
   int k0 = 0;
   if (!PNP_COMPACT && resume) {
     const uint32_t w = st.warn[b];
     if (!(w & PNP_RESUME_FLAG)) return;
     k0 = (int)((w >> PNP_RESUME_SHIFT) & PNP_RESUME_MAXSUB);
   }
-  load_env(m, s, st, b);
+  load_env(m, s, st, b, hand);
   int k = k0;
   if constexpr (TIMED) {
     StageClock clk{prof + (size_t)b * PNP_NSTAGE, 0, 0};
@@ -2842,8 +2872,8 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) step_
     NoClock clk;
     for (; k < nsub && !s.ovf; k++) mj_step_dev(m, s, clk);
   }
-  // compact kernel: sub-step k - 1 overflowed a capacity before changing the state
-  if (PNP_COMPACT && s.ovf && lane_id() == 0)
+  // hand-over: sub-step k - 1 overflowed a capacity before changing the state
+  if (PNP_HANDS && s.ovf && lane_id() == 0)
     s.warn |= PNP_RESUME_FLAG | ((uint32_t)s.ovf << PNP_RESUME_WHY_SHIFT) | ((uint32_t)(k - 1) << PNP_RESUME_SHIFT);
   wsync();
   store_env(m, s, st, b);
@@ -2912,12 +2942,33 @@ int32_t launch_step_compact(const pnp_model* model, const pnp_state_t<float>* st
                                        stream))
     return rc;
   auto k = prof ? step_kernel<float, true> : step_kernel<float, false>;
-  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, B, nsub, prof, 0);
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, B, nsub, prof, 0, 1);
   if (const int32_t rc = pnp_check_launch("step_kernel (compact)")) return rc;
   return lease.launched();
 }
 
 int32_t step_compact_lds_bytes() { return (int32_t)sizeof(Env<float>); }
+
+#elif PNP_WIDE
+// wide tier: the resume pass after the full kernel (resume = 1), or every env from sub-step 0
+// (resume = 0: diagnostic PNP_STEP_COMPACT=3)
+int32_t launch_step_wide(const pnp_model* model, const pnp_state_t<float>* st, int32_t B, int32_t nsub,
+                         void* stream, unsigned long long* prof, int resume) {
+  const DevPhys<float>* src = phys_image<float>(model);
+  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  ResidentLease lease;
+  if (const int32_t rc = lease.acquire(RES_WIDE_F32, model, (const void*)&g_phys_f32, src, sizeof(DevPhys<float>),
+                                       stream))
+    return rc;
+  auto k = prof ? step_kernel<float, true> : step_kernel<float, false>;
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, B, nsub, prof, resume, 0);
+  if (const int32_t rc = pnp_check_launch("step_kernel (wide)")) return rc;
+  return lease.launched();
+}
+
+int32_t step_wide_lds_bytes() { return (int32_t)sizeof(Env<float>); }
+
+#include "env_dev.h"   // the gym step's wide resume pass
 
 #else
 
@@ -2931,15 +2982,21 @@ int32_t phys_resident(const pnp_model* model, void* stream, ResidentLease& lease
 template int32_t phys_resident<float>(const pnp_model*, void*, ResidentLease&);
 template int32_t phys_resident<double>(const pnp_model*, void*, ResidentLease&);
 
-// PNP_STEP_COMPACT: unset / 1 = compact kernel + resume pass (default), 0 = the full kernel alone
-// (A/B runs, equivalence tests), 2 = the compact kernel alone — diagnostic only: handed-over envs
-// are left at their hand-over sub-step with the resume bits set in warn, so that tests can see
-// where hand-overs happen
+// PNP_STEP_COMPACT: unset / 1 = compact kernel + resume passes (default), 0 = the full kernel
+// first (A/B runs, equivalence tests), 2 = the compact kernel alone — diagnostic only: handed-over
+// envs are left at their hand-over sub-step with the resume bits set in warn, so that tests can
+// see where hand-overs happen; 3 = the wide kernel alone (equivalence tests)
 static int compact_mode() {
   const char* e = getenv("PNP_STEP_COMPACT");
-  return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
+  return e && (e[0] == '0' || e[0] == '2' || e[0] == '3') ? e[0] - '0' : 1;
 }
-static bool compact_enabled() { return compact_mode() != 0; }
+static bool compact_enabled() { return compact_mode() == 1 || compact_mode() == 2; }
+// PNP_STEP_WIDE: unset / 1 = fp32 sub-steps that outgrow the full kernel's capacities are finished
+// by the wide tier (default), 0 = the full kernel truncates them with a warning (A/B runs)
+static bool wide_enabled() {
+  const char* e = getenv("PNP_STEP_WIDE");
+  return !(e && e[0] == '0');
+}
 
 template <typename T>
 static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B, int32_t nsub, void* stream,
@@ -2962,19 +3019,27 @@ static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B
     return lease.launched();
   }
   auto k = prof ? step_kernel<T, true> : step_kernel<T, false>;
-  if (sizeof(T) == 4 && nsub <= PNP_RESUME_MAXSUB && compact_enabled()) {
-    // compact kernel over every env, then the full kernel resumes the envs it handed over (an
-    // env not handed over costs the resume pass one load of its warn word)
-    if (const int32_t rc = launch_step_compact(model, reinterpret_cast<const pnp_state_t<float>*>(st), B, nsub,
-                                               stream, prof))
-      return rc;
-    if (compact_mode() == 2) return PNP_OK;
-    hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, nsub, prof, 1);
-    if (const int32_t rc = pnp_check_launch("step_kernel (resume)")) return rc;
+  const bool tiers = sizeof(T) == 4 && nsub <= PNP_RESUME_MAXSUB;   // the resume bits hold the sub-step
+  const int wide = tiers && wide_enabled();
+  const auto* st32 = reinterpret_cast<const pnp_state_t<float>*>(st);
+  if (tiers && compact_mode() == 3) {
+    if (const int32_t rc = launch_step_wide(model, st32, B, nsub, stream, prof, 0)) return rc;
     return lease.launched();
   }
-  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, nsub, prof, 0);
-  if (const int32_t rc = pnp_check_launch("step_kernel")) return rc;
+  if (tiers && compact_enabled()) {
+    // compact kernel over every env, then the full kernel resumes the envs it handed over (an
+    // env not handed over costs the resume pass one load of its warn word), then the wide kernel
+    // the envs the full kernel handed over
+    if (const int32_t rc = launch_step_compact(model, st32, B, nsub, stream, prof)) return rc;
+    if (compact_mode() == 2) return lease.launched();
+    hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, nsub, prof, 1, wide);
+    if (const int32_t rc = pnp_check_launch("step_kernel (resume)")) return rc;
+  } else {
+    hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, nsub, prof, 0, wide);
+    if (const int32_t rc = pnp_check_launch("step_kernel")) return rc;
+  }
+  if (wide)
+    if (const int32_t rc = launch_step_wide(model, st32, B, nsub, stream, prof, 1)) return rc;
   return lease.launched();
 }
 

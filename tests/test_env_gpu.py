@@ -113,6 +113,30 @@ def test_env_logic_short_physics_f32(model):
     _compare_steps(g, o, 3, 1e-4)
 
 
+def test_gym_step_wide_tier_pressed_fingers(model):
+    """Gym steps from closed fingers pressed into each other (52-61 contacts: the wide tier
+    finishes those sub-steps, env_dev.h), fp32 short physics against the oracle env: observations
+    and rewards within 1e-3, flags identical, no truncation warning."""
+    g = _env(torch.float32, **SHORT)
+    o = EnvOracle(B, cfg=OCfg(**SHORT), model=model)
+    g.reset()
+    o.reset()
+    g.state["qpos"][:, 7:9] = -torch.linspace(0.001, 0.004, B, dtype=torch.float32, device="cuda")[:, None]
+    _sync_oracle(g, o)
+    o.st["warn"][:] = 0
+    for k in range(3):
+        a = _actions(B, 40 + k)
+        a[:, 6] = -1.0                       # keep closing
+        obs, r, term, trunc, info = g.step(torch.as_tensor(a, dtype=torch.float32))
+        res = o.step(a)
+        for b in range(B):
+            np.testing.assert_allclose(obs["observation"][b].double().cpu().numpy(), res[b]["obs"]["observation"],
+                                       atol=1e-3)
+            np.testing.assert_allclose(float(r[b]), res[b]["reward"], atol=1e-3)
+            assert float(info["is_success"][b]) == res[b]["is_success"]
+    assert int((g.state["warn"] & 0xFFFF).max()) == 0 and not o.st["warn"].any()
+
+
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_full_gym_step_bounded(model, dtype):
     g = _env(dtype)

@@ -310,7 +310,7 @@ def _step_f32(engine, st, nsub, compact):
 
 
 def test_compact_kernel_hand_over_is_exact(engine, model, scene, mesh_scene):
-    """The fp32 step runs the compact-capacity kernel (20 contacts, 6 envs per CU) and hands any
+    """The fp32 step runs the compact-capacity kernel (20 contacts, 8 envs per CU) and hands any
     env whose sub-step would overflow it to the full kernel from that sub-step (step.hip, resume
     protocol).  Results must be the full kernel's, bit for bit — on envs that stay within the
     compact capacities and on mesh-contact envs that exceed them (up to 40 contacts), with the
@@ -380,6 +380,67 @@ def _run_mode(engine, g, nsub, mode):
 
 def _step_f32_mode(engine, st, nsub, mode):
     return _run_mode(engine, _dev(st, torch.float32), nsub, mode)
+
+
+@pytest.fixture(scope="module")
+def pressed(model):
+    """Closed fingers pressed into each other (pad boxes interpenetrating 1-4 mm, finger servos
+    closing): 52-61 contacts, more than the full tier's 48 -- the closed-gripper states of the
+    random-action gym workload (tools/contact_census.py, tools/gym_profile.py)."""
+    n = 12
+    st = PS.reset_states(n, seed=11, model=model)
+    st["qpos"][:, 7:9] = -np.linspace(0.001, 0.004, n)[:, None]
+    st["ctrl"][:, -2:] = 0.0
+    st["qvel"] += np.random.default_rng(5).normal(size=st["qvel"].shape) * 0.02
+    return st
+
+
+def _run_env(engine, g, nsub, **env):
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        engine.step(g, nsub)
+        torch.cuda.synchronize()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    return g
+
+
+def test_wide_tier_matches_oracle(engine, model, pressed):
+    """Sub-steps with more contacts than the full kernel holds are finished by the wide tier (96
+    contacts): one fp32 step matches the fp64 oracle (which holds 96 too) with no truncation
+    warning; the full kernel alone (PNP_STEP_WIDE=0) truncates at 48 and says so."""
+    n = pressed["qpos"].shape[0]
+    nc = [int(_oracle_fields(pressed, b, model)["ncon"][0]) for b in range(n)]
+    assert min(nc) > 48 and max(nc) <= 96, nc
+    ref = PS.copy_state(pressed)
+    O.step(ref, nsub=1, nthreads=8, model=model)
+    g = _host(_run_env(engine, _dev(pressed, torch.float32), 1, PNP_STEP_COMPACT="1", PNP_STEP_WIDE="1"))
+    assert not (g["warn"] & 0xFFFF).any() and not (ref["warn"]).any()
+    dq = np.abs(g["qpos"] - ref["qpos"]).max()
+    assert dq < 1e-4, dq
+    trunc = _host(_run_env(engine, _dev(pressed, torch.float32), 1, PNP_STEP_COMPACT="1", PNP_STEP_WIDE="0"))
+    assert ((trunc["warn"] & 8) != 0).all()
+
+
+def test_wide_tier_hand_over_is_exact(engine, model, scene, mesh_scene, pressed):
+    """compact -> full -> wide (default), full -> wide (PNP_STEP_COMPACT=0) and the wide kernel
+    alone (3) give the same bits on a batch that mixes envs within the compact capacities, envs
+    between 20 and 48 contacts and envs beyond 48; no resume bit leaks into warn."""
+    st = {k: np.concatenate([scene[k], mesh_scene[k], pressed[k]]) for k in scene}
+    for nsub in (1, 6):
+        a = _run_env(engine, _dev(st, torch.float32), nsub, PNP_STEP_COMPACT="1")
+        b = _run_env(engine, _dev(st, torch.float32), nsub, PNP_STEP_COMPACT="0")
+        c = _run_env(engine, _dev(st, torch.float32), nsub, PNP_STEP_COMPACT="3")
+        for k in a:
+            assert torch.equal(a[k], b[k]), (nsub, k, "full-first")
+            assert torch.equal(a[k], c[k]), (nsub, k, "wide alone")
+        assert not _high_warn_bits(a)
 
 
 def test_mesh_contacts_f32(engine, model, mesh_scene):
