@@ -248,6 +248,177 @@ __global__ void __launch_bounds__(64) ik_dls_kernel(IKSeg<T> c, int max_iters, T
                        ((converged && err < thr * T(2)) ? PNP_IK_SUCCESS : 0u));
 }
 
+// ---------------------------------------------------------------------------- 8-lane groups
+// ik_dls_group_kernel: one solve per 8-lane group (8 solves per wave), lane j < 7 owns joint j.
+// The thread-per-solve kernel above is latency-bound: a batch of 4096 solves is 64 waves on
+// 64 CUs, and the launch lasts as long as the slowest solve (up to max_iters iterations), each
+// iteration one long dependent chain (7 joint rotations composed in order, then the Jacobian, the
+// 3 x 3 solve and the update).  Here every iteration is shallow:
+//   * lane j forms its joint's local transform A_j = [Rpre_j Rz(q_j) | ppre_j] (its own sincos);
+//     lane 7 carries the site offset [I | psite];
+//   * the world frames G_j = A_0 ... A_j are an inclusive prefix product over the group
+//     (Hillis-Steele, 3 DPP row_shr steps); lane 7 ends up holding the site position;
+//   * anchor_j = p(G_j), axis_j = sgn_j R(G_j) e_z (Rz leaves both unchanged, as in ik_fk);
+//   * J J^T is 6 three-step DPP sums over the group (J column j on lane j), the 3 x 3 solve runs
+//     redundantly on every lane, and dq_j = J_j^T y is lane-local.
+// The reference's control flow is kept per group (convergence test before the update, the final
+// position measured after the last update); groups that have stopped are predicated off.  Same
+// formulas as the serial kernel; the frame products associate differently (prefix tree instead
+// of the left-to-right chain), so results agree to rounding (fp64: ~1e-16 relative).
+template <int CTRL, typename T>
+__device__ __forceinline__ T gdpp(T v) {
+  if constexpr (sizeof(T) == 4) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+  } else {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffff), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+  }
+}
+// sum over the 8-lane group, identical bits in every lane
+template <typename T>
+__device__ __forceinline__ T gsum8(T v) {
+  v += gdpp<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += gdpp<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += gdpp<0x141>(v);   // row_half_mirror: the other quad of the group
+  return v;
+}
+// lane 7 of the group to every lane of the group (DPP row_newbcast of lanes 7 and 15 of the row)
+template <typename T>
+__device__ __forceinline__ T gbcast7(T v, bool upper) {
+  const T a = gdpp<0x157>(v), b = gdpp<0x15F>(v);
+  return upper ? b : a;
+}
+// one Hillis-Steele step: G_j <- G_{j-O} G_j for j >= O (row_shr:O inside the row of 16).  A
+// lane j < O composes with the identity instead (1 x + 0 y + 0 z + 0 is x exactly for finite
+// values), so every lane runs the same straight-line code; the value it would receive comes from
+// the neighbouring group and is replaced.
+template <int O, typename T>
+__device__ __forceinline__ void gscan_step(T R[9], T p[3], int j) {
+  const bool take = j >= O;
+  T X[9], xp[3];
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    const T v = gdpp<0x110 + O>(R[k]);
+    X[k] = take ? v : T(k == 0 || k == 4 || k == 8 ? 1 : 0);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const T v = gdpp<0x110 + O>(p[k]);
+    xp[k] = take ? v : T(0);
+  }
+  T N[9], np[3];
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+#pragma unroll
+    for (int c = 0; c < 3; c++) N[3 * r + c] = X[3 * r] * R[c] + X[3 * r + 1] * R[3 + c] + X[3 * r + 2] * R[6 + c];
+    np[r] = X[3 * r] * p[0] + X[3 * r + 1] * p[1] + X[3 * r + 2] * p[2] + xp[r];
+  }
+#pragma unroll
+  for (int k = 0; k < 9; k++) R[k] = N[k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) p[k] = np[k];
+}
+
+// frames of the group at its joint angles: lane j -> (anchor_j, axis_j); every lane -> site
+template <typename T>
+__device__ __forceinline__ void gfk(const T Rp[9], const T pp[3], T sg, T q0, T qj, bool joint, bool upper, int j,
+                                    T anchor[3], T axis[3], T site[3]) {
+  T s, c;
+  KMath<T>::sincos(qj - q0, &s, &c);   // lane 7: sincos(0), and sg = 0
+  s *= sg;
+  (void)joint;
+  T R[9], p[3] = {pp[0], pp[1], pp[2]};
+#pragma unroll
+  for (int r = 0; r < 3; r++) {     // Rpre_j Rz(q_j): rotate columns 0 and 1
+    R[3 * r + 0] = Rp[3 * r + 0] * c + Rp[3 * r + 1] * s;
+    R[3 * r + 1] = Rp[3 * r + 1] * c - Rp[3 * r + 0] * s;
+    R[3 * r + 2] = Rp[3 * r + 2];
+  }
+  gscan_step<1>(R, p, j);
+  gscan_step<2>(R, p, j);
+  gscan_step<4>(R, p, j);
+  anchor[0] = p[0]; anchor[1] = p[1]; anchor[2] = p[2];
+  axis[0] = sg * R[2]; axis[1] = sg * R[5]; axis[2] = sg * R[8];
+#pragma unroll
+  for (int k = 0; k < 3; k++) site[k] = gbcast7(p[k], upper);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(64) ik_dls_group_kernel(IKSeg<T> c, int max_iters, T thr, T damping, T step,
+                                                          const T* __restrict__ q_init, const T* __restrict__ target,
+                                                          T* __restrict__ q_out, T* __restrict__ final_pos,
+                                                          T* __restrict__ pos_error, int32_t* __restrict__ iterations,
+                                                          uint8_t* __restrict__ flags, int B) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = t >> 3, j = t & 7;
+  const bool valid = b < B;          // (a partial group past B runs along, predicated off)
+  const bool joint = j < 7;
+  const bool upper = (threadIdx.x & 8) != 0;
+  // this lane's joint constants (lane 7: the site offset, no rotation)
+  T Rp[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, pp[3] = {c.psite[0], c.psite[1], c.psite[2]};
+  T sg = 0, lo = 0, hi = 0, q0 = 0;
+#pragma unroll
+  for (int jj = 0; jj < 7; jj++) {
+    if (j == jj) {
+#pragma unroll
+      for (int k = 0; k < 9; k++) Rp[k] = c.Rpre[jj][k];
+#pragma unroll
+      for (int k = 0; k < 3; k++) pp[k] = c.ppre[jj][k];
+      sg = c.sgn[jj]; lo = c.lo[jj]; hi = c.hi[jj]; q0 = c.qpos0[jj];
+    }
+  }
+  T q = (valid && joint) ? q_init[(size_t)b * 7 + j] : T(0);
+  T tg[3] = {0, 0, 0};
+  if (valid) { tg[0] = target[(size_t)b * 3]; tg[1] = target[(size_t)b * 3 + 1]; tg[2] = target[(size_t)b * 3 + 2]; }
+  T anchor[3], axis[3], site[3];
+  gfk(Rp, pp, sg, q0, q, joint, upper, j, anchor, axis, site);
+  bool active = valid;
+  int converged = 0, iters = 0;
+  for (int i = 0; i < max_iters; i++) {
+    const T e0 = tg[0] - site[0], e1 = tg[1] - site[1], e2 = tg[2] - site[2];
+    const T n = KMath<T>::sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+    if (active && n < thr) {
+      converged = 1;
+      iters = i + 1;
+      active = false;
+    }
+    if (!__ballot(active)) break;
+    // jacp column j: axis_j x (site - anchor_j)
+    const T r0 = site[0] - anchor[0], r1 = site[1] - anchor[1], r2 = site[2] - anchor[2];
+    const T J0 = joint ? axis[1] * r2 - axis[2] * r1 : T(0);
+    const T J1 = joint ? axis[2] * r0 - axis[0] * r2 : T(0);
+    const T J2 = joint ? axis[0] * r1 - axis[1] * r0 : T(0);
+    T A[9];
+    A[0] = gsum8(J0 * J0) + damping;
+    A[1] = A[3] = gsum8(J0 * J1);
+    A[2] = A[6] = gsum8(J0 * J2);
+    A[4] = gsum8(J1 * J1) + damping;
+    A[5] = A[7] = gsum8(J1 * J2);
+    A[8] = gsum8(J2 * J2) + damping;
+    T y[3] = {e0, e1, e2};
+    solve3(A, y);
+    T dq = J0 * y[0] + J1 * y[1] + J2 * y[2];
+    dq = fmin(fmax(dq, -step), step);
+    const T qn = fmin(fmax(q + dq, lo), hi);
+    q = (active && joint) ? qn : q;
+    iters = active ? i + 1 : iters;
+    gfk(Rp, pp, sg, q0, q, joint, upper, j, anchor, axis, site);
+  }
+  if (!valid) return;
+  const T d0 = site[0] - tg[0], d1 = site[1] - tg[1], d2 = site[2] - tg[2];
+  const T err = KMath<T>::sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+  if (joint) q_out[(size_t)b * 7 + j] = q;
+  if (j < 3) final_pos[(size_t)b * 3 + j] = site[j == 0 ? 0 : (j == 1 ? 1 : 2)];
+  if (j == 0) {
+    pos_error[b] = err;
+    iterations[b] = iters;
+    flags[b] = (uint8_t)((converged ? PNP_IK_CONVERGED : 0u) |
+                         ((converged && err < thr * T(2)) ? PNP_IK_SUCCESS : 0u));
+  }
+}
+
 // ---------------------------------------------------------------------------- host side
 static void mat_mul3(double r[9], const double a[9], const double b[9]) {
   double t[9];
@@ -326,6 +497,12 @@ static bool matches_baked(const IKSeg<double>& s, int site_body) {
   return true;
 }
 
+// PNP_IK_SERIAL=1: the thread-per-solve kernel (A/B runs); default: 8-lane groups
+static bool serial_ik() {
+  const char* e = getenv("PNP_IK_SERIAL");
+  return e && e[0] == '1';
+}
+
 template <typename T>
 static int32_t launch_ik(pnp_model* model, int32_t site, pnp_ik_params prm, const T* q_init,
                          const T* target, T* q_out, T* final_pos, T* pos_error, int32_t* iterations,
@@ -356,12 +533,19 @@ static int32_t launch_ik(pnp_model* model, int32_t site, pnp_ik_params prm, cons
     s.qpos0[j] = (T)s64.qpos0[j];
   }
   for (int t = 0; t < 3; t++) s.psite[t] = (T)s64.psite[t];
-  const bool baked = matches_baked(s64, model->h.site_bodyid[site]);
-  auto kern = baked ? ik_dls_kernel<T, true> : ik_dls_kernel<T, false>;
-  hipLaunchKernelGGL(kern, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, s,
-                     prm.max_iters, (T)prm.pos_thresh, (T)prm.damping, (T)prm.step_limit, q_init,
-                     target, q_out, final_pos, pos_error, iterations, flags, B);
-  return pnp_check_launch("ik_dls_kernel");
+  if (serial_ik()) {
+    const bool baked = matches_baked(s64, model->h.site_bodyid[site]);
+    auto kern = baked ? ik_dls_kernel<T, true> : ik_dls_kernel<T, false>;
+    hipLaunchKernelGGL(kern, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, s,
+                       prm.max_iters, (T)prm.pos_thresh, (T)prm.damping, (T)prm.step_limit, q_init,
+                       target, q_out, final_pos, pos_error, iterations, flags, B);
+    return pnp_check_launch("ik_dls_kernel");
+  }
+  // 8 lanes per solve: 8 solves per 64-lane block
+  hipLaunchKernelGGL(ik_dls_group_kernel<T>, dim3((B + 7) / 8), dim3(64), 0, (hipStream_t)stream, s,
+                     prm.max_iters, (T)prm.pos_thresh, (T)prm.damping, (T)prm.step_limit, q_init, target,
+                     q_out, final_pos, pos_error, iterations, flags, B);
+  return pnp_check_launch("ik_dls_group_kernel");
 }
 
 extern "C" int32_t pnp_ik_dls(pnp_model* model, int32_t site_id, pnp_ik_params params,
