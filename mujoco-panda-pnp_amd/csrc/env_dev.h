@@ -441,7 +441,23 @@ static EnvOutT<T> out_view(const pnp_env_out* o) {
                     o->terminated, o->truncated};
 }
 
-#if PNP_WIDE
+#if PNP_COMPACT
+int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
+                                const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
+                                void* stream) {
+  const DevPhys<float>* src = phys_image<float>(model);
+  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  ResidentLease lease;
+  if (const int32_t rc = lease.acquire(RES_COMPACT_GYM_F32, model, (const void*)&g_phys_f32, src,
+                                       sizeof(DevPhys<float>), stream))
+    return rc;
+  hipLaunchKernelGGL(env_step_kernel<float>, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, *p,
+                     env_view<float>(e), action, out_view<float>(o), B, 0, 1);
+  if (const int32_t rc = pnp_check_launch("env_step_kernel (compact)")) return rc;
+  return lease.launched();
+}
+int32_t env_compact_lds_bytes() { return (int32_t)sizeof(Env<float>); }
+#elif PNP_WIDE
 // wide tier: resume pass of the gym step over the envs the full kernel handed over (launched by
 // the full build's launch_env_step, which holds the full image's lease)
 int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
@@ -536,13 +552,20 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   ResidentLease lease;
   auto k = env_step_kernel<T>;
   if ((rc = env_prep(model, st, k, &dm, "pnp_env_step", stream, lease))) return rc;
-  // fp32: the wide tier finishes the envs whose physics outgrew the full kernel's capacities
-  const int wide = sizeof(T) == 4 && wide_enabled() && p->n_substeps * p->n_calls <= PNP_RESUME_MAXSUB;
+  // fp32 tiers: the compact gym kernel (8 envs per CU) runs every env, the full kernel resumes
+  // the envs it hands over, the wide kernel the envs the full kernel hands over
+  const bool tiers = sizeof(T) == 4 && p->n_substeps * p->n_calls <= PNP_RESUME_MAXSUB;
+  const int wide = tiers && wide_enabled();
+  const bool compact = tiers && gym_compact_enabled();
+  const auto* st32 = reinterpret_cast<const pnp_state_t<float>*>(st);
+  if (compact && (rc = launch_env_step_compact(model, st32, p, e, reinterpret_cast<const float*>(action), o, B,
+                                               stream)))
+    return rc;
+  if (compact && gym_compact_mode() == 2) return lease.launched();
   hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), action,
-                     out_view<T>(o), B, 0, wide);
+                     out_view<T>(o), B, compact ? 1 : 0, wide);
   if ((rc = pnp_check_launch("env_step_kernel"))) return rc;
-  if (wide && (rc = launch_env_step_wide(model, reinterpret_cast<const pnp_state_t<float>*>(st), p, e,
-                                         reinterpret_cast<const float*>(action), o, B, stream)))
+  if (wide && (rc = launch_env_step_wide(model, st32, p, e, reinterpret_cast<const float*>(action), o, B, stream)))
     return rc;
   return lease.launched();
 }

@@ -40,7 +40,12 @@
 #ifndef PNP_WIDE
 #define PNP_WIDE 0
 #endif
-#if PNP_COMPACT
+#ifndef PNP_GYM
+#define PNP_GYM 0   // env_compact.hip: the compact tier's gym kernel (own namespace and image)
+#endif
+#ifdef PNP_NS_NAME
+#define PNP_NS PNP_NS_NAME
+#elif PNP_COMPACT
 #define PNP_NS pnp_compact
 #elif PNP_WIDE
 #define PNP_NS pnp_wide
@@ -212,7 +217,7 @@ struct Env {
   T isl_cost[PH_MAXT], isl_val[PH_MAXT];   // per-island reductions (cost, |grad|^2 ...)
   int isl_flag[PH_MAXT];       // per-island: done (Newton), active set changed
   int isl_hvalid[PH_MAXT];     // per-island: H block is current for the island's active set
-#if !PNP_COMPACT
+#if !PNP_COMPACT || PNP_GYM
   T qpos_pre[PH_MAXQ];         // gym env: qpos of the last forward (pre-integration)
 #endif
   int ovf;                     // a capacity overflowed in this sub-step (hand-over builds)
@@ -2932,7 +2937,12 @@ using namespace PNP_NS;
 // The constant-segment images are made resident through ResidentLease (resident.cpp): stream-
 // ordered copies, readers on other streams ordered after the copy, model switches after the
 // readers of the old image.
-#if PNP_COMPACT
+#if PNP_COMPACT && PNP_GYM
+// compact tier of the gym step (env_compact.hip): every env from sub-step 0; the full build's
+// launch_env_step resumes the envs it hands over
+#include "env_dev.h"
+
+#elif PNP_COMPACT
 int32_t launch_step_compact(const pnp_model* model, const pnp_state_t<float>* st, int32_t B, int32_t nsub,
                             void* stream, unsigned long long* prof) {
   const DevPhys<float>* src = phys_image<float>(model);
@@ -2997,6 +3007,14 @@ static bool wide_enabled() {
   const char* e = getenv("PNP_STEP_WIDE");
   return !(e && e[0] == '0');
 }
+// PNP_GYM_COMPACT: unset / 1 = the fp32 gym step starts in the compact tier (default), 0 = in the
+// full tier (A/B runs)
+// (2: the compact gym kernel alone -- diagnostic: handed-over envs keep their resume bits)
+static int gym_compact_mode() {
+  const char* e = getenv("PNP_GYM_COMPACT");
+  return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
+}
+static bool gym_compact_enabled() { return gym_compact_mode() != 0; }
 
 template <typename T>
 static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B, int32_t nsub, void* stream,

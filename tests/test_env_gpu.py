@@ -137,6 +137,48 @@ def test_gym_step_wide_tier_pressed_fingers(model):
     assert int((g.state["warn"] & 0xFFFF).max()) == 0 and not o.st["warn"].any()
 
 
+def _gym_run(mode, B, nsteps, pressed=False):
+    import os
+    from pnp_amd.envs import BatchedFrankaShelfPNPEnv
+    old = os.environ.get("PNP_GYM_COMPACT")
+    os.environ["PNP_GYM_COMPACT"] = mode
+    try:
+        g = BatchedFrankaShelfPNPEnv(B, autoreset=True)
+        g.reset()
+        if pressed:
+            g.state["qpos"][::3, 7:9] = -0.002          # a third of the envs: pads pressed together
+        rng = np.random.default_rng(21)
+        outs = []
+        for k in range(nsteps):
+            a = torch.as_tensor(rng.uniform(-1, 1, size=(B, 7)), dtype=torch.float32, device="cuda")
+            obs, r, term, trunc, info = g.step(a)
+            outs.append((obs["observation"].clone(), r.clone(), term.clone(), trunc.clone(), info["is_success"].clone()))
+        torch.cuda.synchronize()
+        return g, outs
+    finally:
+        if old is None:
+            del os.environ["PNP_GYM_COMPACT"]
+        else:
+            os.environ["PNP_GYM_COMPACT"] = old
+
+
+def test_gym_compact_tier_is_exact():
+    """The fp32 gym step starts in the compact tier (8 envs per CU) and hands envs over to the full
+    and wide tiers (env_compact.hip, env_dev.h): bit-identical to starting in the full tier, on a
+    batch whose envs stay under 20 contacts, pass 20 (random grippers) and pass 48 (pads pressed)."""
+    a, oa = _gym_run("1", 96, 3, pressed=True)
+    b, ob = _gym_run("0", 96, 3, pressed=True)
+    for x, y in zip(oa, ob):
+        for u, v in zip(x, y):
+            assert torch.equal(u, v)
+    for k in a.state:
+        assert torch.equal(a.state[k], b.state[k]), k
+    for k in a.env:
+        assert torch.equal(a.env[k], b.env[k]), k
+    w = a.state["warn"].to(torch.int64) & 0xFFFFFFFF
+    assert not bool((w >> 16).any()) and int((w & 0xFFFF).max()) == 0
+
+
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_full_gym_step_bounded(model, dtype):
     g = _env(dtype)
