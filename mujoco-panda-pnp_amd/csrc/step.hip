@@ -2372,9 +2372,10 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   // row order, and up to 4 pairs are updated at once; each island sees exactly the sequential
   // order, so the result equals the one-pair-at-a-time sweep.
   const int grp = l >> 4, q = l & 15;
+  int iend[2] = {0, 0};   // end of the group's first / second island in its list (group-uniform)
   {
-    int len = 0;
-    for (int I = grp; I < s.nisland; I += 4) {
+    int len = 0, si = 0;
+    for (int I = grp; I < s.nisland; I += 4, si++) {
       for (int base = s.isl_roff[I]; base < s.isl_roff[I + 1]; base += 16) {
         const int rr = base + q;
         bool start = false;
@@ -2387,6 +2388,7 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
         if (start) s.ns_list[grp][len + __popc(bits & ((1u << q) - 1u))] = (short)r;
         len += __popc(bits);
       }
+      iend[si & 1] = len;
     }
     if (q == 0) s.ns_len[grp] = len;
   }
@@ -2530,6 +2532,117 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
 #pragma unroll
       for (int k = 0; k < NSR; k++)
         if (k < glen && q == 0) { s.efc_force[s.ns_list[grp][k]] = F0[k]; s.efc_force[s.ns_list[grp][k] + 1] = F1[k]; }
+      wsync();
+      return;
+    }
+  }
+  // Long lists (a group with more than NSR pairs: closed fingers pressed together put 50+
+  // contacts on the arm island) whose islands have <= 16 dofs: the island's v in registers, lane
+  // q of the group = the island's dof q.  An update is then two row sums of J v, the 2 x 2
+  // projection and a lane-local v += W df -- no v round trip through LDS and no wave sync
+  // between updates (the streaming path below spends ~1.5k cycles per update on those).  A pair's
+  // J / W entries are read from its packed slots at the lane's dof, one pair ahead, with its 2 x 2
+  // Delassus block.  Islands are independent under Gauss-Seidel, so a group sweeps its (<= 2)
+  // islands one after the other: each island sees the sequential order.  Rounding differs from
+  // the streaming path (row sums in island-dof lane order).
+  if (maxlen > NSR) {
+    bool small = true;
+    for (int I = grp; I < s.nisland; I += 4) small = small && s.isl_n[I] <= 16;
+    if (!__ballot(!small)) {
+      for (int si = 0; si < 2; si++) {
+        const int I = grp + 4 * si;
+        const bool has = I < s.nisland;
+        const int k0 = si ? iend[0] : 0;
+        const int cnt = has ? iend[si] - k0 : 0;
+        const int maxc = max(max(__builtin_amdgcn_readlane(cnt, 0), __builtin_amdgcn_readlane(cnt, 16)),
+                             max(__builtin_amdgcn_readlane(cnt, 32), __builtin_amdgcn_readlane(cnt, 48)));
+        if (maxc == 0) continue;
+        const int n = has ? s.isl_n[I] : 0;
+        const bool lane_on = q < n;
+        const int d = lane_on ? s.isl_dof[I][q] : 0;
+        const int td = s.c_dof_tree[d], dloc = d - s.c_tree_dofadr[td];
+        T v = lane_on ? s.v2[d] : T(0);
+        // software pipeline over the pairs, one LDS level per stage, so that no wait inside the
+        // loop covers a load issued in the same iteration: list entry 3 pairs ahead, the row's
+        // trees and offsets 2 ahead, its J / W / b / f entries 1 ahead; the Delassus block of a
+        // pair is formed at its own update (off the chain through v).  Tree sizes come from
+        // registers.
+        int tdn[PH_MAXT];
+#pragma unroll
+        for (int t = 0; t < PH_MAXT; t++) tdn[t] = s.c_tree_dofnum[t];
+        struct DRow {   // stage 2
+          int j, t0, t1, off0, off1;
+          bool act;
+        };
+        struct DRaw {   // stage 3
+          int j;
+          bool act;
+          T J0, J1, W0, W1, b0, b1, f0, f1;
+        };
+        auto dlist = [&](int k) { return k < cnt ? (int)s.ns_list[grp][k0 + k] : -1; };
+        auto drow = [&](int jj) {
+          DRow x;
+          x.act = jj >= 0;
+          x.j = x.act ? jj : 0;   // (row 0 exists: nefc > 0)
+          x.t0 = s.efc_t0[x.j];
+          x.t1 = s.efc_t1[x.j];
+          x.off0 = s.efc_off[x.j];
+          x.off1 = s.efc_off[x.j + 1];
+          return x;
+        };
+        auto draw = [&](const DRow& x) {
+          int n0 = 0;
+#pragma unroll
+          for (int t = 0; t < PH_MAXT; t++) n0 = x.t0 == t ? tdn[t] : n0;
+          const int slot = td == x.t0 ? dloc : (td == x.t1 ? n0 + dloc : -1);
+          const bool on = x.act && lane_on && slot >= 0;
+          const int sl = on ? slot : 0;                 // unconditional, in-range loads; masked below
+          DRaw p;
+          p.j = x.j;
+          p.act = x.act;
+          const T J0 = s.efc_Jv[x.off0 + sl], J1 = s.efc_Jv[x.off1 + sl];
+          const T W0 = s.efc_Wv[x.off0 + sl], W1 = s.efc_Wv[x.off1 + sl];
+          p.J0 = on ? J0 : T(0);
+          p.J1 = on ? J1 : T(0);
+          p.W0 = on ? W0 : T(0);
+          p.W1 = on ? W1 : T(0);
+          p.b0 = s.efc_bb[x.j];
+          p.b1 = s.efc_bb[x.j + 1];
+          p.f0 = s.efc_force[x.j];
+          p.f1 = s.efc_force[x.j + 1];
+          return p;
+        };
+        for (int iter = 0; iter < m.noslip_iterations; iter++) {
+          DRaw cur = draw(drow(dlist(0)));
+          DRow x1 = drow(dlist(1));
+          int j2 = dlist(2);
+          for (int k = 0; k < maxc; k++) {
+            const int j3 = dlist(k + 3);
+            const DRow x2 = drow(j2);
+            const DRaw nxt = draw(x1);
+            const T a00 = rowsum16(cur.J0 * cur.W0), a01 = rowsum16(cur.J0 * cur.W1);
+            const T a10 = rowsum16(cur.J1 * cur.W0), a11 = rowsum16(cur.J1 * cur.W1);
+            const T r0 = rowsum16(cur.J0 * v) + cur.b0;
+            const T r1 = rowsum16(cur.J1 * v) + cur.b1;
+            const T f0 = cur.f0, f1 = cur.f1;
+            const T bc0 = r0 - (a00 * f0 + a01 * f1), bc1 = r1 - (a10 * f0 + a11 * f1);
+            const T mid = T(0.5) * (f0 + f1);
+            const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;
+            T y = -K0 / K1;
+            y = y < -mid ? -mid : (y > mid ? mid : y);
+            const bool flat = K1 < T(1e-15);
+            const T n0 = flat ? mid : mid + y, n1 = flat ? mid : mid - y;
+            const T d0 = cur.act ? n0 - f0 : T(0), d1 = cur.act ? n1 - f1 : T(0);
+            v += cur.W0 * d0 + cur.W1 * d1;
+            if (cur.act && q == 0) { s.efc_force[cur.j] = n0; s.efc_force[cur.j + 1] = n1; }
+            cur = nxt;
+            x1 = x2;
+            j2 = j3;
+          }
+          wsync();   // the next sweep reads the forces this one wrote
+        }
+        if (lane_on) s.v2[d] = v;
+      }
       wsync();
       return;
     }

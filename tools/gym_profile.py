@@ -66,12 +66,19 @@ def main():
         v = prof[:, i] / nsub
         if names[i].startswith("n_"):
             print(f"  {names[i]:22s} {v.mean():8.2f} per env-sub-step (max {v.max():.2f})")
-    # heavy vs light envs
-    for lo, hi in ((0, 20), (20, 32), (32, 49)):
+    # heavy vs light envs: cycles per sub-step and the top stages of each bucket
+    for lo, hi in ((0, 20), (20, 32), (32, 48), (48, 97)):
         sel = (ncon > lo) & (ncon <= hi)
         if sel.any():
-            c = prof[sel, :16].sum(1).mean() / nsub
-            print(f"  envs with {lo} < contacts <= {hi}: {sel.mean():.3f} of envs, {c:.0f} cycles per sub-step")
+            per = prof[sel, :Engine.N_STAGE_CYCLES].mean(0) / nsub
+            c = per[:16].sum()
+            top = sorted(range(Engine.N_STAGE_CYCLES), key=lambda i: -per[i])[:8]
+            print(f"  envs with {lo} < contacts <= {hi}: {sel.mean():.3f} of envs, {c:.0f} cycles per sub-step; "
+                  + ", ".join(f"{names[i]} {per[i]:.0f}" for i in top))
+            cnt = prof[sel].mean(0) / nsub
+            sub = ("noslip_W", "noslip_lists", "newton_gradient", "newton_hessian", "newton_converge",
+                   "n_noslip_sweep", "n_efc", "n_newton_iter", "n_convex")
+            print("      " + ", ".join(f"{k} {cnt[names.index(k)]:.1f}" for k in sub))
 
 
 if __name__ == "__main__":
