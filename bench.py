@@ -97,6 +97,16 @@ def reduce_max(values, device):
     return [float(v) for v in t]
 
 
+def _progress(rank, msg):
+    """Progress line on stderr (rank 0): the legs take tens of seconds each."""
+    if rank == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def total_steps(B, world, steps):
+    return B * world * steps * NSUB
+
+
 def shard_range(rank, B):
     """Global env indices of rank r: [r*B, (r+1)*B) (inputs depend only on the global index)."""
     return np.arange(rank * B, (rank + 1) * B)
@@ -155,12 +165,14 @@ def run_step(args, engine, model, rank, world, dist):
     B = args.batch
     st, ctrl = step_inputs(engine, model, rank, B)
     torch.cuda.synchronize()
+    _progress(rank, "inputs settled")
 
     def fn(i):
         st["ctrl"] = ctrl[i % NCTRL]
         engine.step(st, NSUB)
 
     elapsed, kern_ms = _timed(fn, args.steps, args.warmup, dist)
+    _progress(rank, f"step leg done: {total_steps(B, world, args.steps) / elapsed / 1e6:.2f} M env-steps/s")
     warn = int(st["warn"].max())
     finite = bool(torch.isfinite(st["qpos"]).all())
     total = B * world * args.steps * NSUB
@@ -195,13 +207,16 @@ def run_step(args, engine, model, rank, world, dist):
     }
     if not args.no_gym:
         rec["gym"] = run_gym(engine, B, rank, world, dist)
+        _progress(rank, f"gym leg done: {rec['gym']['gym_steps_per_s']:.0f} gym-steps/s")
     if not args.no_tqc:
         rec["tqc"] = run_tqc(engine, args.tqc_envs, rank, world, dist)
+        _progress(rank, f"tqc leg done: {rec['tqc']['gym_steps_per_s']:.0f} transitions/s")
     if not args.no_ik:
         ik = run_ik(args, engine, model, rank, world, dist, steps=50, warmup=5, baseline=False)
         rec["ik"] = {k: ik[k] for k in ("value", "unit", "ms_per_step")}
         rec["ik"].update(roofline_frac=ik["roofline"]["frac"], workload=ik["config"]["workload"])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        _progress(rank, "cpu baseline ...")
         rec["cpu_baseline"] = step_cpu_baseline(st, ctrl, args.cpu_budget)
     return rec
 

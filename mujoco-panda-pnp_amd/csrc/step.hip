@@ -1970,9 +1970,45 @@ __device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, C
   clk.aux_lap(SC_AUX0 + 5);   // aux5: line search J p, M p
   const int q = l & 7;
   int itc = 0;   // bracketing iterations of the lane's island (stage profile count)
+  // Islands with more rows than a group's register cache (closed fingers pressed together put
+  // 200-400 rows on the arm island): bracketed on the whole wave, one after the other, each
+  // row read once per bracketing iteration by 64 lanes (the group path below would walk it 8
+  // rows at a time, ~35 dependent LDS rounds per iteration).  Same bracketing; the row sums
+  // reduce over 64 lanes instead of 8 (rounding only).
+  constexpr int RK = 4;
+  const uint32_t big = (uint32_t)__ballot(l < s.nisland && !s.isl_flag[l] &&
+                                          s.isl_roff[l + 1] - s.isl_roff[l] > 8 * RK);
+  for (uint32_t bm = big; bm; bm &= bm - 1) {
+    const int I = __builtin_ctz(bm);
+    const int n = s.isl_n[I];
+    const T A0 = wsum(l < n ? s.v2[s.isl_dof[I][l]] : T(0)), B0 = wsum(l < n ? s.grad[s.isl_dof[I][l]] : T(0));
+    const int r0 = s.isl_roff[I], r1 = s.isl_roff[I + 1];
+    T lo = 0, hi = T(-1), a = 1;
+    int it = 0;
+    for (; it < 60; it++) {
+      T d1 = 0, d2 = 0;
+      for (int rr = r0 + l; rr < r1; rr += NT) {
+        const int r = s.isl_row[rr];
+        const T jp = s.efc_Jp[r], v = s.efc_jar[r] + a * jp;
+        if (r < s.ne || v < 0) { d1 += s.efc_D[r] * v * jp; d2 += s.efc_D[r] * jp * jp; }
+      }
+      d1 = wsum(d1) + A0 * a + B0;
+      d2 = wsum(d2) + A0;
+      if (!(d2 > T(0))) { a = 0; break; }
+      if (d1 == T(0)) break;
+      if (d1 > 0) hi = a; else lo = a;
+      T an = a - d1 / d2;
+      if (!(an > lo) || (hi >= T(0) && !(an < hi))) an = hi >= T(0) ? T(0.5) * (lo + hi) : T(2) * a;
+      const bool fin = fabs(an - a) <= T(4) * PM<T>::eps() * fabs(a) || (hi >= T(0) && hi - lo <= PM<T>::eps() * hi);
+      a = an;
+      if (fin) break;
+    }
+    if (l == 0) s.isl_alpha[I] = a;
+    if ((l >> 3) == I) itc = it + 1;
+  }
   {
     const int I = l >> 3;
-    if (I >= s.nisland) goto ls_done;
+    if (I >= s.nisland || (big >> I & 1u)) goto ls_done;
     if (s.isl_flag[I]) {
       if (q == 0) s.isl_alpha[I] = 0;
       goto ls_done;
@@ -1980,8 +2016,7 @@ __device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, C
     const T A0 = group_sum(s, I, s.v2, (const T*)nullptr), B0 = group_sum(s, I, s.grad, (const T*)nullptr);
     const int r0 = s.isl_roff[I], r1 = s.isl_roff[I + 1];
     // the lane's rows (rr = r0 + q + 8 k) are fixed over the iterations: islands of up to 32
-    // rows keep (Jp, jar, D, equality) in registers, larger ones read LDS each iteration
-    constexpr int RK = 4;
+    // rows keep (Jp, jar, D, equality) in registers (larger ones took the wave path above)
     T rjp[RK], rjar[RK], rD[RK];
     bool req[RK], rin[RK];
 #pragma unroll
