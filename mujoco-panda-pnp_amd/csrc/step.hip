@@ -2126,6 +2126,55 @@ __device__ __attribute__((noinline)) void newton_dir_groups(Env<T>& s, bool done
   if (l < s.nisland && !done) s.isl_hvalid[l] = 1;
 }
 
+// Hessian block of an island with many rows (closed fingers: 200-400 rows on the arm island) on
+// the matrix cores: J^T diag(D) J is a (n x nr) (nr x n) product, n <= 16 island dofs, so one
+// v_mfma_f32_16x16x4_f32 tile per 4 rows (A = J^T: lane l holds J[k0 + l/16][l%16], B = D J:
+// the same element times D), two independent accumulators (the MFMA's dependent latency is 40
+// cycles), then M's block entries added and the lower triangle stored.  The scalar path (lane
+// per entry) walks every row once per entry.  fp32 MFMA is exact f32 (an fmaf chain per
+// element); the sums associate differently from the scalar loop (rounding only).
+__device__ __attribute__((noinline)) void hess_mfma(Env<float>& s, int I) {
+  const DevPhys<float>& m = phys<float>();
+  const int l = lane_id();
+  const int n = s.isl_n[I], r0 = s.isl_roff[I], nr = s.isl_roff[I + 1] - r0;
+  const float* J = s.jt + s.isl_joff[I];
+  const float* D = s.rr_d + r0;
+  const int c = l & 15, kk = l >> 4;
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  auto elem = [&](int k, float& x, float& dx) {
+    const bool on = k < nr && c < n;
+    const float v = J[on ? k * n + c : 0], d = D[k < nr ? k : 0];
+    x = on ? v : 0.f;
+    dx = on ? d * v : 0.f;
+  };
+  int k0 = 0;
+  for (; k0 + 8 <= nr; k0 += 8) {
+    float x0, b0, x1, b1;
+    elem(k0 + kk, x0, b0);
+    elem(k0 + 4 + kk, x1, b1);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0, b0, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1, b1, acc1, 0, 0, 0);
+  }
+  for (; k0 < nr; k0 += 4) {
+    float x0, b0;
+    elem(k0 + kk, x0, b0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0, b0, acc0, 0, 0, 0);
+  }
+  // lane l holds H[4 (l / 16) + r][l % 16], r = 0..3
+  const int e0 = s.isl_eoff[I];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int a = 4 * kk + r, b = c;
+    if (a < n && b <= a) {
+      const int i = s.isl_dof[I][a], j = s.isl_dof[I][b];
+      const int ti = s.c_dof_tree[i], tj = s.c_dof_tree[j];
+      const float h = ti == tj ? s.M[mblk(m, i, j)] : 0.f;
+      s.Hp[e0 + a * (a + 1) / 2 + b] = h + (acc0[r] + acc1[r]);
+    }
+  }
+}
+
 template <typename T, class CLK>
 __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
@@ -2200,10 +2249,37 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
         s.rr_d[rr] = a ? d : T(0);
       }
     wsync();
+    // islands with many rows (closed fingers: 200-400 rows on the arm island): J^T (D jar) on the
+    // whole wave -- lane (dof a, slice k) sums rows a + ... k, k + S, k + 2S .. (S = 64 / n
+    // slices), then lane a adds its S partials -- instead of one lane per dof walking every row;
+    // the sums land in v2 (dead here) for the dof lanes below
+    const uint32_t bigg = jt ? (uint32_t)__ballot(l < nisl && s.isl_roff[l + 1] - s.isl_roff[l] > NT &&
+                                                  s.isl_n[l] <= 32)
+                             : 0u;
+    for (uint32_t bm = bigg; bm; bm &= bm - 1) {
+      const int I = __builtin_ctz(bm);
+      const int n = s.isl_n[I], r0 = s.isl_roff[I], nr = s.isl_roff[I + 1] - r0, S = NT / n;
+      const int a = l % n, k0 = l / n;
+      if (k0 < S) {
+        const T* col = s.jt + s.isl_joff[I] + a;
+        const T* fr = s.rr_f + r0;
+        T part = 0;
+        for (int k = k0; k < nr; k += S) part += col[k * n] * fr[k];
+        s.ntmp[l] = part;
+      }
+      wsync();
+      if (l < n) {
+        T g = 0;
+        for (int k = 0; k < S; k++) g += s.ntmp[l + k * n];
+        s.v2[s.isl_dof[I][l]] = g;
+      }
+      wsync();
+    }
     if (l < m.nv) {
       const int t = s.c_dof_tree[l], I = s.tree_island[t];
       const T mv = mulM_row(m, s, l, s.v1);
-      const T g = jt ? jt_dof_sum(s, I, s.dof_ipos[l], mv, s.rr_f)
+      const T g = (bigg >> I & 1u) ? mv + s.v2[l]
+                : jt ? jt_dof_sum(s, I, s.dof_ipos[l], mv, s.rr_f)
                      : dof_row_sum(mv, s, I, t, l - s.c_tree_dofadr[t], s.efc_D, s.efc_jar, true);
       s.grad[l] = g;
       s.v2[l] = g * g;
@@ -2220,7 +2296,15 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     clk.sub_lap(SC_N_CONV);
     if (!__ballot(!done)) { clk.lap(9); break; }
     // Hessian island blocks (lower triangle, lane per entry): M + sum_active D J J^T; blocks of
-    // islands whose active set is unchanged since their last assembly are reused as they are
+    // islands whose active set is unchanged since their last assembly are reused as they are;
+    // fp32 islands with many rows on the matrix cores (hess_mfma)
+    uint32_t bigh = 0;
+    if constexpr (sizeof(T) == 4) {
+      if (jt)
+        bigh = (uint32_t)__ballot(l < nisl && !s.isl_flag[l] && !s.isl_hvalid[l] &&
+                                  s.isl_roff[l + 1] - s.isl_roff[l] > NT && s.isl_n[l] <= 16);
+      for (uint32_t bm = bigh; bm; bm &= bm - 1) hess_mfma(s, __builtin_ctz(bm));
+    }
     for (int e = l; e < nent; e += NT) {
       // the entry's island: comparisons against the offsets (independent LDS loads issued
       // together) instead of a loop that waits on one load per island
@@ -2229,7 +2313,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       for (int J = 1; J <= PH_MAXT; J++) I += J < nisl && e >= s.isl_eoff[J] ? 1 : 0;
       const int eI = s.isl_eoff[I], nI = s.isl_n[I], r0I = s.isl_roff[I], e1I = s.isl_roff[I + 1],
                 joI = s.isl_joff[I];
-      if (s.isl_flag[I] || s.isl_hvalid[I]) continue;
+      if (s.isl_flag[I] || s.isl_hvalid[I] || (bigh >> I & 1u)) continue;
       const int le = e - eI;
       int a = (int)((PM<float>::sqrt_(8.0f * le + 1.0f) - 1.0f) * 0.5f);
       while (a * (a + 1) / 2 > le) a--;
