@@ -212,9 +212,13 @@ def run_step(args, engine, model, rank, world, dist):
         rec["tqc"] = run_tqc(engine, args.tqc_envs, rank, world, dist)
         _progress(rank, f"tqc leg done: {rec['tqc']['gym_steps_per_s']:.0f} transitions/s")
     if not args.no_ik:
-        ik = run_ik(args, engine, model, rank, world, dist, steps=50, warmup=5, baseline=False)
+        ik = run_ik(args, engine, model, rank, world, dist, steps=50, warmup=5,
+                    baseline=not args.no_cpu_baseline, budget=min(args.cpu_budget, 4.0))
         rec["ik"] = {k: ik[k] for k in ("value", "unit", "ms_per_step")}
         rec["ik"].update(roofline_frac=ik["roofline"]["frac"], workload=ik["config"]["workload"])
+        if "cpu_baseline" in ik:
+            rec["ik"]["cpu_baseline"] = ik["cpu_baseline"]
+        _progress(rank, f"ik leg done: {ik['value'] / 1e6:.1f} M solves/s")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         _progress(rank, "cpu baseline ...")
         rec["cpu_baseline"] = step_cpu_baseline(st, ctrl, args.cpu_budget)
@@ -299,7 +303,7 @@ def ik_cpu_baseline(q_host, tgt_host, prm, budget_s):
                       f"oracle/oracle.c, {nth} pthreads, {dt:.1f} s"}
 
 
-def run_ik(args, engine, model, rank, world, dist, steps=None, warmup=None, baseline=True):
+def run_ik(args, engine, model, rank, world, dist, steps=None, warmup=None, baseline=True, budget=None):
     steps = args.steps if steps is None else steps
     warmup = args.warmup if warmup is None else warmup
     B = args.batch
@@ -337,7 +341,7 @@ def run_ik(args, engine, model, rank, world, dist, steps=None, warmup=None, base
         "host_cores": len(os.sched_getaffinity(0)),
     }
     if baseline and rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec["cpu_baseline"] = ik_cpu_baseline(q_host, tgt_host, prm, args.cpu_budget)
+        rec["cpu_baseline"] = ik_cpu_baseline(q_host, tgt_host, prm, budget or args.cpu_budget)
     return rec
 
 

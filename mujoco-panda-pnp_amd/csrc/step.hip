@@ -56,6 +56,11 @@
 // when its kernel is launched with hand = 1); PNP_LEAN: no debug-only fields outside the unions
 #define PNP_HANDS (!PNP_WIDE)
 #define PNP_LEAN (PNP_COMPACT || PNP_WIDE)
+// PNP_BIG_ISLANDS: the solver's whole-wave paths for islands with more rows than a wave (line
+// search, gradient, MFMA Hessian).  Compiled out of the compact build, which hands such islands
+// over instead (build_islands), so its common case pays nothing for them.
+#define PNP_BIG_ISLANDS (!PNP_COMPACT)
+#define PNP_BIG_ROWS 32   // = 8 lanes x the line search's 4 cached rows per lane
 namespace PNP_NS {
 
 // The physics image lives in the device's constant segment, one resident image per precision
@@ -1783,6 +1788,9 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
   }
   const int rtot = __builtin_amdgcn_readlane(ro, 7), etot = __builtin_amdgcn_readlane(eo, 7),
             jtot = __builtin_amdgcn_readlane(jo, 7);
+  // an island with more rows than the line search's per-group register cache (the solver's
+  // whole-wave paths start there: PNP_BIG_ISLANDS)
+  const bool bigrows = __ballot(isl && rc > PNP_BIG_ROWS) != 0;
   ro -= isl ? rc : 0;
   eo -= isl ? nI * (nI + 1) / 2 : 0;
   jo -= isl ? rc * nI : 0;
@@ -1818,6 +1826,8 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
     // jt is too small); the full / wide Hessian stores fit every island partition of PH_MAXV
     // dofs, the compact build's the common ones
     if ((PNP_COMPACT || (PNP_HANDS && s.hand)) && (!s.jt_ok || etot > PH_HCAP)) s.ovf |= PNP_OVF_JT;
+    // the compact build has no whole-wave solver paths: it hands such islands over
+    if (!PNP_BIG_ISLANDS && bigrows) s.ovf |= PNP_OVF_JT;
   }
   wsync();
   clk.aux_lap(SC_AUX0 + 3);   // aux3: islands (closure, dof lists, row lists)
@@ -1975,9 +1985,10 @@ __device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, C
   // row read once per bracketing iteration by 64 lanes (the group path below would walk it 8
   // rows at a time, ~35 dependent LDS rounds per iteration).  Same bracketing; the row sums
   // reduce over 64 lanes instead of 8 (rounding only).
-  constexpr int RK = 4;
-  const uint32_t big = (uint32_t)__ballot(l < s.nisland && !s.isl_flag[l] &&
-                                          s.isl_roff[l + 1] - s.isl_roff[l] > 8 * RK);
+  constexpr int RK = PNP_BIG_ROWS / 8;
+  const uint32_t big = PNP_BIG_ISLANDS ? (uint32_t)__ballot(l < s.nisland && !s.isl_flag[l] &&
+                                                            s.isl_roff[l + 1] - s.isl_roff[l] > 8 * RK)
+                                       : 0u;
   for (uint32_t bm = big; bm; bm &= bm - 1) {
     const int I = __builtin_ctz(bm);
     const int n = s.isl_n[I];
@@ -2253,9 +2264,9 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     // whole wave -- lane (dof a, slice k) sums rows a + ... k, k + S, k + 2S .. (S = 64 / n
     // slices), then lane a adds its S partials -- instead of one lane per dof walking every row;
     // the sums land in v2 (dead here) for the dof lanes below
-    const uint32_t bigg = jt ? (uint32_t)__ballot(l < nisl && s.isl_roff[l + 1] - s.isl_roff[l] > NT &&
-                                                  s.isl_n[l] <= 32)
-                             : 0u;
+    const uint32_t bigg = PNP_BIG_ISLANDS && jt ? (uint32_t)__ballot(l < nisl && s.isl_roff[l + 1] - s.isl_roff[l] > NT &&
+                                                                     s.isl_n[l] <= 32)
+                                                : 0u;
     for (uint32_t bm = bigg; bm; bm &= bm - 1) {
       const int I = __builtin_ctz(bm);
       const int n = s.isl_n[I], r0 = s.isl_roff[I], nr = s.isl_roff[I + 1] - r0, S = NT / n;
@@ -2299,7 +2310,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     // islands whose active set is unchanged since their last assembly are reused as they are;
     // fp32 islands with many rows on the matrix cores (hess_mfma)
     uint32_t bigh = 0;
-    if constexpr (sizeof(T) == 4) {
+    if constexpr (sizeof(T) == 4 && PNP_BIG_ISLANDS) {
       if (jt)
         bigh = (uint32_t)__ballot(l < nisl && !s.isl_flag[l] && !s.isl_hvalid[l] &&
                                   s.isl_roff[l + 1] - s.isl_roff[l] > NT && s.isl_n[l] <= 16);
