@@ -360,6 +360,9 @@ def main():
     ap.add_argument("--tqc-envs", type=int, default=8192, help="C5 envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="N > 1: nccl (= RCCL over xGMI, one GPU per rank); gloo only to rehearse several "
+                         "ranks on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -367,8 +370,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
     if dist:
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))   # (gloo rehearsal: ranks may share a GPU)
+        if args.dist_backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     engine = get_engine()
