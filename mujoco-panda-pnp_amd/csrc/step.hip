@@ -925,7 +925,7 @@ __device__ __forceinline__ void gch_factor(T Lrow[GCH_N], const T Ad[GCH_N], int
 }
 
 template <typename T>
-__device__ void st_factor_M(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
+__device__ __forceinline__ void st_factor_M(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
   const DevPhys<T>& m = phys<T>();
   const int t = lane_id();
   if (m.ntree <= GCH_GROUPS && !__ballot(t < m.ntree && s.c_tree_dofnum[t] > GCH_N)) {
@@ -1245,7 +1245,7 @@ __device__ T impedance_(const T* si, T x) {
 // position part of the reference acceleration; the velocity part (-b J qvel) is added by
 // finish_rows once the row's Jacobian is complete (b parked in efc_Jp meanwhile)
 template <typename T>
-__device__ void row_imp(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, int r, T pos, T margin, T diag, const T* solref,
+__device__ __forceinline__ void row_imp(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, int r, T pos, T margin, T diag, const T* solref,
                         const T* solimp) {
   const DevPhys<T>& m = phys<T>();
   const T dmax = fmin(fmax(solimp[1], T(0.0001)), T(0.9999));
@@ -1873,7 +1873,7 @@ __device__ __forceinline__ void gather_rows(const Env<T>& s, const T* v, T* out)
 // S = diag(H)^-1/2): islands mix a 1e-12 kg m^2 rotational inertia (the r = 1 mm dummy sphere)
 // with 1e-5 constraint terms, and unscaled fp32 Cholesky would lose most digits there.
 template <typename T, int N>
-__device__ void island_newton_dir_reg(Env<T>& s, int I, int n) {
+__device__ __forceinline__ void island_newton_dir_reg(Env<T>& s, int I, int n) {
   const unsigned char* idx = s.isl_dof[I];
   int id[N];
 #pragma unroll

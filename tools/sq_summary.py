@@ -1,0 +1,43 @@
+"""Per-dispatch averages of rocprofv3 --pmc CSV counter collections for one kernel.
+usage: python tools/sq_summary.py <pass_dir> [<pass_dir> ...] <kernel-name-substring>"""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def main():
+    dirs, kname = sys.argv[1:-1], sys.argv[-1]
+    tot = defaultdict(float)
+    nd = defaultdict(set)
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if kname not in r["Kernel_Name"]:
+                    continue
+                c = r["Counter_Name"]
+                tot[c] += float(r["Counter_Value"])
+                nd[c].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
+    if not tot:
+        raise SystemExit(f"no rows for {kname}")
+    per = {c: tot[c] / max(1, len(nd[c])) for c in tot}
+    print(f"{kname}: per-dispatch averages")
+    for c in sorted(per):
+        print(f"  {c:24s} {per[c]:16.0f}  ({len(nd[c])} dispatches)")
+    w = per.get("SQ_WAVES", 0)
+    if w:
+        print("per wave:")
+        for c in sorted(per):
+            if c != "SQ_WAVES":
+                print(f"  {c:24s} {per[c] / w:14.1f}")
+    wc = per.get("SQ_WAVE_CYCLES")
+    if wc:
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS",
+                  "SQ_WAIT_INST_LDS"):
+            if c in per:
+                print(f"  {c} / SQ_WAVE_CYCLES = {per[c] / wc:.3f}")
+
+
+if __name__ == "__main__":
+    main()
