@@ -332,6 +332,11 @@ typedef struct pnp_env_state {
   void* init_time;       /* [B] */
   uint32_t* episode;     /* [B] resets so far: Philox counter of the reset draws */
   uint32_t* env_index;   /* [B] global env index: Philox counter (shard-invariant) */
+  uint8_t* tier;         /* [B] optional (NULL: off): fp32 routing hint, the tier (0 compact, 1 full,
+                          * 2 wide) the env's next gym step starts in; written by init / reset (0)
+                          * and by the full / wide passes of pnp_env_step.  Routing changes where
+                          * an env's step runs, never its results (the tiers' arithmetic is
+                          * identical); PNP_GYM_ROUTE=0 disables it. */
 } pnp_env_state;
 /* Outputs (any pointer may be NULL to skip it). */
 typedef struct pnp_env_out {

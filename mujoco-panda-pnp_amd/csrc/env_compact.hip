@@ -19,3 +19,6 @@
 #include "step.hip"
 
 static_assert(sizeof(pnp_compact_gym::Env<float>) <= 20480, "compact gym Env must fit 8 envs per CU (160 KB LDS)");
+static_assert(PH_MAXCON == PNP_GC_MAXCON && PH_MAXEFC == PNP_GC_MAXEFC && PH_MAXJSLOT == PNP_GC_MAXJSLOT &&
+                  PH_JTCAP == PNP_GC_JTCAP && PH_HCAP == PNP_GC_HCAP,
+              "env_dev.h's routing estimate (tier_need) must see this tier's capacities");

@@ -99,6 +99,7 @@ template <typename T>
 struct EnvSoA {
   T* goal; int32_t* task; int32_t* elapsed; T* qpos_kin; T* obj_height0; T* init_mocap; T* init_qvel;
   T* init_time; uint32_t* episode; uint32_t* env_index;
+  uint8_t* tier;   // optional (null: no routing): the tier the env's next gym step starts in
 };
 template <typename T>
 struct EnvOutT {
@@ -235,6 +236,7 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_i
     es.task[b] = 0;
     es.elapsed[b] = 0;
     es.episode[b] = 0;
+    if (es.tier) es.tier[b] = 0;
   }
 }
 
@@ -280,6 +282,7 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_r
     es.task[b] = 0;
     es.elapsed[b] = 0;
     es.episode[b] = ep + 1;
+    if (es.tier) es.tier[b] = 0;
   }
   if (l < m.nv) s.qvel[l] = es.init_qvel[(size_t)b * m.nv + l];
   wsync();
@@ -297,6 +300,41 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_r
 }
 
 // ---------------------------------------------------------------- step (FrankaEnv.step)
+// Routing (env_state.tier): the smallest tier whose capacities hold a sub-step with a margin --
+// compact (0), full (1), wide (2).  The full and wide kernels record the largest over the
+// sub-steps they ran as the tier the env's next gym step starts in, so envs that stay heavy
+// (pads pressed, a grasped cube) skip the compact tier and its hand-over wait.  A hint only: a
+// wrong guess costs time (a hand-over, or a light env in a bigger tier), never results.
+// tier byte: bits 0-1 the tier this step started in (read by every pass, stable for the whole
+// step: the routed passes run concurrently), bits 2-3 the next one with bit 4 set once a pass
+// has written it; route_commit_kernel moves it down after the step's last pass.
+// Compact gym capacities (env_compact.hip) and full ones (phys_model.h), checked in those TUs.
+#define PNP_GC_MAXCON 20
+#define PNP_GC_MAXEFC 96
+#define PNP_GC_MAXJSLOT 800
+#define PNP_GC_JTCAP 768
+#define PNP_GC_HCAP 288
+#define PNP_GF_MAXCON 48
+#define PNP_GF_MAXEFC 208
+#define PNP_GF_MAXJSLOT 2048
+#define PNP_GF_JTCAP 1536
+template <typename T>
+__device__ __forceinline__ int tier_need(const DevPhys<T>& m, const Env<T>& s) {
+  const int ne = s.nefc, nc = s.ncon_raw;
+  const int slots = ne ? s.efc_off[ne - 1] + row_width(m, s.efc_t0[ne - 1], s.efc_t1[ne - 1]) : 0;
+  const int nis = ne ? s.nisland : 0;
+  const int l = lane_id();
+  const bool big = __ballot(l < nis && s.isl_roff[l + 1] - s.isl_roff[l] > PNP_BIG_ROWS - 4) != 0;
+  const int jt = nis ? s.isl_joff[nis] : 0, he = nis ? s.isl_eoff[nis] : 0;
+  if (5 * nc <= 4 * PNP_GC_MAXCON && 5 * ne <= 4 * PNP_GC_MAXEFC && 5 * slots <= 4 * PNP_GC_MAXJSLOT && !big &&
+      5 * jt <= 4 * PNP_GC_JTCAP && 5 * he <= 4 * PNP_GC_HCAP)
+    return 0;
+  if (6 * nc <= 5 * PNP_GF_MAXCON && 6 * ne <= 5 * PNP_GF_MAXEFC && 6 * slots <= 5 * PNP_GF_MAXJSLOT &&
+      6 * jt <= 5 * PNP_GF_JTCAP)
+    return 1;
+  return 2;
+}
+
 // Tiers (step.hip): the full build runs the whole gym step; with hand = 1 a physics sub-step that
 // would overflow its capacity stops the env before that sub-step changes the state (controls and
 // state stored, resume bits in warn, no epilogue), and the wide build's resume pass (resume = 1)
@@ -304,13 +342,15 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_r
 template <typename T>
 __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
                                                       pnp_env_params prm, EnvSoA<T> es, const T* __restrict__ action,
-                                                      EnvOutT<T> out, int B, int resume, int hand) {
+                                                      EnvOutT<T> out, int B, int resume, int hand, int only_tier) {
   __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
   Env<T>& s = s_env;
   const DevPhys<T>& m = phys<T>();
   (void)mp;
   const int b = blockIdx.x;
   if (b >= B) return;
+  const int cur = es.tier ? (es.tier[b] & 3) : 0;
+  if (only_tier >= 0 && es.tier && cur != only_tier) return;   // routed to another tier's pass
   const int l = lane_id();
   int k0 = 0;
   if (resume) {
@@ -351,7 +391,12 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
   NoClock clk;
   const int nsub = prm.n_substeps * prm.n_calls;
   int k = k0;
-  for (; k < nsub && !(PNP_HANDS && s.ovf); k++) mj_step_dev(m, s, clk, k == nsub - 1 ? s.qpos_pre : nullptr);
+  const bool track = !PNP_COMPACT && es.tier;
+  int need_tier = 0;
+  for (; k < nsub && !(PNP_HANDS && s.ovf); k++) {
+    mj_step_dev(m, s, clk, k == nsub - 1 ? s.qpos_pre : nullptr);
+    if (track && !(PNP_HANDS && s.ovf)) need_tier = max(need_tier, tier_need(m, s));
+  }
   if (PNP_HANDS && s.ovf) {   // sub-step k - 1 overflowed before changing the state: hand over
     if (l == 0)
       s.warn |= PNP_RESUME_FLAG | ((uint32_t)s.ovf << PNP_RESUME_WHY_SHIFT) | ((uint32_t)(k - 1) << PNP_RESUME_SHIFT);
@@ -362,6 +407,7 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
   }
   store_env(m, s, st, b);
   store_controls(m, s, st, b);
+  if (track && l == 0) es.tier[b] = (uint8_t)(cur | need_tier << 2 | 0x10);
   const T width = s.qpos[prm.finger_qadr[0]] + s.qpos[prm.finger_qadr[1]];
   if (l < m.nq) es.qpos_kin[(size_t)b * m.nq + l] = s.qpos_pre[l];
   // ---- _get_obs at data.site_* (kinematics of qpos_pre) with the integrated qvel
@@ -426,13 +472,23 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
   }
 }
 
+#if !PNP_COMPACT && !PNP_WIDE
+__global__ void route_commit_kernel(uint8_t* __restrict__ tier, int B) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) {
+    const uint8_t t = tier[i];
+    if (t & 0x10) tier[i] = (uint8_t)((t >> 2) & 3);
+  }
+}
+#endif
+
 }  // namespace PNP_NS
 
 // ---------------------------------------------------------------- host launchers
 template <typename T>
 static EnvSoA<T> env_view(const pnp_env_state* e) {
   return EnvSoA<T>{(T*)e->goal, e->task, e->elapsed, (T*)e->qpos_kin, (T*)e->obj_height0, (T*)e->init_mocap,
-                   (T*)e->init_qvel, (T*)e->init_time, e->episode, e->env_index};
+                   (T*)e->init_qvel, (T*)e->init_time, e->episode, e->env_index, e->tier};
 }
 template <typename T>
 static EnvOutT<T> out_view(const pnp_env_out* o) {
@@ -444,7 +500,7 @@ static EnvOutT<T> out_view(const pnp_env_out* o) {
 #if PNP_COMPACT
 int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
                                 const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
-                                void* stream) {
+                                void* stream, int only_tier) {
   const DevPhys<float>* src = phys_image<float>(model);
   if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
   ResidentLease lease;
@@ -452,17 +508,18 @@ int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>
                                        sizeof(DevPhys<float>), stream))
     return rc;
   hipLaunchKernelGGL(env_step_kernel<float>, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, *p,
-                     env_view<float>(e), action, out_view<float>(o), B, 0, 1);
+                     env_view<float>(e), action, out_view<float>(o), B, 0, 1, only_tier);
   if (const int32_t rc = pnp_check_launch("env_step_kernel (compact)")) return rc;
   return lease.launched();
 }
 int32_t env_compact_lds_bytes() { return (int32_t)sizeof(Env<float>); }
 #elif PNP_WIDE
-// wide tier: resume pass of the gym step over the envs the full kernel handed over (launched by
-// the full build's launch_env_step, which holds the full image's lease)
+// wide tier: resume pass of the gym step over the envs the full kernel handed over (resume = 1),
+// or the routed pass over the envs whose step starts in the wide tier (resume = 0, only_tier = 2);
+// launched by the full build's launch_env_step, which holds the full image's lease
 int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
                              const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
-                             void* stream) {
+                             void* stream, int resume, int only_tier) {
   const DevPhys<float>* src = phys_image<float>(model);
   if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
   ResidentLease lease;
@@ -470,8 +527,8 @@ int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* s
                                        stream))
     return rc;
   hipLaunchKernelGGL(env_step_kernel<float>, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, *p,
-                     env_view<float>(e), action, out_view<float>(o), B, 1, 0);
-  if (const int32_t rc = pnp_check_launch("env_step_kernel (wide resume)")) return rc;
+                     env_view<float>(e), action, out_view<float>(o), B, resume, 0, only_tier);
+  if (const int32_t rc = pnp_check_launch("env_step_kernel (wide)")) return rc;
   return lease.launched();
 }
 #else
@@ -541,6 +598,39 @@ static int32_t launch_env_reset(pnp_model* model, const pnp_state_t<T>* st, cons
   if ((rc = pnp_check_launch("env_reset_kernel"))) return rc;
   return lease.launched();
 }
+// PNP_GYM_ROUTE: unset / 1 = with an env_state.tier buffer, envs start their fp32 gym step in the
+// tier their last step finished in (default); 0 = every env starts in the compact tier (A/B runs)
+static bool gym_route_enabled() {
+  const char* e = getenv("PNP_GYM_ROUTE");
+  return !(e && e[0] == '0');
+}
+// Two side streams per device for the routed passes, forked from and joined back into the
+// caller's stream.  Used only while the full image's lease is held (launch_env_step), which
+// serialises their users per device; creation has its own lock.
+struct RouteStreams {
+  hipStream_t side[2] = {nullptr, nullptr};
+  hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+};
+static int32_t route_streams(RouteStreams** out) {
+  static std::mutex mu;
+  static RouteStreams rs[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { pnp_set_error("pnp_env_step: bad device"); return PNP_ERR_HIP; }
+  std::lock_guard<std::mutex> lk(mu);
+  RouteStreams& r = rs[dev];
+  hipError_t e = hipSuccess;
+  // (neither wave priority, s_setprio, for the routed passes nor the highest stream priority
+  // shortened the routed wide pass: its span is the heaviest env's own chain of sub-steps)
+  for (int i = 0; i < 2 && e == hipSuccess; i++) {
+    if (!r.side[i]) e = hipStreamCreateWithFlags(&r.side[i], hipStreamNonBlocking);
+    if (e == hipSuccess && !r.join[i]) e = hipEventCreateWithFlags(&r.join[i], hipEventDisableTiming);
+  }
+  if (e == hipSuccess && !r.fork) e = hipEventCreateWithFlags(&r.fork, hipEventDisableTiming);
+  if (e != hipSuccess) { pnp_set_error("pnp_env_step: route streams: %s", hipGetErrorString(e)); return PNP_ERR_HIP; }
+  *out = &r;
+  return PNP_OK;
+}
+
 template <typename T>
 static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const pnp_env_params* p,
                                const pnp_env_state* e, const T* action, const pnp_env_out* o, int32_t B,
@@ -558,16 +648,43 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   const int wide = tiers && wide_enabled();
   const bool compact = tiers && gym_compact_enabled();
   const auto* st32 = reinterpret_cast<const pnp_state_t<float>*>(st);
-  if (compact && (rc = launch_env_step_compact(model, st32, p, e, reinterpret_cast<const float*>(action), o, B,
-                                               stream)))
-    return rc;
+  const float* a32 = reinterpret_cast<const float*>(action);
+  const hipStream_t s0 = (hipStream_t)stream;
+  // routed: the envs whose last step finished in the full / wide tier start there, on side streams
+  // concurrent with the compact pass; the resume passes then only see this step's new hand-overs
+  const bool route = compact && wide && gym_compact_mode() == 1 && e->tier && gym_route_enabled();
+  RouteStreams* rs = nullptr;
+  if (route) {
+    if ((rc = route_streams(&rs))) return rc;
+    hipError_t he = hipEventRecord(rs->fork, s0);   // after the full image's copy and the last step
+    for (int i = 0; i < 2 && he == hipSuccess; i++) he = hipStreamWaitEvent(rs->side[i], rs->fork, 0);
+    if (he != hipSuccess) { pnp_set_error("pnp_env_step: fork: %s", hipGetErrorString(he)); return PNP_ERR_HIP; }
+    if ((rc = launch_env_step_wide(model, st32, p, e, a32, o, B, rs->side[1], 0, 2))) return rc;
+    hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, rs->side[0], dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
+                       0, wide, 1);
+    if ((rc = pnp_check_launch("env_step_kernel (full, routed)"))) return rc;
+  }
+  if (compact && (rc = launch_env_step_compact(model, st32, p, e, a32, o, B, stream, route ? 0 : -1))) return rc;
   if (compact && gym_compact_mode() == 2) return lease.launched();
-  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), action,
-                     out_view<T>(o), B, compact ? 1 : 0, wide);
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, s0, dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
+                     compact ? 1 : 0, wide, route ? 0 : -1);
   if ((rc = pnp_check_launch("env_step_kernel"))) return rc;
-  if (wide && (rc = launch_env_step_wide(model, st32, p, e, reinterpret_cast<const float*>(action), o, B, stream)))
-    return rc;
-  return lease.launched();
+  if (route) {   // the wide resume pass also takes the routed full pass's hand-overs
+    hipError_t he = hipEventRecord(rs->join[0], rs->side[0]);
+    if (he == hipSuccess) he = hipStreamWaitEvent(s0, rs->join[0], 0);
+    if (he != hipSuccess) { pnp_set_error("pnp_env_step: join: %s", hipGetErrorString(he)); return PNP_ERR_HIP; }
+  }
+  if (wide && (rc = launch_env_step_wide(model, st32, p, e, a32, o, B, stream, 1, -1))) return rc;
+  if (route) {
+    hipError_t he = hipEventRecord(rs->join[1], rs->side[1]);
+    if (he == hipSuccess) he = hipStreamWaitEvent(s0, rs->join[1], 0);
+    if (he != hipSuccess) { pnp_set_error("pnp_env_step: join: %s", hipGetErrorString(he)); return PNP_ERR_HIP; }
+  }
+  if (e->tier) {   // every pass has run: the next step's tiers become current
+    hipLaunchKernelGGL(route_commit_kernel, dim3((B + 255) / 256), dim3(256), 0, s0, e->tier, B);
+    if ((rc = pnp_check_launch("route_commit_kernel"))) return rc;
+  }
+  return lease.launched();   // recorded on the caller's stream, after both joins
 }
 
 extern "C" int32_t pnp_env_params_size(void) { return (int32_t)sizeof(pnp_env_params); }

@@ -111,12 +111,12 @@ int32_t launch_step_wide(const pnp_model* model, const pnp_state_t<float>* st, i
                          void* stream, unsigned long long* prof, int resume);
 int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
                              const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
-                             void* stream);
+                             void* stream, int resume, int only_tier);
 int32_t step_wide_lds_bytes();
 // env_compact.hip: the compact tier of the fp32 gym step (every env from sub-step 0)
 int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
                                 const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
-                                void* stream);
+                                void* stream, int only_tier);
 int32_t env_compact_lds_bytes();
 
 // ---------------------------------------------------------------------------- error plumbing

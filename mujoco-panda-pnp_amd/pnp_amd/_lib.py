@@ -47,7 +47,7 @@ class PnpEnvParams(C.Structure):
 
 
 ENV_STATE_FIELDS = ("goal", "task", "elapsed", "qpos_kin", "obj_height0", "init_mocap", "init_qvel", "init_time",
-                    "episode", "env_index")
+                    "episode", "env_index", "tier")
 ENV_OUT_FIELDS = ("obs", "achieved_goal", "desired_goal", "reward", "is_success", "terminated", "truncated")
 
 

@@ -121,7 +121,8 @@ class BatchedFrankaShelfPNPEnv:
         self.env = dict(goal=z(B, 3), task=z(B, d=torch.int32), elapsed=z(B, d=torch.int32),
                         qpos_kin=z(B, m.nq), obj_height0=z(B), init_mocap=z(B, 7), init_qvel=z(B, m.nv),
                         init_time=z(B), episode=z(B, d=torch.int32),
-                        env_index=torch.arange(env_offset, env_offset + B, dtype=torch.int32, device=dev))
+                        env_index=torch.arange(env_offset, env_offset + B, dtype=torch.int32, device=dev),
+                        tier=z(B, d=torch.uint8))   # fp32 routing hint (include/pnp.h pnp_env_state.tier)
         self.out = dict(obs=z(B, _lib.OBS_DIM), achieved_goal=z(B, 3), desired_goal=z(B, 3), reward=z(B),
                         is_success=z(B), terminated=z(B, d=torch.uint8), truncated=z(B, d=torch.uint8))
         self._S, _, _ = self.engine._state_struct(self.state)

@@ -137,11 +137,12 @@ def test_gym_step_wide_tier_pressed_fingers(model):
     assert int((g.state["warn"] & 0xFFFF).max()) == 0 and not o.st["warn"].any()
 
 
-def _gym_run(mode, B, nsteps, pressed=False):
+def _gym_run(mode, B, nsteps, pressed=False, route="1", tiers=None):
     import os
     from pnp_amd.envs import BatchedFrankaShelfPNPEnv
-    old = os.environ.get("PNP_GYM_COMPACT")
+    old = {k: os.environ.get(k) for k in ("PNP_GYM_COMPACT", "PNP_GYM_ROUTE")}
     os.environ["PNP_GYM_COMPACT"] = mode
+    os.environ["PNP_GYM_ROUTE"] = route
     try:
         g = BatchedFrankaShelfPNPEnv(B, autoreset=True)
         g.reset()
@@ -153,13 +154,16 @@ def _gym_run(mode, B, nsteps, pressed=False):
             a = torch.as_tensor(rng.uniform(-1, 1, size=(B, 7)), dtype=torch.float32, device="cuda")
             obs, r, term, trunc, info = g.step(a)
             outs.append((obs["observation"].clone(), r.clone(), term.clone(), trunc.clone(), info["is_success"].clone()))
+            if tiers is not None:
+                tiers.append(g.env["tier"].clone())
         torch.cuda.synchronize()
         return g, outs
     finally:
-        if old is None:
-            del os.environ["PNP_GYM_COMPACT"]
-        else:
-            os.environ["PNP_GYM_COMPACT"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
 def test_gym_compact_tier_is_exact():
@@ -174,7 +178,30 @@ def test_gym_compact_tier_is_exact():
     for k in a.state:
         assert torch.equal(a.state[k], b.state[k]), k
     for k in a.env:
-        assert torch.equal(a.env[k], b.env[k]), k
+        if k != "tier":   # where the next step starts (a routing hint, not env state)
+            assert torch.equal(a.env[k], b.env[k]), k
+    w = a.state["warn"].to(torch.int64) & 0xFFFFFFFF
+    assert not bool((w >> 16).any()) and int((w & 0xFFFF).max()) == 0
+
+
+def test_gym_routing_is_exact():
+    """Routed gym steps (env_dev.h: envs whose last step finished in the full / wide tier start
+    there, on side streams concurrent with the compact pass) are bit-identical to every env
+    starting in the compact tier, and the routing engages on a batch with pressed pads."""
+    tiers = []
+    a, oa = _gym_run("1", 96, 4, pressed=True, route="1", tiers=tiers)
+    b, ob = _gym_run("1", 96, 4, pressed=True, route="0")
+    for x, y in zip(oa, ob):
+        for u, v in zip(x, y):
+            assert torch.equal(u, v)
+    for k in a.state:
+        assert torch.equal(a.state[k], b.state[k]), k
+    for k in a.env:
+        if k != "tier":
+            assert torch.equal(a.env[k], b.env[k]), k
+    for t in tiers:
+        assert int(t.max()) <= 2                        # committed: no pending bits left
+    assert any(bool((t[::3] > 0).any()) for t in tiers[:-1])   # pressed envs routed past compact
     w = a.state["warn"].to(torch.int64) & 0xFFFFFFFF
     assert not bool((w >> 16).any()) and int((w & 0xFFFF).max()) == 0
 
