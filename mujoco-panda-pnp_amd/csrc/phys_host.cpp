@@ -152,15 +152,6 @@ int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
       ne++;
     }
   d->nmentry = ne;
-  {   // damp_tree (phys_model.h)
-    int nd = 0, td = -1;
-    for (int t = 0; t < ntree; t++) {
-      bool damped = false;
-      for (int i = 0; i < d->tree_dofnum[t]; i++) damped |= s->dof_damping[d->tree_dofadr[t] + i] != 0;
-      if (damped) { nd++; td = t; }
-    }
-    d->damp_tree = nd == 0 ? -1 : (nd == 1 && d->tree_dofnum[td] <= 9 && ntree < 7) ? td : -2;
-  }
   // ---- collidable geoms + pairs
   int ng = 0, map[512];
   for (int g = 0; g < s->ngeom && g < 512; g++) {

@@ -78,10 +78,6 @@ struct DevPhys {
   // trees
   int tree_dofadr[PH_MAXT], tree_dofnum[PH_MAXT], tree_moff[PH_MAXT];   // M stored as per-tree dense blocks
   int nmblock;                                                         // sum of tree_dofnum^2
-  // the Euler stage's implicit damping: the one tree with nonzero dof damping, when it has <= 9
-  // dofs and a spare 9-lane group in st_factor_M (which then factors its M + h D beside M);
-  // -1: no damped tree; -2: anything else (the Euler stage factors M + h D itself)
-  int damp_tree;
   // collidable geoms (compact ids 0..ngeom-1; geom_id = index in the full model)
   int geom_id[PH_MAXG], geom_type[PH_MAXG], geom_bodyid[PH_MAXG], geom_dataid[PH_MAXG];
   int geom_condim[PH_MAXG], geom_priority[PH_MAXG];

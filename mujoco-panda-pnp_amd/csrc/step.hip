@@ -186,7 +186,6 @@ struct Env {
   };
   T M[PH_MAXMBLK];    // per-tree dense blocks
   T L[PH_MAXMBLK];    // Cholesky factors of the blocks
-  T Ldamp[45];        // factor of M + h D for the damped tree (phys damp_tree), packed lower
   // ---- vectors
 #if !PNP_LEAN
   T qfrc_bias[PH_MAXV], qfrc_passive[PH_MAXV], qfrc_act[PH_MAXV];
@@ -930,31 +929,21 @@ __device__ __forceinline__ void st_factor_M(const DevPhys<T>& /*image: phys<T>()
   const DevPhys<T>& m = phys<T>();
   const int t = lane_id();
   if (m.ntree <= GCH_GROUPS && !__ballot(t < m.ntree && s.c_tree_dofnum[t] > GCH_N)) {
-    // every tree block on its own 9-lane group; the next spare group factors the damped tree's
-    // M + h D for the Euler stage (the same inputs and operations as that stage's own factor)
+    // every tree block on its own 9-lane group
     const int g = gch_group(t), r = t - GCH_N * g;
-    const bool dg = m.damp_tree >= 0 && g == m.ntree;
-    const int tg = dg ? m.damp_tree : g;
-    const bool on = g < m.ntree || dg;
-    const int n = on ? s.c_tree_dofnum[tg] : 0, o = on ? s.c_tree_moff[tg] : 0, a = on ? s.c_tree_dofadr[tg] : 0;
-    const T h = m.timestep;
+    const bool on = g < m.ntree;
+    const int n = on ? s.c_tree_dofnum[g] : 0, o = on ? s.c_tree_moff[g] : 0;
     T Lrow[GCH_N], Ad[GCH_N], P[45];
 #pragma unroll
     for (int j = 0; j < GCH_N; j++) {
-      Lrow[j] = r < n && j <= r ? (dg && j == r ? s.M[o + r * n + j] + h * m.dof_damping[a + r] : s.M[o + r * n + j])
-                                : T(r == j);
-      Ad[j] = j < n ? (dg ? s.M[o + j * n + j] + h * m.dof_damping[a + j] : s.M[o + j * n + j]) : T(1);
+      Lrow[j] = r < n && j <= r ? s.M[o + r * n + j] : T(r == j);
+      Ad[j] = j < n ? s.M[o + j * n + j] : T(1);
     }
     gch_factor(Lrow, Ad, r, GCH_N * g, P);
-    if (dg) {   // lane r holds row r of the factor (identity rows past n), = the packed P
-#pragma unroll
-      for (int j = 0; j < GCH_N; j++)
-        if (j <= r && r < GCH_N) s.Ldamp[r * (r + 1) / 2 + j] = Lrow[j];
-    } else if (r < n) {
+    if (r < n)
 #pragma unroll
       for (int j = 0; j < GCH_N; j++)
         if (j <= r) s.L[o + r * n + j] = Lrow[j];
-    }
     wsync();
     return;
   }
@@ -2915,26 +2904,14 @@ __device__ void st_euler(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s) {
     const int g = gch_group(l), r = l - GCH_N * g, base = GCH_N * g;
     const bool on = g < m.ntree;
     const int n = on ? s.c_tree_dofnum[g] : 0, o = on ? s.c_tree_moff[g] : 0, a = on ? s.c_tree_dofadr[g] : 0;
-    T P[45], y[GCH_N];
+    T Lrow[GCH_N], Ad[GCH_N], P[45], y[GCH_N];
 #pragma unroll
-    for (int j = 0; j < GCH_N; j++) y[j] = T(0);
-    if (m.damp_tree != -2) {
-      // the factors st_factor_M made: M + h D of the damped tree, M itself (= M + h 0) for the others
-      const bool dg = g == m.damp_tree;
-#pragma unroll
-      for (int i = 0; i < GCH_N; i++)
-#pragma unroll
-        for (int j = 0; j <= i; j++)
-          P[i * (i + 1) / 2 + j] = dg ? s.Ldamp[i * (i + 1) / 2 + j] : i < n ? s.L[o + i * n + j] : T(i == j);
-    } else {
-      T Lrow[GCH_N], Ad[GCH_N];
-#pragma unroll
-      for (int j = 0; j < GCH_N; j++) {
-        Lrow[j] = r < n && j <= r ? s.M[o + r * n + j] + (j == r ? h * m.dof_damping[a + r] : T(0)) : T(r == j);
-        Ad[j] = j < n ? s.M[o + j * n + j] + h * m.dof_damping[a + j] : T(1);
-      }
-      gch_factor(Lrow, Ad, r, base, P);
+    for (int j = 0; j < GCH_N; j++) {
+      y[j] = T(0);
+      Lrow[j] = r < n && j <= r ? s.M[o + r * n + j] + (j == r ? h * m.dof_damping[a + r] : T(0)) : T(r == j);
+      Ad[j] = j < n ? s.M[o + j * n + j] + h * m.dof_damping[a + j] : T(1);
     }
+    gch_factor(Lrow, Ad, r, base, P);
     chol_solve_reg<T, GCH_N>(P, n, y, s.v1 + a);
     T x = 0;
 #pragma unroll
