@@ -173,7 +173,7 @@ def run_step(args, engine, model, rank, world, dist):
 
     elapsed, kern_ms = _timed(fn, args.steps, args.warmup, dist)
     _progress(rank, f"step leg done: {total_steps(B, world, args.steps) / elapsed / 1e6:.2f} M env-steps/s")
-    warn = int(st["warn"].max())
+    warn = int((st["warn"].to(torch.int64) & 0xFFFFFFFF).max())   # warn is int32: bit 31 reads negative
     finite = bool(torch.isfinite(st["qpos"]).all())
     total = B * world * args.steps * NSUB
     achieved = STEP_BYTES_PER_ENV * B / (kern_ms * 1e-3) / 1e9

@@ -211,7 +211,7 @@ def test_full_size_deterministic_and_shard_invariant(engine, scene):
         assert torch.equal(a[k], b[k]), k
         assert torch.equal(a[k], torch.cat([lo[k], hi[k]])), k
     assert torch.isfinite(a["qpos"]).all() and torch.isfinite(a["qvel"]).all()
-    assert int(a["warn"].max()) == 0
+    assert not bool(a["warn"].ne(0).any())   # (int32: a leaked bit 31 reads negative)
     # replicated envs stay replicas (no cross-env coupling)
     n = scene["qpos"].shape[0]
     assert torch.equal(a["qpos"][:n], a["qpos"][n:2 * n])
@@ -228,7 +228,7 @@ def test_bench_workload_runs_clean(engine, model):
         st["ctrl"] = ctrl[i]
         engine.step(st, bench.NSUB)
     torch.cuda.synchronize()
-    assert int(st["warn"].max()) == 0
+    assert not bool(st["warn"].ne(0).any())   # (int32: a leaked bit 31 reads negative)
     assert torch.isfinite(st["qpos"]).all() and torch.isfinite(st["qvel"]).all()
     d = engine.forward_debug(st)
     D = _lib.DBG
