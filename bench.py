@@ -122,6 +122,14 @@ def _traffic(name, B):
     return None, None
 
 
+def _sq_valu():
+    f = os.path.join(ROOT, "profiles", "sq_counters_step.json")
+    if os.path.exists(f):
+        with open(f) as fh:
+            return json.load(fh).get("valu_issue_frac")
+    return None
+
+
 # ----------------------------------------------------------------------------- C3 / C4 env-step
 def step_inputs(engine, model, rank, B):
     idx = shard_range(rank, B)
@@ -201,7 +209,10 @@ def run_step(args, engine, model, rank, world, dist):
                      # (one or two waves per SIMD, dependent LDS / DPP chains): PMC-measured
                      # bandwidth of the same launch, for scale
                      "pmc_GBps": (traffic / (kern_ms * 1e-3) / 1e9) if traffic else None,
-                     "limiter": "latency (resident waves x cycles per env-sub-step), not HBM"},
+                     # SQ counters of the same kernel (profiles/sq_counters_step.json): the share
+                     # of cycles the SIMDs' vector ALUs issue, all resident waves together
+                     "valu_issue_frac": _sq_valu(),
+                     "limiter": "latency and instruction issue (resident waves x cycles per env-sub-step), not HBM"},
         "state_ok": {"max_warn": warn, "finite": finite},
         "host_cores": len(os.sched_getaffinity(0)),
     }

@@ -17,5 +17,5 @@ for P in "$P1" "$P2"; do
   rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$OUT/${TAG}_p$i.log"; exit $rc; }
 done
 cd "$ROOT"
-python3 tools/sq_summary.py "$OUT/${TAG}_p1" "$OUT/${TAG}_p2" "pnp_compact::step_kernel<float, false>" > "$OUT/${TAG}_summary.txt"
+python3 tools/sq_summary.py "$OUT/${TAG}_p1" "$OUT/${TAG}_p2" "pnp_compact::step_kernel<float, false>" --json "$OUT/${TAG}_sq.json" --waves-per-simd 2 > "$OUT/${TAG}_summary.txt"
 cat "$OUT/${TAG}_summary.txt"

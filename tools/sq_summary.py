@@ -1,5 +1,5 @@
 """Per-dispatch averages of rocprofv3 --pmc CSV counter collections for one kernel.
-usage: python tools/sq_summary.py <pass_dir> [<pass_dir> ...] <kernel-name-substring>"""
+usage: python tools/sq_summary.py <pass_dir> [<pass_dir> ...] <kernel-name-substring> [--json out.json --waves-per-simd N]"""
 import csv
 import glob
 import os
@@ -8,7 +8,17 @@ from collections import defaultdict
 
 
 def main():
-    dirs, kname = sys.argv[1:-1], sys.argv[-1]
+    argv = sys.argv[1:]
+    jpath, wps = None, 2
+    if "--json" in argv:
+        i = argv.index("--json")
+        jpath = argv[i + 1]
+        del argv[i:i + 2]
+    if "--waves-per-simd" in argv:
+        i = argv.index("--waves-per-simd")
+        wps = int(argv[i + 1])
+        del argv[i:i + 2]
+    dirs, kname = argv[:-1], argv[-1]
     tot = defaultdict(float)
     nd = defaultdict(set)
     for d in dirs:
@@ -37,6 +47,16 @@ def main():
                   "SQ_WAIT_INST_LDS"):
             if c in per:
                 print(f"  {c} / SQ_WAVE_CYCLES = {per[c] / wc:.3f}")
+    if jpath and wc and "SQ_ACTIVE_INST_VALU" in per:
+        import json
+        rec = {"kernel": kname, "waves_per_simd": wps,
+               "wave_frac": {c: per[c] / wc for c in ("SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS",
+                                                     "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY") if c in per},
+               "insts_per_wave": {c: per[c] / w for c in per if c.startswith("SQ_INSTS_") and w},
+               # the SIMD's vector ALU: each resident wave keeps it busy its own ACTIVE_INST_VALU share
+               "valu_issue_frac": min(1.0, wps * per["SQ_ACTIVE_INST_VALU"] / wc),
+               "source": "rocprofv3 --pmc SQ_* (two passes of 8 SQ counters), tools/gpu_sq.sh"}
+        json.dump(rec, open(jpath, "w"), indent=1)
 
 
 if __name__ == "__main__":
