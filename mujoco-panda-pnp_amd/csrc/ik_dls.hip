@@ -248,8 +248,14 @@ __global__ void __launch_bounds__(64) ik_dls_kernel(IKSeg<T> c, int max_iters, T
                        ((converged && err < thr * T(2)) ? PNP_IK_SUCCESS : 0u));
 }
 
-// ---------------------------------------------------------------------------- 8-lane groups
-// ik_dls_group_kernel: one solve per 8-lane group (8 solves per wave), lane j < 7 owns joint j.
+// ---------------------------------------------------------------------------- lane groups
+// ik_dls_group_kernel: one solve per 16-lane DPP row (4 solves per wave), lane j < 7 owns joint
+// j, lane 7 the site, lanes 8..15 run along unused.  (v4 packed 8 solves per wave on 8-lane
+// groups; then the row_shr of the scan leaked the neighbouring group's frames into lanes 8..8+O-1
+// and every one of the 12 received entries needed a select.  With a group per row the lanes
+// without a source are exactly j < O and the DPP's zero fill supplies the identity's zeros: 27
+// fewer instructions per iteration, and 4096 solves make 1024 waves -- one per SIMD -- instead of
+// 512 on half the SIMDs.)
 // The thread-per-solve kernel above is latency-bound: a batch of 4096 solves is 64 waves on
 // 64 CUs, and the launch lasts as long as the slowest solve (up to max_iters iterations), each
 // iteration one long dependent chain (7 joint rotations composed in order, then the Jacobian, the
@@ -259,20 +265,21 @@ __global__ void __launch_bounds__(64) ik_dls_kernel(IKSeg<T> c, int max_iters, T
 //   * the world frames G_j = A_0 ... A_j are an inclusive prefix product over the group
 //     (Hillis-Steele, 3 DPP row_shr steps); lane 7 ends up holding the site position;
 //   * anchor_j = p(G_j), axis_j = sgn_j R(G_j) e_z (Rz leaves both unchanged, as in ik_fk);
-//   * J J^T is 6 three-step DPP sums over the group (J column j on lane j), the 3 x 3 solve runs
+//   * J J^T is 6 three-step DPP sums over lanes 0..7 (J column j on lane j), the 3 x 3 solve runs
 //     redundantly on every lane, and dq_j = J_j^T y is lane-local.
 // The reference's control flow is kept per group (convergence test before the update, the final
 // position measured after the last update); groups that have stopped are predicated off.  Same
 // formulas as the serial kernel; the frame products associate differently (prefix tree instead
 // of the left-to-right chain), so results agree to rounding (fp64: ~1e-16 relative).
-template <int CTRL, typename T>
+// ZERO: a lane whose DPP source is outside its row (row_shr:O, lanes 0..O-1) reads 0 (bound_ctrl)
+template <int CTRL, typename T, bool ZERO = false>
 __device__ __forceinline__ T gdpp(T v) {
   if constexpr (sizeof(T) == 4) {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, ZERO));
   } else {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffff), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffff), CTRL, 0xF, 0xF, ZERO);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, ZERO);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
   }
 }
@@ -284,30 +291,30 @@ __device__ __forceinline__ T gsum8(T v) {
   v += gdpp<0x141>(v);   // row_half_mirror: the other quad of the group
   return v;
 }
-// lane 7 of the group to every lane of the group (DPP row_newbcast of lanes 7 and 15 of the row)
+// lane 7 of the group (= of its DPP row) to every lane of the row (row_newbcast:7)
 template <typename T>
-__device__ __forceinline__ T gbcast7(T v, bool upper) {
-  const T a = gdpp<0x157>(v), b = gdpp<0x15F>(v);
-  return upper ? b : a;
+__device__ __forceinline__ T gbcast7(T v) {
+  return gdpp<0x157>(v);
 }
-// one Hillis-Steele step: G_j <- G_{j-O} G_j for j >= O (row_shr:O inside the row of 16).  A
-// lane j < O composes with the identity instead (1 x + 0 y + 0 z + 0 is x exactly for finite
-// values), so every lane runs the same straight-line code; the value it would receive comes from
-// the neighbouring group and is replaced.
+// one Hillis-Steele step: G_j <- G_{j-O} G_j for j >= O (row_shr:O inside the group's row of
+// 16).  A lane j < O has no DPP source in its row and composes with the identity instead (1 x +
+// 0 y + 0 z + 0 is x exactly for finite values), so every lane runs the same straight-line code:
+// the identity's zeros come from the DPP's bound_ctrl zero fill, only its three ones need a select.
 template <int O, typename T>
 __device__ __forceinline__ void gscan_step(T R[9], T p[3], int j) {
   const bool take = j >= O;
   T X[9], xp[3];
 #pragma unroll
   for (int k = 0; k < 9; k++) {
-    const T v = gdpp<0x110 + O>(R[k]);
-    X[k] = take ? v : T(k == 0 || k == 4 || k == 8 ? 1 : 0);
+    if (k == 0 || k == 4 || k == 8) {
+      const T v = gdpp<0x110 + O>(R[k]);
+      X[k] = take ? v : T(1);
+    } else {
+      X[k] = gdpp<0x110 + O, T, true>(R[k]);
+    }
   }
 #pragma unroll
-  for (int k = 0; k < 3; k++) {
-    const T v = gdpp<0x110 + O>(p[k]);
-    xp[k] = take ? v : T(0);
-  }
+  for (int k = 0; k < 3; k++) xp[k] = gdpp<0x110 + O, T, true>(p[k]);
   T N[9], np[3];
 #pragma unroll
   for (int r = 0; r < 3; r++) {
@@ -323,7 +330,7 @@ __device__ __forceinline__ void gscan_step(T R[9], T p[3], int j) {
 
 // frames of the group at its joint angles: lane j -> (anchor_j, axis_j); every lane -> site
 template <typename T>
-__device__ __forceinline__ void gfk(const T Rp[9], const T pp[3], T sg, T q0, T qj, bool joint, bool upper, int j,
+__device__ __forceinline__ void gfk(const T Rp[9], const T pp[3], T sg, T q0, T qj, bool joint, int j,
                                     T anchor[3], T axis[3], T site[3]) {
   T s, c;
   KMath<T>::sincos(qj - q0, &s, &c);   // lane 7: sincos(0), and sg = 0
@@ -342,7 +349,7 @@ __device__ __forceinline__ void gfk(const T Rp[9], const T pp[3], T sg, T q0, T 
   anchor[0] = p[0]; anchor[1] = p[1]; anchor[2] = p[2];
   axis[0] = sg * R[2]; axis[1] = sg * R[5]; axis[2] = sg * R[8];
 #pragma unroll
-  for (int k = 0; k < 3; k++) site[k] = gbcast7(p[k], upper);
+  for (int k = 0; k < 3; k++) site[k] = gbcast7(p[k]);
 }
 
 template <typename T>
@@ -352,11 +359,11 @@ __global__ void __launch_bounds__(64) ik_dls_group_kernel(IKSeg<T> c, int max_it
                                                           T* __restrict__ pos_error, int32_t* __restrict__ iterations,
                                                           uint8_t* __restrict__ flags, int B) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int b = t >> 3, j = t & 7;
+  const int b = t >> 4, j = t & 15;
   const bool valid = b < B;          // (a partial group past B runs along, predicated off)
   const bool joint = j < 7;
-  const bool upper = (threadIdx.x & 8) != 0;
-  // this lane's joint constants (lane 7: the site offset, no rotation)
+  // this lane's joint constants (lane 7: the site offset, no rotation; lanes 8..15 likewise --
+  // they run along and are never read: the group sums cover lanes 0..7 of the row)
   T Rp[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, pp[3] = {c.psite[0], c.psite[1], c.psite[2]};
   T sg = 0, lo = 0, hi = 0, q0 = 0;
 #pragma unroll
@@ -373,10 +380,13 @@ __global__ void __launch_bounds__(64) ik_dls_group_kernel(IKSeg<T> c, int max_it
   T tg[3] = {0, 0, 0};
   if (valid) { tg[0] = target[(size_t)b * 3]; tg[1] = target[(size_t)b * 3 + 1]; tg[2] = target[(size_t)b * 3 + 2]; }
   T anchor[3], axis[3], site[3];
-  gfk(Rp, pp, sg, q0, q, joint, upper, j, anchor, axis, site);
   bool active = valid;
   int converged = 0, iters = 0;
+  // the frames are formed at the top of each iteration (and once more after the loop for the
+  // final position), so only q and the flags are carried around the loop: formed at the bottom,
+  // anchor / axis / site were loop-carried values the compiler copied on every back edge
   for (int i = 0; i < max_iters; i++) {
+    gfk(Rp, pp, sg, q0, q, joint, j, anchor, axis, site);
     const T e0 = tg[0] - site[0], e1 = tg[1] - site[1], e2 = tg[2] - site[2];
     const T n = KMath<T>::sqrt(e0 * e0 + e1 * e1 + e2 * e2);
     if (active && n < thr) {
@@ -385,11 +395,12 @@ __global__ void __launch_bounds__(64) ik_dls_group_kernel(IKSeg<T> c, int max_it
       active = false;
     }
     if (!__ballot(active)) break;
-    // jacp column j: axis_j x (site - anchor_j)
+    // jacp column j: axis_j x (site - anchor_j); lane 7's axis is sg R e_z = 0 (sg = 0), so its
+    // column is exactly zero without a select
     const T r0 = site[0] - anchor[0], r1 = site[1] - anchor[1], r2 = site[2] - anchor[2];
-    const T J0 = joint ? axis[1] * r2 - axis[2] * r1 : T(0);
-    const T J1 = joint ? axis[2] * r0 - axis[0] * r2 : T(0);
-    const T J2 = joint ? axis[0] * r1 - axis[1] * r0 : T(0);
+    const T J0 = axis[1] * r2 - axis[2] * r1;
+    const T J1 = axis[2] * r0 - axis[0] * r2;
+    const T J2 = axis[0] * r1 - axis[1] * r0;
     T A[9];
     A[0] = gsum8(J0 * J0) + damping;
     A[1] = A[3] = gsum8(J0 * J1);
@@ -404,8 +415,8 @@ __global__ void __launch_bounds__(64) ik_dls_group_kernel(IKSeg<T> c, int max_it
     const T qn = fmin(fmax(q + dq, lo), hi);
     q = (active && joint) ? qn : q;
     iters = active ? i + 1 : iters;
-    gfk(Rp, pp, sg, q0, q, joint, upper, j, anchor, axis, site);
   }
+  gfk(Rp, pp, sg, q0, q, joint, j, anchor, axis, site);
   if (!valid) return;
   const T d0 = site[0] - tg[0], d1 = site[1] - tg[1], d2 = site[2] - tg[2];
   const T err = KMath<T>::sqrt(d0 * d0 + d1 * d1 + d2 * d2);
@@ -541,8 +552,8 @@ static int32_t launch_ik(pnp_model* model, int32_t site, pnp_ik_params prm, cons
                        target, q_out, final_pos, pos_error, iterations, flags, B);
     return pnp_check_launch("ik_dls_kernel");
   }
-  // 8 lanes per solve: 8 solves per 64-lane block
-  hipLaunchKernelGGL(ik_dls_group_kernel<T>, dim3((B + 7) / 8), dim3(64), 0, (hipStream_t)stream, s,
+  // one DPP row (16 lanes) per solve: 4 solves per 64-lane block
+  hipLaunchKernelGGL(ik_dls_group_kernel<T>, dim3((B + 3) / 4), dim3(64), 0, (hipStream_t)stream, s,
                      prm.max_iters, (T)prm.pos_thresh, (T)prm.damping, (T)prm.step_limit, q_init, target,
                      q_out, final_pos, pos_error, iterations, flags, B);
   return pnp_check_launch("ik_dls_group_kernel");
