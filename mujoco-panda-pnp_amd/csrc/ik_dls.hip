@@ -61,7 +61,18 @@ __device__ __forceinline__ void fast_sincos(float x, float* s, float* c) {
 
 template <typename T> struct KMath;
 template <> struct KMath<float> {
+  // The hardware v_sin_f32 / v_cos_f32 (argument in revolutions: x * 1/(2 pi), rounded once, so
+  // <= 5e-7 rad absolute over the joint range |x| < 6.3) -- 3 instructions instead of the 27 of
+  // fast_sincos's reduction, polynomials and quadrant selects; the IK iteration is issue-bound on
+  // one wave per SIMD, so that is 8 % of the launch (69.2 -> 64.0 us per 4096 solves, iteration
+  // counts identical on both C2 regimes, profiles/r02/ik_v6_ab.log).  The fp32 parity bars hold:
+  // one DLS iteration within 1e-5 of the fp64 oracle, final_pos within 2e-6 m of the kinematics
+  // kernel (tests/test_ik_gpu.py).  -DPNP_IK_POLYSIN restores fast_sincos (A/B builds).
+#ifdef PNP_IK_POLYSIN
   static __device__ __forceinline__ void sincos(float x, float* s, float* c) { fast_sincos(x, s, c); }
+#else
+  static __device__ __forceinline__ void sincos(float x, float* s, float* c) { *s = __sinf(x); *c = __cosf(x); }
+#endif
   static __device__ __forceinline__ float sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
   static __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 };
