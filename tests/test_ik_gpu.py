@@ -155,6 +155,25 @@ def test_ik_f32_single_iteration(engine, model):
         np.testing.assert_allclose(out["pos_error"].double().cpu().numpy(), ref["pos_error"], atol=1e-5)
 
 
+def test_ik_f32_frames_over_joint_range(engine, model):
+    """The fp32 IK kernel's own forward kinematics (hardware v_sin_f32 / v_cos_f32, argument in
+    revolutions) over the whole joint range, not just the C2 input distribution: with
+    max_iters = 0 the kernel returns final_pos = FK(q_init) and flags 0.  Within 2e-6 m of the
+    fp64 oracle (the hardware sine's argument rounding is <= 5e-7 rad on |q| < 6.3)."""
+    rng = np.random.default_rng(7)
+    lo, hi = model.jnt_range[:7, 0], model.jnt_range[:7, 1]
+    q = rng.uniform(lo, hi, size=(4096, 7))
+    q[:7] = np.array([lo, hi, 0.5 * (lo + hi), lo + 1e-7, hi - 1e-7, np.zeros(7), model.qpos0[:7]])
+    q32 = q.astype(np.float32).astype(np.float64)
+    qf = np.tile(model.qpos0, (len(q), 1))
+    qf[:, :7] = q32
+    ref = O.site_kinematics(qf)[0][:, model.site_id("ee_center_site")]
+    out = engine.ik_dls(_dev(q32, torch.float32), _dev(ref, torch.float32), max_iters=0)
+    assert not out["flags"].any() and not out["iterations"].any()
+    np.testing.assert_array_equal(out["q"].double().cpu().numpy(), q32)
+    np.testing.assert_allclose(out["final_pos"].double().cpu().numpy(), ref, atol=2e-6)
+
+
 @pytest.mark.parametrize("pset", ["default", "ik_test"])
 def test_ik_f32_full_solves_agree(engine, model, pset):
     from pnp_amd import workloads
