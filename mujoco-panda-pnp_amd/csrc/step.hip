@@ -1045,21 +1045,28 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
   }
   clk.aux_lap(SC_AUX0);       // aux0: broadphase pass 1 (body pairs)
   int nlive = 0;
+  // Branch-free per chunk, and the next chunk's two table words are loaded (unconditionally, at
+  // a clamped index) while this one is tested.  With the loads behind the body-pair branch a
+  // chunk waited for pair_pack, then for pair_reach, then for the LDS positions: two serial trips
+  // to the model image (L1/L2) per chunk, ~900 cycles per chunk over the ~16 chunks of the table;
+  // a prefetch under an exec branch does not help either, the wait counter then drains it too.
+  const int plast = max(m.npair - 1, 0);
+  uint32_t pk_n = m.pair_pack[min(l, plast)];
+  T reach_n = m.pair_reach[min(l, plast)];
   for (int base = 0; base < m.npair; base += NT) {
     const int pi = base + l;
-    bool keep = false;
-    if (pi < m.npair) {
-      const uint32_t pk = m.pair_pack[pi];
-      const int bp = pk >> 24;
-      const uint64_t word = bp < 64 ? bpm[0] : bp < 128 ? bpm[1] : bp < 192 ? bpm[2] : bpm[3];
-      keep = (word >> (bp & 63)) & 1;
-      const T reach = m.pair_reach[pi];
-      if (keep && reach >= 0) {
-        const int g1 = pk & 255, g2 = (pk >> 8) & 255;
-        T v[3] = {s.gpos[g1][0] - s.gpos[g2][0], s.gpos[g1][1] - s.gpos[g2][1], s.gpos[g1][2] - s.gpos[g2][2]};
-        keep = t_dot3(v, v) <= reach * reach;
-      }
-    }
+    const uint32_t pk = pk_n;
+    const T reach = reach_n;
+    const int pn = min(pi + NT, plast);
+    pk_n = m.pair_pack[pn];
+    reach_n = m.pair_reach[pn];
+    const int bp = pk >> 24;
+    const uint64_t w01 = (bp & 64) ? bpm[1] : bpm[0], w23 = (bp & 64) ? bpm[3] : bpm[2];
+    const uint64_t word = (bp & 128) ? w23 : w01;
+    const int g1 = pk & 255, g2 = (pk >> 8) & 255;
+    T v[3] = {s.gpos[g1][0] - s.gpos[g2][0], s.gpos[g1][1] - s.gpos[g2][1], s.gpos[g1][2] - s.gpos[g2][2]};
+    const bool keep = (pi < m.npair) & (bool)((word >> (bp & 63)) & 1) &
+                      ((reach < T(0)) | (t_dot3(v, v) <= reach * reach));
     const uint64_t bal = __ballot(keep);
     const int at = nlive + __popcll(bal & ((1ull << l) - 1));
     if (keep && at < PH_MAXLIVE) s.live[at] = (short)pi;
