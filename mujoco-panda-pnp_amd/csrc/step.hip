@@ -1085,24 +1085,29 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
   // both ways, and the plane test; compacted in place (a chunk reads its entries into registers
   // before any lane writes, and writes land at or below the read positions), so that the
   // separating-axis tests below run over one chunk of survivors instead of every chunk
+  // Branch-free like pass 2: every lane runs both tests and selects by kind, and the next
+  // chunk's list entries and table words are fetched while this chunk is tested (they lie at or
+  // above (chunk + 1) * 64, beyond every write of this chunk).
   int nsph = nlive;
   nlive = 0;
+  int pi_n = nsph > 0 ? s.live[min(l, nsph - 1)] : 0;
+  uint32_t pk_p = m.pair_pack[pi_n];
+  T mg_p = m.pair_margin[pi_n];
   for (int base = 0; base < nsph; base += NT) {
     const int k = base + l;
-    bool keep = false;
-    int pi = 0;
-    if (k < nsph) {
-      pi = s.live[k];
-      const uint32_t pk = m.pair_pack[pi];
-      const int g1 = pk & 255, g2 = (pk >> 8) & 255, kind = (pk >> 16) & 255;
-      keep = true;
-      if (kind == PH_PAIR_CONVEX || kind == PH_PAIR_BOX) {
-        const T mg = m.pair_margin[pi] + T(1e-6);
-        keep = !c_sphere_obb_disjoint(m, s, g1, g2, mg) && !c_sphere_obb_disjoint(m, s, g2, g1, mg);
-      } else if (kind == PH_PAIR_PLANE) {
-        keep = !c_plane_obb_clear(m, s, g1, g2, m.pair_margin[pi]);
-      }
-    }
+    const int pi = pi_n;
+    const uint32_t pk = pk_p;
+    const T pmg = mg_p;
+    pi_n = s.live[min(k + NT, nsph - 1)];
+    pk_p = m.pair_pack[pi_n];
+    mg_p = m.pair_margin[pi_n];
+    const int g1 = pk & 255, g2 = (pk >> 8) & 255, kind = (pk >> 16) & 255;
+    const T mg = pmg + T(1e-6);
+    const bool sph = !c_sphere_obb_disjoint(m, s, g1, g2, mg) & !c_sphere_obb_disjoint(m, s, g2, g1, mg);
+    const bool pln = !c_plane_obb_clear(m, s, g1, g2, pmg);
+    const bool keep = (k < nsph) & ((kind == PH_PAIR_CONVEX || kind == PH_PAIR_BOX) ? sph
+                                     : kind == PH_PAIR_PLANE                       ? pln
+                                                                                   : true);
     const uint64_t bal = __ballot(keep);
     wsync();
     if (keep) s.live[nlive + __popcll(bal & ((1ull << l) - 1))] = (short)pi;
