@@ -1281,19 +1281,23 @@ __device__ __forceinline__ void row_imp(const DevPhys<T>& /*image: phys<T>()*/, 
 
 // translational Jacobian column of world point pt on body b at dof d (0 if d does not move b)
 template <typename T>
-__device__ __forceinline__ void jac_col(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int b, int d, const T pt[3], T jp[3], T jr[3]) {
-  const DevPhys<T>& m = phys<T>();
-  if (d < 0 || !(m.body_dofmask[b] >> d & 1)) {
+__device__ __forceinline__ void jac_col_rm(const Env<T>& s, int root, uint64_t dofmask, int d, const T pt[3], T jp[3], T jr[3]) {
+  if (d < 0 || !(dofmask >> d & 1)) {
     jp[0] = jp[1] = jp[2] = 0;
     jr[0] = jr[1] = jr[2] = 0;
     return;
   }
-  const T* c = s.subcom[m.body_rootid[b]];
+  const T* c = s.subcom[root];
   const T off[3] = {pt[0] - c[0], pt[1] - c[1], pt[2] - c[2]};
   const T* cd = s.cdof[d];
   T t[3];
   t_cross(t, cd, off);
   for (int k = 0; k < 3; k++) { jp[k] = cd[3 + k] + t[k]; jr[k] = cd[k]; }
+}
+template <typename T>
+__device__ __forceinline__ void jac_col(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int b, int d, const T pt[3], T jp[3], T jr[3]) {
+  const DevPhys<T>& m = phys<T>();
+  jac_col_rm(s, m.body_rootid[b], m.body_dofmask[b], d, pt, jp, jr);
 }
 
 template <typename T>
@@ -1414,12 +1418,28 @@ __device__ void st_constraints(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s
   const int nc = s.ncon;
   int kept_rows = nrow;
   bool spill = false;
+  // The first 64 contacts' body data stays in the contact's lane (root bodies, dof masks,
+  // invweight sums): the Jacobian-slot and row loops below fetch it by lane shuffles instead of
+  // two more serial trips to the model image (geom -> body -> mask / root) per chunk.
+  const bool fastc = nc <= NT;
+  int kr1 = 0, kr2 = 0;
+  uint64_t km1 = 0, km2 = 0;
+  T ktran = 0, krot = 0;
   for (int cb = 0, rb = nrow, sb = nslot; cb < nc; cb += NT) {
     const int c = cb + l;
     int my_rows = 0, my_slots = 0, t0c = -1, t1c = -1;
     if (c < nc) {
       const Con<T>& con = s.con[c];
-      body_trees(m, m.geom_bodyid[con.g1], m.geom_bodyid[con.g2], t0c, t1c);
+      const int b1 = m.geom_bodyid[con.g1], b2 = m.geom_bodyid[con.g2];
+      body_trees(m, b1, b2, t0c, t1c);
+      if (cb == 0) {
+        kr1 = m.body_rootid[b1];
+        kr2 = m.body_rootid[b2];
+        km1 = m.body_dofmask[b1];
+        km2 = m.body_dofmask[b2];
+        ktran = m.body_invweight0[b1][0] + m.body_invweight0[b2][0];
+        krot = m.body_invweight0[b1][1] + m.body_invweight0[b2][1];
+      }
       my_rows = 2 * (con.dim - 1);
       my_slots = my_rows * row_width(m, t0c, t1c);
     }
@@ -1448,14 +1468,30 @@ __device__ void st_constraints(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s
   for (int base = 0; base < nc * PH_ROWW; base += NT) {
     const int idx = base + l;
     const int c = idx / PH_ROWW, k = idx % PH_ROWW;
+    int r1 = 0, r2 = 0;
+    uint64_t m1 = 0, m2 = 0;
+    if (fastc) {   // (wave-uniform; every lane takes part in the shuffles)
+      const int src = min(c, NT - 1);
+      r1 = __shfl(kr1, src);
+      r2 = __shfl(kr2, src);
+      m1 = __shfl(km1, src);
+      m2 = __shfl(km2, src);
+    }
     if (c >= nc || s.con_rbase[c] < 0) continue;
     const int t0 = s.con_t[c][0], t1 = s.con_t[c][1], w = row_width(m, t0, t1);
     if (k >= w) continue;
     const Con<T>& con = s.con[c];
     const int d = slot_dof(m, t0, t1, k);
+    if (!fastc) {
+      const int b1 = m.geom_bodyid[con.g1], b2 = m.geom_bodyid[con.g2];
+      r1 = m.body_rootid[b1];
+      r2 = m.body_rootid[b2];
+      m1 = m.body_dofmask[b1];
+      m2 = m.body_dofmask[b2];
+    }
     T jp1[3], jr1[3], jp2[3], jr2[3];
-    jac_col(m, s, m.geom_bodyid[con.g1], d, con.pos, jp1, jr1);
-    jac_col(m, s, m.geom_bodyid[con.g2], d, con.pos, jp2, jr2);
+    jac_col_rm(s, r1, m1, d, con.pos, jp1, jr1);
+    jac_col_rm(s, r2, m2, d, con.pos, jp2, jr2);
     const T jd[3] = {jp2[0] - jp1[0], jp2[1] - jp1[1], jp2[2] - jp1[2]};
     T cj[3];
     for (int a = 0; a < 3; a++) cj[a] = con.frame[3 * a] * jd[0] + con.frame[3 * a + 1] * jd[1] + con.frame[3 * a + 2] * jd[2];
@@ -1470,14 +1506,22 @@ __device__ void st_constraints(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s
   for (int base = 0; base < nc * 4; base += NT) {
     const int idx = base + l;
     const int c = idx / 4, q = idx % 4;
+    T tran = 0, rot = 0;
+    if (fastc) {
+      const int src = min(c, NT - 1);
+      tran = __shfl(ktran, src);
+      rot = __shfl(krot, src);
+    }
     if (c >= nc || s.con_rbase[c] < 0) continue;
     const Con<T>& con = s.con[c];
     if (q >= 2 * (con.dim - 1)) continue;
     const int r = s.con_rbase[c] + q, k = q / 2 + 1;
     const int t0 = s.con_t[c][0], t1 = s.con_t[c][1], w = row_width(m, t0, t1);
-    const int b1 = m.geom_bodyid[con.g1], b2 = m.geom_bodyid[con.g2];
-    const T tran = m.body_invweight0[b1][0] + m.body_invweight0[b2][0];
-    const T rot = m.body_invweight0[b1][1] + m.body_invweight0[b2][1];
+    if (!fastc) {
+      const int b1 = m.geom_bodyid[con.g1], b2 = m.geom_bodyid[con.g2];
+      tran = m.body_invweight0[b1][0] + m.body_invweight0[b2][0];
+      rot = m.body_invweight0[b1][1] + m.body_invweight0[b2][1];
+    }
     const T fri = con.friction[k - 1];
     s.efc_off[r] = s.con_sbase[c] + q * w;
     s.efc_t0[r] = t0; s.efc_t1[r] = t1;
