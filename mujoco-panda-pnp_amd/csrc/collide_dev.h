@@ -822,9 +822,8 @@ __device__ void c_params(const DevPhys<T>& /*image: phys<T>()*/, Con<T>& c, int 
 }
 
 template <typename T, class S>
-__device__ void collide_pair(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int pair, S& out) {
+__device__ void collide_geoms(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int g1, int g2, S& out) {
   const DevPhys<T>& m = phys<T>();
-  const int g1 = m.pair_g1[pair], g2 = m.pair_g2[pair];
   const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
   const T *p1 = s.gpos[g1], *R1 = s.gmat[g1], *s1 = m.geom_size[g1];
   const T *p2 = s.gpos[g2], *R2 = s.gmat[g2], *s2 = m.geom_size[g2];
@@ -836,4 +835,9 @@ __device__ void collide_pair(const DevPhys<T>& /*image: phys<T>()*/, const Env<T
   else if (t1 == 2 && t2 == 6) c_sphere_box(p1, s1[0], p2, R2, s2, margin, out);
   else if (t1 == 6 && t2 == 6) c_box_box(p1, R1, s1, p2, R2, s2, margin, out);
   // convex pairs: st_collision's MPR pass
+}
+template <typename T, class S>
+__device__ __forceinline__ void collide_pair(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int pair, S& out) {
+  const DevPhys<T>& m = phys<T>();
+  collide_geoms(m, s, m.pair_g1[pair], m.pair_g2[pair], out);
 }

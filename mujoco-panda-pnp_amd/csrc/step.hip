@@ -1145,16 +1145,21 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
   // pairs produces.  If a chunk stages more than 64 contacts it falls back to a second collide
   // pass writing at the scanned offsets.  Contact order: primitive pairs in pair order, then the
   // convex (MPR) pairs in pair order (st_collision_convex).
+  // (a lane's geoms and kind come from the one packed table word, PH_PAIR_CONVEX being
+  // c_is_convex_pair's test; the staged contacts get their geoms by shuffles: one model-image
+  // trip per chunk for the pair instead of three)
   int ncon = 0, nconvex = 0;
   for (int base = 0; base < nlive; base += NT) {
     const int k = base + l;
     const int pair = k < nlive ? s.live[k] : 0;
-    const bool cvx = k < nlive && c_is_convex_pair(m, m.pair_g1[pair], m.pair_g2[pair]);
+    const uint32_t pk = m.pair_pack[pair];
+    const int pg1 = pk & 255, pg2 = (pk >> 8) & 255;
+    const bool cvx = k < nlive && ((pk >> 16) & 255) == PH_PAIR_CONVEX;
     nconvex += __popcll(__ballot(cvx));
     if (l == 0) s.cst_n = 0;
     wsync();
     StageSink<T> ss{&s.cst_n, s.cst_val, s.cst_key, l};
-    if (k < nlive && !cvx) collide_pair(m, s, pair, ss);
+    if (k < nlive && !cvx) collide_geoms(m, s, pg1, pg2, ss);
     wsync();
     const int staged = s.cst_n;
     int incl = ss.n;
@@ -1168,20 +1173,19 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
       const int key = l < staged ? s.cst_key[l] : 0;
       const int src = key >> 4;
       const int at = __shfl(off, src) + (key & 15);
-      const int sp = __shfl(pair, src);
+      const int sg1 = __shfl(pg1, src), sg2 = __shfl(pg2, src);
       if (l < staged && at < PH_MAXCON) {
         Con<T>& c = s.con[at];
         c.dist = s.cst_val[l][0];
         for (int t = 0; t < 3; t++) c.pos[t] = s.cst_val[l][1 + t];
         for (int t = 0; t < 9; t++) c.frame[t] = t < 3 ? s.cst_val[l][4 + t] : T(0);
-        c_params(m, c, m.pair_g1[sp], m.pair_g2[sp]);
+        c_params(m, c, sg1, sg2);
       }
     } else if (ss.n) {
       LdsSink<T> ls{s.con + off, PH_MAXCON - off};
       if (ls.cap > 0) {
-        collide_pair(m, s, pair, ls);
-        const int g1 = m.pair_g1[pair], g2 = m.pair_g2[pair];
-        for (int c = 0; c < ss.n && c < ls.cap; c++) c_params(m, s.con[off + c], g1, g2);
+        collide_geoms(m, s, pg1, pg2, ls);
+        for (int c = 0; c < ss.n && c < ls.cap; c++) c_params(m, s.con[off + c], pg1, pg2);
       }
     }
     wsync();
