@@ -317,6 +317,11 @@ int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
       d->act_forcerange[i][k] = (T)s->actuator_forcerange[2 * i + k];
     }
   }
+  for (int d0 = 0; d0 < PH_MAXV; d0++) d->dof_act[d0] = -1;
+  for (int i = 0; i < s->nu; i++) {
+    int& da = d->dof_act[d->act_dof[i]];
+    da = da == -1 ? i : -2;
+  }
   // ---- equality
   for (int e = 0; e < s->neq; e++) {
     d->eq_type[e] = s->eq_type[e];

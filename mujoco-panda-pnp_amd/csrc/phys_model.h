@@ -108,6 +108,7 @@ struct DevPhys {
   int act_dof[PH_MAXU], act_qadr[PH_MAXU];
   T act_gear[PH_MAXU], act_gainprm[PH_MAXU][3], act_biasprm[PH_MAXU][3];
   T act_ctrlrange[PH_MAXU][2], act_forcerange[PH_MAXU][2];
+  int dof_act[PH_MAXV];   // the one actuator driving the dof, -1 none, -2 several (summed in order)
   // equality (weld)
   int eq_type[4], eq_obj1id[4], eq_obj2id[4];
   T eq_solref[4][2], eq_solimp[4][5], eq_data[4][11];

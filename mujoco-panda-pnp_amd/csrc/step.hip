@@ -1620,9 +1620,10 @@ __device__ void st_actuation_smooth(const DevPhys<T>& /*image: phys<T>()*/, Env<
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (l < m.nv) {
-    T f = 0;
-    for (int i = 0; i < m.nu; i++) {
-      if (m.act_dof[i] != l) continue;
+    // a dof driven by one actuator (every dof here) reads that actuator's constants by its own
+    // index -- one round of independent loads -- instead of walking all nu actuators with a
+    // compare per step; same arithmetic (f = 0 + gear * force)
+    auto act_force = [&](int i) {
       T ctrl = s.ctrl[i];
       if (m.act_ctrllimited[i]) ctrl = fmin(fmax(ctrl, m.act_ctrlrange[i][0]), m.act_ctrlrange[i][1]);
       const T gear = m.act_gear[i];
@@ -1630,7 +1631,15 @@ __device__ void st_actuation_smooth(const DevPhys<T>& /*image: phys<T>()*/, Env<
       T force = m.act_gainprm[i][0] * ctrl;
       if (m.act_biastype[i]) force += m.act_biasprm[i][0] + m.act_biasprm[i][1] * len + m.act_biasprm[i][2] * vel;
       if (m.act_forcelimited[i]) force = fmin(fmax(force, m.act_forcerange[i][0]), m.act_forcerange[i][1]);
-      f += gear * force;
+      return gear * force;
+    };
+    T f = 0;
+    const int ia = m.dof_act[l];
+    if (ia >= 0) {
+      f += act_force(ia);
+    } else if (ia == -2) {
+      for (int i = 0; i < m.nu; i++)
+        if (m.act_dof[i] == l) f += act_force(i);
     }
     s.qfrc_act[l] = f;
     s.qfrc_smooth[l] = s.qfrc_passive[l] - s.qfrc_bias[l] + f;
