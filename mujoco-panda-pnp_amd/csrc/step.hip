@@ -706,11 +706,25 @@ __device__ void st_compos_crb(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s)
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   // subtree COM of each root body (only roots are read: cinert and cdof are rooted there)
-  if (l > 0 && l < m.nbody && m.body_rootid[l] == l) {
-    T acc[3] = {0, 0, 0};
-    for (int i = 1; i < m.nbody; i++)
-      if (m.body_rootid[i] == l)
-        for (int t = 0; t < 3; t++) acc[t] += s.xipos[i][t] * m.body_mass[i];
+  // Lane i holds body i's mass, position and root; a uniform walk over the bodies reads them by
+  // v_readlane (no memory round trip per body -- the walk used to wait on a scalar load of the
+  // body's root and mass, then an LDS read, for every one of the nbody bodies) and the root
+  // lanes accumulate in body order, as before.
+  const bool lb = l < m.nbody;
+  const T bm = lb ? m.body_mass[l] : T(0);
+  const int br = lb ? m.body_rootid[l] : -1;
+  const T bx0 = lb ? s.xipos[l][0] : T(0), bx1 = lb ? s.xipos[l][1] : T(0), bx2 = lb ? s.xipos[l][2] : T(0);
+  T acc[3] = {0, 0, 0};
+  for (int i = 1; i < m.nbody; i++) {
+    const int ri = __builtin_amdgcn_readlane(br, i);
+    const T mi = rdlane(bm, i), x0 = rdlane(bx0, i), x1 = rdlane(bx1, i), x2 = rdlane(bx2, i);
+    if (ri == l) {
+      acc[0] += x0 * mi;
+      acc[1] += x1 * mi;
+      acc[2] += x2 * mi;
+    }
+  }
+  if (l > 0 && lb && br == l) {
     if (m.body_subtreemass[l] < T(1e-15)) for (int t = 0; t < 3; t++) s.subcom[l][t] = s.xipos[l][t];
     else for (int t = 0; t < 3; t++) s.subcom[l][t] = acc[t] / m.body_subtreemass[l];
   }
