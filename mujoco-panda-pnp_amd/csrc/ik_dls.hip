@@ -302,6 +302,26 @@ __device__ __forceinline__ T gsum8(T v) {
   v += gdpp<0x141>(v);   // row_half_mirror: the other quad of the group
   return v;
 }
+// six group sums at once, level by level: the three DPP steps of one sum each wait on the previous
+// add (a VALU write read by DPP needs two wait states), which the compiler filled with s_nop when
+// the sums were written one after the other; interleaved, each sum's wait is the others' issue.
+// Same additions per value, so the same bits as six gsum8 calls.
+template <typename T>
+__device__ __forceinline__ void gsum8x6(T v[6]) {
+  T t[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) t[k] = gdpp<0xB1>(v[k]);
+#pragma unroll
+  for (int k = 0; k < 6; k++) v[k] += t[k];
+#pragma unroll
+  for (int k = 0; k < 6; k++) t[k] = gdpp<0x4E>(v[k]);
+#pragma unroll
+  for (int k = 0; k < 6; k++) v[k] += t[k];
+#pragma unroll
+  for (int k = 0; k < 6; k++) t[k] = gdpp<0x141>(v[k]);
+#pragma unroll
+  for (int k = 0; k < 6; k++) v[k] += t[k];
+}
 // lane 7 of the group (= of its DPP row) to every lane of the row (row_newbcast:7)
 template <typename T>
 __device__ __forceinline__ T gbcast7(T v) {
@@ -412,13 +432,14 @@ __global__ void __launch_bounds__(64) ik_dls_group_kernel(IKSeg<T> c, int max_it
     const T J0 = axis[1] * r2 - axis[2] * r1;
     const T J1 = axis[2] * r0 - axis[0] * r2;
     const T J2 = axis[0] * r1 - axis[1] * r0;
-    T A[9];
-    A[0] = gsum8(J0 * J0) + damping;
-    A[1] = A[3] = gsum8(J0 * J1);
-    A[2] = A[6] = gsum8(J0 * J2);
-    A[4] = gsum8(J1 * J1) + damping;
-    A[5] = A[7] = gsum8(J1 * J2);
-    A[8] = gsum8(J2 * J2) + damping;
+    T A[9], jj[6] = {J0 * J0, J0 * J1, J0 * J2, J1 * J1, J1 * J2, J2 * J2};
+    gsum8x6(jj);
+    A[0] = jj[0] + damping;
+    A[1] = A[3] = jj[1];
+    A[2] = A[6] = jj[2];
+    A[4] = jj[3] + damping;
+    A[5] = A[7] = jj[4];
+    A[8] = jj[5] + damping;
     T y[3] = {e0, e1, e2};
     solve3(A, y);
     T dq = J0 * y[0] + J1 * y[1] + J2 * y[2];
