@@ -1021,6 +1021,20 @@ __device__ T mulM_row(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, i
   return r;
 }
 
+// inclusive wave scan of a per-lane count, on DPP: row_shr 1, 2, 4, 8 inside each row of 16
+// (bound_ctrl zero fill = the lanes below the shift add nothing), then the row totals by
+// v_readlane.  Integer sums, so the same values as the six ds_bpermute (__shfl_up) steps it
+// replaces, which each waited for an LDS round trip.  Call with the whole wave active.
+__device__ __forceinline__ int wscan_incl(int x) {
+  x += __builtin_amdgcn_mov_dpp(x, 0x111, 0xF, 0xF, true);
+  x += __builtin_amdgcn_mov_dpp(x, 0x112, 0xF, 0xF, true);
+  x += __builtin_amdgcn_mov_dpp(x, 0x114, 0xF, 0xF, true);
+  x += __builtin_amdgcn_mov_dpp(x, 0x118, 0xF, 0xF, true);
+  const int r0 = __builtin_amdgcn_readlane(x, 15), r1 = __builtin_amdgcn_readlane(x, 31),
+            r2 = __builtin_amdgcn_readlane(x, 47);
+  const int row = (int)(threadIdx.x >> 4);
+  return x + (row > 0 ? r0 : 0) + (row > 1 ? r1 : 0) + (row > 2 ? r2 : 0);
+}
 // ============================================================================ collision
 #include "collide_dev.h"
 
@@ -1176,12 +1190,8 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
     if (k < nlive && !cvx) collide_geoms(m, s, pg1, pg2, ss);
     wsync();
     const int staged = s.cst_n;
-    int incl = ss.n;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(incl, o);
-      if (l >= o) incl += y;
-    }
-    const int total = __shfl(incl, 63);
+    const int incl = wscan_incl(ss.n);
+    const int total = __builtin_amdgcn_readlane(incl, 63);
     const int off = ncon + incl - ss.n;
     if (staged <= NT && !__ballot(ss.n >= 16)) {
       const int key = l < staged ? s.cst_key[l] : 0;
@@ -1329,13 +1339,8 @@ __device__ __forceinline__ void body_trees(const DevPhys<T>& /*image: phys<T>()*
 
 // exclusive wave scan of a per-lane count; returns the offset, total in *tot
 __device__ __forceinline__ int wscan(int n, int* tot) {
-  const int l = threadIdx.x;
-  int incl = n;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(incl, o);
-    if (l >= o) incl += y;
-  }
-  *tot = __shfl(incl, 63);
+  const int incl = wscan_incl(n);
+  *tot = __builtin_amdgcn_readlane(incl, 63);
   return incl - n;
 }
 
@@ -1864,11 +1869,16 @@ __device__ void build_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
   // ... exclusive prefix sums over the island lanes (row, Hessian and dense-block offsets) ...
   const bool isl = l < nis;
   int ro = isl ? rc : 0, eo = isl ? nI * (nI + 1) / 2 : 0, jo = isl ? rc * nI : 0;
-#pragma unroll
-  for (int o = 1; o < 8; o <<= 1) {
-    const int a = __shfl_up(ro, o), e = __shfl_up(eo, o), j = __shfl_up(jo, o);
-    if (l >= o) { ro += a; eo += e; jo += j; }
-  }
+  // (row_shr inside the first DPP row, zero-filled below the shift: lanes 0..7 get the scan)
+  ro += __builtin_amdgcn_mov_dpp(ro, 0x111, 0xF, 0xF, true);
+  eo += __builtin_amdgcn_mov_dpp(eo, 0x111, 0xF, 0xF, true);
+  jo += __builtin_amdgcn_mov_dpp(jo, 0x111, 0xF, 0xF, true);
+  ro += __builtin_amdgcn_mov_dpp(ro, 0x112, 0xF, 0xF, true);
+  eo += __builtin_amdgcn_mov_dpp(eo, 0x112, 0xF, 0xF, true);
+  jo += __builtin_amdgcn_mov_dpp(jo, 0x112, 0xF, 0xF, true);
+  ro += __builtin_amdgcn_mov_dpp(ro, 0x114, 0xF, 0xF, true);
+  eo += __builtin_amdgcn_mov_dpp(eo, 0x114, 0xF, 0xF, true);
+  jo += __builtin_amdgcn_mov_dpp(jo, 0x114, 0xF, 0xF, true);
   const int rtot = __builtin_amdgcn_readlane(ro, 7), etot = __builtin_amdgcn_readlane(eo, 7),
             jtot = __builtin_amdgcn_readlane(jo, 7);
   // an island with more rows than the line search's per-group register cache (the solver's
