@@ -1478,9 +1478,11 @@ __device__ void st_constraints(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s
       s.con_dim[c] = (unsigned char)s.con[c].dim;
     }
     spill |= __ballot(c < nc && !fits) != 0;
-    // last contact that fits bounds the row count (contacts are added in order)
-    int lastrow = (c < nc && fits) ? rbase + my_rows : 0;
-    for (int o = 32; o > 0; o >>= 1) lastrow = max(lastrow, __shfl_xor(lastrow, o));
+    // last contact that fits bounds the row count (contacts are added in order; the row bases are
+    // a prefix sum, so the highest fitting lane holds the largest end -- read it directly instead
+    // of a six-step shuffle max)
+    const uint64_t fm = __ballot(fits);
+    const int lastrow = fm ? __builtin_amdgcn_readlane(rbase + my_rows, 63 - __builtin_clzll(fm)) : 0;
     kept_rows = max(kept_rows, lastrow);
     rb += trows;
     sb += tslots;
@@ -1695,6 +1697,32 @@ __device__ __forceinline__ T group_sum(const Env<T>& s, int I, const T* vd, cons
   if (vr)
     for (int rr = s.isl_roff[I] + q; rr < s.isl_roff[I + 1]; rr += 8) acc += vr[s.isl_row[rr]];
   return rowsum8(acc);
+}
+// two island sums in one pass: out[I] over island I's dofs of vd and rows of vr, out2[I] over its
+// rows of vr2 -- one row walk, the two group reductions interleaved, one sync (same additions in
+// the same order as island_sums(vd, vr) and island_sums(nullptr, vr2))
+template <typename T>
+__device__ __forceinline__ void island_sums2(Env<T>& s, const T* vd, const T* vr, T* out, const T* vr2, T* out2) {
+  const int l = lane_id();
+  const int I = l >> 3, q = l & 7;
+  if (I < s.nisland) {
+    T a = 0, b = 0;
+    const int n = s.isl_n[I];
+    for (int c = q; c < n; c += 8) a += vd[s.isl_dof[I][c]];
+    for (int rr = s.isl_roff[I] + q; rr < s.isl_roff[I + 1]; rr += 8) {
+      const int r = s.isl_row[rr];
+      a += vr[r];
+      b += vr2[r];
+    }
+    T ta = dpp_f<0xB1>(a), tb = dpp_f<0xB1>(b);
+    a += ta; b += tb;
+    ta = dpp_f<0x4E>(a); tb = dpp_f<0x4E>(b);
+    a += ta; b += tb;
+    ta = dpp_f<0x141>(a); tb = dpp_f<0x141>(b);
+    a += ta; b += tb;
+    if (q == 0) { out[I] = a; out2[I] = b; }
+  }
+  wsync();
 }
 // out[I] = group_sum for every island (vd / vr in LDS)
 template <typename T>
@@ -2307,8 +2335,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     s.efc_Jp[r] = r < s.ne || bs < 0 ? T(0.5) * s.efc_D[r] * bs * bs : T(0);
   }
   wsync();
-  island_sums(s, s.v2, s.ntmp, s.isl_val);
-  island_sums(s, (const T*)nullptr, s.efc_Jp, s.isl_cost);
+  island_sums2(s, s.v2, s.ntmp, s.isl_val, s.efc_Jp, s.isl_cost);
   if (l < PH_MAXT) {
     const bool ws = l < s.nisland && s.isl_val[l] < s.isl_cost[l];
     s.isl_alpha[l] = ws ? T(1) : T(0);
