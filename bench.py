@@ -54,9 +54,19 @@ NCTRL = 64                      # distinct per-step ctrl draws, cycled
 
 
 def host_threads():
-    n = len(os.sched_getaffinity(0))
-    cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
-    return max(1, min(n, cap, 16))
+    """Every core this process may run on (the CPU baseline runs over all cores)."""
+    return max(1, len(os.sched_getaffinity(0)))
+
+
+def cpu_quota():
+    """cgroup v2 CPU quota in cores (None: unlimited / unknown) -- reported beside the thread
+    count, since a quota below the affinity set caps what those threads can do."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+        return None if q == "max" else float(q) / float(p)
+    except (OSError, ValueError):
+        return None
 
 
 def _oracle():
@@ -135,11 +145,16 @@ def _traffic(name, B):
 
 
 def _sq_valu():
+    """VALU issue share from the committed SQ-counter pass (profiles/sq_counters_step.json): a
+    figure measured by a separate rocprofv3 run, not by this one -- returned with its provenance
+    (file, kernel build it was measured on) so a stale value is visible."""
     f = os.path.join(ROOT, "profiles", "sq_counters_step.json")
     if os.path.exists(f):
         with open(f) as fh:
-            return json.load(fh).get("valu_issue_frac")
-    return None
+            j = json.load(fh)
+        return j.get("valu_issue_frac"), {"file": "profiles/sq_counters_step.json", "measured_in_this_run": False,
+                                           "kernel_version": j.get("kernel_version"), "source": j.get("source")}
+    return None, None
 
 
 # ----------------------------------------------------------------------------- C3 / C4 env-step
@@ -164,7 +179,7 @@ def step_cpu_baseline(st, ctrl, budget_s):
     """fp64 oracle mj_step x NSUB on host threads, over a bounded sample of the same settled envs."""
     O = _oracle()
     nth = host_threads()
-    n = min(st["qpos"].shape[0], 256)
+    n = min(st["qpos"].shape[0], max(256, 2 * nth))   # >= 2 envs per thread
     sample = {k: (v[:n].cpu().numpy().astype(np.uint32) if k == "warn" else v[:n].double().cpu().numpy())
               for k, v in st.items()}
     ctab = ctrl[:, :n].double().cpu().numpy()
@@ -176,7 +191,7 @@ def step_cpu_baseline(st, ctrl, budget_s):
         done += n * NSUB
         reps += 1
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "env-steps/s", "cores": nth, "kind": "port",
+    return {"value": done / dt, "unit": "env-steps/s", "cores": nth, "kind": "port", "cpu_quota": cpu_quota(),
             "sample": f"{reps} steps x {n} envs x {NSUB} sub-steps of the same settled C3 envs "
                       f"(envs 0..{n - 1}), fp64 oracle oracle/physics.c, {nth} pthreads, {dt:.1f} s"}
 
@@ -198,6 +213,7 @@ def run_step(args, engine, model, rank, world, dist):
     total = B * world * args.steps * NSUB
     achieved = STEP_BYTES_PER_ENV * B / (kern_ms * 1e-3) / 1e9
     traffic, src = _traffic("pmc_traffic_step.json", B)
+    valu, valu_src = _sq_valu()
     rec = {
         "metric": BASELINE_METRIC,
         "value": total / elapsed,
@@ -222,8 +238,9 @@ def run_step(args, engine, model, rank, world, dist):
                      # bandwidth of the same launch, for scale
                      "pmc_GBps": (traffic / (kern_ms * 1e-3) / 1e9) if traffic else None,
                      # SQ counters of the same kernel (profiles/sq_counters_step.json): the share
-                     # of cycles the SIMDs' vector ALUs issue, all resident waves together
-                     "valu_issue_frac": _sq_valu(),
+                     # of cycles the SIMDs' vector ALUs issue, all resident waves together --
+                     # from a separate rocprofv3 pass, provenance alongside
+                     "valu_issue_frac": valu, "valu_issue_frac_source": valu_src,
                      "limiter": "latency and instruction issue (resident waves x cycles per env-sub-step), not HBM"},
         "state_ok": {"max_warn": warn, "finite": finite},
         "host_cores": len(os.sched_getaffinity(0)),
@@ -289,8 +306,13 @@ def run_tqc(engine, B, rank, world, dist, steps=3, warmup=2, learner_reps=20):
     torch.cuda.synchronize()
     learner_ms = (time.perf_counter() - t0) / learner_reps * 1e3
     sub = env.cfg.n_substeps * env.cfg.n_calls
+    step_ms = elapsed / steps * 1e3
+    # the reference's update-to-data ratio (one gradient step per 4 transitions: sb3 defaults over
+    # 4 SubprocVecEnv workers) would add (B / 4 - 1) more gradient steps per vector step
+    ref_utd_ms = step_ms + (B / 4 - 1) * learner_ms
     return {"gym_steps_per_s": B * world * steps / elapsed, "env_steps_per_s": B * world * steps * sub / elapsed,
-            "ms_per_step": elapsed / steps * 1e3, "learner_ms_per_update": learner_ms,
+            "ms_per_step": step_ms, "learner_ms_per_update": learner_ms,
+            "transitions_per_s_at_reference_utd": B * world / (ref_utd_ms * 1e-3),
             "workload": f"C5: TQC (train.py hyper-parameters) on {B} FrankaShelfPNPDense envs per GPU, "
                         f"one gym step + one gradient step per step"}
 
@@ -321,7 +343,7 @@ def ik_cpu_baseline(q_host, tgt_host, prm, budget_s):
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "solves/s", "cores": nth, "kind": "port",
+    return {"value": done / dt, "unit": "solves/s", "cores": nth, "kind": "port", "cpu_quota": cpu_quota(),
             "sample": f"{reps} x {n} solves of the same C2 inputs (envs 0..{n - 1}), fp64 oracle "
                       f"oracle/oracle.c, {nth} pthreads, {dt:.1f} s"}
 
@@ -383,7 +405,7 @@ def main():
     ap.add_argument("--no-tqc", action="store_true", help="step workload: skip the secondary C5 TQC-loop timing")
     ap.add_argument("--tqc-envs", type=int, default=8192, help="C5 envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (C3 leg)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="N > 1: nccl (= RCCL over xGMI, one GPU per rank); gloo only to rehearse several "
                          "ranks on one GPU")

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 6
+#define PNP_ABI_VERSION 7
 
 #define PNP_OK 0
 #define PNP_ERR_ARG -1
@@ -369,6 +369,21 @@ int32_t pnp_env_step(pnp_model* model, const pnp_state* state, const pnp_env_par
 int32_t pnp_env_step_f64(pnp_model* model, const pnp_state_f64* state, const pnp_env_params* params,
                          const pnp_env_state* env, const double* action, const pnp_env_out* out, int32_t B,
                          void* stream);
+
+/* FrankaEnv._get_obs (panda_env.py:279-301) + compute_reward / _is_success (:205-245, :303-306)
+ * at the current state, without stepping: data.site_* of the last forward (env->qpos_kin), the
+ * current qvel / finger qpos, current_task_index, initial_object_height.  ag / dg ([B*3], same
+ * dtype, device; NULL = the observed achieved goal / the env's goal) are compute_reward's
+ * achieved_goal / desired_goal arguments.  Writes obs / achieved_goal / desired_goal (observed)
+ * and reward / is_success (for ag, dg) to out; terminated / truncated untouched.  The state and
+ * the env state are read only (reference test/reward_test.py:69-74 calls _get_obs and
+ * compute_reward between physics steps this way). */
+int32_t pnp_env_evaluate(pnp_model* model, const pnp_state* state, const pnp_env_params* params,
+                         const pnp_env_state* env, const float* ag, const float* dg, const pnp_env_out* out,
+                         int32_t B, void* stream);
+int32_t pnp_env_evaluate_f64(pnp_model* model, const pnp_state_f64* state, const pnp_env_params* params,
+                             const pnp_env_state* env, const double* ag, const double* dg, const pnp_env_out* out,
+                             int32_t B, void* stream);
 
 #ifdef __cplusplus
 }

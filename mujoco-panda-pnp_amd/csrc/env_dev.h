@@ -299,6 +299,73 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_r
   store_controls(m, s, st, b);
 }
 
+// ---------------------------------------------------------------- reward (compute_reward)
+// FrankaEnv.compute_reward (panda_env.py:205-245) + _is_success (:303-306) for achieved goal ag and
+// desired goal dg, at the ee frame (ee_p, ee_R) of the last forward, finger width `width`,
+// initial_object_height h0 and current_task_index `task`; *placed = _is_success.
+template <typename T>
+__device__ T env_reward(const pnp_env_params& prm, const T ee_p[3], const T ee_R[9], const T ag[3], const T dg[3],
+                        T width, T h0, int task, bool* placed) {
+  const T dr[3] = {ee_p[0] - ag[0], ee_p[1] - ag[1], ee_p[2] - ag[2]};
+  const T dp[3] = {ag[0] - dg[0], ag[1] - dg[1], ag[2] - dg[2]};
+  const T d_reach = PM<T>::sqrt_(dr[0] * dr[0] + dr[1] * dr[1] + dr[2] * dr[2]);
+  const T d_place = PM<T>::sqrt_(dp[0] * dp[0] + dp[1] * dp[1] + dp[2] * dp[2]);
+  *placed = d_place < (T)prm.distance_threshold;
+  const bool gripped = width < (T)prm.grip_width && d_reach < (T)prm.reach_thresh;
+  const bool lifted = gripped && ag[2] - h0 > (T)prm.lift_height;
+  T eq[4];
+  g_mat2quat(ee_R, eq);
+  T need[4] = {1, 0, 0, 0};   // VERTICAL_QUAT = euler2quat(0)
+  if (ag[2] > (T)prm.high_pick_z) {
+    const T hz[3] = {T(-1.5707963267948966), 0, 0};   // HORIZONTAL_QUAT = euler2quat([-pi/2, 0, 0])
+    g_euler2quat(hz, need);
+  }
+  const T ori_err = T(1) - fabs(eq[0] * need[0] + eq[1] * need[1] + eq[2] * need[2] + eq[3] * need[3]);
+  if (!prm.reward_dense) return *placed ? T(0) : T(-1);
+  T reward = T(-0.003) - fmin(d_reach, (T)prm.reach_thresh);
+  if (gripped) reward += T(2) + (T(1) - ori_err);
+  if (lifted) reward += T(4);
+  if (*placed) reward += T(10);
+  reward += T(0.5) * (T(task) / T(prm.n_tasks));
+  return reward;
+}
+
+// ---------------------------------------------------------------- evaluate (_get_obs + compute_reward)
+// FrankaEnv._get_obs (panda_env.py:279-301) at the current state -- data.site_* of the last
+// forward (qpos_kin), the current qvel and finger qpos -- and compute_reward / _is_success
+// (:205-245, :303-306) for the given goals (ag / dg: [B*3], NULL = the observed ones).  Reads the
+// state only: no sub-step, no task update, no TimeLimit count.
+template <typename T>
+__global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_eval_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
+                                                      pnp_env_params prm, EnvSoA<T> es, const T* __restrict__ ag_in,
+                                                      const T* __restrict__ dg_in, EnvOutT<T> out, int B) {
+  __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
+  Env<T>& s = s_env;
+  const DevPhys<T>& m = phys<T>();
+  (void)mp;
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  const int l = lane_id();
+  load_env(m, s, st, b);
+  kin_at(m, s, es.qpos_kin + (size_t)b * m.nq, true);
+  const T width = s.qpos[prm.finger_qadr[0]] + s.qpos[prm.finger_qadr[1]];
+  const int task = es.task[b];
+  T goal[3], ee_p[3], ee_R[9], ob_p[3];
+  for (int t = 0; t < 3; t++) goal[t] = es.goal[(size_t)b * 3 + t];
+  env_observe(m, s, prm, task, goal, out, b, width, ee_p, ee_R, ob_p);
+  T ag[3], dg[3];
+  for (int t = 0; t < 3; t++) {
+    ag[t] = ag_in ? ag_in[(size_t)b * 3 + t] : ob_p[t];
+    dg[t] = dg_in ? dg_in[(size_t)b * 3 + t] : goal[t];
+  }
+  bool placed;
+  const T reward = env_reward(prm, ee_p, ee_R, ag, dg, width, es.obj_height0[b], task, &placed);
+  if (l == 0) {
+    if (out.reward) out.reward[b] = (T)(float)reward;   // compute_reward returns np.float32
+    if (out.success) out.success[b] = placed ? T(1) : T(0);
+  }
+}
+
 // ---------------------------------------------------------------- step (FrankaEnv.step)
 // Routing (env_state.tier): the smallest tier whose capacities hold a sub-step with a margin --
 // compact (0), full (1), wide (2).  The full and wide kernels record the largest over the
@@ -421,31 +488,8 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
   T ob_p[3];
   env_observe(m, s, prm, task, dg, out, b, width, ee_p, ee_R, ob_p);
   // ---- _is_success / compute_reward (before the task update)
-  const T dr[3] = {ee_p[0] - ob_p[0], ee_p[1] - ob_p[1], ee_p[2] - ob_p[2]};
-  const T dp[3] = {ob_p[0] - dg[0], ob_p[1] - dg[1], ob_p[2] - dg[2]};
-  const T d_reach = PM<T>::sqrt_(dr[0] * dr[0] + dr[1] * dr[1] + dr[2] * dr[2]);
-  const T d_place = PM<T>::sqrt_(dp[0] * dp[0] + dp[1] * dp[1] + dp[2] * dp[2]);
-  const bool placed = d_place < (T)prm.distance_threshold;
-  const bool gripped = width < (T)prm.grip_width && d_reach < (T)prm.reach_thresh;
-  const bool lifted = gripped && ob_p[2] - es.obj_height0[b] > (T)prm.lift_height;
-  T eq[4];
-  g_mat2quat(ee_R, eq);
-  T need[4] = {1, 0, 0, 0};   // VERTICAL_QUAT = euler2quat(0)
-  if (ob_p[2] > (T)prm.high_pick_z) {
-    const T hz[3] = {T(-1.5707963267948966), 0, 0};   // HORIZONTAL_QUAT = euler2quat([-pi/2, 0, 0])
-    g_euler2quat(hz, need);
-  }
-  const T ori_err = T(1) - fabs(eq[0] * need[0] + eq[1] * need[1] + eq[2] * need[2] + eq[3] * need[3]);
-  T reward;
-  if (!prm.reward_dense) {
-    reward = placed ? T(0) : T(-1);
-  } else {
-    reward = T(-0.003) - fmin(d_reach, (T)prm.reach_thresh);
-    if (gripped) reward += T(2) + (T(1) - ori_err);
-    if (lifted) reward += T(4);
-    if (placed) reward += T(10);
-    reward += T(0.5) * (T(task) / T(prm.n_tasks));
-  }
+  bool placed;
+  const T reward = env_reward(prm, ee_p, ee_R, ob_p, dg, width, es.obj_height0[b], task, &placed);
   // ---- task sequencing, TimeLimit
   bool terminated = false;
   int ntask = task;
@@ -598,6 +642,21 @@ static int32_t launch_env_reset(pnp_model* model, const pnp_state_t<T>* st, cons
   if ((rc = pnp_check_launch("env_reset_kernel"))) return rc;
   return lease.launched();
 }
+template <typename T>
+static int32_t launch_env_eval(pnp_model* model, const pnp_state_t<T>* st, const pnp_env_params* p,
+                               const pnp_env_state* e, const T* ag, const T* dg, const pnp_env_out* o, int32_t B,
+                               void* stream) {
+  int32_t rc = env_check(model, st, p, e, B, "pnp_env_evaluate");
+  if (rc || B == 0) return rc;
+  const DevPhys<T>* dm;
+  ResidentLease lease;
+  auto k = env_eval_kernel<T>;
+  if ((rc = env_prep(model, st, k, &dm, "pnp_env_evaluate", stream, lease))) return rc;
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), ag, dg,
+                     out_view<T>(o), B);
+  if ((rc = pnp_check_launch("env_eval_kernel"))) return rc;
+  return lease.launched();
+}
 // PNP_GYM_ROUTE: unset / 1 = with an env_state.tier buffer, envs start their fp32 gym step in the
 // tier their last step finished in (default); 0 = every env starts in the compact tier (A/B runs)
 static bool gym_route_enabled() {
@@ -654,35 +713,62 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   // concurrent with the compact pass; the resume passes then only see this step's new hand-overs
   const bool route = compact && wide && gym_compact_mode() == 1 && e->tier && gym_route_enabled();
   RouteStreams* rs = nullptr;
+  // join side stream i back into the caller's stream (its kernels read the full image and write
+  // the state: later work on s0, and the next model switch, must be ordered after them)
+  auto join_side = [&](int i) -> hipError_t {
+    hipError_t he = hipEventRecord(rs->join[i], rs->side[i]);
+    if (he == hipSuccess) he = hipStreamWaitEvent(s0, rs->join[i], 0);
+    return he;
+  };
+  // an error after the fork still joins both side streams and records the lease's use on s0
+  // before it is reported (the routed passes already enqueued keep running)
+  bool forked = false;
+  auto fail = [&](int32_t code) -> int32_t {
+    if (forked) {
+      join_side(0);
+      join_side(1);
+      lease.launched();
+    }
+    return code;
+  };
   if (route) {
     if ((rc = route_streams(&rs))) return rc;
     hipError_t he = hipEventRecord(rs->fork, s0);   // after the full image's copy and the last step
     for (int i = 0; i < 2 && he == hipSuccess; i++) he = hipStreamWaitEvent(rs->side[i], rs->fork, 0);
     if (he != hipSuccess) { pnp_set_error("pnp_env_step: fork: %s", hipGetErrorString(he)); return PNP_ERR_HIP; }
-    if ((rc = launch_env_step_wide(model, st32, p, e, a32, o, B, rs->side[1], 0, 2))) return rc;
+    forked = true;
+    if ((rc = launch_env_step_wide(model, st32, p, e, a32, o, B, rs->side[1], 0, 2))) return fail(rc);
     hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, rs->side[0], dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
                        0, wide, 1);
-    if ((rc = pnp_check_launch("env_step_kernel (full, routed)"))) return rc;
+    if ((rc = pnp_check_launch("env_step_kernel (full, routed)"))) return fail(rc);
   }
-  if (compact && (rc = launch_env_step_compact(model, st32, p, e, a32, o, B, stream, route ? 0 : -1))) return rc;
-  if (compact && gym_compact_mode() == 2) return lease.launched();
+  if (compact && (rc = launch_env_step_compact(model, st32, p, e, a32, o, B, stream, route ? 0 : -1))) return fail(rc);
+  if (compact && gym_compact_mode() == 2) {
+    if (forked) {
+      join_side(0);
+      join_side(1);
+    }
+    return lease.launched();
+  }
   hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, s0, dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
                      compact ? 1 : 0, wide, route ? 0 : -1);
-  if ((rc = pnp_check_launch("env_step_kernel"))) return rc;
+  if ((rc = pnp_check_launch("env_step_kernel"))) return fail(rc);
   if (route) {   // the wide resume pass also takes the routed full pass's hand-overs
-    hipError_t he = hipEventRecord(rs->join[0], rs->side[0]);
-    if (he == hipSuccess) he = hipStreamWaitEvent(s0, rs->join[0], 0);
-    if (he != hipSuccess) { pnp_set_error("pnp_env_step: join: %s", hipGetErrorString(he)); return PNP_ERR_HIP; }
+    if (const hipError_t he = join_side(0)) {
+      pnp_set_error("pnp_env_step: join: %s", hipGetErrorString(he));
+      return fail(PNP_ERR_HIP);
+    }
   }
-  if (wide && (rc = launch_env_step_wide(model, st32, p, e, a32, o, B, stream, 1, -1))) return rc;
+  if (wide && (rc = launch_env_step_wide(model, st32, p, e, a32, o, B, stream, 1, -1))) return fail(rc);
   if (route) {
-    hipError_t he = hipEventRecord(rs->join[1], rs->side[1]);
-    if (he == hipSuccess) he = hipStreamWaitEvent(s0, rs->join[1], 0);
-    if (he != hipSuccess) { pnp_set_error("pnp_env_step: join: %s", hipGetErrorString(he)); return PNP_ERR_HIP; }
+    if (const hipError_t he = join_side(1)) {
+      pnp_set_error("pnp_env_step: join: %s", hipGetErrorString(he));
+      return fail(PNP_ERR_HIP);
+    }
   }
   if (e->tier) {   // every pass has run: the next step's tiers become current
     hipLaunchKernelGGL(route_commit_kernel, dim3((B + 255) / 256), dim3(256), 0, s0, e->tier, B);
-    if ((rc = pnp_check_launch("route_commit_kernel"))) return rc;
+    if ((rc = pnp_check_launch("route_commit_kernel"))) return fail(rc);
   }
   return lease.launched();   // recorded on the caller's stream, after both joins
 }
@@ -706,6 +792,16 @@ extern "C" int32_t pnp_env_reset_f64(pnp_model* model, const pnp_state_f64* st, 
                                      const pnp_env_state* e, const uint8_t* mask, const pnp_env_out* o, int32_t B,
                                      void* stream) {
   return launch_env_reset<double>(model, reinterpret_cast<const pnp_state_t<double>*>(st), p, e, mask, o, B, stream);
+}
+extern "C" int32_t pnp_env_evaluate(pnp_model* model, const pnp_state* st, const pnp_env_params* p,
+                                    const pnp_env_state* e, const float* ag, const float* dg, const pnp_env_out* o,
+                                    int32_t B, void* stream) {
+  return launch_env_eval<float>(model, reinterpret_cast<const pnp_state_t<float>*>(st), p, e, ag, dg, o, B, stream);
+}
+extern "C" int32_t pnp_env_evaluate_f64(pnp_model* model, const pnp_state_f64* st, const pnp_env_params* p,
+                                        const pnp_env_state* e, const double* ag, const double* dg,
+                                        const pnp_env_out* o, int32_t B, void* stream) {
+  return launch_env_eval<double>(model, reinterpret_cast<const pnp_state_t<double>*>(st), p, e, ag, dg, o, B, stream);
 }
 extern "C" int32_t pnp_env_step(pnp_model* model, const pnp_state* st, const pnp_env_params* p,
                                 const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,

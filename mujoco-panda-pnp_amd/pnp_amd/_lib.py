@@ -9,7 +9,7 @@ from .model import PnpIKParams, PnpModelDesc
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpnp.so")
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # every symbol include/pnp.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -18,7 +18,7 @@ EXPORTS = [
     "pnp_jac_site_f64", "pnp_jac_site_full", "pnp_jac_site_full_f64", "pnp_ik_dls", "pnp_ik_dls_f64", "pnp_step", "pnp_step_f64",
     "pnp_forward_debug", "pnp_forward_debug_f64", "pnp_step_lds_bytes", "pnp_step_profile",
     "pnp_env_params_size", "pnp_env_init", "pnp_env_init_f64", "pnp_env_reset", "pnp_env_reset_f64",
-    "pnp_env_step", "pnp_env_step_f64",
+    "pnp_env_step", "pnp_env_step_f64", "pnp_env_evaluate", "pnp_env_evaluate_f64",
 ]
 
 STATE_FIELDS = ("qpos", "qvel", "ctrl", "mocap_pos", "mocap_quat", "qacc_warmstart", "time", "warn")
@@ -129,6 +129,10 @@ def load():
     for name in ("pnp_env_step", "pnp_env_step_f64"):
         f = getattr(L, name)
         f.argtypes = [P, SP, EP, ES, P, EO, I32, P]
+        f.restype = I32
+    for name in ("pnp_env_evaluate", "pnp_env_evaluate_f64"):
+        f = getattr(L, name)
+        f.argtypes = [P, SP, EP, ES, P, P, EO, I32, P]
         f.restype = I32
     if L.pnp_abi_version() != ABI_VERSION:
         raise PnpError(f"libpnp ABI {L.pnp_abi_version()} != binding ABI {ABI_VERSION}")

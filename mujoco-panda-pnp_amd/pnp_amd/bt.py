@@ -104,6 +104,16 @@ class Retry(Behaviour):
             return Status.FAILURE
         return st
 
+    def stop(self, new_status: Status = Status.INVALID) -> None:
+        """py_trees.decorators.Decorator.stop: an INVALID stop (a parent resetting) stops the
+        child too, and a child still RUNNING is stopped whatever the decorator's own status."""
+        self.terminate(new_status)
+        if new_status == Status.INVALID:
+            self.child.stop(new_status)
+        if self.child.status == Status.RUNNING:
+            self.child.stop(Status.INVALID)
+        self.status = new_status
+
 
 class BehaviourTree:
     def __init__(self, root: Behaviour):

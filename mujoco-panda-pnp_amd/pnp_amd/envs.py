@@ -130,6 +130,11 @@ class BatchedFrankaShelfPNPEnv:
         self._O = _lib.PnpEnvOut(*[self.out[k].data_ptr() for k in _lib.ENV_OUT_FIELDS])
         f64 = dt == torch.float64
         L = self.engine.lib
+        self._eval = L.pnp_env_evaluate_f64 if f64 else L.pnp_env_evaluate
+        self.eval_out = dict(obs=z(B, _lib.OBS_DIM), achieved_goal=z(B, 3), desired_goal=z(B, 3), reward=z(B),
+                             is_success=z(B))
+        self._EO = _lib.PnpEnvOut(*[self.eval_out[k].data_ptr() if k in self.eval_out else None
+                                    for k in _lib.ENV_OUT_FIELDS])
         self._init = L.pnp_env_init_f64 if f64 else L.pnp_env_init
         self._reset = L.pnp_env_reset_f64 if f64 else L.pnp_env_reset
         self._step = L.pnp_env_step_f64 if f64 else L.pnp_env_step
@@ -178,6 +183,21 @@ class BatchedFrankaShelfPNPEnv:
                 self.reset(done)
         obs = {k: v.clone() for k, v in self._obs().items()}
         return obs, reward, term, trunc, info
+
+    def evaluate(self, achieved_goal=None, desired_goal=None):
+        """_get_obs + compute_reward / _is_success at the current state, no step (pnp_env_evaluate):
+        returns the eval_out dict (obs / achieved_goal / desired_goal observed, reward / is_success
+        for the given goals, default the observed ones).  Views: copy before the next call."""
+        def goals(g):
+            if g is None:
+                return None, None
+            t = torch.as_tensor(g, device=self.device).to(self.dtype).reshape(self.num_envs, 3).contiguous()
+            return t, _ptr(t)
+        ag, agp = goals(achieved_goal)
+        dg, dgp = goals(desired_goal)
+        _lib.check(self._eval(self.engine._h, C.byref(self._S), C.byref(self.params), C.byref(self._E), agp, dgp,
+                              C.byref(self._EO), self.num_envs, _stream()), "pnp_env_evaluate")
+        return self.eval_out
 
     # ---------------------------------------------------------------- helpers (panda_env.py:317-352)
     def _site_frames(self):
@@ -319,6 +339,40 @@ class FrankaShelfPNPEnv:
 
     def close(self):
         pass
+
+    # ---------------------------------------------------------------- reward / observation (panda_env.py:205-315)
+    def _evaluate(self, achieved_goal=None, desired_goal=None):
+        self._push()
+        return self._b.evaluate(achieved_goal, desired_goal)
+
+    def _get_obs(self):
+        """FrankaEnv._get_obs (panda_env.py:279-301) at the current data (device: pnp_env_evaluate)."""
+        out = self._evaluate()
+        return {"observation": out["obs"][0].double().cpu().numpy(),
+                "achieved_goal": out["achieved_goal"][0].double().cpu().numpy(),
+                "desired_goal": out["desired_goal"][0].double().cpu().numpy()}
+
+    def compute_reward(self, achieved_goal, desired_goal, info):
+        """FrankaEnv.compute_reward (panda_env.py:205-245): np.float32 reward for one achieved /
+        desired goal pair at the current data (device: pnp_env_evaluate)."""
+        out = self._evaluate(np.asarray(achieved_goal, np.float64).reshape(1, 3),
+                             np.asarray(desired_goal, np.float64).reshape(1, 3))
+        return np.float32(out["reward"][0].item())
+
+    def _is_success(self, achieved_goal, desired_goal):
+        """FrankaEnv._is_success (panda_env.py:303-306)."""
+        out = self._evaluate(np.asarray(achieved_goal, np.float64).reshape(1, 3),
+                             np.asarray(desired_goal, np.float64).reshape(1, 3))
+        return np.float32(out["is_success"][0].item())
+
+    @staticmethod
+    def goal_distance(a, b):
+        """FrankaEnv.goal_distance (panda_env.py:311-315)."""
+        return np.linalg.norm(np.array(a) - np.array(b), axis=-1)
+
+    @property
+    def initial_object_height(self):
+        return float(self._b.env["obj_height0"][0])
 
     # ---------------------------------------------------------------- helpers (panda_env.py:317-352)
     def get_ee_position(self):

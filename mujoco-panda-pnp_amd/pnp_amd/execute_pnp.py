@@ -50,9 +50,11 @@ def build_pick_place_tasks(env):
     return tasks
 
 
-def run(env_id="FrankaShelfPNPDense-v0", max_tick=3000, sim_steps=5, task_sequence=None, verbose=True):
+def run(env_id="FrankaShelfPNPDense-v0", max_tick=3000, sim_steps=5, task_sequence=None, verbose=True,
+        record_reward=False):
     """execute_pnp.py:46-124 without rendering.  Returns a dict: success, ticks, wall seconds,
-    final object / target positions."""
+    final object / target positions; with record_reward, also the step reward after every tick
+    (_get_obs + compute_reward at the tick's end state, as test/reward_test.py:69-74 records it)."""
     env = make(env_id)
     env.reset()
     u = env.unwrapped
@@ -65,11 +67,14 @@ def run(env_id="FrankaShelfPNPDense-v0", max_tick=3000, sim_steps=5, task_sequen
     tasks = build_pick_place_tasks(env)
     tree = build_pnp_tree(env, [{"obj_meta": t["pick_meta"], "place_meta": t["place_meta"]} for t in tasks],
                           retry_pick=1)
-    success, ticks = False, 0
+    success, ticks, rewards = False, 0, []
     for t in range(max_tick):
         tree.tick()
         u._mujoco.mj_step(u.model, u.data, nstep=sim_steps)   # = sim_steps x mj_step(nstep=1)
         ticks = t + 1
+        if record_reward:
+            o = u._get_obs()
+            rewards.append(float(u.compute_reward(o["achieved_goal"], o["desired_goal"], {})))
         if tree.root.status == Status.SUCCESS:
             success = True
             break
@@ -85,7 +90,8 @@ def run(env_id="FrankaShelfPNPDense-v0", max_tick=3000, sim_steps=5, task_sequen
             print(f"    {n}: at {np.round(obj[n], 3)}, target {np.round(tgt[n], 3)}, "
                   f"distance {np.linalg.norm(obj[n] - tgt[n]):.3f} m")
     env.close()
-    return {"success": success, "ticks": ticks, "wall_s": wall, "objects": obj, "targets": tgt}
+    return {"success": success, "ticks": ticks, "wall_s": wall, "objects": obj, "targets": tgt,
+            "rewards": np.asarray(rewards)}
 
 
 def main(argv=None):

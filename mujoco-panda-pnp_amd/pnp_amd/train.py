@@ -10,6 +10,12 @@ instead of 4 SubprocVecEnv workers.  Same hyper-parameters (pnp_amd.tqc.TQCConfi
 Like the reference, ``task_sequence = ["cube1"]`` is NOT applied (train.py:58 sets it on the
 wrapper, where it has no effect: SURVEY App. B quirk 8); ``--task-sequence cube1`` applies it for
 real.
+
+Update-to-data ratio: the reference's sb3 TQC (train_freq 1, gradient_steps 1) over 4
+SubprocVecEnv workers makes one gradient step per vector step of 4 envs, i.e. one per 4
+transitions (~500k updates over 2M transitions).  ``--gradient-steps`` defaults to the same ratio
+here (``envs // 4`` gradient steps per vector step of ``--envs`` envs); ``--gradient-steps 1``
+gives one update per vector step (the bench's C5 leg: env-bound, ~2000x fewer updates).
 """
 from __future__ import annotations
 
@@ -36,6 +42,9 @@ def main(argv=None):
     ap.add_argument("--task-sequence", default=None, help="comma-separated objects (default: all three)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--log-every", type=int, default=10)
+    ap.add_argument("--gradient-steps", type=int, default=-1,
+                    help="gradient steps per vector step (default -1: envs // 4, the reference's "
+                         "one update per 4 transitions)")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -50,9 +59,11 @@ def main(argv=None):
     env = BatchedFrankaShelfPNPEnv(args.envs, reward_type=reward_type, env_offset=rank * args.envs, config=cfg)
     eval_env = BatchedFrankaShelfPNPEnv(args.eval_episodes, reward_type=reward_type, config=cfg,
                                         env_offset=10 ** 8 + rank * args.eval_episodes)
-    model = TQC(env, TQCConfig(seed=args.seed))
+    gsteps = args.gradient_steps if args.gradient_steps > 0 else max(1, args.envs // 4)
+    model = TQC(env, TQCConfig(seed=args.seed, gradient_steps=gsteps))
     if rank == 0:
-        print(f"==> Training on {env_id} | device=cuda:{local} | {args.envs} envs x {world} GPU(s)", flush=True)
+        print(f"==> Training on {env_id} | device=cuda:{local} | {args.envs} envs x {world} GPU(s) | "
+              f"{gsteps} gradient steps per vector step", flush=True)
     ckpt = Path(args.ckpt_dir)
     ckpt.mkdir(exist_ok=True)
     tag = "sparse" if args.sparse else "dense"

@@ -72,3 +72,24 @@ def test_build_pnp_tree_shape():
     assert kinds == [["PickNode", "PlaceNode", "HomeNode"]] * 3
     t3 = bt.build_pnp_tree(Env(), tasks[:1], retry_pick=3)
     assert type(t3.root.children[0].children[0]).__name__ == "Retry"
+
+
+def test_sequence_reset_stops_a_retried_child():
+    """py_trees Decorator.stop: when a Sequence restarts (its children stopped with INVALID), a
+    Retry stops its decorated child too, so the child's status and state do not stay stale; a child
+    still RUNNING when the decorator itself finishes is stopped as well."""
+    log = []
+    child = Rec("pick", [R], log)
+    seq = bt.Sequence("s", [bt.Retry("r", child, num_failures=3)])
+    assert seq.tick() == R and child.status == R
+    seq.status = bt.Status.INVALID              # parent interrupted: the next tick restarts it
+    log.clear()
+    seq.tick()
+    assert ("term", "pick", bt.Status.INVALID) in log
+    assert log.index(("term", "pick", bt.Status.INVALID)) < log.index(("init", "pick"))
+    log2 = []
+    c2 = Rec("c", [R], log2)
+    r = bt.Retry("r", c2, num_failures=2)
+    r.tick()
+    r.stop(bt.Status.FAILURE)                   # decorator ends while the child still runs
+    assert c2.status == bt.Status.INVALID and ("term", "c", bt.Status.INVALID) in log2

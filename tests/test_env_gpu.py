@@ -12,6 +12,7 @@ step, inside the divergence horizon), and the full configuration with bounds:
   * short physics, fp32: observation within 1e-4, rewards within 1e-4, flags identical;
   * full 250 sub-steps, one gym step from the same state: observation within 5e-3, flags identical.
 """
+import os
 import numpy as np
 import pytest
 import torch
@@ -372,3 +373,42 @@ def test_gpu_env_matches_reference_env_golden(dtype, tol):
     """The fused env kernel against the reference's own FrankaEnv code (golden fixture)."""
     from test_env_oracle import replay_golden
     replay_golden(lambda idx, cfg: _GpuAdapter(idx, dict(cfg), dtype), _close, tol)
+
+
+@pytest.mark.timeout(600)
+def test_gym_full_size_random_actions():
+    """The bench's gym leg at full size -- the workload whose clamped-index build faulted in round
+    2 (profiles/r02/ab_branchless_fault.log): 4096 fp32 envs, routed tiers, 4 gym steps of uniform
+    random actions (pads pressing, cubes knocked over: every tier and the hand-overs run).  No
+    fault, finite state and outputs, no bad-state reset or truncation, no leaked hand-over bits,
+    and the routed run equals the unrouted one bit for bit."""
+    from pnp_amd.envs import BatchedFrankaShelfPNPEnv
+    B = 4096
+    acts = torch.as_tensor(np.random.default_rng(7).uniform(-1, 1, size=(4, B, 7)), dtype=torch.float32, device="cuda")
+    runs = []
+    for route in ("1", "0"):
+        old = os.environ.get("PNP_GYM_ROUTE")
+        os.environ["PNP_GYM_ROUTE"] = route
+        try:
+            env = BatchedFrankaShelfPNPEnv(B, autoreset=False)
+            env.reset()
+            rewards = []
+            for i in range(4):
+                obs, r, term, trunc, info = env.step(acts[i])
+                rewards.append(r)
+                assert bool(torch.isfinite(obs["observation"]).all()) and bool(torch.isfinite(r).all())
+            torch.cuda.synchronize()
+        finally:
+            if old is None:
+                del os.environ["PNP_GYM_ROUTE"]
+            else:
+                os.environ["PNP_GYM_ROUTE"] = old
+        assert bool(torch.isfinite(env.state["qpos"]).all()) and bool(torch.isfinite(env.state["qvel"]).all())
+        w = env.state["warn"].to(torch.int64) & 0xFFFFFFFF
+        assert int((w & 0x1F).max()) == 0, "bad-state reset or contact / row truncation"
+        assert not bool((w >> 16).any()), "a tier hand-over bit leaked out of the call"
+        runs.append((env, torch.stack(rewards)))
+    (a, ra), (b, rb) = runs
+    assert torch.equal(ra, rb)
+    for k in a.state:
+        assert torch.equal(a.state[k], b.state[k]), k

@@ -71,3 +71,29 @@ def test_c5_full_physics_learner_steps():
     assert int((env.state["warn"] & 7).max()) == 0          # no bad-state resets
     for p in list(agent.actor.parameters()) + list(agent.critic.parameters()):
         assert bool(torch.isfinite(p).all())
+
+
+@pytest.mark.timeout(600)
+def test_c5_config_8192_envs():
+    """BASELINE configs[4] at its own size: TQC (train.py hyper-parameters) over 8192 fused gym
+    envs on one GPU, 2 collect + train steps: replay rows = env outputs, finite losses / weights,
+    no bad-state reset, no capacity truncation (warn bits 0..4 clear)."""
+    from pnp_amd.envs import BatchedFrankaShelfPNPEnv
+    from pnp_amd.tqc import TQC, TQCConfig, flat_obs
+    B = 8192
+    env = BatchedFrankaShelfPNPEnv(B)
+    agent = TQC(env, TQCConfig(learning_starts=0))
+    agent.total_timesteps = 2_000_000
+    agent.reset()
+    for k in range(2):
+        reward, done, info = agent.collect_step()
+        assert torch.equal(agent.buffer.rewards[k], reward)
+        assert torch.equal(agent.buffer.next_obs[k][~done], flat_obs(env._obs())[~done])
+        logs = agent.train()
+        assert all(math.isfinite(v) for v in logs.values()), logs
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(agent.buffer.next_obs[:2]).all())
+    assert bool(torch.isfinite(env.state["qpos"]).all()) and bool(torch.isfinite(env.state["qvel"]).all())
+    w = env.state["warn"].to(torch.int64) & 0xFFFFFFFF
+    assert int((w & 0x1F).max()) == 0, "bad-state reset or contact / row truncation"
+    assert int((w >> 16).max()) == 0, "a tier hand-over bit leaked out of the call"
