@@ -152,6 +152,10 @@ const char* pnp_last_error(void);
  * current HIP device (fp32 and fp64 images). */
 int32_t pnp_model_create(const pnp_model_desc* desc, pnp_model** out);
 int32_t pnp_model_destroy(pnp_model* model);
+/* Host-only validation of a model description (no HIP call): builds every host-side image
+ * pnp_model_create would upload (kinematics tables, both precisions' physics images) and reports
+ * the first capacity / consistency error.  0 = the step kernel accepts the model. */
+int32_t pnp_model_check(const pnp_model_desc* desc);
 
 /* Batched mj_kinematics restricted to what the hot path reads (site frames), reference
  * skills/ik_solver.py:58-59, envs/panda_env.py:285-291,344-346, 337-342 (site_xpos / site_xmat).

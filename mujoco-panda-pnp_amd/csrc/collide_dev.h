@@ -179,13 +179,18 @@ __device__ __forceinline__ bool c_clip_seg(const T* p0, const T* p1, T A, T B, T
 // box_face_contacts, same vertex order): clipped incident-edge points, then reference corners
 // strictly inside the incident face.  Fully unrolled: every array index is a compile-time
 // constant, so the polygon lives in VGPRs (no private-memory scratch).
+// Positions relative to the reference box: dpi = pi - pr (formed once from the two centres), the
+// reference face centre at nr * sr[ia]; only the emitted contact position goes back to world
+// coordinates.  (In fp32, world coordinates ~1 m carry 1e-7 m rounding, which the contact
+// stiffness turns into a 1e-5-relative error of the reference acceleration; the box-frame
+// differences here are ~0.05 m.)
 template <typename T, class S>
-__device__ void c_box_face(const T* pr, const T* Rr, const T* sr, int ia, const T* nr, const T* pi, const T* Ri,
+__device__ void c_box_face(const T* pr, const T* Rr, const T* sr, int ia, const T* nr, const T* dpi, const T* Ri,
                            const T* si, const T* nframe, T margin, S& out) {
   const int iu = (ia + 1) % 3, iv = (ia + 2) % 3;
   const T u[3] = {Rr[iu], Rr[3 + iu], Rr[6 + iu]}, v[3] = {Rr[iv], Rr[3 + iv], Rr[6 + iv]};
-  T cref[3];
-  for (int k = 0; k < 3; k++) cref[k] = pr[k] + nr[k] * sr[ia];
+  T cref[3];   // reference face centre relative to pr
+  for (int k = 0; k < 3; k++) cref[k] = nr[k] * sr[ia];
   int ja = 0;
   T best = -1;
   for (int j = 0; j < 3; j++) {
@@ -203,7 +208,7 @@ __device__ void c_box_face(const T* pr, const T* Rr, const T* sr, int ia, const 
   for (int q = 0; q < 4; q++) {
     T w[3];
 #pragma unroll
-    for (int k = 0; k < 3; k++) w[k] = pi[k] + sg * bj[k] * hj + su[q] * bu[k] * hu + sv[q] * bv[k] * hv - cref[k];
+    for (int k = 0; k < 3; k++) w[k] = dpi[k] + sg * bj[k] * hj + su[q] * bu[k] * hu + sv[q] * bv[k] * hv - cref[k];
     P[q][0] = t_dot3(w, u); P[q][1] = t_dot3(w, v); P[q][2] = t_dot3(w, nr);
   }
   const T A = sr[iu] + T(C_BB_TOL), B = sr[iv] + T(C_BB_TOL);   // rectangle grown by the band
@@ -212,7 +217,7 @@ __device__ void c_box_face(const T* pr, const T* Rr, const T* sr, int ia, const 
     if (cnt >= 8 || z > margin + T(C_BB_TOL)) return;
     T pos[3];
 #pragma unroll
-    for (int k = 0; k < 3; k++) pos[k] = cref[k] + u[k] * x + v[k] * y + nr[k] * z * T(0.5);
+    for (int k = 0; k < 3; k++) pos[k] = pr[k] + (cref[k] + u[k] * x + v[k] * y + nr[k] * z * T(0.5));
     out.emit(z, pos, nframe);
     cnt++;
   };
@@ -298,13 +303,15 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
     const T len = PM<T>::sqrt_(t_dot3(L, L));
     for (int k = 0; k < 3; k++) bestn[k] = btl >= 0 ? L[k] / len : -L[k] / len;
   }
-  if (btype == 0) { c_box_face(p1, R1, s1, bi, bestn, p2, R2, s2, bestn, margin, out); return; }
+  if (btype == 0) { c_box_face(p1, R1, s1, bi, bestn, Tv, R2, s2, bestn, margin, out); return; }
   if (btype == 1) {
     const T nr[3] = {-bestn[0], -bestn[1], -bestn[2]};
-    c_box_face(p2, R2, s2, bj, nr, p1, R1, s1, bestn, margin, out);
+    const T dp1[3] = {-Tv[0], -Tv[1], -Tv[2]};
+    c_box_face(p2, R2, s2, bj, nr, dp1, R1, s1, bestn, margin, out);
     return;
   }
-  T pa[3] = {p1[0], p1[1], p1[2]}, pb[3] = {p2[0], p2[1], p2[2]};
+  // edge-edge: the closest points of the two edges, relative to p1
+  T pa[3] = {0, 0, 0}, pb[3] = {Tv[0], Tv[1], Tv[2]};
   for (int t = 0; t < 3; t++) {
     if (t != bi) {
       const T sg = t_dot3(A[t], bestn) > 0 ? T(1) : T(-1);
@@ -322,7 +329,7 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
   if (den > T(1e-12)) { ta = (a * e - dd) / den; tb = (e - a * dd) / den; }
   for (int k = 0; k < 3; k++) { pa[k] += ta * ua[k]; pb[k] += tb * ub[k]; }
   T pos[3];
-  for (int k = 0; k < 3; k++) pos[k] = T(0.5) * (pa[k] + pb[k]);
+  for (int k = 0; k < 3; k++) pos[k] = p1[k] + T(0.5) * (pa[k] + pb[k]);
   out.emit(best, pos, bestn);
 }
 

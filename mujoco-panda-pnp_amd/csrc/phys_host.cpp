@@ -20,6 +20,34 @@ int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
     snprintf(err, errlen, "model exceeds the step kernel's compiled capacity");
     return -1;
   }
+  // index consistency of the tables read below (a malformed description must not read past them)
+  for (int k = 0; k < s->nmesh; k++)
+    if (s->mesh_vertadr[k] < 0 || s->mesh_vertnum[k] < 0 || s->mesh_vertadr[k] + s->mesh_vertnum[k] > s->nmeshvert) {
+      snprintf(err, errlen, "mesh %d: vertices [%d, %d) outside the %d mesh vertices", k, s->mesh_vertadr[k],
+               s->mesh_vertadr[k] + s->mesh_vertnum[k], s->nmeshvert);
+      return -1;
+    }
+  if (s->ngeom > 512) {   // (the collidable-geom map below)
+    snprintf(err, errlen, "more than 512 geoms");
+    return -1;
+  }
+  for (int g = 0; g < s->ngeom; g++)
+    if (s->geom_bodyid[g] < 0 || s->geom_bodyid[g] >= s->nbody ||
+        ((s->geom_contype[g] || s->geom_conaffinity[g]) && s->geom_type[g] == 7 && s->geom_dataid[g] >= s->nmesh)) {
+      snprintf(err, errlen, "geom %d: body or mesh id out of range", g);
+      return -1;
+    }
+  for (int b = 0; b < s->nbody; b++)
+    if (s->body_parentid[b] < 0 || s->body_parentid[b] >= s->nbody || (b > 0 && s->body_parentid[b] >= b) ||
+        s->body_jntadr[b] + s->body_jntnum[b] > s->njnt || s->body_dofadr[b] + s->body_dofnum[b] > s->nv) {
+      snprintf(err, errlen, "body %d: parent / joint / dof ids out of range", b);
+      return -1;
+    }
+  for (int j = 0; j < s->njnt; j++)
+    if (s->jnt_qposadr[j] < 0 || s->jnt_qposadr[j] >= s->nq || s->jnt_dofadr[j] < 0 || s->jnt_dofadr[j] >= s->nv) {
+      snprintf(err, errlen, "joint %d: qpos / dof address out of range", j);
+      return -1;
+    }
   d->nq = s->nq; d->nv = s->nv; d->nu = s->nu; d->nbody = s->nbody; d->njnt = s->njnt;
   d->nmocap = s->nmocap; d->neq = s->neq;
   d->timestep = (T)s->timestep;
@@ -333,6 +361,27 @@ int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
   }
   for (int b = 0; b < s->nbody; b++)
     if (s->body_mocapid[b] >= 0) d->mocap_body[s->body_mocapid[b]] = b;
+  // ---- fp64 chain constants + the first weld (see DevPhys::kd_*)
+  d->weld_eq = -1;
+  d->weld_body[0] = d->weld_body[1] = -1;
+  for (int e = 0; e < s->neq && d->weld_eq < 0; e++)
+    if (s->eq_type[e] == 1) {
+      d->weld_eq = e;
+      d->weld_body[0] = s->eq_obj1id[e];
+      d->weld_body[1] = s->eq_obj2id[e];
+      for (int k = 0; k < 11; k++) d->kd_eq_data[k] = s->eq_data[11 * e + k];
+    }
+  for (int b = 0; b < s->nbody; b++) {
+    for (int k = 0; k < 3; k++) d->kd_body_pos[b][k] = s->body_pos[3 * b + k];
+    for (int k = 0; k < 4; k++) d->kd_body_quat[b][k] = s->body_quat[4 * b + k];
+    const int j = s->body_jntadr[b];
+    const bool one = s->body_jntnum[b] == 1;
+    for (int k = 0; k < 3; k++) {
+      d->kd_jnt_pos[b][k] = one ? s->jnt_pos[3 * j + k] : 0.0;
+      d->kd_jnt_axis[b][k] = one ? s->jnt_axis[3 * j + k] : 0.0;
+    }
+    d->kd_qpos0[b] = one && s->jnt_type[j] != 0 ? s->qpos0[s->jnt_qposadr[j]] : 0.0;
+  }
   // ---- sites
   d->nsite = s->nsite;
   for (int i = 0; i < s->nsite; i++) {

@@ -118,4 +118,13 @@ struct DevPhys {
   int nsite;
   int site_bodyid[PH_MAXS];
   T site_pos[PH_MAXS][3], site_quat[PH_MAXS][4];
+  // fp64 copies of the kinematic chain's constants (per body: offset, its one joint) and of the
+  // first weld's data.  The fp32 build carries the weld bodies' poses in fp64 as well
+  // (st_kinematics -> weld_pose_f64, st_constraints): the weld (solref 0.01) turns a 1e-7 m
+  // position rounding of fp32 kinematics into a 2e-3 m/s^2 error of its reference acceleration,
+  // the dominant fp32 error of the arm's constrained acceleration (DESIGN.md §2, fp32 precision).
+  double kd_body_pos[PH_MAXB][3], kd_body_quat[PH_MAXB][4];
+  double kd_jnt_pos[PH_MAXB][3], kd_jnt_axis[PH_MAXB][3], kd_qpos0[PH_MAXB];
+  double kd_eq_data[11];
+  int weld_eq, weld_body[2];   // the first weld equality and its bodies (-1: none)
 };

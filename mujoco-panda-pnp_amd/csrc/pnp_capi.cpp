@@ -67,6 +67,45 @@ static void fill_dev(DevModel<T>* d, const pnp_model_desc* s) {
   }
 }
 
+// Host-only check of a model description: the kinematics image (fill_dev) and both precisions'
+// physics images (build_phys: pair tables, broadphase groups, hulls, fp64 chain tables) are built
+// in host memory and discarded -- no HIP call, so it runs (and is sanitised) without a GPU.
+extern "C" int32_t pnp_model_check(const pnp_model_desc* desc) {
+  if (!desc) {
+    pnp_set_error("pnp_model_check: null argument");
+    return PNP_ERR_ARG;
+  }
+  if (desc->nbody > PNP_MAXBODY || desc->njnt > PNP_MAXJNT || desc->nq > PNP_MAXQ ||
+      desc->nv > PNP_MAXV || desc->nsite > PNP_MAXSITE || desc->nmocap > PNP_MAXMOCAP ||
+      desc->nbody < 1) {
+    pnp_set_error("pnp_model_check: model exceeds compiled capacity (nbody=%d njnt=%d nq=%d nv=%d nsite=%d)",
+                  desc->nbody, desc->njnt, desc->nq, desc->nv, desc->nsite);
+    return PNP_ERR_MODEL;
+  }
+  DevModel<double>* h = new (std::nothrow) DevModel<double>();
+  DevModel<float>* hf = new (std::nothrow) DevModel<float>();
+  DevPhys<float>* pf = new (std::nothrow) DevPhys<float>();
+  DevPhys<double>* pd = new (std::nothrow) DevPhys<double>();
+  int32_t rc = PNP_OK;
+  char err[256] = {0};
+  if (!h || !hf || !pf || !pd) {
+    pnp_set_error("pnp_model_check: out of host memory");
+    rc = PNP_ERR_ARG;
+  } else {
+    fill_dev(h, desc);
+    fill_dev(hf, desc);
+    if (build_phys(desc, pf, err, sizeof(err)) != 0 || build_phys(desc, pd, err, sizeof(err)) != 0) {
+      pnp_set_error("pnp_model_check: %s", err);
+      rc = PNP_ERR_MODEL;
+    }
+  }
+  delete h;
+  delete hf;
+  delete pf;
+  delete pd;
+  return rc;
+}
+
 extern "C" int32_t pnp_model_create(const pnp_model_desc* desc, pnp_model** out) {
   if (!desc || !out) {
     pnp_set_error("pnp_model_create: null argument");

@@ -134,6 +134,7 @@ struct Env {
   int ncon, nefc, ne, nisland, solver_iter;
   int nlive, ncon_raw;     // collision: broadphase survivors, contacts before the capacity cap
   int nconvex;             // collision: live convex (MPR) pairs
+  double wpose[2][7];      // fp32 builds: the first weld's two body poses in fp64 (pos, quat)
   union {
     struct {
       // kinematics -> velocity stage (and the gym epilogue's site frames / Jacobians)
@@ -487,15 +488,46 @@ __device__ __forceinline__ T row_dot(const Env<T>& s, int r, const T* x, T v) {
 #define mblk(m, i, j) mblk_(s, i, j)
 
 // ============================================================================ position stage
+// sin / cos of an fp64 half joint angle: Taylor series to x^23 / x^24 for |x| <= 2 (truncation
+// below 3e-16; every hinge of the arm stays within +-3.75 rad of qpos0), the math library's
+// sincos otherwise (wave-uniform test: that branch only runs in states outside the joint range)
+__device__ __forceinline__ void half_angle_sincos(double x, double* sn, double* cs) {
+  if (__ballot(!(fabs(x) <= 2.0)) == 0) {
+    const double x2 = x * x;
+    // sin x = x sum_k (-1)^k x^2k / (2k+1)!, cos x = sum_k (-1)^k x^2k / (2k)!, Horner in x^2
+    const double s0 = 1.0, s1 = -1.0 / 6, s2 = 1.0 / 120, s3 = -1.0 / 5040, s4 = 1.0 / 362880,
+                 s5 = -1.0 / 39916800, s6 = 1.0 / 6227020800.0, s7 = -1.0 / 1307674368000.0,
+                 s8 = 1.0 / 355687428096000.0, s9 = -1.0 / 121645100408832000.0,
+                 s10 = 1.0 / 51090942171709440000.0, s11 = -1.0 / 25852016738884976640000.0;
+    const double c0 = 1.0, c1 = -0.5, c2 = 1.0 / 24, c3 = -1.0 / 720, c4 = 1.0 / 40320, c5 = -1.0 / 3628800,
+                 c6 = 1.0 / 479001600, c7 = -1.0 / 87178291200.0, c8 = 1.0 / 20922789888000.0,
+                 c9 = -1.0 / 6402373705728000.0, c10 = 1.0 / 2432902008176640000.0,
+                 c11 = -1.0 / 1124000727777607680000.0, c12 = 1.0 / 620448401733239439360000.0;
+    double a = s11;
+    a = fma(a, x2, s10); a = fma(a, x2, s9); a = fma(a, x2, s8); a = fma(a, x2, s7); a = fma(a, x2, s6);
+    a = fma(a, x2, s5); a = fma(a, x2, s4); a = fma(a, x2, s3); a = fma(a, x2, s2); a = fma(a, x2, s1);
+    a = fma(a, x2, s0);
+    double c = c12;
+    c = fma(c, x2, c11); c = fma(c, x2, c10); c = fma(c, x2, c9); c = fma(c, x2, c8); c = fma(c, x2, c7);
+    c = fma(c, x2, c6); c = fma(c, x2, c5); c = fma(c, x2, c4); c = fma(c, x2, c3); c = fma(c, x2, c2);
+    c = fma(c, x2, c1); c = fma(c, x2, c0);
+    *sn = a * x;
+    *cs = c;
+  } else {
+    sincos(x, sn, cs);
+  }
+}
+
 template <typename T, class CLK>
 __device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
   clk.sub_start();
-  // Bodies with at most one joint (this scene): pointer jumping over parent-relative transforms
-  // (below).  Otherwise a level-synchronous tree pass (mj_kinematics order): a body's frame is
-  // its parent's composed with its own offset and joints, the parent's read from LDS one level
-  // earlier.  Either way the per-body work that does not need the parent -- the model constants
-  // and a single hinge's rotation (sincos) -- is done by every lane at once up front.
+  // Bodies with at most one joint (this scene): pointer jumping over parent-relative transforms,
+  // in fp64 (below).  Otherwise a level-synchronous tree pass in T (mj_kinematics order): a
+  // body's frame is its parent's composed with its own offset and joints, the parent's read from
+  // LDS one level earlier.  Either way the per-body work that does not need the parent -- the
+  // model constants and a single hinge's rotation (sincos) -- is done by every lane at once up
+  // front.
   const int b = lane_id();
   const bool mine = b > 0 && b < m.nbody;
   const int bb = mine ? b : 1;
@@ -503,6 +535,104 @@ __device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
   const int pid = m.body_parentid[bb], ja = m.body_jntadr[bb], jn = m.body_jntnum[bb];
   const int jt = jn > 0 ? m.jnt_type[ja] : -1;
   const int mid = m.body_mocapid[bb];
+  const bool one = jn == 1;
+  const int qa1 = one ? m.jnt_qposadr[ja] : 0;
+  if (!__ballot(mine && jn > 1)) {
+    // Pointer jumping, every frame in fp64 and rounded once to T: every body's frame relative to
+    // its parent (offset, then its one joint) is formed by all lanes at once from the model's fp64
+    // chain constants (DevPhys::kd_*) and the state's exact values, then each lane composes with
+    // its ancestor's accumulated transform and jumps to that ancestor's ancestor --
+    // ceil(log2(depth)) = 4 register exchanges (ds_bpermute) for the arm's 11 levels instead of
+    // one LDS round trip per level.  Rigid transforms compose associatively, so the frames are
+    // MuJoCo's up to fp64 rounding (the order of the compositions differs).  Free-joint and mocap
+    // bodies hang off the world.  Why fp64: an fp32 chain accumulates ~1e-7 m of rounding at the
+    // hand, which the weld (solref 0.01) turns into a 2e-3 m/s^2 error of its reference
+    // acceleration and the contact stiffness into a 1e-5-relative one; in fp64
+    // every frame is within half an fp32 ulp of MuJoCo's, and the first weld's two body poses are
+    // kept in fp64 (s.wpose) for its residual rows (st_constraints).
+    double p[3] = {0, 0, 0}, q[4] = {1, 0, 0, 0}, jax[3] = {0, 0, 0}, jpos[3] = {0, 0, 0}, sl = 0;
+    int anc = 0;
+    if (mine) {
+      if (mid >= 0) {
+        for (int t = 0; t < 3; t++) p[t] = (double)s.mocap_pos[3 * mid + t];
+        for (int t = 0; t < 4; t++) q[t] = (double)s.mocap_quat[4 * mid + t];
+        t_normalize4(q);
+        anc = pid;
+      } else if (one && jt == 0) {
+        for (int t = 0; t < 3; t++) p[t] = (double)s.qpos[qa1 + t];
+        for (int t = 0; t < 4; t++) q[t] = (double)s.qpos[qa1 + 3 + t];
+        t_normalize4(q);
+      } else {
+        double bq[4];
+        for (int t = 0; t < 3; t++) p[t] = m.kd_body_pos[bb][t];
+        for (int t = 0; t < 4; t++) q[t] = bq[t] = m.kd_body_quat[bb][t];
+        if (one) {
+          for (int t = 0; t < 3; t++) { jax[t] = m.kd_jnt_axis[bb][t]; jpos[t] = m.kd_jnt_pos[bb][t]; }
+          sl = (double)s.qpos[qa1] - m.kd_qpos0[bb];
+          if (jt == 2) {
+            double ax[3];
+            t_rotvecquat_mj(ax, jax, bq);
+            for (int t = 0; t < 3; t++) p[t] += ax[t] * sl;
+          } else if (jt == 3 && sl != 0.0) {
+            // rotation qh about the axis through jpos: p += R(bq) (jpos - R(qh) jpos), q = bq qh
+            double sn, cs, qh[4], v[3], u[3], wv[3];
+            half_angle_sincos(sl * 0.5, &sn, &cs);
+            qh[0] = cs; qh[1] = jax[0] * sn; qh[2] = jax[1] * sn; qh[3] = jax[2] * sn;
+            t_rotvecquat_mj(v, jpos, qh);
+            for (int t = 0; t < 3; t++) wv[t] = jpos[t] - v[t];
+            t_rotvecquat_mj(u, wv, bq);
+            for (int t = 0; t < 3; t++) p[t] += u[t];
+            d_mulquat(q, bq, qh);
+          }
+        }
+        anc = pid;
+      }
+    }
+    clk.sub_lap(SC_K_PRE);
+    while (__ballot(anc > 0)) {
+      const int a = anc > 0 ? anc : 0;
+      double pa[3], qa[4];
+      for (int t = 0; t < 3; t++) pa[t] = __shfl(p[t], a);
+      for (int t = 0; t < 4; t++) qa[t] = __shfl(q[t], a);
+      const int a2 = __shfl(anc, a);
+      if (anc > 0) {
+        double r[3];
+        t_rotvecquat_mj(r, p, qa);
+        for (int t = 0; t < 3; t++) p[t] = pa[t] + r[t];
+        d_mulquat(q, qa, q);
+        anc = a2;
+      }
+    }
+    if (mine) {
+      t_normalize4(q);
+      double R[9];
+      d_quat2mat(R, q);
+      for (int t = 0; t < 3; t++) s.xpos[b][t] = (T)p[t];
+      for (int t = 0; t < 4; t++) s.xquat[b][t] = (T)q[t];
+      for (int t = 0; t < 9; t++) s.xmat[b][t] = (T)R[t];
+      if (one && jt == 0) {
+        for (int t = 0; t < 3; t++) { s.xanchor[ja][t] = (T)p[t]; s.xaxis[ja][t] = m.jnt_axis[ja][t]; }
+      } else if (one) {
+        // the joint's axis and anchor in the body's final frame: a hinge leaves its axis and the
+        // point jpos fixed; a slide moved the frame by axis * sl
+        double ax[3], an[3];
+        t_rotvecquat_mj(ax, jax, q);
+        t_rotvecquat_mj(an, jpos, q);
+        for (int t = 0; t < 3; t++) {
+          s.xanchor[ja][t] = (T)(an[t] + p[t] - (jt == 2 ? ax[t] * sl : 0.0));
+          s.xaxis[ja][t] = (T)ax[t];
+        }
+      }
+      if (sizeof(T) == 4 && m.weld_eq >= 0)
+        for (int k = 0; k < 2; k++)
+          if (b == m.weld_body[k]) {
+            for (int t = 0; t < 3; t++) s.wpose[k][t] = p[t];
+            for (int t = 0; t < 4; t++) s.wpose[k][3 + t] = q[t];
+          }
+    }
+  } else {
+  // the body's own constants and joint, loaded up front: offset, a single joint's constants and
+  // qpos, and a single hinge's local rotation (sincos)
   T bp[3], bq[4];
   for (int t = 0; t < 3; t++) bp[t] = m.body_pos[bb][t];
   for (int t = 0; t < 4; t++) bq[t] = m.body_quat[bb][t];
@@ -511,10 +641,6 @@ __device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
     for (int t = 0; t < 4; t++) bq[t] = s.mocap_quat[4 * mid + t];
     t_normalize4(bq);
   }
-  // the body's own joint, loaded up front (bodies here carry at most one joint; a body with more
-  // takes the generic loop): constants, its qpos, and a single hinge's local rotation (sincos)
-  const bool one = jn == 1;
-  const int qa1 = one ? m.jnt_qposadr[ja] : 0;
   T jax[3] = {0, 0, 0}, jpos[3] = {0, 0, 0}, fq[7] = {0, 0, 0, 1, 0, 0, 0}, sl = 0;
   if (one) {
     for (int t = 0; t < 3; t++) { jax[t] = m.jnt_axis[ja][t]; jpos[t] = m.jnt_pos[ja][t]; }
@@ -530,75 +656,6 @@ __device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
     qh[0] = cs; qh[1] = jax[0] * sn; qh[2] = jax[1] * sn; qh[3] = jax[2] * sn;
   }
   clk.sub_lap(SC_K_PRE);
-  if (!__ballot(mine && jn > 1)) {
-    // Pointer jumping: every body's frame relative to its parent (offset, then its one joint) is
-    // formed by all lanes at once, then each lane composes with its ancestor's accumulated
-    // transform and jumps to that ancestor's ancestor -- ceil(log2(depth)) = 4 register
-    // exchanges (ds_bpermute) for the arm's 11 levels instead of one LDS round trip per level.
-    // Rigid transforms compose associatively, so the frames are MuJoCo's up to rounding (the
-    // order of the compositions differs).  Free-joint and mocap bodies hang off the world.
-    T p[3] = {0, 0, 0}, q[4] = {1, 0, 0, 0};
-    int anc = 0;
-    if (mine) {
-      if (one && jt == 0) {
-        p[0] = fq[0]; p[1] = fq[1]; p[2] = fq[2];
-        q[0] = fq[3]; q[1] = fq[4]; q[2] = fq[5]; q[3] = fq[6];
-        t_normalize4(q);
-      } else {
-        for (int t = 0; t < 3; t++) p[t] = bp[t];
-        for (int t = 0; t < 4; t++) q[t] = bq[t];
-        if (one && jt == 2) {
-          T ax[3];
-          t_rotvecquat_mj(ax, jax, bq);
-          for (int t = 0; t < 3; t++) p[t] += ax[t] * sl;
-        } else if (one && jt == 3) {
-          // rotation qh about the axis through jpos: p += R(bq) (jpos - R(qh) jpos), q = bq qh
-          T v[3], w[3], u[3];
-          t_rotvecquat_mj(v, jpos, qh);
-          for (int t = 0; t < 3; t++) w[t] = jpos[t] - v[t];
-          t_rotvecquat_mj(u, w, bq);
-          for (int t = 0; t < 3; t++) p[t] += u[t];
-          d_mulquat(q, bq, qh);
-        }
-        anc = pid;
-      }
-    }
-    while (__ballot(anc > 0)) {
-      const int a = anc > 0 ? anc : 0;
-      T pa[3], qa[4];
-      for (int t = 0; t < 3; t++) pa[t] = __shfl(p[t], a);
-      for (int t = 0; t < 4; t++) qa[t] = __shfl(q[t], a);
-      const int a2 = __shfl(anc, a);
-      if (anc > 0) {
-        T r[3];
-        t_rotvecquat_mj(r, p, qa);
-        for (int t = 0; t < 3; t++) p[t] = pa[t] + r[t];
-        d_mulquat(q, qa, q);
-        anc = a2;
-      }
-    }
-    if (mine) {
-      t_normalize4(q);
-      T R[9];
-      d_quat2mat(R, q);
-      for (int t = 0; t < 3; t++) s.xpos[b][t] = p[t];
-      for (int t = 0; t < 4; t++) s.xquat[b][t] = q[t];
-      for (int t = 0; t < 9; t++) s.xmat[b][t] = R[t];
-      if (one && jt == 0) {
-        for (int t = 0; t < 3; t++) { s.xanchor[ja][t] = p[t]; s.xaxis[ja][t] = jax[t]; }
-      } else if (one) {
-        // the joint's axis and anchor in the body's final frame: a hinge leaves its axis and the
-        // point jpos fixed; a slide moved the frame by axis * sl
-        T ax[3], an[3];
-        t_rotvecquat_mj(ax, jax, q);
-        t_rotvecquat_mj(an, jpos, q);
-        for (int t = 0; t < 3; t++) {
-          s.xanchor[ja][t] = an[t] + p[t] - (jt == 2 ? ax[t] * sl : T(0));
-          s.xaxis[ja][t] = ax[t];
-        }
-      }
-    }
-  } else
   for (int d = 1; __ballot(mine && depth >= d); d++) {
     if (mine && depth == d) {
       T p[3], q[4];
@@ -669,7 +726,17 @@ __device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
     }
     wsync();
   }
+  if (sizeof(T) == 4 && m.weld_eq >= 0 && b < 2) {   // (multi-joint bodies: the T frames)
+    const int wb = m.weld_body[b];
+    for (int t = 0; t < 3; t++) s.wpose[b][t] = s.xpos[wb][t];
+    for (int t = 0; t < 4; t++) s.wpose[b][3 + t] = s.xquat[wb][t];
+  }
+  }
   if (b == 0) {
+    if (sizeof(T) == 4 && m.weld_eq >= 0)
+      for (int k = 0; k < 2; k++)
+        if (m.weld_body[k] == 0)
+          for (int t = 0; t < 7; t++) s.wpose[k][t] = t == 3 ? 1.0 : 0.0;
     for (int t = 0; t < 3; t++) s.xpos[0][t] = 0;
     s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
     for (int t = 0; t < 9; t++) s.xmat[0][t] = (t % 4 == 0) ? T(1) : T(0);
@@ -1369,12 +1436,31 @@ __device__ void st_constraints(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s
     d_mulquat(q, s.xquat[id0], data + 6);
     q1[0] = s.xquat[id1][0]; q1[1] = -s.xquat[id1][1]; q1[2] = -s.xquat[id1][2]; q1[3] = -s.xquat[id1][3];
     d_mulquat(q2, q1, q);
+    T err[6];
+    for (int k = 0; k < 3; k++) { err[k] = pos0[k] - pos1[k]; err[3 + k] = q2[1 + k] * ts; }
+    if (sizeof(T) == 4 && e == m.weld_eq) {
+      // the same residual from the fp64 poses (weld_pose_f64) and fp64 weld data, rounded once
+      const double* kd = m.kd_eq_data;
+      double p0[3], p1[3], qq[4], qc[4], qe[4];
+      t_rotvecquat_mj(p0, kd + 3, &s.wpose[0][3]);
+      t_rotvecquat_mj(p1, kd, &s.wpose[1][3]);
+      d_mulquat(qq, &s.wpose[0][3], kd + 6);
+      qc[0] = s.wpose[1][3]; qc[1] = -s.wpose[1][4]; qc[2] = -s.wpose[1][5]; qc[3] = -s.wpose[1][6];
+      d_mulquat(qe, qc, qq);
+      for (int k = 0; k < 3; k++) {
+        err[k] = (T)((p0[k] + s.wpose[0][k]) - (p1[k] + s.wpose[1][k]));
+        err[3 + k] = (T)(qe[1 + k] * kd[10]);
+      }
+    }
+    T my_err = err[0];
+#pragma unroll
+    for (int k = 1; k < 6; k++) my_err = l == k ? err[k] : my_err;   // (no private-array indexing)
     if (l < 6) {
       const int r = nrow + l;
       s.efc_off[r] = nslot + l * w;
       s.efc_t0[r] = t0; s.efc_t1[r] = t1;
       s.efc_type[r] = 0; s.efc_id[r] = e;
-      row_imp(m, s, r, l < 3 ? pos0[l] - pos1[l] : q2[1 + (l - 3)] * ts, T(0),
+      row_imp(m, s, r, my_err, T(0),
               l < 3 ? m.body_invweight0[id0][0] + m.body_invweight0[id1][0]
                     : m.body_invweight0[id0][1] + m.body_invweight0[id1][1],
               m.eq_solref[e], m.eq_solimp[e]);

@@ -7,14 +7,15 @@ import os
 
 from .model import PnpIKParams, PnpModelDesc
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpnp.so")
+# PNP_LIB: another build of the same sources (tools/asan_cpu_tests.sh: the host-sanitizer build)
+LIB_PATH = os.environ.get("PNP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpnp.so")
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
 ABI_VERSION = 7
 
 # every symbol include/pnp.h declares (tests check the library exports all of them)
 EXPORTS = [
     "pnp_abi_version", "pnp_model_desc_size", "pnp_last_error", "pnp_model_create",
-    "pnp_model_destroy", "pnp_site_kinematics", "pnp_site_kinematics_f64", "pnp_jac_site",
+    "pnp_model_destroy", "pnp_model_check", "pnp_site_kinematics", "pnp_site_kinematics_f64", "pnp_jac_site",
     "pnp_jac_site_f64", "pnp_jac_site_full", "pnp_jac_site_full_f64", "pnp_ik_dls", "pnp_ik_dls_f64", "pnp_step", "pnp_step_f64",
     "pnp_forward_debug", "pnp_forward_debug_f64", "pnp_step_lds_bytes", "pnp_step_profile",
     "pnp_env_params_size", "pnp_env_init", "pnp_env_init_f64", "pnp_env_reset", "pnp_env_reset_f64",
@@ -86,6 +87,8 @@ def load():
     L.pnp_last_error.restype = C.c_char_p
     L.pnp_model_create.argtypes = [C.POINTER(PnpModelDesc), C.POINTER(P)]
     L.pnp_model_create.restype = I32
+    L.pnp_model_check.argtypes = [C.POINTER(PnpModelDesc)]
+    L.pnp_model_check.restype = I32
     L.pnp_model_destroy.argtypes = [P]
     L.pnp_model_destroy.restype = I32
     for name in ("pnp_site_kinematics", "pnp_site_kinematics_f64"):

@@ -18,7 +18,8 @@ ROOT = os.path.dirname(HERE)
 sys.path.insert(0, os.path.join(ROOT, "mujoco-panda-pnp_amd"))
 from pnp_amd.model import PnpIKParams, load_model  # noqa: E402  (host-side model data only)
 
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+# PNP_ORACLE_LIB: another build of the same sources (tools/asan_cpu_tests.sh: liboracle_asan.so)
+LIB_PATH = os.environ.get("PNP_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 
 
 def build():

@@ -104,3 +104,33 @@ def test_debug_layout_matches_header():
     hdr = open(os.path.join(ROOT, "include", "pnp.h")).read()
     defs = {k: int(v) for k, v in re.findall(r"#define PNP_DBG_(\w+) (\d+)", hdr)}
     assert defs == _lib.DBG
+
+
+def test_model_check_builds_host_images_without_gpu(model):
+    """pnp_model_check runs every host-side image builder pnp_model_create uploads (kinematics
+    tables, both physics images: pair tables, broadphase body groups, hulls, the fp64 chain
+    tables) with no HIP call -- the scene passes; descriptions past the compiled capacities or
+    inconsistent ones are refused with a message.  (tools/asan_cpu_tests.sh runs this under
+    ASan + UBSan.)"""
+    from pnp_amd import _lib
+    L = _lib.load()
+    d = model.desc()
+    assert L.pnp_model_check(C.byref(d)) == 0, L.pnp_last_error()
+    assert L.pnp_model_check(None) == -1
+    fresh = lambda: type(d).from_buffer_copy(model.desc())   # (desc() is cached: mutate copies)
+    for field, value in (("nbody", 1000), ("nq", 10_000), ("nbody", 0)):
+        bad = fresh()
+        setattr(bad, field, value)
+        assert L.pnp_model_check(C.byref(bad)) < 0, field
+        assert L.pnp_last_error()
+    bad = fresh()
+    bad.nmeshvert = 100_000          # hulls past the step kernel's vertex capacity
+    assert L.pnp_model_check(C.byref(bad)) == -3 and b"capacity" in L.pnp_last_error()
+    # a hull whose vertex range runs past the vertex table: refused before any read of it
+    import numpy as np
+    vn = np.array(model.mesh_vertnum, np.int32).copy()
+    vn[0] = model.nmeshvert + 5
+    bad = fresh()
+    bad.mesh_vertnum = vn.ctypes.data_as(C.POINTER(C.c_int32))
+    assert L.pnp_model_check(C.byref(bad)) == -3 and b"mesh 0" in L.pnp_last_error()
+    assert L.pnp_model_check(C.byref(model.desc())) == 0
