@@ -374,6 +374,15 @@ int32_t pnp_env_step_f64(pnp_model* model, const pnp_state_f64* state, const pnp
                          const pnp_env_state* env, const double* action, const pnp_env_out* out, int32_t B,
                          void* stream);
 
+/* ------------------------------------------------------------------ skills */
+/* RotateSkill.reset's trajectory (reference skills/rotate.py:39-46) for B skills: target =
+ * R(start) * R(delta) and scipy Slerp([0, 1], [start, target]) at np.linspace(0, 1, steps).
+ * Quaternions scalar-last (scipy's x, y, z, w: the skill hands MuJoCo's w, x, y, z to scipy
+ * unchanged), device fp64 arrays: start[B*4], delta[B*4] -> target[B*4]
+ * (may be NULL), track[B*steps*4]. */
+int32_t pnp_slerp_track_f64(const double* start_xyzw, const double* delta_xyzw, int32_t steps,
+                            double* target_xyzw, double* track_xyzw, int32_t B, void* stream);
+
 /* FrankaEnv._get_obs (panda_env.py:279-301) + compute_reward / _is_success (:205-245, :303-306)
  * at the current state, without stepping: data.site_* of the last forward (env->qpos_kin), the
  * current qvel / finger qpos, current_task_index, initial_object_height.  ag / dg ([B*3], same

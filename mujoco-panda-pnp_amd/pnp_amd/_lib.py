@@ -20,6 +20,7 @@ EXPORTS = [
     "pnp_forward_debug", "pnp_forward_debug_f64", "pnp_step_lds_bytes", "pnp_step_profile",
     "pnp_env_params_size", "pnp_env_init", "pnp_env_init_f64", "pnp_env_reset", "pnp_env_reset_f64",
     "pnp_env_step", "pnp_env_step_f64", "pnp_env_evaluate", "pnp_env_evaluate_f64",
+    "pnp_slerp_track_f64",
 ]
 
 STATE_FIELDS = ("qpos", "qvel", "ctrl", "mocap_pos", "mocap_quat", "qacc_warmstart", "time", "warn")
@@ -137,6 +138,8 @@ def load():
         f = getattr(L, name)
         f.argtypes = [P, SP, EP, ES, P, P, EO, I32, P]
         f.restype = I32
+    L.pnp_slerp_track_f64.argtypes = [P, P, I32, P, P, I32, P]
+    L.pnp_slerp_track_f64.restype = I32
     if L.pnp_abi_version() != ABI_VERSION:
         raise PnpError(f"libpnp ABI {L.pnp_abi_version()} != binding ABI {ABI_VERSION}")
     if L.pnp_env_params_size() != C.sizeof(PnpEnvParams):

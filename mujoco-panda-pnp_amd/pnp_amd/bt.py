@@ -12,9 +12,15 @@ start, HomeNode moves to ``env.home_pos`` over 30 steps.
 from __future__ import annotations
 
 import enum
+import types
 from typing import Any, Dict, List
 
-from .skills import GripperSkill, MoveIKSkill, MoveSkill, RotateSkill
+from . import skills as _default_skills
+
+# the skill classes the nodes build (a namespace: the batched runner, pnp_amd.batched_bt, passes
+# variants whose IK goes through its batched server)
+DEFAULT_SKILLS = types.SimpleNamespace(RotateSkill=_default_skills.RotateSkill, MoveIKSkill=_default_skills.MoveIKSkill,
+                                       MoveSkill=_default_skills.MoveSkill, GripperSkill=_default_skills.GripperSkill)
 
 
 class Status(enum.Enum):
@@ -129,10 +135,11 @@ class BehaviourTree:
 class PickNode(Behaviour):
     """nodes/pick.py: Rotate -> MoveIK approach_wpt1 -> MoveIK obj_pos -> Grasp -> MoveIK approach_wpt2."""
 
-    def __init__(self, env: Any, meta: Dict[str, Any], name: str | None = None):
+    def __init__(self, env: Any, meta: Dict[str, Any], name: str | None = None, skills=None):
         super().__init__(name or f"Pick-{meta.get('id', 'obj')}")
         self.env, self.meta = env, meta
-        self.skills: List[Any] = [RotateSkill(env, meta["delta_q"])]
+        self.sk = skills or DEFAULT_SKILLS
+        self.skills: List[Any] = [self.sk.RotateSkill(env, meta["delta_q"])]
         self.phase = 0
         self.curr = None
 
@@ -147,13 +154,13 @@ class PickNode(Behaviour):
         if getattr(self.curr, "done", False):
             self.phase += 1
             if self.phase == 1:
-                self.skills.append(MoveIKSkill(self.env, self.meta["approach_wpt1"]))
+                self.skills.append(self.sk.MoveIKSkill(self.env, self.meta["approach_wpt1"]))
             elif self.phase == 2:
-                self.skills.append(MoveIKSkill(self.env, self.meta["obj_pos"]))
+                self.skills.append(self.sk.MoveIKSkill(self.env, self.meta["obj_pos"]))
             elif self.phase == 3:
-                self.skills.append(GripperSkill.close(self.env))
+                self.skills.append(self.sk.GripperSkill.close(self.env))
             elif self.phase == 4:
-                self.skills.append(MoveIKSkill(self.env, self.meta["approach_wpt2"]))
+                self.skills.append(self.sk.MoveIKSkill(self.env, self.meta["approach_wpt2"]))
             if self.phase >= len(self.skills):
                 return Status.SUCCESS
             self.curr = self.skills[self.phase]
@@ -168,9 +175,10 @@ class PickNode(Behaviour):
 class PlaceNode(Behaviour):
     """nodes/place.py: MoveIK approach_wpt1 -> MoveIK home_wpt -> Rotate back -> MoveIK approach_wpt2 -> open."""
 
-    def __init__(self, env: Any, meta: Dict[str, Any], name: str = "Place"):
+    def __init__(self, env: Any, meta: Dict[str, Any], name: str = "Place", skills=None):
         super().__init__(name)
         self.env, self.meta = env, meta
+        self.sk = skills or DEFAULT_SKILLS
         self.skills: List[Any] = []
         self.phase = 0
         self.curr = None
@@ -194,15 +202,15 @@ class PlaceNode(Behaviour):
 
     def _build_skill(self, phase: int):
         if phase == 0:
-            return MoveIKSkill(self.env, self.meta["approach_wpt1"])
+            return self.sk.MoveIKSkill(self.env, self.meta["approach_wpt1"])
         if phase == 1:
-            return MoveIKSkill(self.env, self.meta["home_wpt"])
+            return self.sk.MoveIKSkill(self.env, self.meta["home_wpt"])
         if phase == 2:
-            return RotateSkill(self.env, self.meta["rotate_back_quat"])
+            return self.sk.RotateSkill(self.env, self.meta["rotate_back_quat"])
         if phase == 3:
-            return MoveIKSkill(self.env, self.meta["approach_wpt2"])
+            return self.sk.MoveIKSkill(self.env, self.meta["approach_wpt2"])
         if phase == 4:
-            return GripperSkill.open(self.env)
+            return self.sk.GripperSkill.open(self.env)
         raise ValueError(f"[PlaceNode] Invalid phase {phase}")
 
     def terminate(self, new_status: Status) -> None:
@@ -218,16 +226,17 @@ class PlaceNode(Behaviour):
 class HomeNode(Behaviour):
     """nodes/home.py: MoveSkill to env.home_pos over 30 steps."""
 
-    def __init__(self, env: Any, name: str = "Home"):
+    def __init__(self, env: Any, name: str = "Home", skills=None):
         super().__init__(name)
         self.env = env
+        self.sk = skills or DEFAULT_SKILLS
         self.skill = None
 
     def initialise(self) -> None:
         home_pos = getattr(self.env, "home_pos", None)
         if home_pos is None:
             home_pos = self.env.get_ee_position()
-        self.skill = MoveSkill(self.env, target_pos=home_pos, steps=30)
+        self.skill = self.sk.MoveSkill(self.env, target_pos=home_pos, steps=30)
         self.skill.reset()
 
     def update(self) -> Status:
@@ -243,15 +252,16 @@ class HomeNode(Behaviour):
         return self.status == Status.SUCCESS
 
 
-def build_pnp_tree(env: Any, tasks: List[Dict[str, Any]], retry_pick: int = 3) -> BehaviourTree:
-    """trees/pnp_tree.py: root Sequence(memory) of per-object Sequence(Pick [Retry], Place, Home)."""
+def build_pnp_tree(env: Any, tasks: List[Dict[str, Any]], retry_pick: int = 3, skills=None) -> BehaviourTree:
+    """trees/pnp_tree.py: root Sequence(memory) of per-object Sequence(Pick [Retry], Place, Home).
+    ``skills``: the skill classes the nodes build (default: pnp_amd.skills)."""
     root = Sequence(name="PnP-Root")
     for i, task in enumerate(tasks):
-        pick: Behaviour = PickNode(env, meta=task["obj_meta"], name=f"Pick-{i}")
+        pick: Behaviour = PickNode(env, meta=task["obj_meta"], name=f"Pick-{i}", skills=skills)
         if retry_pick > 1:
             pick = Retry(name=f"RetryPick-{i}", child=pick, num_failures=retry_pick)
-        place = PlaceNode(env, meta=task["place_meta"], name=f"Place-{i}")
-        home = HomeNode(env, name=f"Home-{i}")
+        place = PlaceNode(env, meta=task["place_meta"], name=f"Place-{i}", skills=skills)
+        home = HomeNode(env, name=f"Home-{i}", skills=skills)
         sub = Sequence(name=f"PnP-Task-{i}")
         sub.add_children([pick, place, home])
         root.add_child(sub)

@@ -8,6 +8,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+import numpy as np
+
 import torch
 
 from . import _lib
@@ -192,6 +194,23 @@ class Engine:
                    iterations=torch.empty(B, dtype=torch.int32, device=dev),
                    flags=torch.empty(B, dtype=torch.uint8, device=dev))
         return self.ik_dls_into(q_init, target, out, site=site, **params)
+
+
+    # ------------------------------------------------------------------ skills
+    def slerp_track(self, start_xyzw, delta_xyzw, steps):
+        """RotateSkill's trajectories for B skills (pnp_slerp_track_f64, reference
+        skills/rotate.py:39-46): returns (target [B,4], track [B,steps,4]), scipy x, y, z, w."""
+        dev = self.device
+        a = torch.as_tensor(np.asarray(start_xyzw, np.float64).reshape(-1, 4), device=dev).contiguous()
+        d = torch.as_tensor(np.asarray(delta_xyzw, np.float64).reshape(-1, 4), device=dev).contiguous()
+        B = a.shape[0]
+        if d.shape[0] != B:
+            raise ValueError("start and delta quaternions must have the same batch size")
+        tgt = torch.empty(B, 4, dtype=torch.float64, device=dev)
+        trk = torch.empty(B, int(steps), 4, dtype=torch.float64, device=dev)
+        _lib.check(self.lib.pnp_slerp_track_f64(_ptr(a), _ptr(d), int(steps), _ptr(tgt), _ptr(trk), B, _stream()),
+                   "pnp_slerp_track_f64")
+        return tgt.cpu().numpy(), trk.cpu().numpy()
 
 
 _ENGINES = {}

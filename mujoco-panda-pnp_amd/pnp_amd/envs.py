@@ -199,6 +199,31 @@ class BatchedFrankaShelfPNPEnv:
                               C.byref(self._EO), self.num_envs, _stream()), "pnp_env_evaluate")
         return self.eval_out
 
+    def step_subset(self, idx, actions):
+        """FrankaEnv.step for the envs ``idx`` only (no auto-reset): their state and episode
+        state are gathered into a contiguous sub-batch, stepped by one pnp_env_step launch and
+        scattered back; the other envs are untouched.  Per env the result is the full-batch
+        step's (envs are independent).  Returns the sub-batch's outputs (device tensors)."""
+        idx = torch.as_tensor(idx, dtype=torch.long, device=self.device)
+        n = int(idx.numel())
+        a = torch.as_tensor(actions, device=self.device).to(self.dtype).reshape(n, 7).contiguous()
+        st = {k: v.index_select(0, idx).contiguous() for k, v in self.state.items()}
+        ev = {k: v.index_select(0, idx).contiguous() for k, v in self.env.items()}
+        z = lambda *sh, d=self.dtype: torch.zeros(*sh, dtype=d, device=self.device)
+        out = dict(obs=z(n, _lib.OBS_DIM), achieved_goal=z(n, 3), desired_goal=z(n, 3), reward=z(n),
+                   is_success=z(n), terminated=z(n, d=torch.uint8), truncated=z(n, d=torch.uint8))
+        S, _, _ = self.engine._state_struct(st)
+        E = _lib.PnpEnvState(*[ev[k].data_ptr() for k in _lib.ENV_STATE_FIELDS])
+        O = _lib.PnpEnvOut(*[out[k].data_ptr() for k in _lib.ENV_OUT_FIELDS])
+        if n:
+            _lib.check(self._step(self.engine._h, C.byref(S), C.byref(self.params), C.byref(E), _ptr(a), C.byref(O), n,
+                                  _stream()), "pnp_env_step")
+        for k, v in st.items():
+            self.state[k].index_copy_(0, idx, v)
+        for k, v in ev.items():
+            self.env[k].index_copy_(0, idx, v)
+        return out
+
     # ---------------------------------------------------------------- helpers (panda_env.py:317-352)
     def _site_frames(self):
         """site_xpos / site_xmat of the last forward (data.site_*)."""
@@ -282,12 +307,14 @@ class FrankaShelfPNPEnv:
     metadata = {"render_modes": [], "render_fps": 20}
 
     def __init__(self, reward_type="dense", render_mode=None, device=None, dtype=torch.float64,
-                 max_episode_steps=300, config: EnvConfig | None = None):
+                 max_episode_steps=300, config: EnvConfig | None = None, env_index: int = 0):
         from .mjshim import MjData, MujocoShim, UtilsShim
         if render_mode not in (None,):
             raise ValueError("rendering is not part of this engine (render_mode must be None)")
         cfg = dataclasses.replace(config or EnvConfig(), max_episode_steps=max_episode_steps)
-        self._b = BatchedFrankaShelfPNPEnv(1, reward_type, device=device, dtype=dtype, autoreset=False, config=cfg)
+        # env_index: the Philox counter of this env's reset draws (env i of a batched run)
+        self._b = BatchedFrankaShelfPNPEnv(1, reward_type, device=device, dtype=dtype, autoreset=False, config=cfg,
+                                           env_offset=int(env_index))
         self.model = self._b.model
         self.data = MjData(self.model)
         self._mujoco = MujocoShim(self._b.engine, dtype)
@@ -364,6 +391,11 @@ class FrankaShelfPNPEnv:
         out = self._evaluate(np.asarray(achieved_goal, np.float64).reshape(1, 3),
                              np.asarray(desired_goal, np.float64).reshape(1, 3))
         return np.float32(out["is_success"][0].item())
+
+    def slerp_track(self, start_xyzw, delta_xyzw, steps):
+        """RotateSkill's target and slerp trajectory on the device (pnp_slerp_track_f64)."""
+        t, trk = self._b.engine.slerp_track(start_xyzw, delta_xyzw, steps)
+        return t[0], trk[0]
 
     @staticmethod
     def goal_distance(a, b):

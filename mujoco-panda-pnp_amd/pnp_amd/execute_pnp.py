@@ -50,23 +50,20 @@ def build_pick_place_tasks(env):
     return tasks
 
 
-def run(env_id="FrankaShelfPNPDense-v0", max_tick=3000, sim_steps=5, task_sequence=None, verbose=True,
-        record_reward=False):
-    """execute_pnp.py:46-124 without rendering.  Returns a dict: success, ticks, wall seconds,
-    final object / target positions; with record_reward, also the step reward after every tick
-    (_get_obs + compute_reward at the tick's end state, as test/reward_test.py:69-74 records it)."""
-    env = make(env_id)
-    env.reset()
+def run_on(env, max_tick=3000, sim_steps=5, record_reward=False, skills=None):
+    """execute_pnp.py:79-114 on an env that has been reset and given its task sequence: 20 gym
+    steps with the gripper opening, the pick / place tasks from the current site poses,
+    build_pnp_tree(retry_pick=1), then ticks with ``sim_steps`` extra mj_step's each until the tree
+    succeeds.  ``skills``: the skill classes the tree builds (pnp_amd.bt.DEFAULT_SKILLS).
+    Returns (success, ticks, rewards)."""
     u = env.unwrapped
-    u.task_sequence[:] = list(task_sequence) if task_sequence else ["cube1", "cube2", "cube3"]
-    t0 = time.perf_counter()
     open_act = np.zeros(env.action_space.shape, dtype=np.float32)
     open_act[-1] = 1.0
     for _ in range(20):
         env.step(open_act)
     tasks = build_pick_place_tasks(env)
     tree = build_pnp_tree(env, [{"obj_meta": t["pick_meta"], "place_meta": t["place_meta"]} for t in tasks],
-                          retry_pick=1)
+                          retry_pick=1, skills=skills)
     success, ticks, rewards = False, 0, []
     for t in range(max_tick):
         tree.tick()
@@ -78,6 +75,21 @@ def run(env_id="FrankaShelfPNPDense-v0", max_tick=3000, sim_steps=5, task_sequen
         if tree.root.status == Status.SUCCESS:
             success = True
             break
+    return success, ticks, np.asarray(rewards)
+
+
+def run(env_id="FrankaShelfPNPDense-v0", max_tick=3000, sim_steps=5, task_sequence=None, verbose=True,
+        record_reward=False, env_index=0):
+    """execute_pnp.py:46-124 without rendering.  Returns a dict: success, ticks, wall seconds,
+    final object / target positions; with record_reward, also the step reward after every tick
+    (_get_obs + compute_reward at the tick's end state, as test/reward_test.py:69-74 records it).
+    ``env_index``: the env's Philox counter (the reset draws of env i of a batched run)."""
+    env = make(env_id, env_index=env_index)
+    env.reset()
+    u = env.unwrapped
+    u.task_sequence[:] = list(task_sequence) if task_sequence else ["cube1", "cube2", "cube3"]
+    t0 = time.perf_counter()
+    success, ticks, rewards = run_on(env, max_tick, sim_steps, record_reward)
     wall = time.perf_counter() - t0
     obj = {n: u._utils.get_site_xpos(u.model, u.data, f"{n}_site").copy() for n in u.task_sequence}
     tgt = {n: u._utils.get_site_xpos(u.model, u.data, f"target_{n}").copy() for n in u.task_sequence}
@@ -91,7 +103,7 @@ def run(env_id="FrankaShelfPNPDense-v0", max_tick=3000, sim_steps=5, task_sequen
                   f"distance {np.linalg.norm(obj[n] - tgt[n]):.3f} m")
     env.close()
     return {"success": success, "ticks": ticks, "wall_s": wall, "objects": obj, "targets": tgt,
-            "rewards": np.asarray(rewards)}
+            "rewards": rewards}
 
 
 def main(argv=None):

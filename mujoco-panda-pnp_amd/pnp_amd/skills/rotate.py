@@ -34,8 +34,14 @@ class RotateSkill(Skill):
         self.done = False
         self.start_pos = self.env.get_ee_position().copy()
         self.start_quat = self.env.get_ee_orientation().copy()
-        self.target_quat = (Rotation.from_quat(self.start_quat) * Rotation.from_quat(self.delta_quat)).as_quat()
-        self.quat_traj = slerp_track(self.start_quat, self.target_quat, self.steps)
+        dev = getattr(self.env.unwrapped, "slerp_track", None)
+        if dev is not None:
+            # on the device (pnp_slerp_track_f64: scipy's composition + Slerp restated, within
+            # 1e-15 of them); batched envs serve many resets in one launch (pnp_amd.batched_bt)
+            self.target_quat, self.quat_traj = dev(self.start_quat, self.delta_quat, self.steps)
+        else:
+            self.target_quat = (Rotation.from_quat(self.start_quat) * Rotation.from_quat(self.delta_quat)).as_quat()
+            self.quat_traj = slerp_track(self.start_quat, self.target_quat, self.steps)
 
     def step(self) -> np.ndarray:
         if self.done:

@@ -31,3 +31,24 @@ def test_execute_pnp_three_cubes():
     obj, tgt = r["objects"]["cube1"], r["targets"]["cube1"]
     shelf_z = 0.73                                   # cube1 rests on the middle board (shelf_pnp.xml)
     assert abs(obj[2] - shelf_z) > 0.05 or np.linalg.norm(obj - tgt) < 0.2, (obj, tgt)
+
+
+@pytest.mark.timeout(900)
+def test_batched_bt_equals_sequential_facade_runs():
+    """§8 f4: the behaviour tree batched over 64 envs of one device env (pnp_amd.batched_bt: every
+    env's own tree / skills / planner in a host thread, their physics, IK and slerp requests
+    served in batched launches) gives, env by env, the sequential facade run of the same env
+    index: same success, same tick count (8 envs checked against sequential runs, every 8th)."""
+    from pnp_amd.batched_bt import run_batched
+    from pnp_amd.execute_pnp import run
+    B = 64
+    res = run_batched(B, task_sequence=["cube1"], max_tick=1500)
+    print(f"batched: success {res['success'].mean():.2f}, ticks {res['ticks'].min()}..{res['ticks'].max()}, "
+          f"{res['rounds']} rounds, launches {res['launches']}")
+    for b in range(0, B, 8):
+        r = run(task_sequence=["cube1"], max_tick=1500, verbose=False, env_index=b)
+        assert (r["success"], r["ticks"]) == (bool(res["success"][b]), int(res["ticks"][b])), (b, r["ticks"], res["ticks"][b])
+    assert res["success"].mean() >= 0.5
+    # batching really happened: the 128 RotateSkill resets (2 per env) took fewer than B slerp
+    # launches, and the planners' IK solves one launch per round at most
+    assert res["launches"]["ik"] < res["rounds"] and res["launches"]["slerp"] < B

@@ -142,3 +142,24 @@ def test_batched_moveik_planner_matches_sequential(model):
         assert logs[b] == lb, b
     n_solves = sum(len(p) for p, _ in got)
     assert planner.launches < n_solves                             # batching saved launches
+
+
+def test_device_slerp_matches_scipy():
+    """RotateSkill's trajectory on the device (pnp_slerp_track_f64) against scipy itself
+    (Rotation composition + Slerp at np.linspace(0, 1, steps), reference skills/rotate.py:39-46)
+    on random and near-identity rotations: within 1e-14."""
+    from scipy.spatial.transform import Rotation, Slerp
+    from pnp_amd.engine import get_engine
+    rng = np.random.default_rng(0)
+    B, steps = 64, 50
+    q0 = rng.normal(size=(B, 4))
+    dq = rng.normal(size=(B, 4))
+    dq[::4] = Rotation.from_euler("y", -90, degrees=True).as_quat()
+    dq[1::4] = [0, 0, 1e-6, 1.0]                       # small-angle branch of as_rotvec / from_rotvec
+    tgt, trk = get_engine().slerp_track(q0, dq, steps)
+    for b in range(B):
+        t_ref = (Rotation.from_quat(q0[b]) * Rotation.from_quat(dq[b])).as_quat()
+        ref = Slerp([0, 1], Rotation.from_quat([q0[b] / np.linalg.norm(q0[b]), t_ref]))(
+            np.linspace(0, 1, steps, endpoint=True)).as_quat()
+        assert np.abs(tgt[b] - t_ref).max() < 1e-14
+        assert np.abs(trk[b] - ref).max() < 1e-14, b

