@@ -568,10 +568,11 @@ def test_wide_tier_matches_oracle(engine, model, pressed):
     dq = np.abs(g["qpos"] - ref["qpos"]).max()
     assert dq < 1e-4, dq
     trunc = _host(_run_env(engine, _dev(pressed, torch.float32), 1, PNP_STEP_COMPACT="1", PNP_STEP_WIDE="0"))
-    # (an env only a contact or two past 48 may land on either side in fp32: its pad points sit on
-    # the clipping band's edge -- the pads interpenetrate face to face)
+    # which envs overflow 48 is decided on the state the kernel gets (fp32-rounded): rounding moves
+    # the most-pressed env's pad pairs across the contact margin (61 -> 45 contacts in the oracle)
+    nc32 = np.array([int(_oracle_fields(_round32(pressed), b, model)["ncon"][0]) for b in range(n)])
     flagged = (trunc["warn"] & 8) != 0
-    assert flagged[np.array(nc) > 50].all() and flagged.sum() >= n - 2, (nc, trunc["warn"])
+    assert (flagged == (nc32 > 48)).all(), (nc32, trunc["warn"])
 
 
 def test_wide_tier_hand_over_is_exact(engine, model, scene, mesh_scene, pressed):
