@@ -54,8 +54,13 @@ NCTRL = 64                      # distinct per-step ctrl draws, cycled
 
 
 def host_threads():
-    """Every core this process may run on (the CPU baseline runs over all cores)."""
-    return max(1, len(os.sched_getaffinity(0)))
+    """The cores this process can actually use (the CPU baseline runs over all
+    cores): its affinity set, bounded by the cgroup CPU quota when one is set -- the GPU box
+    shows 256 cores but grants a 16-CPU quota, and 256 threads on it measured 35 % slower than
+    16 (CFS throttling: profiles/r03/bench_step_v16.log, 78 k vs 122 k env-steps/s)."""
+    n = max(1, len(os.sched_getaffinity(0)))
+    q = cpu_quota()
+    return max(1, min(n, int(np.ceil(q)))) if q else n
 
 
 def cpu_quota():
@@ -192,6 +197,7 @@ def step_cpu_baseline(st, ctrl, budget_s):
         reps += 1
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "env-steps/s", "cores": nth, "kind": "port", "cpu_quota": cpu_quota(),
+            "host_cores": len(os.sched_getaffinity(0)),
             "sample": f"{reps} steps x {n} envs x {NSUB} sub-steps of the same settled C3 envs "
                       f"(envs 0..{n - 1}), fp64 oracle oracle/physics.c, {nth} pthreads, {dt:.1f} s"}
 
@@ -344,6 +350,7 @@ def ik_cpu_baseline(q_host, tgt_host, prm, budget_s):
             break
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "solves/s", "cores": nth, "kind": "port", "cpu_quota": cpu_quota(),
+            "host_cores": len(os.sched_getaffinity(0)),
             "sample": f"{reps} x {n} solves of the same C2 inputs (envs 0..{n - 1}), fp64 oracle "
                       f"oracle/oracle.c, {nth} pthreads, {dt:.1f} s"}
 
