@@ -2903,9 +2903,13 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
         // trees and offsets 2 ahead, its J / W / b / f entries 1 ahead; the Delassus block of a
         // pair is formed at its own update (off the chain through v).  Tree sizes come from
         // registers.
-        int tdn[PH_MAXT];
+        // tree sizes packed 4 bits each (dofnum - 1, <= PH_MAXTDOF = 16): a row's first-tree width
+        // is one bit-field extract, not a select chain over the trees
+        static_assert(PH_MAXT <= 8 && PH_MAXTDOF <= 16, "tree sizes must pack into 4-bit fields");
+        uint32_t tdn_pack = 0;
 #pragma unroll
-        for (int t = 0; t < PH_MAXT; t++) tdn[t] = s.c_tree_dofnum[t];
+        for (int t = 0; t < PH_MAXT; t++)
+          tdn_pack |= (uint32_t)((t < m.ntree ? s.c_tree_dofnum[t] : 1) - 1) << (4 * t);
         struct DRow {   // stage 2
           int j, t0, t1, off0, off1;
           bool act;
@@ -2927,9 +2931,7 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
           return x;
         };
         auto draw = [&](const DRow& x) {
-          int n0 = 0;
-#pragma unroll
-          for (int t = 0; t < PH_MAXT; t++) n0 = x.t0 == t ? tdn[t] : n0;
+          const int n0 = x.t0 >= 0 ? (int)((tdn_pack >> (4 * x.t0)) & 15u) + 1 : 0;
           const int slot = td == x.t0 ? dloc : (td == x.t1 ? n0 + dloc : -1);
           const bool on = x.act && lane_on && slot >= 0;
           const int sl = on ? slot : 0;                 // unconditional, in-range loads; masked below
