@@ -663,6 +663,13 @@ static bool gym_route_enabled() {
   const char* e = getenv("PNP_GYM_ROUTE");
   return !(e && e[0] == '0');
 }
+// PNP_GYM_FULL_RESUME: unset / 1 = the compact pass's hand-overs are resumed by the full tier,
+// whose own hand-overs go on to the wide resume pass (default); 0 = routed steps send the compact
+// pass's hand-overs straight to the wide resume pass (A/B runs)
+static bool gym_full_resume_enabled() {
+  const char* e = getenv("PNP_GYM_FULL_RESUME");
+  return !(e && e[0] == '0');
+}
 // Two side streams per device for the routed passes, forked from and joined back into the
 // caller's stream.  Used only while the full image's lease is held (launch_env_step), which
 // serialises their users per device; creation has its own lock.
@@ -750,9 +757,11 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
     }
     return lease.launched();
   }
-  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, s0, dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
-                     compact ? 1 : 0, wide, route ? 0 : -1);
-  if ((rc = pnp_check_launch("env_step_kernel"))) return fail(rc);
+  if (!route || gym_full_resume_enabled()) {
+    hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, s0, dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
+                       compact ? 1 : 0, wide, route ? 0 : -1);
+    if ((rc = pnp_check_launch("env_step_kernel"))) return fail(rc);
+  }
   if (route) {   // the wide resume pass also takes the routed full pass's hand-overs
     if (const hipError_t he = join_side(0)) {
       pnp_set_error("pnp_env_step: join: %s", hipGetErrorString(he));

@@ -2132,35 +2132,70 @@ __device__ __forceinline__ void island_newton_dir_reg(Env<T>& s, int I, int n) {
     if (i < n) s.p[id[i]] = -y[i] * sc[i];
 }
 
-// generic (merged islands of any size): in-place Cholesky of the packed island block, LDS resident
+// Newton direction of one island of more than 9 dofs (a merged island: the arm holding a box, or
+// resting on one) on the whole wave, in place of the packed block (the factor consumes H).  Jacobi
+// scaling as island_newton_dir_reg.  Factor: left-looking Cholesky in chol_reg's operation order;
+// lane r keeps row r of the scaled block in registers and publishes each finished entry L[r][j]
+// into the packed block, and column j's pivot and every lane's row term read the finished row j
+// from there (one address per wave: broadcast reads).  Solves by columns: forward, y_k from lane
+// k's right-hand side (readlane) and every lane r > k subtracting L[r][k] y_k from its own (the
+// row-oriented order); back, x_k likewise and lane r < k subtracting L[k][r] x_k, read from the
+// packed factor.  (Lane-serial, this island's factor and solves were a chain of ~n^3 / 3
+// dependent LDS round trips: 100-200k cycles per Newton iteration for 15-21 dofs.)
 template <typename T>
-__device__ void island_newton_dir_lds(Env<T>& s, int I, int n) {
-  const unsigned char* idx = s.isl_dof[I];
-  for (int jj = 0; jj < n; jj++) {
-    T sjj = HI(I, jj, jj);
-    for (int kk = 0; kk < jj; kk++) sjj -= HI(I, jj, kk) * HI(I, jj, kk);
-    sjj = PM<T>::sqrt_(sjj > T(0) ? sjj : T(1e-30));
-    HI(I, jj, jj) = sjj;
-    const T inv = T(1) / sjj;
-    for (int ii = jj + 1; ii < n; ii++) {
-      T t = HI(I, ii, jj);
-      for (int kk = 0; kk < jj; kk++) t -= HI(I, ii, kk) * HI(I, jj, kk);
-      HI(I, ii, jj) = t * inv;
+__device__ __attribute__((noinline)) void island_newton_dir_wave(Env<T>& s, int I, int n) {
+  constexpr int NB = PH_MAXV;
+  const int l = lane_id();
+  const bool lr = l < n;
+  const int rc = lr ? l : 0;
+  T* Hb = s.Hp + s.isl_eoff[I];   // entry (a, b), a >= b, at a (a + 1) / 2 + b
+  const int id = s.isl_dof[I][rc];
+  const T hd = Hb[rc * (rc + 1) / 2 + rc];
+  const T sc = lr && hd > T(0) ? T(1) / PM<T>::sqrt_(hd) : T(1);
+  T A[NB];
+#pragma unroll
+  for (int j = 0; j < NB; j++) {
+    const T sj = rdlane(sc, j < NT ? j : 0);
+    const T h = Hb[rc * (rc + 1) / 2 + (j <= rc ? j : 0)];
+    A[j] = lr && j <= l ? h * sc * sj : T(l == j);
+  }
+  wsync();   // every row is in registers before the factor overwrites the block
+#pragma unroll
+  for (int j = 0; j < NB; j++) {
+    if (j >= n) break;
+    const T* Lj = Hb + j * (j + 1) / 2;   // finished row j of the factor (entries k < j)
+    T td = rdlane(A[j], j);
+    T t = A[j];
+#pragma unroll
+    for (int k = 0; k < j; k++) {
+      const T ljk = Lj[k];
+      td -= ljk * ljk;
+      t -= A[k] * ljk;
     }
+    const T d = PM<T>::sqrt_(td > T(0) ? td : T(1e-30));
+    const T inv = T(1) / d;
+    A[j] = l == j ? d : (l > j ? t * inv : A[j]);
+    if (lr && l >= j) Hb[l * (l + 1) / 2 + j] = A[j];
+    wsync();
   }
-  for (int ii = 0; ii < n; ii++) {
-    const int i = idx[ii];
-    T v = s.grad[i];
-    for (int kk = 0; kk < ii; kk++) v -= HI(I, ii, kk) * s.p[idx[kk]];
-    s.p[i] = v / HI(I, ii, ii);
+  // forward: y = L^-1 (S g)
+  T b = lr ? s.grad[id] * sc : T(0);
+#pragma unroll
+  for (int k = 0; k < NB; k++) {
+    if (k >= n) break;
+    const T yk = rdlane(b, k) / rdlane(A[k], k);
+    b = l == k ? yk : (l > k ? b - A[k] * yk : b);
   }
-  for (int ii = n - 1; ii >= 0; ii--) {
-    const int i = idx[ii];
-    T v = s.p[i];
-    for (int kk = ii + 1; kk < n; kk++) v -= HI(I, kk, ii) * s.p[idx[kk]];
-    s.p[i] = v / HI(I, ii, ii);
+  // back: x = L^-T y
+#pragma unroll
+  for (int k = NB - 1; k >= 0; k--) {
+    if (k >= n) continue;
+    const T lkr = Hb[k * (k + 1) / 2 + (l < k ? l : 0)];
+    const T xk = rdlane(b, k) / rdlane(A[k], k);
+    b = l == k ? xk : (l < k ? b - lkr * xk : b);
   }
-  for (int ii = 0; ii < n; ii++) s.p[idx[ii]] = -s.p[idx[ii]];
+  if (lr) s.p[id] = -b * sc;
+  wsync();
 }
 
 // Exact minimiser of each island's convex piecewise quadratic phi_I(a) = cost_I(x + a p)
@@ -2568,13 +2603,18 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     // in-place LDS path (merged islands > 9 dofs) consumes it
     if (gch) {
       newton_dir_groups(s, done);
-    } else if (!done) {
+    } else {
       // one unrolled register variant (islands of <= 9 dofs padded with identity): lanes holding
-      // 6- and 9-dof islands run the same code instead of two divergent copies
-      const int n = s.isl_n[l];
-      if (n <= 9) island_newton_dir_reg<T, 9>(s, l, n);
-      else island_newton_dir_lds(s, l, n);
-      s.isl_hvalid[l] = n <= 9;
+      // 6- and 9-dof islands run the same code instead of two divergent copies; larger (merged)
+      // islands one after the other on the whole wave
+      const int n = !done ? s.isl_n[l] : 0;
+      if (!done && n <= 9) island_newton_dir_reg<T, 9>(s, l, n);
+      if (!done) s.isl_hvalid[l] = n <= 9;
+      wsync();
+      for (uint32_t bm = (uint32_t)__ballot(n > 9); bm; bm &= bm - 1) {
+        const int I = __builtin_ctz(bm);
+        island_newton_dir_wave(s, I, s.isl_n[I]);
+      }
     }
     wsync();
     clk.lap(10);

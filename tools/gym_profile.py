@@ -79,6 +79,15 @@ def main():
             sub = ("noslip_W", "noslip_lists", "newton_gradient", "newton_hessian", "newton_converge",
                    "n_noslip_sweep", "n_efc", "n_newton_iter", "n_convex")
             print("      " + ", ".join(f"{k} {cnt[names.index(k)]:.1f}" for k in sub))
+    # the slowest envs (the gym step's span is the slowest env's sub-step chain): every stage
+    tot_env = prof[:, :16].sum(1)
+    for b in np.argsort(-tot_env)[:4]:
+        per = prof[b] / nsub
+        top = sorted(range(Engine.N_STAGE_CYCLES), key=lambda i: -per[i])[:12]
+        print(f"  slow env {b}: {per[:16].sum():.0f} cycles per sub-step, {ncon[b]:.1f} contacts; "
+              + ", ".join(f"{names[i]} {per[i]:.0f}" for i in top))
+        print("      " + ", ".join(f"{k} {per[names.index(k)]:.1f}" for k in names[Engine.N_STAGE_CYCLES:]
+                                   if k.startswith("n_")))
 
 
 if __name__ == "__main__":
