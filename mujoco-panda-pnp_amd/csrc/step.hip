@@ -355,6 +355,15 @@ __device__ __forceinline__ double rdlane(double v, int l) {
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+// a sum's DPP operand: bound_ctrl set, so that fp32 `v += dpp_s<C>(v)` folds into one
+// v_add_f32_dpp (0 is the identity of the add; every source lane of these in-row patterns is
+// valid); fp64 adds take no DPP operand and keep the move
+template <int CTRL>
+__device__ __forceinline__ float dpp_s(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_s(double v) { return dpp_f<CTRL>(v); }
 // lane K of each row of 16 to the whole row (gfx90a+ DPP row_newbcast)
 template <int K>
 __device__ __forceinline__ float rowbcast(float v) { return dpp_f<0x150 + K>(v); }
@@ -363,10 +372,10 @@ __device__ __forceinline__ double rowbcast(double v) { return dpp_f<0x150 + K>(v
 // sum over each row of 16 lanes, result in every lane of the row
 template <typename T>
 __device__ __forceinline__ T rowsum16(T v) {
-  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
-  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
-  v += dpp_f<0x141>(v);   // row_half_mirror
-  v += dpp_f<0x140>(v);   // row_mirror
+  v += dpp_s<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_s<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_s<0x141>(v);   // row_half_mirror
+  v += dpp_s<0x140>(v);   // row_mirror
   return v;
 }
 // sum over the wave, result (wave-uniform) in every lane
@@ -1768,9 +1777,9 @@ __device__ void st_actuation_smooth(const DevPhys<T>& /*image: phys<T>()*/, Env<
 // its dofs / rows, rowsum8 (three DPP steps) finishes; the groups run concurrently.
 template <typename T>
 __device__ __forceinline__ T rowsum8(T v) {
-  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
-  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
-  v += dpp_f<0x141>(v);   // row_half_mirror: the other quad of the 8
+  v += dpp_s<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_s<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_s<0x141>(v);   // row_half_mirror: the other quad of the 8
   return v;
 }
 template <typename T>
@@ -1800,11 +1809,11 @@ __device__ __forceinline__ void island_sums2(Env<T>& s, const T* vd, const T* vr
       a += vr[r];
       b += vr2[r];
     }
-    T ta = dpp_f<0xB1>(a), tb = dpp_f<0xB1>(b);
+    T ta = dpp_s<0xB1>(a), tb = dpp_s<0xB1>(b);
     a += ta; b += tb;
-    ta = dpp_f<0x4E>(a); tb = dpp_f<0x4E>(b);
+    ta = dpp_s<0x4E>(a); tb = dpp_s<0x4E>(b);
     a += ta; b += tb;
-    ta = dpp_f<0x141>(a); tb = dpp_f<0x141>(b);
+    ta = dpp_s<0x141>(a); tb = dpp_s<0x141>(b);
     a += ta; b += tb;
     if (q == 0) { out[I] = a; out2[I] = b; }
   }
