@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 7
+#define PNP_ABI_VERSION 8
 
 #define PNP_OK 0
 #define PNP_ERR_ARG -1
@@ -271,9 +271,10 @@ int32_t pnp_forward_debug_f64(pnp_model* model, const pnp_state_f64* state, int3
  * kinematics inertial/geom frames, Newton gradient, Newton convergence test, Newton Hessian; then per-sub-step counts summed over the sub-steps (not
  * cycles): ncon, nefc, Newton iterations, live convex pairs, islands, noslip sweep length,
  * broadphase survivors; then 8 ad-hoc sub-stage timers (aux0..aux7, cycles; what each brackets is
- * stated at its sub_lap call in csrc/step.hip).  Separate instantiation: the product kernel
+ * stated at its sub_lap call in csrc/step.hip); then two more counts: noslip sub-steps on the
+ * dense long-list path and on the streaming path.  Separate instantiation: the product kernel
  * carries no timers. */
-#define PNP_NSTAGE 42
+#define PNP_NSTAGE 44
 #define PNP_NSTAGE_CYCLES 27
 int32_t pnp_step_profile(pnp_model* model, const pnp_state* state, int32_t B, int32_t nsub,
                          unsigned long long* stage_cycles, void* stream);

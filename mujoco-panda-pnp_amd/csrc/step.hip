@@ -177,7 +177,9 @@ struct Env {
           T NL[7][9][9];       // island Hessian factors of the group-parallel path (GCH_*), kept while isl_hvalid
         };
         struct {               // no-slip: W = M^-1 J^T and the per-group pair lists
-          T efc_Wv[PH_MAXJSLOT + 8];   // + 8: unmasked 8-slot reads past the last row (zeroed)
+          // packed like efc_Jv (+ 8: unmasked 8-slot reads past the last row, zeroed), or dense
+          // island blocks laid out like jt (st_noslip's dense long-list path)
+          T efc_Wv[PH_MAXJSLOT + 8 > PH_JTCAP ? PH_MAXJSLOT + 8 : PH_JTCAP];
           short ns_list[4][PH_MAXEFC / 2];
           int ns_len[4];
           T rr_g[PH_MAXEFC];   // island row order: forces
@@ -315,7 +317,8 @@ enum {
   SC_BROAD = 16, SC_NARROW, SC_CONVEX, SC_NS_W, SC_NS_LISTS, SC_K_PRE, SC_K_LEVELS, SC_K_FRAMES, SC_N_GRAD,
   SC_N_CONV, SC_N_HESS,
   SN_CON = 27, SN_EFC, SN_ITER, SN_CONVEX, SN_ISLAND, SN_NS_SWEEP, SN_LIVE,
-  SC_AUX0 = 34   // 8 ad-hoc sub-stage timers, SC_AUX0 .. SC_AUX0 + 7
+  SC_AUX0 = 34,  // 8 ad-hoc sub-stage timers, SC_AUX0 .. SC_AUX0 + 7
+  SN_NS_DENSE = 42, SN_NS_STREAM
 };
 
 // ============================================================================ small helpers
@@ -2151,9 +2154,10 @@ __device__ __forceinline__ void island_newton_dir_reg(Env<T>& s, int I, int n) {
 // row-oriented order); back, x_k likewise and lane r < k subtracting L[k][r] x_k, read from the
 // packed factor.  (Lane-serial, this island's factor and solves were a chain of ~n^3 / 3
 // dependent LDS round trips: 100-200k cycles per Newton iteration for 15-21 dofs.)
-template <typename T>
+// NB: the register row length, a compile-time bound on n (16 / 24 / PH_MAXV instantiations: the
+// loops must unroll completely, or the row array goes to scratch)
+template <typename T, int NB>
 __device__ __attribute__((noinline)) void island_newton_dir_wave(Env<T>& s, int I, int n) {
-  constexpr int NB = PH_MAXV;
   const int l = lane_id();
   const bool lr = l < n;
   const int rc = lr ? l : 0;
@@ -2169,39 +2173,44 @@ __device__ __attribute__((noinline)) void island_newton_dir_wave(Env<T>& s, int 
     A[j] = lr && j <= l ? h * sc * sj : T(l == j);
   }
   wsync();   // every row is in registers before the factor overwrites the block
+  // (every loop has a constant trip count and guards on n, so that all of them unroll and the
+  // row stays in registers)
 #pragma unroll
   for (int j = 0; j < NB; j++) {
-    if (j >= n) break;
-    const T* Lj = Hb + j * (j + 1) / 2;   // finished row j of the factor (entries k < j)
-    T td = rdlane(A[j], j);
-    T t = A[j];
+    if (j < n) {
+      const T* Lj = Hb + j * (j + 1) / 2;   // finished row j of the factor (entries k < j)
+      T td = rdlane(A[j], j);
+      T t = A[j];
 #pragma unroll
-    for (int k = 0; k < j; k++) {
-      const T ljk = Lj[k];
-      td -= ljk * ljk;
-      t -= A[k] * ljk;
+      for (int k = 0; k < j; k++) {
+        const T ljk = Lj[k];
+        td -= ljk * ljk;
+        t -= A[k] * ljk;
+      }
+      const T d = PM<T>::sqrt_(td > T(0) ? td : T(1e-30));
+      const T inv = T(1) / d;
+      A[j] = l == j ? d : (l > j ? t * inv : A[j]);
+      if (lr && l >= j) Hb[l * (l + 1) / 2 + j] = A[j];
+      wsync();
     }
-    const T d = PM<T>::sqrt_(td > T(0) ? td : T(1e-30));
-    const T inv = T(1) / d;
-    A[j] = l == j ? d : (l > j ? t * inv : A[j]);
-    if (lr && l >= j) Hb[l * (l + 1) / 2 + j] = A[j];
-    wsync();
   }
   // forward: y = L^-1 (S g)
   T b = lr ? s.grad[id] * sc : T(0);
 #pragma unroll
   for (int k = 0; k < NB; k++) {
-    if (k >= n) break;
-    const T yk = rdlane(b, k) / rdlane(A[k], k);
-    b = l == k ? yk : (l > k ? b - A[k] * yk : b);
+    if (k < n) {
+      const T yk = rdlane(b, k) / rdlane(A[k], k);
+      b = l == k ? yk : (l > k ? b - A[k] * yk : b);
+    }
   }
   // back: x = L^-T y
 #pragma unroll
   for (int k = NB - 1; k >= 0; k--) {
-    if (k >= n) continue;
-    const T lkr = Hb[k * (k + 1) / 2 + (l < k ? l : 0)];
-    const T xk = rdlane(b, k) / rdlane(A[k], k);
-    b = l == k ? xk : (l < k ? b - lkr * xk : b);
+    if (k < n) {
+      const T lkr = Hb[k * (k + 1) / 2 + (l < k ? l : 0)];
+      const T xk = rdlane(b, k) / rdlane(A[k], k);
+      b = l == k ? xk : (l < k ? b - lkr * xk : b);
+    }
   }
   if (lr) s.p[id] = -b * sc;
   wsync();
@@ -2621,8 +2630,10 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       if (!done) s.isl_hvalid[l] = n <= 9;
       wsync();
       for (uint32_t bm = (uint32_t)__ballot(n > 9); bm; bm &= bm - 1) {
-        const int I = __builtin_ctz(bm);
-        island_newton_dir_wave(s, I, s.isl_n[I]);
+        const int I = __builtin_ctz(bm), nI = s.isl_n[I];
+        if (nI <= 16) island_newton_dir_wave<T, 16>(s, I, nI);
+        else if (nI <= 24) island_newton_dir_wave<T, 24>(s, I, nI);
+        else island_newton_dir_wave<T, PH_MAXV>(s, I, nI);
       }
     }
     wsync();
@@ -2697,67 +2708,155 @@ __device__ __forceinline__ void tree_solve_fixed(const T* L, const T* j, T* x_ou
   for (int i = 0; i < N; i++) x_out[i] = x[i];
 }
 
+// Dense long-list sweep (st_noslip): the group's island v in registers, lane q = island dof q;
+// each pair's J and W rows are read at the lane's island position straight from the dense
+// blocks (jt, and W in jt's layout), its 2 x 2 Delassus block from the per-call table (efc_jar /
+// efc_Jp at the pair's island row position, both dead after the Newton stage), so an update is
+// two row sums of J v, the projection and a lane-local v += W df.  List entries are island row
+// positions.  Software pipeline: list entry 3 pairs ahead, the row's efc index 2 ahead, its
+// J / W / b / f / Delassus entries 1 ahead.  Islands are independent under Gauss-Seidel: a group
+// sweeps its (<= 2) islands one after the other, each in its own row order.
+template <typename T>
+__device__ __attribute__((noinline)) void st_noslip_dense_sweep(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
+                                                                int iend0, int iend1) {
+  const DevPhys<T>& m = phys<T>();
+  const int l = lane_id(), grp = l >> 4, q = l & 15;
+  {   // Delassus blocks, lane per pair: A_ab = J_a . W_b over the island's dofs
+    const int L0 = s.ns_len[0], L1 = s.ns_len[1], L2 = s.ns_len[2], L3 = s.ns_len[3];
+    const int tot = L0 + L1 + L2 + L3;
+    for (int e = l; e < tot; e += NT) {
+      const int g = e < L0 ? 0 : (e < L0 + L1 ? 1 : (e < L0 + L1 + L2 ? 2 : 3));
+      const int k = e - (g > 0 ? L0 : 0) - (g > 1 ? L1 : 0) - (g > 2 ? L2 : 0);
+      const int p = s.ns_list[g][k];
+      const int I = s.tree_island[s.efc_t0[s.isl_row[p]]], n = s.isl_n[I];
+      const int o = s.isl_joff[I] + (p - s.isl_roff[I]) * n;
+      const T* J = s.jt + o;
+      const T* W = s.efc_Wv + o;
+      T a00 = 0, a01 = 0, a10 = 0, a11 = 0;
+      for (int c = 0; c < n; c++) {
+        const T j0 = J[c], j1 = J[n + c], w0 = W[c], w1 = W[n + c];
+        a00 += j0 * w0;
+        a01 += j0 * w1;
+        a10 += j1 * w0;
+        a11 += j1 * w1;
+      }
+      s.efc_jar[p] = a00;
+      s.efc_jar[p + 1] = a01;
+      s.efc_Jp[p] = a10;
+      s.efc_Jp[p + 1] = a11;
+    }
+  }
+  wsync();
+  for (int si = 0; si < 2; si++) {
+    const int I = grp + 4 * si;
+    const bool has = I < s.nisland;
+    const int k0 = si ? iend0 : 0;
+    const int cnt = has ? (si ? iend1 : iend0) - k0 : 0;
+    const int maxc = max(max(__builtin_amdgcn_readlane(cnt, 0), __builtin_amdgcn_readlane(cnt, 16)),
+                         max(__builtin_amdgcn_readlane(cnt, 32), __builtin_amdgcn_readlane(cnt, 48)));
+    if (maxc == 0) continue;
+    const int n = has ? s.isl_n[I] : 0;
+    const int r0 = has ? s.isl_roff[I] : 0;
+    const bool lane_on = q < n;
+    const int qq = lane_on ? q : 0;
+    const int d = lane_on ? s.isl_dof[I][q] : 0;
+    const int jo = has ? s.isl_joff[I] - r0 * n : 0;   // (row position p, island dof c) at jo + p n + c
+    T v = lane_on ? s.v2[d] : T(0);
+    struct DRow {   // stage 2
+      int p, j;
+      bool act;
+    };
+    struct DRaw {   // stage 1
+      int j;
+      bool act;
+      T J0, J1, W0, W1, b0, b1, f0, f1, a00, a01, a10, a11;
+    };
+    auto dlist = [&](int k) { return k < cnt ? (int)s.ns_list[grp][k0 + k] : -1; };
+    auto drow = [&](int p) {
+      DRow x;
+      x.act = p >= 0;
+      x.p = x.act ? p : r0;   // (an inactive slot reads the island's first row, masked below)
+      x.j = s.isl_row[x.p];
+      return x;
+    };
+    auto draw = [&](const DRow& x) {
+      DRaw w;
+      w.j = x.j;
+      w.act = x.act;
+      const int o = jo + x.p * n + qq;
+      const T J0 = s.jt[o], J1 = s.jt[o + n], W0 = s.efc_Wv[o], W1 = s.efc_Wv[o + n];
+      const bool on = x.act && lane_on;
+      w.J0 = on ? J0 : T(0);
+      w.J1 = on ? J1 : T(0);
+      w.W0 = on ? W0 : T(0);
+      w.W1 = on ? W1 : T(0);
+      w.b0 = s.efc_bb[x.j];
+      w.b1 = s.efc_bb[x.j + 1];
+      w.f0 = s.efc_force[x.j];
+      w.f1 = s.efc_force[x.j + 1];
+      w.a00 = s.efc_jar[x.p];
+      w.a01 = s.efc_jar[x.p + 1];
+      w.a10 = s.efc_Jp[x.p];
+      w.a11 = s.efc_Jp[x.p + 1];
+      return w;
+    };
+    auto update = [&](const DRaw& cur) {
+      const T r0v = rowsum16(cur.J0 * v) + cur.b0;
+      const T r1v = rowsum16(cur.J1 * v) + cur.b1;
+      const T f0 = cur.f0, f1 = cur.f1;
+      const T a00 = cur.a00, a01 = cur.a01, a10 = cur.a10, a11 = cur.a11;
+      const T bc0 = r0v - (a00 * f0 + a01 * f1), bc1 = r1v - (a10 * f0 + a11 * f1);
+      const T mid = T(0.5) * (f0 + f1);
+      const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;
+      T y = -K0 / K1;
+      y = y < -mid ? -mid : (y > mid ? mid : y);
+      const bool flat = K1 < T(1e-15);
+      const T n0 = flat ? mid : mid + y, n1 = flat ? mid : mid - y;
+      const T d0 = cur.act ? n0 - f0 : T(0), d1 = cur.act ? n1 - f1 : T(0);
+      v += cur.W0 * d0 + cur.W1 * d1;
+      if (cur.act && q == 0) { s.efc_force[cur.j] = n0; s.efc_force[cur.j + 1] = n1; }
+    };
+    for (int iter = 0; iter < m.noslip_iterations; iter++) {
+      // unrolled by two with the stage registers alternating (ra / rb), so that the loop carries
+      // no register moves and no wait on the loads it has just issued
+      DRaw ra = draw(drow(dlist(0)));
+      DRow x1 = drow(dlist(1));
+      int p2 = dlist(2);
+      for (int k = 0; k < maxc; k += 2) {
+        const int p3 = dlist(k + 3);
+        const DRow x2 = drow(p2);
+        const DRaw rb = draw(x1);
+        update(ra);
+        if (k + 1 >= maxc) break;
+        const int p4 = dlist(k + 4);
+        const DRow x3 = drow(p3);
+        ra = draw(x2);
+        update(rb);
+        x1 = x3;
+        p2 = p4;
+      }
+      wsync();   // the next sweep reads the forces this one wrote
+    }
+    if (lane_on) s.v2[d] = v;
+  }
+  wsync();
+}
+
 template <typename T, class CLK>
 __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (m.noslip_iterations <= 0 || s.nefc == 0) return;
   clk.sub_start();
-  {   // zero the 8 slots past the last row: the tail of the force-space setup's unmasked reads
-    const int rl = s.nefc - 1;
-    const int end = s.efc_off[rl] + row_width(m, s.efc_t0[rl], s.efc_t1[rl]);
-    if (l < 8) s.efc_Wv[end + l] = T(0);
-  }
-  // W_r = M^-1 J_r^T for contact rows (block-diagonal M: solve per tree of the row)
-  for (int r = l; r < s.nefc; r += NT) {
-    if (s.efc_type[r] != 6) continue;
-    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
-    int base = 0;
-    for (int h = 0; h < 2; h++) {
-      const int t = h ? t1 : t0;
-      if (t < 0) continue;
-      const int n = s.c_tree_dofnum[t], o = s.c_tree_moff[t];
-      if (n == 9 || n == 6) {
-        const T* Jr = s.efc_Jv + s.efc_off[r] + base;
-        T* Wr = s.efc_Wv + s.efc_off[r] + base;
-        if (n == 9) tree_solve_fixed<9>(s.L + o, Jr, Wr);
-        else tree_solve_fixed<6>(s.L + o, Jr, Wr);
-        base += n;
-        continue;
-      }
-      T y[PH_MAXTDOF];
-      for (int i = 0; i < n; i++) {
-        T v = EJ(r, base + i);
-        for (int k = 0; k < i; k++) v -= s.L[o + i * n + k] * y[k];
-        y[i] = v / s.L[o + i * n + i];
-      }
-      for (int i = n - 1; i >= 0; i--) {
-        T v = y[i];
-        for (int k = i + 1; k < n; k++) v -= s.L[o + k * n + i] * EW(r, base + k);
-        EW(r, base + i) = v / s.L[o + i * n + i];
-      }
-      base += n;
-    }
-  }
-  clk.sub_lap(SC_NS_W);
-  // v = M^-1 J^T f over the dof's island rows
-  const bool jt = s.jt_ok;
-  if (jt) {
-    gather_rows(s, s.efc_force, s.rr_g);
-    wsync();
-  }
-  if (l < m.nv) {
-    const int t = s.c_dof_tree[l], I = s.tree_island[t];
-    const T g = jt ? jt_dof_sum(s, I, s.dof_ipos[l], T(0), s.rr_g)
-                   : dof_row_sum(T(0), s, I, t, l - s.c_tree_dofadr[t], s.efc_force, (const T*)nullptr, false);
-    s.v2[l] = g;
-  }
+  constexpr int NSR = 8;   // short lists (see the force-space path below)
   // Pair lists: islands are independent under Gauss-Seidel (block-diagonal M, rows inside one
   // island), so island I runs on DPP row (I mod 4) — 16 lanes, one slot per lane — in its own
   // row order, and up to 4 pairs are updated at once; each island sees exactly the sequential
   // order, so the result equals the one-pair-at-a-time sweep.
   const int grp = l >> 4, q = l & 15;
-  int iend[2] = {0, 0};   // end of the group's first / second island in its list (group-uniform)
+  // end of the group's first / second island in its list (group-uniform; two scalars, not an
+  // array: a runtime index would put it in scratch)
+  int iend0 = 0, iend1 = 0;
   {
     int len = 0, si = 0;
     for (int I = grp; I < s.nisland; I += 4, si++) {
@@ -2773,16 +2872,122 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
         if (start) s.ns_list[grp][len + __popc(bits & ((1u << q) - 1u))] = (short)r;
         len += __popc(bits);
       }
-      iend[si & 1] = len;
+      if (si == 0) iend0 = len;
+      else iend1 = len;
     }
     if (q == 0) s.ns_len[grp] = len;
   }
   wsync();
+  const int maxlen = max(max(s.ns_len[0], s.ns_len[1]), max(s.ns_len[2], s.ns_len[3]));
+  bool small = true;
+  for (int I = grp; I < s.nisland; I += 4) small = small && s.isl_n[I] <= 16;
+  // Dense long lists: a group with more than NSR pairs (closed fingers pressed together put
+  // 50-150 pairs on the arm island) on islands of <= 16 dofs, with the dense island Jacobian
+  // blocks (jt): W is built in jt's layout and each pair's 2 x 2 Delassus block once per call
+  // (st_noslip_dense_sweep).  Every tier takes this path under the same conditions (jt_ok
+  // holds below the wide tier, which hands over otherwise).
+  const bool dense = s.jt_ok && maxlen > NSR && !__ballot(!small);
+  if (dense) {
+    // the list entries become island row positions (jt / W row index); efc_Jp is free here
+    for (int rr = l; rr < s.nefc; rr += NT) s.efc_Jp[s.isl_row[rr]] = T(rr);
+    wsync();
+#pragma unroll
+    for (int g = 0; g < 4; g++)
+      for (int k = l; k < s.ns_len[g]; k += NT) s.ns_list[g][k] = (short)(int)s.efc_Jp[s.ns_list[g][k]];
+    // W_r = M^-1 J_r^T for contact rows, dense: the row's island block row, zero off its trees
+    for (int rr = l; rr < s.nefc; rr += NT) {
+      const int r = s.isl_row[rr];
+      if (s.efc_type[r] != 6) continue;
+      const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
+      const int I = s.tree_island[t0], n = s.isl_n[I];
+      T* row = s.efc_Wv + s.isl_joff[I] + (rr - s.isl_roff[I]) * n;
+      for (int c = 0; c < n; c++) row[c] = T(0);
+      int base = 0;
+      for (int h = 0; h < 2; h++) {
+        const int t = h ? t1 : t0;
+        if (t < 0) continue;
+        const int nt = s.c_tree_dofnum[t], o = s.c_tree_moff[t];
+        const T* Jr = s.efc_Jv + s.efc_off[r] + base;
+        T* Wr = row + s.tree_ipos[t];   // the tree's dofs are contiguous in island order
+        if (nt == 9) tree_solve_fixed<9>(s.L + o, Jr, Wr);
+        else if (nt == 6) tree_solve_fixed<6>(s.L + o, Jr, Wr);
+        else {
+          T y[PH_MAXTDOF];
+          for (int i = 0; i < nt; i++) {
+            T v = Jr[i];
+            for (int k = 0; k < i; k++) v -= s.L[o + i * nt + k] * y[k];
+            y[i] = v / s.L[o + i * nt + i];
+          }
+          for (int i = nt - 1; i >= 0; i--) {
+            T v = y[i];
+            for (int k = i + 1; k < nt; k++) v -= s.L[o + k * nt + i] * Wr[k];
+            Wr[i] = v / s.L[o + i * nt + i];
+          }
+        }
+        base += nt;
+      }
+    }
+  } else {
+    {   // zero the 8 slots past the last row: the tail of the force-space setup's unmasked reads
+      const int rl = s.nefc - 1;
+      const int end = s.efc_off[rl] + row_width(m, s.efc_t0[rl], s.efc_t1[rl]);
+      if (l < 8) s.efc_Wv[end + l] = T(0);
+    }
+    // W_r = M^-1 J_r^T for contact rows (block-diagonal M: solve per tree of the row)
+    for (int r = l; r < s.nefc; r += NT) {
+      if (s.efc_type[r] != 6) continue;
+      const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
+      int base = 0;
+      for (int h = 0; h < 2; h++) {
+        const int t = h ? t1 : t0;
+        if (t < 0) continue;
+        const int n = s.c_tree_dofnum[t], o = s.c_tree_moff[t];
+        if (n == 9 || n == 6) {
+          const T* Jr = s.efc_Jv + s.efc_off[r] + base;
+          T* Wr = s.efc_Wv + s.efc_off[r] + base;
+          if (n == 9) tree_solve_fixed<9>(s.L + o, Jr, Wr);
+          else tree_solve_fixed<6>(s.L + o, Jr, Wr);
+          base += n;
+          continue;
+        }
+        T y[PH_MAXTDOF];
+        for (int i = 0; i < n; i++) {
+          T v = EJ(r, base + i);
+          for (int k = 0; k < i; k++) v -= s.L[o + i * n + k] * y[k];
+          y[i] = v / s.L[o + i * n + i];
+        }
+        for (int i = n - 1; i >= 0; i--) {
+          T v = y[i];
+          for (int k = i + 1; k < n; k++) v -= s.L[o + k * n + i] * EW(r, base + k);
+          EW(r, base + i) = v / s.L[o + i * n + i];
+        }
+        base += n;
+      }
+    }
+  }
+  clk.sub_lap(SC_NS_W);
+  // v = M^-1 J^T f over the dof's island rows
+  const bool jt = s.jt_ok;
+  if (jt) {
+    gather_rows(s, s.efc_force, s.rr_g);
+    wsync();
+  }
+  if (l < m.nv) {
+    const int t = s.c_dof_tree[l], I = s.tree_island[t];
+    const T g = jt ? jt_dof_sum(s, I, s.dof_ipos[l], T(0), s.rr_g)
+                   : dof_row_sum(T(0), s, I, t, l - s.c_tree_dofadr[t], s.efc_force, (const T*)nullptr, false);
+    s.v2[l] = g;
+  }
+  wsync();
   solve_M(m, s, s.v2, s.v2);
   const int glen = s.ns_len[grp];
-  const int maxlen = max(max(s.ns_len[0], s.ns_len[1]), max(s.ns_len[2], s.ns_len[3]));
   clk.sub_lap(SC_NS_LISTS);
   clk.count(SN_NS_SWEEP, maxlen);
+  clk.count(SN_NS_DENSE, dense ? 1 : 0);
+  if (dense) {
+    st_noslip_dense_sweep(m, s, iend0, iend1);
+    return;
+  }
   // One pair of opposing pyramid edges per group and step; sparse rows have <= 16 slots = one
   // DPP row.  A pair's J, W, b and slot dofs are read-only here, so the next pair's are loaded
   // while the current one is updated; only v2 and the forces (written by the previous update)
@@ -2817,7 +3022,6 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   // update is then one LDS read of v at the slot's dof, two row sums, the 2 x 2 projection and
   // the write back of v; the forces return to LDS once, after the last iteration.  Same
   // arithmetic in the same order as the streaming path below.
-  constexpr int NSR = 8;
   // Force space (the common case: every group's pairs act on the same trees, so their packed
   // slots address the same dofs): lane q of a group owns pair-row q (pair q / 2, edge q & 1) of
   // the group's list and keeps its residual r_q = J_q v + b_q and its row of the Delassus block
@@ -2931,14 +3135,12 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   // islands one after the other: each island sees the sequential order.  Rounding differs from
   // the streaming path (row sums in island-dof lane order).
   if (maxlen > NSR) {
-    bool small = true;
-    for (int I = grp; I < s.nisland; I += 4) small = small && s.isl_n[I] <= 16;
     if (!__ballot(!small)) {
       for (int si = 0; si < 2; si++) {
         const int I = grp + 4 * si;
         const bool has = I < s.nisland;
-        const int k0 = si ? iend[0] : 0;
-        const int cnt = has ? iend[si] - k0 : 0;
+        const int k0 = si ? iend0 : 0;
+        const int cnt = has ? (si ? iend1 : iend0) - k0 : 0;
         const int maxc = max(max(__builtin_amdgcn_readlane(cnt, 0), __builtin_amdgcn_readlane(cnt, 16)),
                              max(__builtin_amdgcn_readlane(cnt, 32), __builtin_amdgcn_readlane(cnt, 48)));
         if (maxc == 0) continue;
@@ -3078,6 +3280,7 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     wsync();
     return;
   }
+  clk.count(SN_NS_STREAM, 1);
   for (int iter = 0; iter < m.noslip_iterations; iter++) {
     NsPair cur = fetch(0);
     for (int k = 0; k < maxlen; k++) {

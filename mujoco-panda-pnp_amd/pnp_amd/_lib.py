@@ -10,7 +10,7 @@ from .model import PnpIKParams, PnpModelDesc
 # PNP_LIB: another build of the same sources (tools/asan_cpu_tests.sh: the host-sanitizer build)
 LIB_PATH = os.environ.get("PNP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpnp.so")
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # every symbol include/pnp.h declares (tests check the library exports all of them)
 EXPORTS = [

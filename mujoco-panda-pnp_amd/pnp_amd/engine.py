@@ -148,7 +148,9 @@ class Engine:
               # per-sub-step counts (summed over sub-steps), not cycles
               "n_con", "n_efc", "n_newton_iter", "n_convex", "n_island", "n_noslip_sweep", "n_live",
               # ad-hoc sub-stage timers (cycles; see the sub_lap calls in csrc/step.hip)
-              "aux0", "aux1", "aux2", "aux3", "aux4", "aux5", "aux6", "aux7")
+              "aux0", "aux1", "aux2", "aux3", "aux4", "aux5", "aux6", "aux7",
+              # noslip path counts (sub-steps on the dense long-list / the streaming path)
+              "n_ns_dense", "n_ns_stream")
     N_STAGE_CYCLES = 27
 
     def step_profile(self, st, nsub=1):
