@@ -2154,8 +2154,9 @@ __device__ __forceinline__ void island_newton_dir_reg(Env<T>& s, int I, int n) {
 // row-oriented order); back, x_k likewise and lane r < k subtracting L[k][r] x_k, read from the
 // packed factor.  (Lane-serial, this island's factor and solves were a chain of ~n^3 / 3
 // dependent LDS round trips: 100-200k cycles per Newton iteration for 15-21 dofs.)
-// NB: the register row length, a compile-time bound on n (16 / 24 / PH_MAXV instantiations: the
-// loops must unroll completely, or the row array goes to scratch)
+// NB: the register row length, a compile-time bound on n (the loops must unroll completely, or
+// the row array goes to scratch).  One instantiation (PH_MAXV): a dispatch over 16 / 24 / 36 cost
+// C3 1.1 % through st_newton's register allocation around the three call sites.
 template <typename T, int NB>
 __device__ __attribute__((noinline)) void island_newton_dir_wave(Env<T>& s, int I, int n) {
   const int l = lane_id();
@@ -2631,9 +2632,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       wsync();
       for (uint32_t bm = (uint32_t)__ballot(n > 9); bm; bm &= bm - 1) {
         const int I = __builtin_ctz(bm), nI = s.isl_n[I];
-        if (nI <= 16) island_newton_dir_wave<T, 16>(s, I, nI);
-        else if (nI <= 24) island_newton_dir_wave<T, 24>(s, I, nI);
-        else island_newton_dir_wave<T, PH_MAXV>(s, I, nI);
+        island_newton_dir_wave<T, PH_MAXV>(s, I, nI);
       }
     }
     wsync();
