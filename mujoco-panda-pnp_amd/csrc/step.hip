@@ -2739,10 +2739,13 @@ __device__ __attribute__((noinline)) void st_noslip_dense_sweep(const DevPhys<T>
         a10 += j1 * w0;
         a11 += j1 * w1;
       }
-      s.efc_jar[p] = a00;
-      s.efc_jar[p + 1] = a01;
-      s.efc_Jp[p] = a10;
-      s.efc_Jp[p + 1] = a11;
+      // the projection's coefficients (see update below); 1 / K1 = 0 for a flat pair (K1 < 1e-15),
+      // whose forces then stay at their mean
+      const T K1 = a00 + a11 - a01 - a10;
+      s.efc_jar[p] = a00 - a11;
+      s.efc_jar[p + 1] = a00 - a10;
+      s.efc_Jp[p] = a01 - a11;
+      s.efc_Jp[p + 1] = K1 < T(1e-15) ? T(0) : T(1) / K1;
     }
   }
   wsync();
@@ -2768,7 +2771,7 @@ __device__ __attribute__((noinline)) void st_noslip_dense_sweep(const DevPhys<T>
     struct DRaw {   // stage 1
       int j;
       bool act;
-      T J0, J1, W0, W1, b0, b1, f0, f1, a00, a01, a10, a11;
+      T Jd, W0, W1, bd, f0, f1, pc, u, w, iK1;
     };
     auto dlist = [&](int k) { return k < cnt ? (int)s.ns_list[grp][k0 + k] : -1; };
     auto drow = [&](int p) {
@@ -2785,34 +2788,32 @@ __device__ __attribute__((noinline)) void st_noslip_dense_sweep(const DevPhys<T>
       const int o = jo + x.p * n + qq;
       const T J0 = s.jt[o], J1 = s.jt[o + n], W0 = s.efc_Wv[o], W1 = s.efc_Wv[o + n];
       const bool on = x.act && lane_on;
-      w.J0 = on ? J0 : T(0);
-      w.J1 = on ? J1 : T(0);
+      w.Jd = on ? J0 - J1 : T(0);
       w.W0 = on ? W0 : T(0);
       w.W1 = on ? W1 : T(0);
-      w.b0 = s.efc_bb[x.j];
-      w.b1 = s.efc_bb[x.j + 1];
+      w.bd = s.efc_bb[x.j] - s.efc_bb[x.j + 1];
       w.f0 = s.efc_force[x.j];
       w.f1 = s.efc_force[x.j + 1];
-      w.a00 = s.efc_jar[x.p];
-      w.a01 = s.efc_jar[x.p + 1];
-      w.a10 = s.efc_Jp[x.p];
-      w.a11 = s.efc_Jp[x.p + 1];
+      w.pc = s.efc_jar[x.p];
+      w.u = s.efc_jar[x.p + 1];
+      w.w = s.efc_Jp[x.p];
+      w.iK1 = s.efc_Jp[x.p + 1];
       return w;
     };
+    // The pair's 2 x 2 projection (the streaming path's, rearranged): with r = J v + b and
+    // A the Delassus block, K0 = mid (a00 - a11) + (r0 - r1) - (a00 - a10) f0 - (a01 - a11) f1,
+    // y = clamp(-K0 / K1, +-mid) -- only r0 - r1 = (J0 - J1) v + b0 - b1 is needed, one row sum
+    // instead of two, and the per-pair coefficients come from the table.  An inactive slot has
+    // zero J and W, so v does not move.
     auto update = [&](const DRaw& cur) {
-      const T r0v = rowsum16(cur.J0 * v) + cur.b0;
-      const T r1v = rowsum16(cur.J1 * v) + cur.b1;
+      const T rd = rowsum16(cur.Jd * v) + cur.bd;
       const T f0 = cur.f0, f1 = cur.f1;
-      const T a00 = cur.a00, a01 = cur.a01, a10 = cur.a10, a11 = cur.a11;
-      const T bc0 = r0v - (a00 * f0 + a01 * f1), bc1 = r1v - (a10 * f0 + a11 * f1);
       const T mid = T(0.5) * (f0 + f1);
-      const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;
-      T y = -K0 / K1;
+      const T K0 = mid * cur.pc + rd - cur.u * f0 - cur.w * f1;
+      T y = -K0 * cur.iK1;
       y = y < -mid ? -mid : (y > mid ? mid : y);
-      const bool flat = K1 < T(1e-15);
-      const T n0 = flat ? mid : mid + y, n1 = flat ? mid : mid - y;
-      const T d0 = cur.act ? n0 - f0 : T(0), d1 = cur.act ? n1 - f1 : T(0);
-      v += cur.W0 * d0 + cur.W1 * d1;
+      const T n0 = mid + y, n1 = mid - y;
+      v += cur.W0 * (n0 - f0) + cur.W1 * (n1 - f1);
       if (cur.act && q == 0) { s.efc_force[cur.j] = n0; s.efc_force[cur.j + 1] = n1; }
     };
     for (int iter = 0; iter < m.noslip_iterations; iter++) {
