@@ -3085,7 +3085,8 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
           A[j] = a;
         }
       }
-      T F0[NSR], F1[NSR], A00[NSR], A01[NSR], A10[NSR], A11[NSR];
+      // per pair: the projection's coefficients from its 2 x 2 Delassus block (see NS_UPD)
+      T F0[NSR], F1[NSR], PC[NSR], PU[NSR], PW[NSR], IK[NSR];
 #pragma unroll
       for (int k = 0; k < NSR; k++) {
         const int jk = k < glen ? s.ns_list[grp][k] : 0;
@@ -3093,23 +3094,28 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
         F1[k] = s.efc_force[jk + 1];
       }
 #define NS_BC(K)                                                                          \
-      A00[K] = rowbcast<2 * K>(A[2 * K]); A01[K] = rowbcast<2 * K>(A[2 * K + 1]);         \
-      A10[K] = rowbcast<2 * K + 1>(A[2 * K]); A11[K] = rowbcast<2 * K + 1>(A[2 * K + 1]);
+      {                                                                                   \
+        const T a00 = rowbcast<2 * K>(A[2 * K]), a01 = rowbcast<2 * K>(A[2 * K + 1]);     \
+        const T a10 = rowbcast<2 * K + 1>(A[2 * K]), a11 = rowbcast<2 * K + 1>(A[2 * K + 1]); \
+        const T K1 = a00 + a11 - a01 - a10;                                               \
+        PC[K] = a00 - a11; PU[K] = a00 - a10; PW[K] = a01 - a11;                          \
+        IK[K] = K1 < T(1e-15) ? T(0) : T(1) / K1;                                         \
+      }
       NS_BC(0) NS_BC(1) NS_BC(2) NS_BC(3) NS_BC(4) NS_BC(5) NS_BC(6) NS_BC(7)
 #undef NS_BC
       for (int iter = 0; iter < m.noslip_iterations; iter++) {
+      // the 2 x 2 projection rearranged as in st_noslip_dense_sweep: K0 = mid (a00 - a11) +
+      // (r0 - r1) - (a00 - a10) f0 - (a01 - a11) f1, y = clamp(-K0 / K1, +-mid), 1 / K1 = 0 for
+      // a flat pair (its forces stay at their mean)
 #define NS_UPD(K)                                                                          \
         if (K < maxlen) {                                                                 \
-          const T r0 = rowbcast<2 * K>(r), r1 = rowbcast<2 * K + 1>(r);                  \
+          const T rd = rowbcast<2 * K>(r) - rowbcast<2 * K + 1>(r);                      \
           const T f0 = F0[K], f1 = F1[K];                                                 \
-          const T a00 = A00[K], a01 = A01[K], a10 = A10[K], a11 = A11[K];                 \
-          const T bc0 = r0 - (a00 * f0 + a01 * f1), bc1 = r1 - (a10 * f0 + a11 * f1);     \
           const T mid = T(0.5) * (f0 + f1);                                               \
-          const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;         \
-          T y = -K0 / K1;                                                                 \
+          const T K0 = mid * PC[K] + rd - PU[K] * f0 - PW[K] * f1;                         \
+          T y = -K0 * IK[K];                                                              \
           y = y < -mid ? -mid : (y > mid ? mid : y);                                      \
-          const bool flat = K1 < T(1e-15);                                                \
-          const T n0 = flat ? mid : mid + y, n1 = flat ? mid : mid - y;                   \
+          const T n0 = mid + y, n1 = mid - y;                                             \
           const bool act = K < glen;                                                      \
           const T d0 = act ? n0 - f0 : T(0), d1 = act ? n1 - f1 : T(0);                   \
           r += A[2 * K] * d0 + A[2 * K + 1] * d1;                                         \
