@@ -390,7 +390,7 @@ __device__ __forceinline__ T c_wave_max(T v) {
 template <typename T>
 __device__ void c_load_shape(const DevPhys<T>& /*image: phys<T>()*/, CShape<T>& sh) {
   const DevPhys<T>& m = phys<T>();
-  const int l = threadIdx.x;
+  const int l = threadIdx.x & 63;
   sh.vadr = sh.type == 7 ? m.mesh_vertadr[sh.mesh] : 0;
   sh.nvert = sh.type == 7 ? m.mesh_vertnum[sh.mesh] : 0;
 #pragma unroll
@@ -403,7 +403,7 @@ __device__ void c_load_shape(const DevPhys<T>& /*image: phys<T>()*/, CShape<T>& 
 template <typename T>
 __device__ int c_mesh_argmax(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& s, const T* ld) {
   const DevPhys<T>& m = phys<T>();
-  const int l = threadIdx.x, n = s.nvert;
+  const int l = threadIdx.x & 63, n = s.nvert;
   T dv[C_WV], bd = T(-1e30);
 #pragma unroll
   for (int j = 0; j < C_WV; j++) {

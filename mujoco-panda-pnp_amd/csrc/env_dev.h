@@ -406,26 +406,20 @@ __device__ __forceinline__ int tier_need(const DevPhys<T>& m, const Env<T>& s) {
 // would overflow its capacity stops the env before that sub-step changes the state (controls and
 // state stored, resume bits in warn, no epilogue), and the wide build's resume pass (resume = 1)
 // finishes the physics from that sub-step and runs the epilogue.
+// One env's gym step on its workgroup's wave 0 (env_step_kernel: one env per workgroup; the wide
+// build's env_step_wide_kernel: a persistent loop over the selected envs).  k0: the sub-step to
+// resume from (resume passes); cur: the env's current tier; mw: the workgroup's waves.
 template <typename T>
-__global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
-                                                      pnp_env_params prm, EnvSoA<T> es, const T* __restrict__ action,
-                                                      EnvOutT<T> out, int B, int resume, int hand, int only_tier) {
-  __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
-  Env<T>& s = s_env;
-  const DevPhys<T>& m = phys<T>();
-  (void)mp;
-  const int b = blockIdx.x;
-  if (b >= B) return;
-  const int cur = es.tier ? (es.tier[b] & 3) : 0;
-  if (only_tier >= 0 && es.tier && cur != only_tier) return;   // routed to another tier's pass
+__device__ __forceinline__ void env_step_one(const DevPhys<T>& m, Env<T>& s, const pnp_state_t<T>& st,
+                                             const pnp_env_params& prm, const EnvSoA<T>& es, const T* __restrict__ action,
+                                             const EnvOutT<T>& out, int b, int cur, int k0, int resume, int hand, int mw) {
+  (void)mw;
   const int l = lane_id();
-  int k0 = 0;
-  if (resume) {
-    const uint32_t w = st.warn[b];
-    if (!(w & PNP_RESUME_FLAG)) return;
-    k0 = (int)((w >> PNP_RESUME_SHIFT) & PNP_RESUME_MAXSUB);
-  }
   load_env(m, s, st, b, hand);
+#if PNP_WIDE
+  if (l == 0) s.mw = mw;
+  wsync();
+#endif
   T ee_p[3], ee_R[9], ee_q[4];
   if (!resume) {
   // ---- _set_action: ee pose from the last forward's site frame
@@ -516,6 +510,85 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
   }
 }
 
+template <typename T>
+__global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
+                                                      pnp_env_params prm, EnvSoA<T> es, const T* __restrict__ action,
+                                                      EnvOutT<T> out, int B, int resume, int hand, int only_tier) {
+  __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
+  Env<T>& s = s_env;
+  const DevPhys<T>& m = phys<T>();
+  (void)mp;
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  const int cur = es.tier ? (es.tier[b] & 3) : 0;
+  if (only_tier >= 0 && es.tier && cur != only_tier) return;   // routed to another tier's pass
+  int k0 = 0;
+  if (resume) {
+    const uint32_t w = st.warn[b];
+    if (!(w & PNP_RESUME_FLAG)) return;
+    k0 = (int)((w >> PNP_RESUME_SHIFT) & PNP_RESUME_MAXSUB);
+  }
+  env_step_one(m, s, st, prm, es, action, out, b, cur, k0, resume, hand, 1);
+}
+
+#if PNP_WIDE
+// Wide tier, persistent: the selection kernel lists the envs the pass runs (list[0] = count), and
+// a grid of two workgroups per CU loops over the list.  Each workgroup is MW_WAVES waves: wave 0
+// steps its env, the other is a helper wave for the convex pass (step.hip, mw_helper).  Multi-wave
+// workgroups launched one per env (4096 per pass, nearly all exiting at once) made the gym step
+// 25 % slower even with the helpers idle; a resident grid over the selected envs does not.
+__global__ void __launch_bounds__(1024) wide_select_kernel(const uint8_t* __restrict__ tier,
+                                                           const uint32_t* __restrict__ warn, int B, int resume,
+                                                           int only_tier, int* __restrict__ list) {
+  __shared__ int wcount[16];
+  __shared__ int base;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) base = 0;
+  __syncthreads();
+  for (int c = 0; c < B; c += 1024) {
+    const int b = c + t;
+    bool sel = false;
+    if (b < B)
+      sel = (only_tier < 0 || !tier || (tier[b] & 3) == only_tier) && (!resume || (warn[b] & PNP_RESUME_FLAG));
+    const uint64_t bal = __ballot(sel);
+    if (lane == 0) wcount[w] = __popcll(bal);
+    __syncthreads();
+    int off = base;
+    for (int i = 0; i < w; i++) off += wcount[i];
+    if (sel) list[1 + off + __popcll(bal & ((1ull << lane) - 1ull))] = b;
+    __syncthreads();
+    if (t == 0) {
+      int tot = 0;
+      for (int i = 0; i < 16; i++) tot += wcount[i];
+      base += tot;
+    }
+    __syncthreads();
+  }
+  if (t == 0) list[0] = base;
+}
+__global__ void __launch_bounds__(NT * MW_WAVES, 2) env_step_wide_kernel(pnp_state_t<float> st, pnp_env_params prm,
+                                                                          EnvSoA<float> es, const float* __restrict__ action,
+                                                                          EnvOutT<float> out, const int* __restrict__ list,
+                                                                          int resume) {
+  __shared__ __attribute__((aligned(16))) Env<float> s_env;   // static LDS: see env_lds_note
+  Env<float>& s = s_env;
+  const DevPhys<float>& m = phys<float>();
+  if (threadIdx.x >= NT) {   // helper waves: wave 0's commands until MW_EXIT
+    mw_helper(s);
+    return;
+  }
+  const int count = list[0];
+  for (int i = blockIdx.x; i < count; i += gridDim.x) {
+    const int b = list[1 + i];
+    const int cur = es.tier ? (es.tier[b] & 3) : 0;
+    const int k0 = resume ? (int)((st.warn[b] >> PNP_RESUME_SHIFT) & PNP_RESUME_MAXSUB) : 0;
+    env_step_one(m, s, st, prm, es, action, out, b, cur, k0, resume, 0, MW_WAVES);
+  }
+  if (lane_id() == 0) s.mw_cmd = MW_EXIT;   // every path of wave 0 ends here
+  __syncthreads();
+}
+#endif
+
 #if !PNP_COMPACT && !PNP_WIDE
 __global__ void route_commit_kernel(uint8_t* __restrict__ tier, int B) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -561,18 +634,55 @@ int32_t env_compact_lds_bytes() { return (int32_t)sizeof(Env<float>); }
 // wide tier: resume pass of the gym step over the envs the full kernel handed over (resume = 1),
 // or the routed pass over the envs whose step starts in the wide tier (resume = 0, only_tier = 2);
 // launched by the full build's launch_env_step, which holds the full image's lease
+// The selection lists (one per pass kind: the routed pass on its side stream and the resume pass
+// on the caller's stream can be in flight together), per device; their users are serialised by
+// the full image's lease like the route streams.
+struct WideLists {
+  int* list[2] = {nullptr, nullptr};
+  int cap[2] = {0, 0};
+  int ncu = 0;
+};
+static int32_t wide_list(int kind, int32_t B, int** out, int* ncu) {
+  static std::mutex mu;
+  static WideLists wl[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { pnp_set_error("pnp_env_step: bad device"); return PNP_ERR_HIP; }
+  std::lock_guard<std::mutex> lk(mu);
+  WideLists& w = wl[dev];
+  hipError_t e = hipSuccess;
+  if (!w.ncu) e = hipDeviceGetAttribute(&w.ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess && w.cap[kind] < B + 1) {
+    if (w.list[kind]) e = hipFree(w.list[kind]);   // (synchronises: only when a larger batch arrives)
+    w.list[kind] = nullptr;
+    w.cap[kind] = 0;
+    if (e == hipSuccess) e = hipMalloc((void**)&w.list[kind], sizeof(int) * (size_t)(B + 1));
+    if (e == hipSuccess) w.cap[kind] = B + 1;
+  }
+  if (e != hipSuccess) { pnp_set_error("pnp_env_step: wide list: %s", hipGetErrorString(e)); return PNP_ERR_HIP; }
+  *out = w.list[kind];
+  *ncu = w.ncu > 0 ? w.ncu : 256;
+  return PNP_OK;
+}
 int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
                              const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
                              void* stream, int resume, int only_tier) {
   const DevPhys<float>* src = phys_image<float>(model);
   if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  if (B <= 0) return PNP_OK;
+  int* list = nullptr;
+  int ncu = 0;
+  if (const int32_t rc = wide_list(resume ? 1 : 0, B, &list, &ncu)) return rc;
   ResidentLease lease;
   if (const int32_t rc = lease.acquire(RES_WIDE_F32, model, (const void*)&g_phys_f32, src, sizeof(DevPhys<float>),
                                        stream))
     return rc;
-  hipLaunchKernelGGL(env_step_kernel<float>, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, *p,
-                     env_view<float>(e), action, out_view<float>(o), B, resume, 0, only_tier);
-  if (const int32_t rc = pnp_check_launch("env_step_kernel (wide)")) return rc;
+  hipLaunchKernelGGL(wide_select_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, e->tier, st->warn, B, resume,
+                     only_tier, list);
+  if (const int32_t rc = pnp_check_launch("wide_select_kernel")) return rc;
+  const int grid = B < 2 * ncu ? B : 2 * ncu;   // two envs per CU (LDS)
+  hipLaunchKernelGGL(env_step_wide_kernel, dim3(grid), dim3(NT * MW_WAVES), 0, (hipStream_t)stream, *st, *p,
+                     env_view<float>(e), action, out_view<float>(o), (const int*)list, resume);
+  if (const int32_t rc = pnp_check_launch("env_step_wide_kernel")) return rc;
   return lease.launched();
 }
 #else

@@ -230,6 +230,10 @@ struct Env {
 #endif
   int ovf;                     // a capacity overflowed in this sub-step (hand-over builds)
   int hand;                    // full build: overflows hand over (1) or truncate with a warning (0)
+#if PNP_WIDE
+  int mw;                      // waves of the env's workgroup (the wide gym kernel: helper waves, mw_helper)
+  int mw_cmd;                  // helper command (MW_*), posted by wave 0 before a workgroup barrier
+#endif
 };
 static_assert(sizeof(((Env<float>*)0)->efc_Jv) >= 7 * 4 * NT + 2 * NT + 4 + 2 * PH_MAXLIVE,
               "collision staging + broadphase survivors must fit the efc_Jv union");
@@ -322,7 +326,7 @@ enum {
 };
 
 // ============================================================================ small helpers
-__device__ __forceinline__ int lane_id() { return threadIdx.x; }
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (NT - 1); }   // (the wide gym kernel runs 4 waves)
 // Lane hand-off through LDS inside the env's single wave.  The DS instructions of one wave execute
 // in issue order, so a store by one lane is seen by a later load of any lane of the same wave
 // without an s_waitcnt drain: a wavefront-scope fence (no instruction, a compiler ordering point)
@@ -1111,7 +1115,7 @@ __device__ __forceinline__ int wscan_incl(int x) {
   x += __builtin_amdgcn_mov_dpp(x, 0x118, 0xF, 0xF, true);
   const int r0 = __builtin_amdgcn_readlane(x, 15), r1 = __builtin_amdgcn_readlane(x, 31),
             r2 = __builtin_amdgcn_readlane(x, 47);
-  const int row = (int)(threadIdx.x >> 4);
+  const int row = lane_id() >> 4;
   return x + (row > 0 ? r0 : 0) + (row > 1 ? r1 : 0) + (row > 2 ? r2 : 0);
 }
 // ============================================================================ collision
@@ -1304,6 +1308,94 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
   wsync();
   clk.sub_lap(SC_NARROW);
 }
+
+#if PNP_WIDE
+// ---- helper wave of the wide gym kernel (env_step_wide_kernel runs MW_WAVES waves per env; wave
+// 0 runs the step, the others wait in mw_helper).  Wave 0 posts a command in s.mw_cmd and meets the
+// helpers at a workgroup barrier (A), every wave does its part, and a second barrier (B) ends the
+// part; MW_EXIT (posted once, at the end of the kernel) releases them.  Wave 0 issues no other
+// workgroup barrier while helpers wait (its stage clock is the NoClock).
+enum { MW_EXIT = 0, MW_MPR = 1 };
+// two waves: the convex pairs split over two MPR runs at a time (gym 25.2 k -> 26.6 k gym-steps/s);
+// four made the gym step slower (23.2 k, and 18.7 k with one four-wave workgroup per env), as the
+// extra waves' registers and scratch cut how many envs stay resident (profiles/r03/ab_mpr_helper_waves.log)
+constexpr int MW_WAVES = 2;
+// Convex pairs with ordinal (live-list order) in [64 r, 64 r + 64) and ordinal = w mod mw: the
+// same wave-cooperative MPR per pair as st_collision_convex, its result staged at the ordinal's
+// slot (cst_val: dist, pos, normal; cst_key: pair | 0x8000 on contact) for wave 0 to append.
+__device__ void convex_part(Env<float>& s, int w, int r) {
+  const DevPhys<float>& m = phys<float>();
+  const int l = lane_id();
+  const int nlive = s.nlive, mw = s.mw;
+  int ord = 0;
+  for (int base = 0; base < nlive; base += NT) {
+    const int k = base + l;
+    const int pair = k < nlive ? s.live[k] : 0;
+    uint64_t todo = __ballot(k < nlive && c_is_convex_pair(m, m.pair_g1[pair], m.pair_g2[pair]));
+    while (todo) {
+      const int src = __ffsll((unsigned long long)todo) - 1;
+      todo &= todo - 1;
+      const int o = ord++;
+      if (o < NT * r || o % mw != w) continue;
+      if (o >= NT * (r + 1)) return;
+      const int p = __builtin_amdgcn_readlane(pair, src);
+      const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
+      float dist = 0, pos[3] = {0, 0, 0}, nrm[3] = {0, 0, 0};
+      const bool hit = c_convex(m, s, g1, g2, fmaxf(m.geom_margin[g1], m.geom_margin[g2]), dist, pos, nrm);
+      if (l == 0) {
+        const int slot = o - NT * r;
+        s.cst_key[slot] = (unsigned short)(p | (hit ? 0x8000 : 0));
+        s.cst_val[slot][0] = dist;
+        for (int t = 0; t < 3; t++) { s.cst_val[slot][1 + t] = pos[t]; s.cst_val[slot][4 + t] = nrm[t]; }
+      }
+    }
+  }
+}
+__device__ void mw_helper(Env<float>& s) {
+  const int w = (int)(threadIdx.x / NT);
+  for (;;) {
+    __syncthreads();   // A: a command is posted
+    const int cmd = s.mw_cmd;
+    if ((cmd & 255) == MW_EXIT) return;
+    if ((cmd & 255) == MW_MPR) convex_part(s, w, cmd >> 8);
+    __syncthreads();   // B: the part is done
+  }
+}
+// wave 0: the convex pass on every wave, then the staged contacts appended in ordinal order
+// (the order st_collision_convex's one-pair-at-a-time loop produces; same bits)
+__device__ __attribute__((noinline)) void st_collision_convex_mw(Env<float>& s) {
+  const DevPhys<float>& m = phys<float>();
+  const int l = lane_id();
+  int ncon = s.ncon_raw;
+  const int nconv = s.nconvex;
+  for (int r = 0; NT * r < nconv; r++) {
+    if (l == 0) s.mw_cmd = MW_MPR | (r << 8);
+    __syncthreads();   // A
+    convex_part(s, 0, r);
+    __syncthreads();   // B
+    const int o = NT * r + l;
+    const unsigned key = o < nconv ? s.cst_key[l] : 0u;
+    const bool hit = (key & 0x8000u) != 0;
+    const uint64_t hits = __ballot(hit);
+    const int at = ncon + __popcll(hits & ((1ull << l) - 1ull));
+    if (hit && at < PH_MAXCON) {
+      const int p = (int)(key & 0x7FFFu), g1 = m.pair_g1[p], g2 = m.pair_g2[p];
+      const float pos[3] = {s.cst_val[l][1], s.cst_val[l][2], s.cst_val[l][3]};
+      const float nrm[3] = {s.cst_val[l][4], s.cst_val[l][5], s.cst_val[l][6]};
+      LdsSink<float> ls{s.con + at, 1};
+      ls.emit(s.cst_val[l][0], pos, nrm);
+      c_params(m, s.con[at], g1, g2);
+    }
+    ncon += __popcll(hits);
+    wsync();
+  }
+  if (l == 0) {
+    if (ncon > PH_MAXCON) CAP_FULL(8u);
+    s.ncon = min(ncon, PH_MAXCON);
+  }
+  wsync();
+}
+#endif
 
 // Convex (MPR) pairs of the live list, appended after the primitive contacts.  A stage of its
 // own, out of line, and only called when the broadphase kept a convex pair: MPR's portal state
@@ -3456,7 +3548,16 @@ __device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& 
   st_collision(m, s, clk);
   if (s.nconvex) {
     clk.sub_start();
+#if PNP_WIDE
+    if constexpr (sizeof(T) == 4) {
+      if (s.mw > 1) st_collision_convex_mw(s);
+      else st_collision_convex(m, s);
+    } else {
+      st_collision_convex(m, s);
+    }
+#else
     st_collision_convex(m, s);
+#endif
     clk.sub_lap(SC_CONVEX);
   }
   clk.lap(4);
@@ -3543,6 +3644,9 @@ __device__ void load_env(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, cons
   if (l < 3 * m.nmocap) s.mocap_pos[l] = st.mocap_pos[(size_t)b * 3 * m.nmocap + l];
   if (l < 4 * m.nmocap) s.mocap_quat[l] = st.mocap_quat[(size_t)b * 4 * m.nmocap + l];
   if (l == 0) { s.time = st.time[b]; s.warn = st.warn[b] & 0xFFFFu; s.ovf = 0; s.hand = hand; }
+#if PNP_WIDE
+  if (l == 0) s.mw = 1;   // single-wave unless the kernel says otherwise (env_step_kernel)
+#endif
   wsync();
 }
 
