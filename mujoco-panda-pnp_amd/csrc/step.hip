@@ -233,6 +233,7 @@ struct Env {
 #if PNP_WIDE
   int mw;                      // waves of the env's workgroup (the wide gym kernel: helper waves, mw_helper)
   int mw_cmd;                  // helper command (MW_*), posted by wave 0 before a workgroup barrier
+  int mw_next;                 // the convex pass's next pair (LDS counter)
 #endif
 };
 static_assert(sizeof(((Env<float>*)0)->efc_Jv) >= 7 * 4 * NT + 2 * NT + 4 + 2 * PH_MAXLIVE,
@@ -1320,61 +1321,75 @@ enum { MW_EXIT = 0, MW_MPR = 1 };
 // four made the gym step slower (23.2 k, and 18.7 k with one four-wave workgroup per env), as the
 // extra waves' registers and scratch cut how many envs stay resident (profiles/r03/ab_mpr_helper_waves.log)
 constexpr int MW_WAVES = 2;
-// Convex pairs with ordinal (live-list order) in [64 r, 64 r + 64) and ordinal = w mod mw: the
-// same wave-cooperative MPR per pair as st_collision_convex, its result staged at the ordinal's
-// slot (cst_val: dist, pos, normal; cst_key: pair | 0x8000 on contact) for wave 0 to append.
-__device__ void convex_part(Env<float>& s, int w, int r) {
+// The convex pairs of one round (up to 64, listed by wave 0 in cst_key in live-list order), taken
+// one at a time by whichever wave is free (an LDS counter): the same wave-cooperative MPR per pair
+// as st_collision_convex, its result staged at the pair's slot (cst_val: dist, pos, normal;
+// cst_key bit 15: contact) for wave 0 to append.
+__device__ void convex_part(Env<float>& s, int n) {
   const DevPhys<float>& m = phys<float>();
   const int l = lane_id();
-  const int nlive = s.nlive, mw = s.mw;
-  int ord = 0;
-  for (int base = 0; base < nlive; base += NT) {
-    const int k = base + l;
-    const int pair = k < nlive ? s.live[k] : 0;
-    uint64_t todo = __ballot(k < nlive && c_is_convex_pair(m, m.pair_g1[pair], m.pair_g2[pair]));
-    while (todo) {
-      const int src = __ffsll((unsigned long long)todo) - 1;
-      todo &= todo - 1;
-      const int o = ord++;
-      if (o < NT * r || o % mw != w) continue;
-      if (o >= NT * (r + 1)) return;
-      const int p = __builtin_amdgcn_readlane(pair, src);
-      const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
-      float dist = 0, pos[3] = {0, 0, 0}, nrm[3] = {0, 0, 0};
-      const bool hit = c_convex(m, s, g1, g2, fmaxf(m.geom_margin[g1], m.geom_margin[g2]), dist, pos, nrm);
-      if (l == 0) {
-        const int slot = o - NT * r;
-        s.cst_key[slot] = (unsigned short)(p | (hit ? 0x8000 : 0));
-        s.cst_val[slot][0] = dist;
-        for (int t = 0; t < 3; t++) { s.cst_val[slot][1 + t] = pos[t]; s.cst_val[slot][4 + t] = nrm[t]; }
-      }
+  // n and the taken slot are wave-uniform (SGPRs), so the loop's exit is a scalar branch: with
+  // a per-lane exit the compiler's structured loop could run on with lane 0 masked off, where
+  // readfirstlane no longer reads the lane that took the slot.  At most n trips in any case.
+  n = __builtin_amdgcn_readfirstlane(n);
+  for (int it = 0; it < n; it++) {
+    int o = 0;
+    if (l == 0) o = atomicAdd(&s.mw_next, 1);
+    o = __builtin_amdgcn_readfirstlane(__shfl(o, 0));
+    if (o >= n) return;
+    const int p = s.cst_key[o];
+    const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
+    float dist = 0, pos[3] = {0, 0, 0}, nrm[3] = {0, 0, 0};
+    const bool hit = c_convex(m, s, g1, g2, fmaxf(m.geom_margin[g1], m.geom_margin[g2]), dist, pos, nrm);
+    if (l == 0) {
+      s.cst_key[o] = (unsigned short)(p | (hit ? 0x8000 : 0));
+      s.cst_val[o][0] = dist;
+      for (int t = 0; t < 3; t++) { s.cst_val[o][1 + t] = pos[t]; s.cst_val[o][4 + t] = nrm[t]; }
     }
   }
 }
 __device__ void mw_helper(Env<float>& s) {
-  const int w = (int)(threadIdx.x / NT);
   for (;;) {
     __syncthreads();   // A: a command is posted
     const int cmd = s.mw_cmd;
     if ((cmd & 255) == MW_EXIT) return;
-    if ((cmd & 255) == MW_MPR) convex_part(s, w, cmd >> 8);
+    if ((cmd & 255) == MW_MPR) convex_part(s, cmd >> 8);
     __syncthreads();   // B: the part is done
   }
 }
-// wave 0: the convex pass on every wave, then the staged contacts appended in ordinal order
-// (the order st_collision_convex's one-pair-at-a-time loop produces; same bits)
+// wave 0: per round of up to 64 convex pairs, list them, run them on every wave, then append the
+// staged contacts in live-list order (the order st_collision_convex's one-pair-at-a-time loop
+// produces; same bits)
 __device__ __attribute__((noinline)) void st_collision_convex_mw(Env<float>& s) {
   const DevPhys<float>& m = phys<float>();
   const int l = lane_id();
   int ncon = s.ncon_raw;
-  const int nconv = s.nconvex;
+  const int nconv = s.nconvex, nlive = s.nlive;
+  int base = 0, ord = 0;   // live-list chunk and convex ordinal the listing has reached
   for (int r = 0; NT * r < nconv; r++) {
-    if (l == 0) s.mw_cmd = MW_MPR | (r << 8);
+    const int n = min(NT, nconv - NT * r);
+    int got = 0;
+    while (got < n && base < nlive) {   // list this round's pairs (chunks may straddle rounds)
+      const int k = base + l;
+      const int pair = k < nlive ? s.live[k] : 0;
+      const bool cvx = k < nlive && c_is_convex_pair(m, m.pair_g1[pair], m.pair_g2[pair]);
+      const uint64_t bal = __ballot(cvx);
+      const int o = ord + __popcll(bal & ((1ull << l) - 1ull));
+      if (cvx && o >= NT * r && o < NT * r + n) s.cst_key[o - NT * r] = (unsigned short)pair;
+      const int c = __popcll(bal);
+      if (ord + c > NT * r + n) break;   // this chunk continues into the next round: keep it
+      ord += c;
+      got = ord - NT * r;
+      base += NT;
+    }
+    if (l == 0) {
+      s.mw_next = 0;
+      s.mw_cmd = MW_MPR | (n << 8);
+    }
     __syncthreads();   // A
-    convex_part(s, 0, r);
+    convex_part(s, n);
     __syncthreads();   // B
-    const int o = NT * r + l;
-    const unsigned key = o < nconv ? s.cst_key[l] : 0u;
+    const unsigned key = l < n ? s.cst_key[l] : 0u;
     const bool hit = (key & 0x8000u) != 0;
     const uint64_t hits = __ballot(hit);
     const int at = ncon + __popcll(hits & ((1ull << l) - 1ull));
