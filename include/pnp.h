@@ -230,7 +230,7 @@ typedef struct pnp_state_f64 {
  * nsub = 25, ten times; skills/base.py:43 and scripts/execute_pnp.py:103 with nsub = 1).
  * ctrl and mocap are held constant over the nsub sub-steps, as in the reference.
  * fp32: three capacity tiers of one kernel source -- compact (20 contacts, 8 envs per CU), full
- * (48 contacts, 4 per CU), wide (96 contacts, 2 per CU).  Each runs the envs the previous tier
+ * (48 contacts, 4 per CU), wide (192 contacts, 1 per CU).  Each runs the envs the previous tier
  * handed over, from the sub-step that would have overflowed its capacities, so results equal the
  * wide kernel's bit for bit; only the wide tier truncates (PNP_WARN_CONTACTFULL / CNSTRFULL).
  * fp64 (debugging instantiation): the full kernel alone, truncating at 48 contacts.

@@ -764,31 +764,6 @@ __device__ __forceinline__ bool c_plane_obb_clear(const DevPhys<T>& /*image: phy
   return d - ext > margin + T(1e-6);
 }
 
-// mjc_Convex by MPR (the OBB pre-test ran in the broadphase): at most one contact.  Wave-uniform
-// call: every lane passes the same pair and gets the same result.
-template <typename T>
-__device__ __forceinline__ bool c_convex(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int g1, int g2, T margin,
-                                                    T& dist, T* pos, T* nrm) {
-  const DevPhys<T>& m = phys<T>();
-  CShape<T> sh[2];
-  const int gs[2] = {g1, g2};
-#pragma unroll
-  for (int i = 0; i < 2; i++) {
-    const int g = gs[i];
-    sh[i].type = m.geom_type[g];
-    sh[i].mesh = m.geom_dataid[g];
-    sh[i].margin = margin;
-    for (int k = 0; k < 3; k++) { sh[i].pos[k] = s.gpos[g][k]; sh[i].size[k] = m.geom_size[g][k]; }
-    for (int k = 0; k < 9; k++) sh[i].R[k] = s.gmat[g][k];
-    c_load_shape(m, sh[i]);
-  }
-  T depth;
-  if (!c_mpr(m, sh[0], sh[1], depth, nrm, pos)) return false;
-  if (nrm[0] == 0 && nrm[1] == 0 && nrm[2] == 0) return false;
-  dist = margin - depth;
-  return true;
-}
-
 template <typename T>
 __device__ void t_makeframe(T f[9]) {
   t_normalize3(f);
@@ -800,6 +775,109 @@ __device__ void t_makeframe(T f[9]) {
   f[3] -= f[0] * d; f[4] -= f[1] * d; f[5] -= f[2] * d;
   t_normalize3(f + 3);
   t_cross(f + 6, f, f + 3);
+}
+
+// mjc_Convex (oracle/convex.c): MPR (the OBB pre-test ran in the broadphase), mjc_fixNormal for the
+// sphere, and with multiccd (shelf_pnp.xml:5) four more MPR runs with the geoms rotated in opposite
+// senses by +-1e-3 rad about the first contact's tangent axes; a contact farther than 1e-3 x
+// min(rbound) from the pair's earlier ones is added.  Up to C_MULTI contacts, staged at val[0 ..)
+// (dist, pos, normal) by lane 0; returns their number.  Wave-uniform call: every lane passes the
+// same pair and gets the same result.
+constexpr int C_MULTI = 5;
+template <typename T>
+__device__ __forceinline__ bool c_mpr_contact(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>* sh, T margin,
+                                              T* c) {
+  const DevPhys<T>& m = phys<T>();
+  T depth, nrm[3], pos[3];
+  if (!c_mpr(m, sh[0], sh[1], depth, nrm, pos)) return false;
+  if (nrm[0] == 0 && nrm[1] == 0 && nrm[2] == 0) return false;   // normal undefined
+  if (sh[0].type == 2) {   // mjc_fixNormal: the sphere's normal at the contact point (g1 of its pairs)
+    T n[3];
+    cs3(n, pos, sh[0].pos);
+    const T len = PM<T>::sqrt_(cd3(n, n));
+    if (len < T(1e-15)) { nrm[0] = 1; nrm[1] = 0; nrm[2] = 0; }
+    else { nrm[0] = n[0] / len; nrm[1] = n[1] / len; nrm[2] = n[2] / len; }
+  }
+  c[0] = margin - depth;
+  for (int k = 0; k < 3; k++) { c[1 + k] = pos[k]; c[4 + k] = nrm[k]; }
+  return true;
+}
+template <typename T>
+__device__ __forceinline__ int c_convex(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int g1, int g2, T margin,
+                                        T (*val)[7]) {
+  const DevPhys<T>& m = phys<T>();
+  const int l = threadIdx.x & 63;
+  CShape<T> sh[2];
+  const int gs[2] = {g1, g2};
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const int g = gs[i];
+    sh[i].type = m.geom_type[g];
+    sh[i].mesh = m.geom_dataid[g];
+    sh[i].margin = margin;
+    // origin at geom 1's centre (oracle/convex.c): centimetre-scale support points, so the fp32
+    // Minkowski differences keep ~20x more bits than in world coordinates
+    for (int k = 0; k < 3; k++) { sh[i].pos[k] = s.gpos[g][k] - s.gpos[g1][k]; sh[i].size[k] = m.geom_size[g][k]; }
+    for (int k = 0; k < 9; k++) sh[i].R[k] = s.gmat[g][k];
+    c_load_shape(m, sh[i]);
+  }
+  const T org[3] = {s.gpos[g1][0], s.gpos[g1][1], s.gpos[g1][2]};
+  T c[7];
+  if (!c_mpr_contact(m, sh, margin, c)) return 0;
+  if (l == 0) {   // (positions relative to geom 1's centre until the fan is complete)
+    for (int k = 0; k < 7; k++) val[0][k] = c[k];
+    if (!m.multiccd)
+      for (int k = 0; k < 3; k++) val[0][1 + k] += org[k];
+  }
+  if (!m.multiccd) return 1;
+  // the first contact's frame (mju_makeFrame of its normal): perturbation axes frame[3..5], [6..8]
+  T f[9] = {c[4], c[5], c[6], 0, 0, 0, 0, 0, 0};
+  t_makeframe(f);
+  const T tol = T(1e-3) * fmin(m.geom_rbound[g1], m.geom_rbound[g2]);
+  T R0[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+    for (int k = 0; k < 9; k++) R0[i][k] = sh[i].R[k];
+  int n = 1;
+  for (int t = 0; t < 4; t++) {
+    // q = (cos(a/2), axis sin(a/2)), a = -+1e-3 (oracle: sp_axisangle2quat); R(q^-1) = R(q)^T
+    const T* ax = f + 3 + 3 * (t >> 1);
+    const T sh_ = (t & 1) ? T(0.0004999999791666669) : T(-0.0004999999791666669), q0 = T(0.9999998750000026);
+    const T q[4] = {q0, ax[0] * sh_, ax[1] * sh_, ax[2] * sh_};
+    T Rq[9];
+    {
+      const T q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
+      const T q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
+      const T q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
+      Rq[0] = q00 + q11 - q22 - q33; Rq[4] = q00 - q11 + q22 - q33; Rq[8] = q00 - q11 - q22 + q33;
+      Rq[1] = 2 * (q12 - q03); Rq[2] = 2 * (q13 + q02); Rq[3] = 2 * (q12 + q03);
+      Rq[5] = 2 * (q23 - q01); Rq[6] = 2 * (q13 - q02); Rq[7] = 2 * (q23 + q01);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        sh[0].R[3 * i + j] = Rq[3 * i] * R0[0][j] + Rq[3 * i + 1] * R0[0][3 + j] + Rq[3 * i + 2] * R0[0][6 + j];
+        sh[1].R[3 * i + j] = Rq[i] * R0[1][j] + Rq[3 + i] * R0[1][3 + j] + Rq[6 + i] * R0[1][6 + j];
+      }
+    if (!c_mpr_contact(m, sh, margin, c)) continue;
+    wsync();
+    bool distinct = true;
+    for (int i = 0; i < n; i++) {
+      const T e[3] = {c[1] - val[i][1], c[2] - val[i][2], c[3] - val[i][3]};
+      if (PM<T>::sqrt_(cd3(e, e)) <= tol) distinct = false;
+    }
+    if (!distinct) continue;
+    if (l == 0)
+      for (int k = 0; k < 7; k++) val[n][k] = c[k];
+    n++;
+  }
+  wsync();
+  if (l == 0)
+    for (int i = 0; i < n; i++)
+      for (int k = 0; k < 3; k++) val[i][1 + k] += org[k];
+  wsync();
+  return n;
 }
 
 template <typename T>

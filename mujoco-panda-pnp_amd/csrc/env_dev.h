@@ -533,7 +533,7 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
 
 #if PNP_WIDE
 // Wide tier, persistent: the selection kernel lists the envs the pass runs (list[0] = count), and
-// a grid of two workgroups per CU loops over the list.  Each workgroup is MW_WAVES waves: wave 0
+// a grid of as many workgroups per CU as the LDS holds (one at 192 contacts) loops over the list.  Each workgroup is MW_WAVES waves: wave 0
 // steps its env, the other is a helper wave for the convex pass (step.hip, mw_helper).  Multi-wave
 // workgroups launched one per env (4096 per pass, nearly all exiting at once) made the gym step
 // 25 % slower even with the helpers idle; a resident grid over the selected envs does not.
@@ -679,7 +679,8 @@ int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* s
   hipLaunchKernelGGL(wide_select_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, e->tier, st->warn, B, resume,
                      only_tier, list);
   if (const int32_t rc = pnp_check_launch("wide_select_kernel")) return rc;
-  const int grid = B < 2 * ncu ? B : 2 * ncu;   // two envs per CU (LDS)
+  const int per_cu = (int)(163840 / sizeof(Env<float>)) > 0 ? (int)(163840 / sizeof(Env<float>)) : 1;   // envs per CU (LDS)
+  const int grid = B < per_cu * ncu ? B : per_cu * ncu;
   hipLaunchKernelGGL(env_step_wide_kernel, dim3(grid), dim3(NT * MW_WAVES), 0, (hipStream_t)stream, *st, *p,
                      env_view<float>(e), action, out_view<float>(o), (const int*)list, resume);
   if (const int32_t rc = pnp_check_launch("env_step_wide_kernel")) return rc;

@@ -54,6 +54,7 @@ int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
   for (int k = 0; k < 3; k++) d->gravity[k] = (T)s->gravity[k];
   d->noslip_iterations = s->noslip_iterations;
   d->iterations = s->iterations;
+  d->multiccd = s->multiccd;
   // ---- bodies
   for (int b = 0; b < s->nbody; b++) {
     d->body_parentid[b] = s->body_parentid[b];

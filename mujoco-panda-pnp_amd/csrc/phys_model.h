@@ -53,7 +53,7 @@ template <typename T>
 struct DevPhys {
   int nq, nv, nu, nbody, njnt, ngeom, npair, nmocap, neq, ntree, nmentry;
   T timestep, gravity[3];
-  int noslip_iterations, iterations;
+  int noslip_iterations, iterations, multiccd;   // multiccd: mjENBL_MULTICCD (mjc_Convex's perturbed contacts)
   // bodies
   int body_parentid[PH_MAXB], body_rootid[PH_MAXB], body_weldid[PH_MAXB], body_mocapid[PH_MAXB];
   int body_jntadr[PH_MAXB], body_jntnum[PH_MAXB], body_dofadr[PH_MAXB], body_dofnum[PH_MAXB];

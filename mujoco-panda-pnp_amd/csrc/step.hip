@@ -27,13 +27,13 @@
 //   step_compact.hip  pnp_compact  20 contacts / 96 rows: 20 KB of LDS per env, 8 envs per CU
 //   step.hip          pnp_full     48 contacts / 208 rows: 38 KB, 4 envs per CU; also the fp64
 //                                  debugging instantiation, the debug kernels and the C ABI
-//   step_wide.hip     pnp_wide     96 contacts / 400 rows: 2 envs per CU
+//   step_wide.hip     pnp_wide     192 contacts / 784 rows: 1 env per CU
 // A sub-step that would overflow a tier's capacity is abandoned before it changes the state and
 // re-run from that sub-step by the next tier's resume pass (protocol: PNP_RESUME_* below), so an
 // fp32 result is that of the widest tier, bit for bit, whichever tier finished each sub-step.  The
 // widest tier, and the full tier when it runs alone (fp64, diagnostics), truncate like MuJoCo at a
-// full buffer (warning bits CONTACTFULL / CNSTRFULL).  Closed fingers pressed together make 50-100
-// contacts (box-box pad pairs, mesh-pad pairs), so the gym workload needs the wide tier.
+// full buffer (warning bits CONTACTFULL / CNSTRFULL).  Closed fingers pressed together make 50-150
+// contacts (box-box pad pairs, multiccd mesh pairs), so the gym workload needs the wide tier.
 #ifndef PNP_COMPACT
 #define PNP_COMPACT 0
 #endif
@@ -1332,6 +1332,7 @@ __device__ void convex_part(Env<float>& s, int n) {
   // a per-lane exit the compiler's structured loop could run on with lane 0 masked off, where
   // readfirstlane no longer reads the lane that took the slot.  At most n trips in any case.
   n = __builtin_amdgcn_readfirstlane(n);
+  const int per = m.multiccd ? C_MULTI : 1;   // staging slots per pair
   for (int it = 0; it < n; it++) {
     int o = 0;
     if (l == 0) o = atomicAdd(&s.mw_next, 1);
@@ -1339,13 +1340,8 @@ __device__ void convex_part(Env<float>& s, int n) {
     if (o >= n) return;
     const int p = s.cst_key[o];
     const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
-    float dist = 0, pos[3] = {0, 0, 0}, nrm[3] = {0, 0, 0};
-    const bool hit = c_convex(m, s, g1, g2, fmaxf(m.geom_margin[g1], m.geom_margin[g2]), dist, pos, nrm);
-    if (l == 0) {
-      s.cst_key[o] = (unsigned short)(p | (hit ? 0x8000 : 0));
-      s.cst_val[o][0] = dist;
-      for (int t = 0; t < 3; t++) { s.cst_val[o][1 + t] = pos[t]; s.cst_val[o][4 + t] = nrm[t]; }
-    }
+    const int nc = c_convex(m, s, g1, g2, fmaxf(m.geom_margin[g1], m.geom_margin[g2]), s.cst_val + per * o);
+    if (l == 0) s.cst_key[o] = (unsigned short)(p | nc << 12);   // pair (< 1024) | its contact count
   }
 }
 __device__ void mw_helper(Env<float>& s) {
@@ -1365,9 +1361,11 @@ __device__ __attribute__((noinline)) void st_collision_convex_mw(Env<float>& s) 
   const int l = lane_id();
   int ncon = s.ncon_raw;
   const int nconv = s.nconvex, nlive = s.nlive;
+  // a round's pairs stage up to `per` contacts each in the 64 staging slots
+  const int per = m.multiccd ? C_MULTI : 1, RN = NT / per;
   int base = 0, ord = 0;   // live-list chunk and convex ordinal the listing has reached
-  for (int r = 0; NT * r < nconv; r++) {
-    const int n = min(NT, nconv - NT * r);
+  for (int r = 0; RN * r < nconv; r++) {
+    const int n = min(RN, nconv - RN * r);
     int got = 0;
     while (got < n && base < nlive) {   // list this round's pairs (chunks may straddle rounds)
       const int k = base + l;
@@ -1375,11 +1373,11 @@ __device__ __attribute__((noinline)) void st_collision_convex_mw(Env<float>& s) 
       const bool cvx = k < nlive && c_is_convex_pair(m, m.pair_g1[pair], m.pair_g2[pair]);
       const uint64_t bal = __ballot(cvx);
       const int o = ord + __popcll(bal & ((1ull << l) - 1ull));
-      if (cvx && o >= NT * r && o < NT * r + n) s.cst_key[o - NT * r] = (unsigned short)pair;
+      if (cvx && o >= RN * r && o < RN * r + n) s.cst_key[o - RN * r] = (unsigned short)pair;
       const int c = __popcll(bal);
-      if (ord + c > NT * r + n) break;   // this chunk continues into the next round: keep it
+      if (ord + c > RN * r + n) break;   // this chunk continues into the next round: keep it
       ord += c;
-      got = ord - NT * r;
+      got = ord - RN * r;
       base += NT;
     }
     if (l == 0) {
@@ -1389,19 +1387,24 @@ __device__ __attribute__((noinline)) void st_collision_convex_mw(Env<float>& s) 
     __syncthreads();   // A
     convex_part(s, n);
     __syncthreads();   // B
+    // append in pair order: pair o's contacts at ncon + (contacts of pairs before o) + k
     const unsigned key = l < n ? s.cst_key[l] : 0u;
-    const bool hit = (key & 0x8000u) != 0;
-    const uint64_t hits = __ballot(hit);
-    const int at = ncon + __popcll(hits & ((1ull << l) - 1ull));
-    if (hit && at < PH_MAXCON) {
-      const int p = (int)(key & 0x7FFFu), g1 = m.pair_g1[p], g2 = m.pair_g2[p];
+    const int cnt = (int)(key >> 12);
+    const int excl = wscan_incl(cnt) - cnt;
+    const int tot = __builtin_amdgcn_readlane(excl + cnt, 63);
+    const int o = l / per, kk = l - o * per;   // staging slot l holds contact kk of pair o
+    const int co = __shfl(cnt, o), eo = __shfl(excl, o);
+    const unsigned ko = (unsigned)__shfl((int)key, o);
+    const int at = ncon + eo + kk;
+    if (o < n && kk < co && at < PH_MAXCON) {
+      const int p = (int)(ko & 0x3FFu), g1 = m.pair_g1[p], g2 = m.pair_g2[p];
       const float pos[3] = {s.cst_val[l][1], s.cst_val[l][2], s.cst_val[l][3]};
       const float nrm[3] = {s.cst_val[l][4], s.cst_val[l][5], s.cst_val[l][6]};
       LdsSink<float> ls{s.con + at, 1};
       ls.emit(s.cst_val[l][0], pos, nrm);
       c_params(m, s.con[at], g1, g2);
     }
-    ncon += __popcll(hits);
+    ncon += tot;
     wsync();
   }
   if (l == 0) {
@@ -1432,14 +1435,17 @@ __device__ __attribute__((noinline)) void st_collision_convex(const DevPhys<T>& 
       todo &= todo - 1;
       const int p = __builtin_amdgcn_readlane(pair, src);
       const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
-      T dist = 0, pos[3] = {0, 0, 0}, nrm[3] = {0, 0, 0};
-      if (!c_convex(m, s, g1, g2, fmax(m.geom_margin[g1], m.geom_margin[g2]), dist, pos, nrm)) continue;
-      if (l == 0 && ncon < PH_MAXCON) {
-        LdsSink<T> ls{s.con + ncon, 1};
-        ls.emit(dist, pos, nrm);
-        c_params(m, s.con[ncon], g1, g2);
+      // the pair's contacts (up to C_MULTI with multiccd) staged in cst_val, then lanes 0.. append
+      const int n = c_convex(m, s, g1, g2, fmax(m.geom_margin[g1], m.geom_margin[g2]), s.cst_val);
+      if (l < n && ncon + l < PH_MAXCON) {
+        const T pos[3] = {s.cst_val[l][1], s.cst_val[l][2], s.cst_val[l][3]};
+        const T nrm[3] = {s.cst_val[l][4], s.cst_val[l][5], s.cst_val[l][6]};
+        LdsSink<T> ls{s.con + ncon + l, 1};
+        ls.emit(s.cst_val[l][0], pos, nrm);
+        c_params(m, s.con[ncon + l], g1, g2);
       }
-      ncon++;
+      ncon += n;
+      wsync();
     }
   }
   if (l == 0) {

@@ -13,9 +13,19 @@
  * hull vertex maximising d, each inflated by margin/2 along d; ties are resolved with a 1e-9 band
  * (first vertex within it of the maximum, + box corner for |d_k| < 1e-12) so that flat faces
  * facing each other — a finger hull on a shelf board — do not flip the portal with rounding.
- * Deviations from MuJoCo, documented in DESIGN.md: the multiccd extra contacts are not
- * generated (one contact per convex pair); mjc_fixNormal's analytic normals for smooth geoms
- * (sphere) are not applied.
+ * mjc_MPRIteration: an MPR contact whose normal is undefined (zero) is dropped; mjc_fixNormal
+ * replaces the normal by the analytic one for smooth geoms (here: the sphere, the only smooth
+ * type in a convex pair of this scene).
+ * multiccd (shelf_pnp.xml:5 enables it; mjENBL_MULTICCD in mjc_Convex): after the first contact,
+ * MPR is re-run four times with the two geoms rotated in opposite senses about their own centres
+ * by +-perturbation_angle (1e-3 rad) about the two tangent axes of the first contact's frame
+ * (mju_makeFrame of its normal): (t1, -a), (t1, +a), (t2, -a), (t2, +a), geom 1 by q and geom 2
+ * by q^-1.  A contact found this way is appended when its position is farther than
+ * relative_tolerance (1e-3) x min(rbound1, rbound2) from every contact the pair already has
+ * (up to 5 per pair).  MuJoCo applies the rotation inside the support function (direction
+ * rotated in, support point rotated out); rotating the geom frame once per run is the same map.
+ * Restated from MuJoCo 2.3.3's published engine_collision_convex.c (not present here, so the
+ * constants and the trial order are unverified: parity unpinned).
  * Pairs whose oriented bounding boxes are disjoint cannot touch; they skip MPR (result-neutral).
  */
 #include <float.h>
@@ -363,6 +373,31 @@ static int obb_disjoint(const double* p1, const double* R1, const double* h1, co
   return 0;
 }
 
+/* mjc_MPRIteration: one MPR run; 1 and the contact (normal fixed, mjc_fixNormal) on contact */
+static int mpr_contact(const shape* s, double margin, orc_contact* c) {
+  double depth, dir[3], pos[3];
+  if (mpr_penetration(&s[0], &s[1], &depth, dir, pos) != 0) return 0;
+  if (dir[0] == 0 && dir[1] == 0 && dir[2] == 0) return 0;   /* normal undefined */
+  c->dist = margin - depth;
+  memcpy(c->pos, pos, sizeof(pos));
+  memset(c->frame, 0, sizeof(c->frame));
+  memcpy(c->frame, dir, sizeof(dir));
+  /* mjc_fixNormal: the sphere's normal at the contact point (from its centre, unperturbed
+     frame); sphere is geom 1 of its pairs (lower type), its normal points to geom 2.  Both
+     smooth would average; a second smooth geom does not occur (g2 is a mesh). */
+  if (s[0].type == C_SPHERE) {
+    double n[3];
+    sub3(n, c->pos, s[0].pos);
+    double len = sqrt(d3(n, n));
+    if (len < 1e-15) { n[0] = 1; n[1] = n[2] = 0; }
+    else { n[0] /= len; n[1] /= len; n[2] /= len; }
+    memcpy(c->frame, n, sizeof(n));
+  }
+  return 1;
+}
+
+static int mpr_fan(Mdl* m, shape* s, int g1, int g2, double margin, orc_contact* out, int cap);
+
 int orc_convex_collide(Mdl* m, const orc_data* d, int g1, int g2, double margin, orc_contact* out, int cap) {
   if (cap < 1) return 0;
   shape s[2];
@@ -382,14 +417,54 @@ int orc_convex_collide(Mdl* m, const orc_data* d, int g1, int g2, double margin,
       bp[i][k] = s[i].pos[k] + s[i].R[3 * k] * bc[i][0] + s[i].R[3 * k + 1] * bc[i][1] + s[i].R[3 * k + 2] * bc[i][2];
   }
   if (obb_disjoint(bp[0], s[0].R, bh[0], bp[1], s[1].R, bh[1], margin)) return 0;
-  double depth, dir[3], pos[3];
-  if (mpr_penetration(&s[0], &s[1], &depth, dir, pos) != 0) return 0;
-  if (dir[0] == 0 && dir[1] == 0 && dir[2] == 0) return 0;   /* normal undefined */
-  out[0].dist = margin - depth;
-  memcpy(out[0].pos, pos, sizeof(pos));
-  memset(out[0].frame, 0, sizeof(out[0].frame));
-  memcpy(out[0].frame, dir, sizeof(dir));
-  return 1;
+  /* MPR runs with the origin at geom 1's centre (support points of centimetre magnitude instead of
+     world coordinates ~1 m: the fp32 kernel's Minkowski differences keep 20x more bits; a
+     translation of both shapes leaves the algorithm's result unchanged) */
+  const double o[3] = {s[0].pos[0], s[0].pos[1], s[0].pos[2]};
+  for (int i = 0; i < 2; i++) sub3(s[i].pos, s[i].pos, o);
+  int n = mpr_fan(m, s, g1, g2, margin, out, cap);
+  for (int i = 0; i < n; i++)
+    for (int k = 0; k < 3; k++) out[i].pos[k] += o[k];
+  return n;
+}
+
+/* mjc_Convex after the pre-test: MPR, then multiccd's perturbed runs */
+static int mpr_fan(Mdl* m, shape* s, int g1, int g2, double margin, orc_contact* out, int cap) {
+  if (!mpr_contact(s, margin, &out[0])) return 0;
+  int n = 1;
+  if (!m->multiccd) return n;
+  /* multiccd: perturbed runs about the first contact's tangent axes */
+  const double relative_tolerance = 1e-3, perturbation_angle = 1e-3;
+  double frame[9];
+  memcpy(frame, out[0].frame, sizeof(frame));
+  frame[3] = frame[4] = frame[5] = 0;
+  sp_makeframe(frame);
+  double r1 = m->geom_rbound[g1], r2 = m->geom_rbound[g2];
+  const double tol = relative_tolerance * (r1 < r2 ? r1 : r2);
+  const double R0[2][9] = {
+      {s[0].R[0], s[0].R[1], s[0].R[2], s[0].R[3], s[0].R[4], s[0].R[5], s[0].R[6], s[0].R[7], s[0].R[8]},
+      {s[1].R[0], s[1].R[1], s[1].R[2], s[1].R[3], s[1].R[4], s[1].R[5], s[1].R[6], s[1].R[7], s[1].R[8]}};
+  for (int ax = 0; ax < 2; ax++)
+    for (int sg = 0; sg < 2; sg++) {
+      const double ang = sg ? perturbation_angle : -perturbation_angle;
+      double q[4], qi[4], Rq[9], Rqi[9];
+      sp_axisangle2quat(q, frame + 3 + 3 * ax, ang);
+      sp_negquat(qi, q);
+      sp_quat2mat(Rq, q);
+      sp_quat2mat(Rqi, qi);
+      mulmat3(s[0].R, Rq, R0[0]);    /* geom 1 rotated by q about its centre */
+      mulmat3(s[1].R, Rqi, R0[1]);   /* geom 2 by q^-1 */
+      orc_contact c;
+      if (!mpr_contact(s, margin, &c)) continue;
+      int distinct = 1;
+      for (int i = 0; i < n; i++) {
+        double e[3];
+        sub3(e, c.pos, out[i].pos);
+        if (sqrt(d3(e, e)) <= tol) { distinct = 0; break; }
+      }
+      if (distinct && n < cap) out[n++] = c;
+    }
+  return n;
 }
 
 /* test probe: MPR on any (sphere | box | mesh) geom pair of a forward'ed orc_data, no OBB

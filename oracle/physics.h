@@ -14,8 +14,8 @@
 #define ORC_MAXU 12
 #define ORC_MAXG 112
 #define ORC_MAXS 12
-#define ORC_MAXCON 96
-#define ORC_MAXEFC 420
+#define ORC_MAXCON 192
+#define ORC_MAXEFC 784
 
 /* constraint types (mjtConstraint) */
 #define ORC_CNSTR_EQUALITY 0

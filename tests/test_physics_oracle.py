@@ -186,3 +186,45 @@ def test_mpr_separated_and_contact_list(model):
     far = PS.reset_states(1, seed=0, model=model)
     hit, _, _ = O.convex_probe(_row(far, 0), g_box, 69, model=model)
     assert hit is None
+
+
+def _pair_contacts(model, row, g1, g2):
+    f = O.forward_fields(row, ["contact", "ncon"], model=model)
+    c = f["contact"].reshape(int(f["ncon"][0]), 30)
+    return c[(c[:, 27] == g1) & (c[:, 28] == g2)]
+
+
+def test_multiccd_contact_fan(model):
+    """multiccd (shelf_pnp.xml:5, mjc_Convex): the first contact of a convex pair is MPR's own
+    (= the probe, = the single contact with the flag off); the perturbed runs add contacts on the
+    flat faces, each farther than 1e-3 x min(rbound) from the pair's others, at most 5 per pair."""
+    assert model.opt_multiccd == 1
+    from pnp_amd.model import PandaModel
+    off = PandaModel()   # (load_model() is the shared instance)
+    off.opt_multiccd = 0
+    off._desc = None
+    st = PS.reset_states(1, seed=11, model=model)
+    st["qpos"][:, 7:9] = 0.004
+    sx, _ = O.site_kinematics(st["qpos"], model=model)
+    a = int(model.jnt_qposadr[model.joint_id("cube1_joint")])
+    st["qpos"][0, a:a + 3] = sx[0, model.site_id("ee_center_site")] + [0.0, 0.0, 0.075]   # into the palm
+    row = _row(st, 0)
+    g_box, g_mesh = _gid(model, "cube1_geom"), 69
+    fan = _pair_contacts(model, row, g_box, g_mesh)
+    one = _pair_contacts(off, row, g_box, g_mesh)
+    assert len(one) == 1 and 2 <= len(fan) <= 5, (len(one), len(fan))
+    assert np.array_equal(fan[0], one[0])
+    hit, _, _ = O.convex_probe(row, g_box, g_mesh, model=model)
+    assert abs(hit[0] - fan[0, 12]) < 1e-12 and np.allclose(hit[1], fan[0, :3], atol=1e-12)
+    tol = 1e-3 * min(model.geom_rbound[g_box], model.geom_rbound[g_mesh])
+    for i in range(len(fan)):
+        for j in range(i):
+            assert np.linalg.norm(fan[i, :3] - fan[j, :3]) > tol
+    # every contact of the fan is a penetration along a unit normal with a completed frame
+    assert np.all(fan[:, 12] < 0)
+    fr = fan[:, 3:12].reshape(-1, 3, 3)
+    assert np.allclose(np.einsum("nij,nkj->nik", fr, fr), np.eye(3), atol=1e-12)
+    # across the scene's convex pairs: more contacts with the flag, never more than 5 per pair
+    f_on = O.forward_fields(row, ["ncon"], model=model)["ncon"][0]
+    f_off = O.forward_fields(row, ["ncon"], model=off)["ncon"][0]
+    assert f_on > f_off
