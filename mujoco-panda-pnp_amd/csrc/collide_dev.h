@@ -802,12 +802,12 @@ __device__ __forceinline__ bool c_mpr_contact(const DevPhys<T>& /*image: phys<T>
   for (int k = 0; k < 3; k++) { c[1 + k] = pos[k]; c[4 + k] = nrm[k]; }
   return true;
 }
+// the pair's two shapes, origin at geom 1's centre (oracle/convex.c): centimetre-scale support
+// points, so the fp32 Minkowski differences keep ~20x more bits than in world coordinates
 template <typename T>
-__device__ __forceinline__ int c_convex(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int g1, int g2, T margin,
-                                        T (*val)[7]) {
+__device__ __forceinline__ void c_convex_shapes(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int g1, int g2,
+                                                T margin, CShape<T>* sh) {
   const DevPhys<T>& m = phys<T>();
-  const int l = threadIdx.x & 63;
-  CShape<T> sh[2];
   const int gs[2] = {g1, g2};
 #pragma unroll
   for (int i = 0; i < 2; i++) {
@@ -815,67 +815,106 @@ __device__ __forceinline__ int c_convex(const DevPhys<T>& /*image: phys<T>()*/, 
     sh[i].type = m.geom_type[g];
     sh[i].mesh = m.geom_dataid[g];
     sh[i].margin = margin;
-    // origin at geom 1's centre (oracle/convex.c): centimetre-scale support points, so the fp32
-    // Minkowski differences keep ~20x more bits than in world coordinates
     for (int k = 0; k < 3; k++) { sh[i].pos[k] = s.gpos[g][k] - s.gpos[g1][k]; sh[i].size[k] = m.geom_size[g][k]; }
     for (int k = 0; k < 9; k++) sh[i].R[k] = s.gmat[g][k];
     c_load_shape(m, sh[i]);
   }
-  const T org[3] = {s.gpos[g1][0], s.gpos[g1][1], s.gpos[g1][2]};
-  T c[7];
-  if (!c_mpr_contact(m, sh, margin, c)) return 0;
-  if (l == 0) {   // (positions relative to geom 1's centre until the fan is complete)
-    for (int k = 0; k < 7; k++) val[0][k] = c[k];
-    if (!m.multiccd)
-      for (int k = 0; k < 3; k++) val[0][1 + k] += org[k];
-  }
-  if (!m.multiccd) return 1;
-  // the first contact's frame (mju_makeFrame of its normal): perturbation axes frame[3..5], [6..8]
-  T f[9] = {c[4], c[5], c[6], 0, 0, 0, 0, 0, 0};
-  t_makeframe(f);
-  const T tol = T(1e-3) * fmin(m.geom_rbound[g1], m.geom_rbound[g2]);
-  T R0[2][9];
+}
+// multiccd trial t (0..3): geom 1 rotated by q, geom 2 by q^-1 about their centres, q the rotation
+// by a = -+1e-3 rad about the first contact's tangent axis t >> 1 (frame f = mju_makeFrame of its
+// normal): q = (cos(a/2), axis sin(a/2)) (oracle: sp_axisangle2quat), R(q^-1) = R(q)^T.  Ra, Rb:
+// the unperturbed frames (the Env's geom frames: nothing extra held in registers across MPR).
+// (One function for the serial and the multi-wave convex passes: same bits.)
+template <typename T>
+__device__ __forceinline__ void c_fan_rotate(CShape<T>* sh, const T* Ra, const T* Rb, const T* f, int t) {
+  const bool second = (t >> 1) != 0;   // (selects, not an index: f stays in registers)
+  const T ax[3] = {second ? f[6] : f[3], second ? f[7] : f[4], second ? f[8] : f[5]};
+  const T sh_ = (t & 1) ? T(0.0004999999791666669) : T(-0.0004999999791666669), q0 = T(0.9999998750000026);
+  const T q[4] = {q0, ax[0] * sh_, ax[1] * sh_, ax[2] * sh_};
+  T Rq[9];
+  const T q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
+  const T q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
+  const T q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
+  Rq[0] = q00 + q11 - q22 - q33; Rq[4] = q00 - q11 + q22 - q33; Rq[8] = q00 - q11 - q22 + q33;
+  Rq[1] = 2 * (q12 - q03); Rq[2] = 2 * (q13 + q02); Rq[3] = 2 * (q12 + q03);
+  Rq[5] = 2 * (q23 - q01); Rq[6] = 2 * (q13 - q02); Rq[7] = 2 * (q23 + q01);
 #pragma unroll
-  for (int i = 0; i < 2; i++)
-    for (int k = 0; k < 9; k++) R0[i][k] = sh[i].R[k];
-  int n = 1;
-  for (int t = 0; t < 4; t++) {
-    // q = (cos(a/2), axis sin(a/2)), a = -+1e-3 (oracle: sp_axisangle2quat); R(q^-1) = R(q)^T
-    const T* ax = f + 3 + 3 * (t >> 1);
-    const T sh_ = (t & 1) ? T(0.0004999999791666669) : T(-0.0004999999791666669), q0 = T(0.9999998750000026);
-    const T q[4] = {q0, ax[0] * sh_, ax[1] * sh_, ax[2] * sh_};
-    T Rq[9];
-    {
-      const T q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
-      const T q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
-      const T q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
-      Rq[0] = q00 + q11 - q22 - q33; Rq[4] = q00 - q11 + q22 - q33; Rq[8] = q00 - q11 - q22 + q33;
-      Rq[1] = 2 * (q12 - q03); Rq[2] = 2 * (q13 + q02); Rq[3] = 2 * (q12 + q03);
-      Rq[5] = 2 * (q23 - q01); Rq[6] = 2 * (q13 - q02); Rq[7] = 2 * (q23 + q01);
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      sh[0].R[3 * i + j] = Rq[3 * i] * Ra[j] + Rq[3 * i + 1] * Ra[3 + j] + Rq[3 * i + 2] * Ra[6 + j];
+      sh[1].R[3 * i + j] = Rq[i] * Rb[j] + Rq[3 + i] * Rb[3 + j] + Rq[6 + i] * Rb[6 + j];
     }
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-#pragma unroll
-      for (int j = 0; j < 3; j++) {
-        sh[0].R[3 * i + j] = Rq[3 * i] * R0[0][j] + Rq[3 * i + 1] * R0[0][3 + j] + Rq[3 * i + 2] * R0[0][6 + j];
-        sh[1].R[3 * i + j] = Rq[i] * R0[1][j] + Rq[3 + i] * R0[1][3 + j] + Rq[6 + i] * R0[1][6 + j];
-      }
-    if (!c_mpr_contact(m, sh, margin, c)) continue;
+}
+// the perturbation frame from the first contact's normal n0
+template <typename T>
+__device__ __forceinline__ void c_fan_frame(const T* n0, T* f) {
+  f[0] = n0[0]; f[1] = n0[1]; f[2] = n0[2];
+  for (int k = 3; k < 9; k++) f[k] = 0;
+  t_makeframe(f);
+}
+// distinct-contact tolerance (relative_tolerance x min rbound) and test (positions of one frame)
+template <typename T>
+__device__ __forceinline__ T c_fan_tol(const DevPhys<T>& /*image: phys<T>()*/, int g1, int g2) {
+  const DevPhys<T>& m = phys<T>();
+  return T(1e-3) * fmin(m.geom_rbound[g1], m.geom_rbound[g2]);
+}
+template <typename T>
+__device__ __forceinline__ bool c_fan_close(const T* a, const T* b, T tol) {
+  const T e[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+  return PM<T>::sqrt_(cd3(e, e)) <= tol;
+}
+// One MPR run of the pair (g1, g2): the first (t = -1) or multiccd trial t (the perturbation frame
+// from val[0]'s normal, the pair's staged first contact); lane 0 stages the contact (position
+// relative to geom 1's centre) at val[slot].  Wave-uniform result.  One call site per pass: with
+// the first run and the trials at two call sites, the convex stage's spills grew the compact
+// build's scratch 304 -> 896 B per lane and cost C3 2 % although C3 never runs the stage (392 B and
+// -1.0 % with one).  The serial and the multi-wave convex passes both call it: the same bits.
+#if PNP_WIDE
+#define C_RUN_INLINE __attribute__((noinline))   // two call sites (serial and multi-wave passes)
+#else
+#define C_RUN_INLINE __forceinline__              // one call site (c_convex's loop)
+#endif
+template <typename T>
+__device__ C_RUN_INLINE bool c_convex_run(const Env<T>& s, int g1, int g2, T margin, int t, T (*val)[7], int slot) {
+  const DevPhys<T>& m = phys<T>();
+  CShape<T> sh[2];
+  c_convex_shapes(m, s, g1, g2, margin, sh);
+  if (t >= 0) {
+    T f[9];
+    c_fan_frame(val[0] + 4, f);
+    c_fan_rotate(sh, s.gmat[g1], s.gmat[g2], f, t);
+  }
+  T c[7];
+  const bool hit = c_mpr_contact(m, sh, margin, c);
+  if (hit && (threadIdx.x & 63) == 0)
+    for (int k = 0; k < 7; k++) val[slot][k] = c[k];
+  return hit;
+}
+template <typename T>
+__device__ __forceinline__ int c_convex(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int g1, int g2, T margin,
+                                        T (*val)[7]) {
+  const DevPhys<T>& m = phys<T>();
+  const int l = threadIdx.x & 63;
+  const int trips = m.multiccd ? 4 : 0;
+  int n = 0;
+  for (int t = -1; t < trips; t++) {   // t = -1: the first run; then the multiccd trials
+    wsync();
+    if (!c_convex_run(s, g1, g2, margin, t, val, n)) {
+      if (t < 0) return 0;
+      continue;
+    }
     wsync();
     bool distinct = true;
-    for (int i = 0; i < n; i++) {
-      const T e[3] = {c[1] - val[i][1], c[2] - val[i][2], c[3] - val[i][3]};
-      if (PM<T>::sqrt_(cd3(e, e)) <= tol) distinct = false;
-    }
-    if (!distinct) continue;
-    if (l == 0)
-      for (int k = 0; k < 7; k++) val[n][k] = c[k];
-    n++;
+    const T tol = c_fan_tol(m, g1, g2);
+    for (int i = 0; i < n; i++)
+      if (c_fan_close(val[n] + 1, val[i] + 1, tol)) distinct = false;
+    if (distinct) n++;
   }
   wsync();
   if (l == 0)
     for (int i = 0; i < n; i++)
-      for (int k = 0; k < 3; k++) val[i][1 + k] += org[k];
+      for (int k = 0; k < 3; k++) val[i][1 + k] += s.gpos[g1][k];
   wsync();
   return n;
 }

@@ -534,7 +534,7 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
 #if PNP_WIDE
 // Wide tier, persistent: the selection kernel lists the envs the pass runs (list[0] = count), and
 // a grid of as many workgroups per CU as the LDS holds (one at 192 contacts) loops over the list.  Each workgroup is MW_WAVES waves: wave 0
-// steps its env, the other is a helper wave for the convex pass (step.hip, mw_helper).  Multi-wave
+// steps its env, the others are helper waves for the convex pass (step.hip, mw_helper).  Multi-wave
 // workgroups launched one per env (4096 per pass, nearly all exiting at once) made the gym step
 // 25 % slower even with the helpers idle; a resident grid over the selected envs does not.
 __global__ void __launch_bounds__(1024) wide_select_kernel(const uint8_t* __restrict__ tier,
@@ -566,7 +566,7 @@ __global__ void __launch_bounds__(1024) wide_select_kernel(const uint8_t* __rest
   }
   if (t == 0) list[0] = base;
 }
-__global__ void __launch_bounds__(NT * MW_WAVES, 2) env_step_wide_kernel(pnp_state_t<float> st, pnp_env_params prm,
+__global__ void __launch_bounds__(NT * MW_WAVES, 1) env_step_wide_kernel(pnp_state_t<float> st, pnp_env_params prm,
                                                                           EnvSoA<float> es, const float* __restrict__ action,
                                                                           EnvOutT<float> out, const int* __restrict__ list,
                                                                           int resume) {

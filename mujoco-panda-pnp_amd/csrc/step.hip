@@ -234,6 +234,8 @@ struct Env {
   int mw;                      // waves of the env's workgroup (the wide gym kernel: helper waves, mw_helper)
   int mw_cmd;                  // helper command (MW_*), posted by wave 0 before a workgroup barrier
   int mw_next;                 // the convex pass's next pair (LDS counter)
+  unsigned char mw_hit[NT];    // the convex pass: staging slot holds a contact
+  unsigned char mw_fan[NT];    // the convex pass: round-local pairs whose multiccd trials run
 #endif
 };
 static_assert(sizeof(((Env<float>*)0)->efc_Jv) >= 7 * 4 * NT + 2 * NT + 4 + 2 * PH_MAXLIVE,
@@ -1316,32 +1318,39 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
 // helpers at a workgroup barrier (A), every wave does its part, and a second barrier (B) ends the
 // part; MW_EXIT (posted once, at the end of the kernel) releases them.  Wave 0 issues no other
 // workgroup barrier while helpers wait (its stage clock is the NoClock).
-enum { MW_EXIT = 0, MW_MPR = 1 };
-// two waves: the convex pairs split over two MPR runs at a time (gym 25.2 k -> 26.6 k gym-steps/s);
-// four made the gym step slower (23.2 k, and 18.7 k with one four-wave workgroup per env), as the
-// extra waves' registers and scratch cut how many envs stay resident (profiles/r03/ab_mpr_helper_waves.log)
-constexpr int MW_WAVES = 2;
-// The convex pairs of one round (up to 64, listed by wave 0 in cst_key in live-list order), taken
-// one at a time by whichever wave is free (an LDS counter): the same wave-cooperative MPR per pair
-// as st_collision_convex, its result staged at the pair's slot (cst_val: dist, pos, normal;
-// cst_key bit 15: contact) for wave 0 to append.
-__device__ void convex_part(Env<float>& s, int n) {
+enum { MW_EXIT = 0, MW_MPR = 1, MW_FAN = 2 };
+// Four waves, one per SIMD: the wide tier's Env (192 contacts) holds one env per CU, so the helpers
+// cost no residency, and multiccd makes up to five MPR runs per convex pair to spread.  (Round 2 /
+// early round 3, at two envs per CU: two waves, four were slower -- profiles/r03/ab_mpr_helper_waves.log.)
+constexpr int MW_WAVES = 4;
+// A round's convex pairs (up to RN, listed by wave 0 in cst_key in live-list order), each with
+// `per` staging slots (cst_val, mw_hit): slot per o holds pair o's first MPR contact, slots
+// per o + 1 + t its multiccd trial t (positions relative to geom 1's centre).  Items are taken one
+// at a time by whichever wave is free (an LDS counter): MW_MPR items are the pairs, MW_FAN items
+// (pair, trial) of the pairs with a first contact.  The same functions as st_collision_convex's
+// serial c_convex (c_convex_shapes / c_mpr_contact / c_fan_rotate): the same bits.
+__device__ void convex_part(Env<float>& s, int cmd) {
   const DevPhys<float>& m = phys<float>();
   const int l = lane_id();
+  const int kind = cmd & 255;
   // n and the taken slot are wave-uniform (SGPRs), so the loop's exit is a scalar branch: with
   // a per-lane exit the compiler's structured loop could run on with lane 0 masked off, where
   // readfirstlane no longer reads the lane that took the slot.  At most n trips in any case.
-  n = __builtin_amdgcn_readfirstlane(n);
-  const int per = m.multiccd ? C_MULTI : 1;   // staging slots per pair
+  const int n = __builtin_amdgcn_readfirstlane(cmd >> 8);
+  const int per = m.multiccd ? C_MULTI : 1;
   for (int it = 0; it < n; it++) {
     int o = 0;
     if (l == 0) o = atomicAdd(&s.mw_next, 1);
     o = __builtin_amdgcn_readfirstlane(__shfl(o, 0));
     if (o >= n) return;
-    const int p = s.cst_key[o];
+    const int po = kind == MW_FAN ? s.mw_fan[o >> 2] : o;   // round-local pair
+    const int slot = per * po + (kind == MW_FAN ? 1 + (o & 3) : 0);
+    const int p = s.cst_key[po];
     const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
-    const int nc = c_convex(m, s, g1, g2, fmaxf(m.geom_margin[g1], m.geom_margin[g2]), s.cst_val + per * o);
-    if (l == 0) s.cst_key[o] = (unsigned short)(p | nc << 12);   // pair (< 1024) | its contact count
+    const float margin = fmaxf(m.geom_margin[g1], m.geom_margin[g2]);
+    const bool hit = c_convex_run(s, g1, g2, margin, kind == MW_FAN ? (o & 3) : -1, s.cst_val + per * po,
+                                  slot - per * po);
+    if (l == 0) s.mw_hit[slot] = hit;
   }
 }
 __device__ void mw_helper(Env<float>& s) {
@@ -1349,19 +1358,29 @@ __device__ void mw_helper(Env<float>& s) {
     __syncthreads();   // A: a command is posted
     const int cmd = s.mw_cmd;
     if ((cmd & 255) == MW_EXIT) return;
-    if ((cmd & 255) == MW_MPR) convex_part(s, cmd >> 8);
+    convex_part(s, cmd);
     __syncthreads();   // B: the part is done
   }
 }
-// wave 0: per round of up to 64 convex pairs, list them, run them on every wave, then append the
-// staged contacts in live-list order (the order st_collision_convex's one-pair-at-a-time loop
-// produces; same bits)
+// wave 0: run one part on every wave of the workgroup
+__device__ __forceinline__ void mw_run(Env<float>& s, int cmd) {
+  if (lane_id() == 0) {
+    s.mw_next = 0;
+    s.mw_cmd = cmd;
+  }
+  __syncthreads();   // A
+  convex_part(s, cmd);
+  __syncthreads();   // B
+}
+// wave 0: per round of up to RN convex pairs, list them, run their first MPR and then their
+// multiccd trials on every wave, decide each pair's fan in trial order (lane per pair: the same
+// distinct-position tests as c_convex) and append the contacts in live-list order (the order
+// st_collision_convex's one-pair-at-a-time loop produces; same bits)
 __device__ __attribute__((noinline)) void st_collision_convex_mw(Env<float>& s) {
   const DevPhys<float>& m = phys<float>();
   const int l = lane_id();
   int ncon = s.ncon_raw;
   const int nconv = s.nconvex, nlive = s.nlive;
-  // a round's pairs stage up to `per` contacts each in the 64 staging slots
   const int per = m.multiccd ? C_MULTI : 1, RN = NT / per;
   int base = 0, ord = 0;   // live-list chunk and convex ordinal the listing has reached
   for (int r = 0; RN * r < nconv; r++) {
@@ -1380,30 +1399,51 @@ __device__ __attribute__((noinline)) void st_collision_convex_mw(Env<float>& s) 
       got = ord - RN * r;
       base += NT;
     }
-    if (l == 0) {
-      s.mw_next = 0;
-      s.mw_cmd = MW_MPR | (n << 8);
+    if (l < NT) s.mw_hit[l] = 0;
+    wsync();
+    mw_run(s, MW_MPR | (n << 8));
+    const bool first = l < n && s.mw_hit[per * l];
+    if (per > 1) {   // the trials of the pairs with a first contact
+      const uint64_t hb = __ballot(first);
+      if (first) s.mw_fan[__popcll(hb & ((1ull << l) - 1ull))] = (unsigned char)l;
+      wsync();
+      const int nh = __popcll(hb);
+      if (nh) mw_run(s, MW_FAN | ((4 * nh) << 8));
     }
-    __syncthreads();   // A
-    convex_part(s, n);
-    __syncthreads();   // B
-    // append in pair order: pair o's contacts at ncon + (contacts of pairs before o) + k
-    const unsigned key = l < n ? s.cst_key[l] : 0u;
-    const int cnt = (int)(key >> 12);
+    // lane o: pair o's fan in trial order (accepted slots as a bit mask)
+    unsigned acc = 0;
+    int cnt = 0, pg1 = 0;
+    if (first) {
+      const int p = s.cst_key[l];
+      pg1 = m.pair_g1[p];
+      const float tol = c_fan_tol(m, pg1, m.pair_g2[p]);
+      acc = 1;
+      for (int t = 1; t < per; t++) {
+        if (!s.mw_hit[per * l + t]) continue;
+        bool distinct = true;
+        for (int i = 0; i < t; i++)
+          if (((acc >> i) & 1) && c_fan_close(s.cst_val[per * l + t] + 1, s.cst_val[per * l + i] + 1, tol)) distinct = false;
+        if (distinct) acc |= 1u << t;
+      }
+      cnt = __popc(acc);
+    }
     const int excl = wscan_incl(cnt) - cnt;
     const int tot = __builtin_amdgcn_readlane(excl + cnt, 63);
-    const int o = l / per, kk = l - o * per;   // staging slot l holds contact kk of pair o
-    const int co = __shfl(cnt, o), eo = __shfl(excl, o);
-    const unsigned ko = (unsigned)__shfl((int)key, o);
-    const int at = ncon + eo + kk;
-    if (o < n && kk < co && at < PH_MAXCON) {
-      const int p = (int)(ko & 0x3FFu), g1 = m.pair_g1[p], g2 = m.pair_g2[p];
-      const float pos[3] = {s.cst_val[l][1], s.cst_val[l][2], s.cst_val[l][3]};
+    // staging slot l holds trial j of pair o: its place if accepted
+    const int o = l / per, j = l - o * per;
+    const unsigned ao = (unsigned)__shfl((int)acc, o);
+    const int eo = __shfl(excl, o);
+    const int at = ncon + eo + __popc(ao & ((1u << j) - 1u));
+    if (o < n && ((ao >> j) & 1) && at < PH_MAXCON) {
+      const int p = s.cst_key[o], g1 = m.pair_g1[p], g2 = m.pair_g2[p];
+      const float* org = s.gpos[g1];
+      const float pos[3] = {s.cst_val[l][1] + org[0], s.cst_val[l][2] + org[1], s.cst_val[l][3] + org[2]};
       const float nrm[3] = {s.cst_val[l][4], s.cst_val[l][5], s.cst_val[l][6]};
       LdsSink<float> ls{s.con + at, 1};
       ls.emit(s.cst_val[l][0], pos, nrm);
       c_params(m, s.con[at], g1, g2);
     }
+    (void)pg1;
     ncon += tot;
     wsync();
   }
