@@ -416,7 +416,7 @@ __device__ __forceinline__ void env_step_one(const DevPhys<T>& m, Env<T>& s, con
   (void)mw;
   const int l = lane_id();
   load_env(m, s, st, b, hand);
-#if PNP_WIDE
+#if PNP_MW
   if (l == 0) s.mw = mw;
   wsync();
 #endif
@@ -531,8 +531,8 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
   env_step_one(m, s, st, prm, es, action, out, b, cur, k0, resume, hand, 1);
 }
 
-#if PNP_WIDE
-// Wide tier, persistent: the selection kernel lists the envs the pass runs (list[0] = count), and
+#if PNP_MW
+// Wide and full tiers, persistent: the selection kernel lists the envs the pass runs (list[0] = count), and
 // a grid of as many workgroups per CU as the LDS holds (one at 192 contacts) loops over the list.  Each workgroup is MW_WAVES waves: wave 0
 // steps its env, the others are helper waves for the convex pass (step.hip, mw_helper).  Multi-wave
 // workgroups launched one per env (4096 per pass, nearly all exiting at once) made the gym step
@@ -566,10 +566,10 @@ __global__ void __launch_bounds__(1024) wide_select_kernel(const uint8_t* __rest
   }
   if (t == 0) list[0] = base;
 }
-__global__ void __launch_bounds__(NT * MW_WAVES, 1) env_step_wide_kernel(pnp_state_t<float> st, pnp_env_params prm,
+__global__ void __launch_bounds__(NT * MW_WAVES, PNP_WIDE ? 1 : 4) env_step_wide_kernel(pnp_state_t<float> st, pnp_env_params prm,
                                                                           EnvSoA<float> es, const float* __restrict__ action,
                                                                           EnvOutT<float> out, const int* __restrict__ list,
-                                                                          int resume) {
+                                                                          int resume, int hand) {
   __shared__ __attribute__((aligned(16))) Env<float> s_env;   // static LDS: see env_lds_note
   Env<float>& s = s_env;
   const DevPhys<float>& m = phys<float>();
@@ -582,7 +582,7 @@ __global__ void __launch_bounds__(NT * MW_WAVES, 1) env_step_wide_kernel(pnp_sta
     const int b = list[1 + i];
     const int cur = es.tier ? (es.tier[b] & 3) : 0;
     const int k0 = resume ? (int)((st.warn[b] >> PNP_RESUME_SHIFT) & PNP_RESUME_MAXSUB) : 0;
-    env_step_one(m, s, st, prm, es, action, out, b, cur, k0, resume, 0, MW_WAVES);
+    env_step_one(m, s, st, prm, es, action, out, b, cur, k0, resume, hand, MW_WAVES);
   }
   if (lane_id() == 0) s.mw_cmd = MW_EXIT;   // every path of wave 0 ends here
   __syncthreads();
@@ -614,29 +614,7 @@ static EnvOutT<T> out_view(const pnp_env_out* o) {
                     o->terminated, o->truncated};
 }
 
-#if PNP_COMPACT
-int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
-                                const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
-                                void* stream, int only_tier) {
-  const DevPhys<float>* src = phys_image<float>(model);
-  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
-  ResidentLease lease;
-  if (const int32_t rc = lease.acquire(RES_COMPACT_GYM_F32, model, (const void*)&g_phys_f32, src,
-                                       sizeof(DevPhys<float>), stream))
-    return rc;
-  hipLaunchKernelGGL(env_step_kernel<float>, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, *p,
-                     env_view<float>(e), action, out_view<float>(o), B, 0, 1, only_tier);
-  if (const int32_t rc = pnp_check_launch("env_step_kernel (compact)")) return rc;
-  return lease.launched();
-}
-int32_t env_compact_lds_bytes() { return (int32_t)sizeof(Env<float>); }
-#elif PNP_WIDE
-// wide tier: resume pass of the gym step over the envs the full kernel handed over (resume = 1),
-// or the routed pass over the envs whose step starts in the wide tier (resume = 0, only_tier = 2);
-// launched by the full build's launch_env_step, which holds the full image's lease
-// The selection lists (one per pass kind: the routed pass on its side stream and the resume pass
-// on the caller's stream can be in flight together), per device; their users are serialised by
-// the full image's lease like the route streams.
+#if PNP_MW
 struct WideLists {
   int* list[2] = {nullptr, nullptr};
   int cap[2] = {0, 0};
@@ -663,27 +641,59 @@ static int32_t wide_list(int kind, int32_t B, int** out, int* ncu) {
   *ncu = w.ncu > 0 ? w.ncu : 256;
   return PNP_OK;
 }
-int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
-                             const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
-                             void* stream, int resume, int only_tier) {
-  const DevPhys<float>* src = phys_image<float>(model);
-  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+// persistent multi-wave gym pass of this build's tier over the envs the selection kernel lists
+static int32_t launch_env_step_mw(const pnp_state_t<float>* st, const pnp_env_params* p, const pnp_env_state* e,
+                                  const float* action, const pnp_env_out* o, int32_t B, void* stream, int resume,
+                                  int only_tier, int hand, const char* what) {
   if (B <= 0) return PNP_OK;
   int* list = nullptr;
   int ncu = 0;
   if (const int32_t rc = wide_list(resume ? 1 : 0, B, &list, &ncu)) return rc;
-  ResidentLease lease;
-  if (const int32_t rc = lease.acquire(RES_WIDE_F32, model, (const void*)&g_phys_f32, src, sizeof(DevPhys<float>),
-                                       stream))
-    return rc;
   hipLaunchKernelGGL(wide_select_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, e->tier, st->warn, B, resume,
                      only_tier, list);
   if (const int32_t rc = pnp_check_launch("wide_select_kernel")) return rc;
   const int per_cu = (int)(163840 / sizeof(Env<float>)) > 0 ? (int)(163840 / sizeof(Env<float>)) : 1;   // envs per CU (LDS)
   const int grid = B < per_cu * ncu ? B : per_cu * ncu;
   hipLaunchKernelGGL(env_step_wide_kernel, dim3(grid), dim3(NT * MW_WAVES), 0, (hipStream_t)stream, *st, *p,
-                     env_view<float>(e), action, out_view<float>(o), (const int*)list, resume);
-  if (const int32_t rc = pnp_check_launch("env_step_wide_kernel")) return rc;
+                     env_view<float>(e), action, out_view<float>(o), (const int*)list, resume, hand);
+  return pnp_check_launch(what);
+}
+#endif
+#if PNP_COMPACT
+int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
+                                const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
+                                void* stream, int only_tier) {
+  const DevPhys<float>* src = phys_image<float>(model);
+  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  ResidentLease lease;
+  if (const int32_t rc = lease.acquire(RES_COMPACT_GYM_F32, model, (const void*)&g_phys_f32, src,
+                                       sizeof(DevPhys<float>), stream))
+    return rc;
+  hipLaunchKernelGGL(env_step_kernel<float>, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, *p,
+                     env_view<float>(e), action, out_view<float>(o), B, 0, 1, only_tier);
+  if (const int32_t rc = pnp_check_launch("env_step_kernel (compact)")) return rc;
+  return lease.launched();
+}
+int32_t env_compact_lds_bytes() { return (int32_t)sizeof(Env<float>); }
+#elif PNP_WIDE
+// wide tier: resume pass of the gym step over the envs the full kernel handed over (resume = 1),
+// or the routed pass over the envs whose step starts in the wide tier (resume = 0, only_tier = 2);
+// launched by the full build's launch_env_step, which holds the full image's lease
+// The selection lists (one per pass kind: the routed pass on its side stream and the resume pass
+// on the caller's stream can be in flight together), per device; their users are serialised by
+// the full image's lease like the route streams.
+int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
+                             const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
+                             void* stream, int resume, int only_tier) {
+  const DevPhys<float>* src = phys_image<float>(model);
+  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  if (B <= 0) return PNP_OK;
+  ResidentLease lease;
+  if (const int32_t rc = lease.acquire(RES_WIDE_F32, model, (const void*)&g_phys_f32, src, sizeof(DevPhys<float>),
+                                       stream))
+    return rc;
+  if (const int32_t rc = launch_env_step_mw(st, p, e, action, o, B, stream, resume, only_tier, 0, "env_step_wide_kernel"))
+    return rc;
   return lease.launched();
 }
 #else
@@ -781,6 +791,15 @@ static bool gym_full_resume_enabled() {
   const char* e = getenv("PNP_GYM_FULL_RESUME");
   return !(e && e[0] == '0');
 }
+// PNP_GYM_FULL_MW: 1 = the fp32 gym step's full-tier passes run the persistent two-wave kernel
+// (env_step_wide_kernel of the full build: the helper wave takes half of the convex pass); unset /
+// 0 = one single-wave workgroup per env (default: the two-wave pass measured 5 % slower on the gym
+// step, 18.0 k vs 18.9 k gym-steps/s -- a persistent grid walks the selected envs in list order,
+// while one workgroup per env lets the dispatcher balance the CUs; profiles/r03/ab_gym_full_mw.log)
+static bool gym_full_mw_enabled() {
+  const char* e = getenv("PNP_GYM_FULL_MW");
+  return e && e[0] == '1';
+}
 // Two side streams per device for the routed passes, forked from and joined back into the
 // caller's stream.  Used only while the full image's lease is held (launch_env_step), which
 // serialises their users per device; creation has its own lock.
@@ -830,6 +849,8 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   // routed: the envs whose last step finished in the full / wide tier start there, on side streams
   // concurrent with the compact pass; the resume passes then only see this step's new hand-overs
   const bool route = compact && wide && gym_compact_mode() == 1 && e->tier && gym_route_enabled();
+  // fp32 full-tier passes: persistent, two waves per env (helper wave for the convex pass)
+  const bool full_mw = tiers && gym_full_mw_enabled();
   RouteStreams* rs = nullptr;
   // join side stream i back into the caller's stream (its kernels read the full image and write
   // the state: later work on s0, and the next model switch, must be ordered after them)
@@ -856,9 +877,14 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
     if (he != hipSuccess) { pnp_set_error("pnp_env_step: fork: %s", hipGetErrorString(he)); return PNP_ERR_HIP; }
     forked = true;
     if ((rc = launch_env_step_wide(model, st32, p, e, a32, o, B, rs->side[1], 0, 2))) return fail(rc);
-    hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, rs->side[0], dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
-                       0, wide, 1);
-    if ((rc = pnp_check_launch("env_step_kernel (full, routed)"))) return fail(rc);
+    if (full_mw) {
+      rc = launch_env_step_mw(st32, p, e, a32, o, B, rs->side[0], 0, 1, wide, "env_step_wide_kernel (full, routed)");
+    } else {
+      hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, rs->side[0], dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
+                         0, wide, 1);
+      rc = pnp_check_launch("env_step_kernel (full, routed)");
+    }
+    if (rc) return fail(rc);
   }
   if (compact && (rc = launch_env_step_compact(model, st32, p, e, a32, o, B, stream, route ? 0 : -1))) return fail(rc);
   if (compact && gym_compact_mode() == 2) {
@@ -869,9 +895,15 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
     return lease.launched();
   }
   if (!route || gym_full_resume_enabled()) {
-    hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, s0, dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
-                       compact ? 1 : 0, wide, route ? 0 : -1);
-    if ((rc = pnp_check_launch("env_step_kernel"))) return fail(rc);
+    if (full_mw) {
+      rc = launch_env_step_mw(st32, p, e, a32, o, B, stream, compact ? 1 : 0, route ? 0 : -1, wide,
+                              "env_step_wide_kernel (full)");
+    } else {
+      hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, s0, dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
+                         compact ? 1 : 0, wide, route ? 0 : -1);
+      rc = pnp_check_launch("env_step_kernel");
+    }
+    if (rc) return fail(rc);
   }
   if (route) {   // the wide resume pass also takes the routed full pass's hand-overs
     if (const hipError_t he = join_side(0)) {

@@ -55,6 +55,9 @@
 // PNP_HANDS: this build can hand an overflowing sub-step to the next tier (the full build only
 // when its kernel is launched with hand = 1); PNP_LEAN: no debug-only fields outside the unions
 #define PNP_HANDS (!PNP_WIDE)
+// PNP_MW: the fp32 gym kernels of this build run several waves per env (helper waves for the convex
+// pass): the wide build (4 waves, 1 env per CU) and the full build (2 waves, 4 envs per CU)
+#define PNP_MW (PNP_WIDE || (!PNP_COMPACT && !PNP_GYM))
 #define PNP_LEAN (PNP_COMPACT || PNP_WIDE)
 // PNP_BIG_ISLANDS: the solver's whole-wave paths for islands with more rows than a wave (line
 // search, gradient, MFMA Hessian).  Compiled out of the compact build, which hands such islands
@@ -230,7 +233,7 @@ struct Env {
 #endif
   int ovf;                     // a capacity overflowed in this sub-step (hand-over builds)
   int hand;                    // full build: overflows hand over (1) or truncate with a warning (0)
-#if PNP_WIDE
+#if PNP_MW
   int mw;                      // waves of the env's workgroup (the wide gym kernel: helper waves, mw_helper)
   int mw_cmd;                  // helper command (MW_*), posted by wave 0 before a workgroup barrier
   int mw_next;                 // the convex pass's next pair (LDS counter)
@@ -1312,7 +1315,7 @@ __device__ void st_collision(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, 
   clk.sub_lap(SC_NARROW);
 }
 
-#if PNP_WIDE
+#if PNP_MW
 // ---- helper wave of the wide gym kernel (env_step_wide_kernel runs MW_WAVES waves per env; wave
 // 0 runs the step, the others wait in mw_helper).  Wave 0 posts a command in s.mw_cmd and meets the
 // helpers at a workgroup barrier (A), every wave does its part, and a second barrier (B) ends the
@@ -1322,7 +1325,7 @@ enum { MW_EXIT = 0, MW_MPR = 1, MW_FAN = 2 };
 // Four waves, one per SIMD: the wide tier's Env (192 contacts) holds one env per CU, so the helpers
 // cost no residency, and multiccd makes up to five MPR runs per convex pair to spread.  (Round 2 /
 // early round 3, at two envs per CU: two waves, four were slower -- profiles/r03/ab_mpr_helper_waves.log.)
-constexpr int MW_WAVES = 4;
+constexpr int MW_WAVES = PNP_WIDE ? 4 : 2;   // full build: 2 x 4 envs per CU = 2 waves per SIMD
 // A round's convex pairs (up to RN, listed by wave 0 in cst_key in live-list order), each with
 // `per` staging slots (cst_val, mw_hit): slot per o holds pair o's first MPR contact, slots
 // per o + 1 + t its multiccd trial t (positions relative to geom 1's centre).  Items are taken one
@@ -3609,7 +3612,7 @@ __device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& 
   st_collision(m, s, clk);
   if (s.nconvex) {
     clk.sub_start();
-#if PNP_WIDE
+#if PNP_MW
     if constexpr (sizeof(T) == 4) {
       if (s.mw > 1) st_collision_convex_mw(s);
       else st_collision_convex(m, s);
@@ -3705,7 +3708,7 @@ __device__ void load_env(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, cons
   if (l < 3 * m.nmocap) s.mocap_pos[l] = st.mocap_pos[(size_t)b * 3 * m.nmocap + l];
   if (l < 4 * m.nmocap) s.mocap_quat[l] = st.mocap_quat[(size_t)b * 4 * m.nmocap + l];
   if (l == 0) { s.time = st.time[b]; s.warn = st.warn[b] & 0xFFFFu; s.ovf = 0; s.hand = hand; }
-#if PNP_WIDE
+#if PNP_MW
   if (l == 0) s.mw = 1;   // single-wave unless the kernel says otherwise (env_step_kernel)
 #endif
   wsync();
