@@ -53,7 +53,7 @@ template <typename T>
 struct DevPhys {
   int nq, nv, nu, nbody, njnt, ngeom, npair, nmocap, neq, ntree, nmentry;
   T timestep, gravity[3];
-  int noslip_iterations, iterations, multiccd;   // multiccd: mjENBL_MULTICCD (mjc_Convex's perturbed contacts)
+  int noslip_iterations, iterations;
   // bodies
   int body_parentid[PH_MAXB], body_rootid[PH_MAXB], body_weldid[PH_MAXB], body_mocapid[PH_MAXB];
   int body_jntadr[PH_MAXB], body_jntnum[PH_MAXB], body_dofadr[PH_MAXB], body_dofnum[PH_MAXB];
@@ -127,4 +127,5 @@ struct DevPhys {
   double kd_jnt_pos[PH_MAXB][3], kd_jnt_axis[PH_MAXB][3], kd_qpos0[PH_MAXB];
   double kd_eq_data[11];
   int weld_eq, weld_body[2];   // the first weld equality and its bodies (-1: none)
+  int multiccd;   // mjENBL_MULTICCD (mjc_Convex's perturbed contacts)
 };

@@ -25,7 +25,7 @@ def main():
             if cur:
                 steps.append(cur)
             cur = []
-        elif "env_step_kernel" in name:
+        elif "env_step_kernel" in name or "env_step_wide_kernel" in name:
             if not commit and "pnp_compact_gym::" in name and cur:
                 steps.append(cur)
                 cur = []
