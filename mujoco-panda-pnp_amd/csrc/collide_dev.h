@@ -896,7 +896,7 @@ __device__ __forceinline__ int c_convex(const DevPhys<T>& /*image: phys<T>()*/, 
                                         T (*val)[7]) {
   const DevPhys<T>& m = phys<T>();
   const int l = threadIdx.x & 63;
-  const int trips = m.multiccd ? 4 : 0;
+  const int trips = (!PNP_COMPACT && m.multiccd) ? 4 : 0;   // (the compact build hands fans over: step.hip)
   int n = 0;
   for (int t = -1; t < trips; t++) {   // t = -1: the first run; then the multiccd trials
     wsync();

@@ -1480,6 +1480,18 @@ __device__ __attribute__((noinline)) void st_collision_convex(const DevPhys<T>& 
       const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
       // the pair's contacts (up to C_MULTI with multiccd) staged in cst_val, then lanes 0.. append
       const int n = c_convex(m, s, g1, g2, fmax(m.geom_margin[g1], m.geom_margin[g2]), s.cst_val);
+#if PNP_COMPACT
+      // The compact build carries no multiccd fan (c_convex stops after the first run): a convex
+      // pair in contact hands the sub-step to the full tier, like a capacity overflow.  The fan's
+      // code in this build grew its frames (forward 48 -> 64, the stage 180 -> 284 B per lane),
+      // its scratch footprint and write-back (PMC 760 -> 989 MB per launch), and cost C3 1 %,
+      // although C3's settled envs never make a convex contact.
+      if (n && m.multiccd) {
+        if (l == 0) CAP_FULL(8u);
+        wsync();
+        return;
+      }
+#endif
       if (l < n && ncon + l < PH_MAXCON) {
         const T pos[3] = {s.cst_val[l][1], s.cst_val[l][2], s.cst_val[l][3]};
         const T nrm[3] = {s.cst_val[l][4], s.cst_val[l][5], s.cst_val[l][6]};
