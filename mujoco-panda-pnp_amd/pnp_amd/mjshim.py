@@ -59,29 +59,46 @@ class MujocoShim:
         self._st = engine.new_state(1, dtype)
 
     # ---------------------------------------------------------------- mirror <-> device
+    # One packed host->device copy per upload and one device->host copy per download (each
+    # pageable copy is a synchronisation: per-field copies made a BT tick ~20 round trips).
     def upload(self, data, st=None):
         st = self._st if st is None else st
-        for k in MjData.STATE:
-            st[k][0].copy_(torch.from_numpy(np.ascontiguousarray(getattr(data, k), np.float64).reshape(-1)))
-        st["time"][0] = float(data.time)
+        parts = [np.ascontiguousarray(getattr(data, k), np.float64).reshape(-1) for k in MjData.STATE]
+        d = torch.from_numpy(np.concatenate(parts + [np.array([float(data.time)])])).to(self.engine.device)
+        o = 0
+        for k, p in zip(MjData.STATE, parts):
+            st[k][0].copy_(d[o:o + p.size])
+            o += p.size
+        st["time"][0].copy_(d[o])
         st["warn"][0] = int(data.warn)
         return st
 
-    def download(self, data, st=None):
-        st = self._st if st is None else st
-        host = {k: v[0].double().cpu().numpy() for k, v in st.items()}
+    def _fetch(self, tensors):
+        """Device tensors -> float64 numpy arrays, in one transfer."""
+        flat = torch.cat([t.reshape(-1).double() for t in tensors]).cpu().numpy()
+        out, o = [], 0
+        for t in tensors:
+            out.append(flat[o:o + t.numel()])
+            o += t.numel()
+        return out
+
+    def _store(self, data, host):
         for k in MjData.STATE:
             getattr(data, k)[...] = host[k].reshape(getattr(data, k).shape)
-        data.time = float(host["time"])
-        data.warn = int(host["warn"])
+        data.time = float(host["time"][0])
+        data.warn = int(host["warn"][0])
+
+    def download(self, data, st=None):
+        st = self._st if st is None else st
+        keys = list(st.keys())
+        self._store(data, dict(zip(keys, self._fetch([st[k][0] for k in keys]))))
 
     def frames(self, data):
         """site_xpos / site_xmat of data.qpos_kin (the last forward)."""
         t = lambda a: torch.as_tensor(np.asarray(a, np.float64).reshape(1, -1), dtype=self.dtype,
                                       device=self.engine.device)
         sx, sm = self.engine.site_kinematics(t(data.qpos_kin), t(data.mocap_pos), t(data.mocap_quat))
-        data.site_xpos[...] = sx[0].double().cpu().numpy()
-        data.site_xmat[...] = sm[0].double().cpu().numpy()
+        data.site_xpos[...], data.site_xmat[...] = (a.reshape(data.site_xpos.shape[0], -1) for a in self._fetch([sx[0], sm[0]]))
 
     # ---------------------------------------------------------------- the binding's functions
     def mj_step(self, model, data, nstep=1):
@@ -91,14 +108,23 @@ class MujocoShim:
         st = self.upload(data)
         if nstep > 1:
             self.engine.step(st, nstep - 1)
-        qk = st["qpos"][0].double().cpu().numpy()
-        w0 = int(st["warn"][0])
+        qk = st["qpos"][0:1].clone()          # the last sub-step's forward runs at this qpos
+        w0 = st["warn"][0].clone()
         self.engine.step(st, 1)
-        self.download(data, st)
-        if (data.warn & BAD_STATE_BITS) & ~(w0 & BAD_STATE_BITS):
-            qk = np.array(self.model.qpos0, np.float64)
-        data.qpos_kin = qk
-        self.frames(data)
+        # data.site_* of the last forward, launched before the one download
+        sx, sm = self.engine.site_kinematics(qk, st["mocap_pos"][0:1].contiguous(), st["mocap_quat"][0:1].contiguous())
+        keys = list(st.keys())
+        got = self._fetch([st[k][0] for k in keys] + [qk[0], w0, sx[0], sm[0]])
+        host = dict(zip(keys, got[:len(keys)]))
+        self._store(data, host)
+        q_kin, w_before = got[len(keys)], int(got[len(keys) + 1][0])
+        if (data.warn & BAD_STATE_BITS) & ~(w_before & BAD_STATE_BITS):
+            data.qpos_kin = np.array(self.model.qpos0, np.float64)   # bad-state reset: frames at qpos0
+            self.frames(data)
+            return
+        data.qpos_kin = np.array(q_kin, np.float64)
+        data.site_xpos[...] = got[len(keys) + 2].reshape(data.site_xpos.shape)
+        data.site_xmat[...] = got[len(keys) + 3].reshape(data.site_xmat.shape)
 
     def mj_forward(self, model, data):
         data.qpos_kin = np.array(data.qpos, np.float64)
