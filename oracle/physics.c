@@ -606,7 +606,15 @@ static void solve_noslip(Mdl* m, orc_data* d, int maxiter) {
       A[r * n + c] = s;
     }
   double* f = d->efc_force;
+  /* diagnostic: the per-sweep improvement MuJoCo's mj_solNoSlip tests against noslip_tolerance
+     (the cost decrease 0.5 dT A d + dT res of every pair update, scaled by 1 / (meaninertia nv));
+     recorded only -- this oracle always runs maxiter sweeps (not restated) */
+  double mi = 0;
+  for (int i = 0; i < nv; i++) mi += d->qM[i * nv + i];
+  const double nscale = 1.0 / ((mi / nv) * (nv > 1 ? nv : 1));
+  for (int k = 0; k < 8; k++) d->noslip_improvement[k] = -1;
   for (int iter = 0; iter < maxiter; iter++) {
+    double impr = 0;
     for (int i = d->ne; i < n; i++) {
       if (d->efc_type[i] != ORC_CNSTR_CONTACT_PYRAMIDAL) continue;
       int dim = d->contact[d->efc_id[i]].dim;
@@ -632,9 +640,13 @@ static void solve_noslip(Mdl* m, orc_data* d, int maxiter) {
           f[j] = mid + y;
           f[j + 1] = mid - y;
         }
+        const double dl[2] = {f[j] - old[0], f[j + 1] - old[1]};
+        impr -= 0.5 * (dl[0] * (Ac[0] * dl[0] + Ac[1] * dl[1]) + dl[1] * (Ac[2] * dl[0] + Ac[3] * dl[1])) +
+                dl[0] * res[0] + dl[1] * res[1];
       }
       i += 2 * (dim - 1) - 1;
     }
+    if (iter < 8) d->noslip_improvement[iter] = impr * nscale;
   }
   free(MinvJt);
   free(A);
@@ -855,6 +867,7 @@ int orc_field(Mdl* m, const orc_data* d, const char* name, double* out, int cap)
   else if (!strcmp(name, "ncon")) { tmp[0] = d->ncon; src = tmp; n = 1; }
   else if (!strcmp(name, "nefc")) { tmp[0] = d->nefc; src = tmp; n = 1; }
   else if (!strcmp(name, "solver_iter")) { tmp[0] = d->solver_iter; src = tmp; n = 1; }
+  else if (!strcmp(name, "noslip_improvement")) { src = d->noslip_improvement; n = 8; }
   else if (!strcmp(name, "warn")) { tmp[0] = d->warn; src = tmp; n = 1; }
   else if (!strcmp(name, "contact")) {
     /* per contact: pos3 frame9 dist includemargin friction5 solref2 solimp5 dim geom1 geom2 = 30 */

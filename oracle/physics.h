@@ -73,6 +73,7 @@ typedef struct {
   double qfrc_constraint[ORC_MAXV], qacc[ORC_MAXV], qacc_newton[ORC_MAXV];
   int solver_iter;
   double solver_improvement, solver_gradient;
+  double noslip_improvement[8];   /* diagnostic: MuJoCo's scaled noslip improvement per sweep (not used to stop) */
 } orc_data;
 
 #endif
