@@ -398,9 +398,76 @@ def run_ik(args, engine, model, rank, world, dist, steps=None, warmup=None, base
     return rec
 
 
+def launch_plan(gpus, environ):
+    """How `bench.py --gpus N` runs.  Under a launcher (torchrun sets WORLD_SIZE) this process is
+    one rank: ("run", WORLD_SIZE), and --gpus must agree with it.  Without one, N > 1 means
+    ("spawn", N): this process starts the N rank processes itself (one per GPU, below); N = 1
+    runs here.  --gpus omitted = WORLD_SIZE or 1."""
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        ws = int(ws)
+        if gpus is not None and gpus != ws:
+            raise SystemExit(f"bench.py: --gpus {gpus} disagrees with WORLD_SIZE={ws} set by the launcher")
+        return "run", ws
+    n = 1 if gpus is None else int(gpus)
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {n}")
+    return ("spawn", n) if n > 1 else ("run", 1)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv, poll_s=0.2):
+    """One process per GPU, started by this one BEFORE it touches the GPU (no HIP call here:
+    `torch.cuda.device_count()` does not initialise the runtime): rank r gets RANK = LOCAL_RANK =
+    r, WORLD_SIZE = n and a 127.0.0.1 rendezvous, i.e. exactly what `torch.distributed.run
+    --nproc-per-node n` would give it, and selects device r itself.  If a rank fails the others
+    are stopped (they would wait at the next barrier).  Returns the job's exit code."""
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:
+                    q.terminate()
+        time.sleep(poll_s)
+    return rc
+
+
+def _launch_selftest(rank, world):
+    """--launch-selftest: the rank wiring alone (gloo, no GPU): every rank joins the group and
+    the job's view of it is printed by rank 0 (tests/test_dist_cpu.py)."""
+    torch.distributed.init_process_group("gloo")
+    t = torch.tensor([rank, 1], dtype=torch.int64)
+    torch.distributed.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"world": torch.distributed.get_world_size(), "rank_sum": int(t[0]), "ranks": int(t[1]),
+                          "local_ranks": os.environ.get("LOCAL_RANK")}), flush=True)
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks) of the job; without torchrun, N > 1 starts N rank processes")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096, help="envs per GPU")
@@ -416,11 +483,20 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="N > 1: nccl (= RCCL over xGMI, one GPU per rank); gloo only to rehearse several "
                          "ranks on one GPU")
+    ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    mode, world = launch_plan(args.gpus, os.environ)
+    if mode == "spawn":
+        if not args.launch_selftest and args.dist_backend == "nccl" and torch.cuda.device_count() < world:
+            raise SystemExit(f"bench.py: --gpus {world} with nccl needs {world} visible GPUs, "
+                             f"found {torch.cuda.device_count()}")
+        sys.exit(spawn_ranks(world, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_selftest:
+        _launch_selftest(rank, world)
+        return
     dist = world > 1
     if dist:
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))   # (gloo rehearsal: ranks may share a GPU)

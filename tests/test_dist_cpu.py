@@ -80,3 +80,37 @@ def test_two_rank_shards_match_global_batch(model):
     assert np.array_equal(cat("q"), qi) and np.array_equal(cat("d"), d)
     assert not np.array_equal(got[0]["qpos"], got[1]["qpos"])   # shards differ
     assert bench.shard_range(1, 4096)[0] == 4096
+
+
+def test_launch_plan():
+    """bench.py --gpus N: inside torchrun (WORLD_SIZE set) the flag must agree with the launcher;
+    without one N > 1 starts N ranks itself."""
+    import bench
+    assert bench.launch_plan(None, {}) == ("run", 1)
+    assert bench.launch_plan(1, {}) == ("run", 1)
+    assert bench.launch_plan(8, {}) == ("spawn", 8)
+    assert bench.launch_plan(4, {"WORLD_SIZE": "4"}) == ("run", 4)
+    assert bench.launch_plan(None, {"WORLD_SIZE": "2"}) == ("run", 2)
+    with pytest.raises(SystemExit):
+        bench.launch_plan(8, {"WORLD_SIZE": "1"})
+    with pytest.raises(SystemExit):
+        bench.launch_plan(0, {})
+
+
+@pytest.mark.timeout(300)
+def test_bench_spawns_ranks_from_gpus_flag():
+    """`python bench.py --gpus 2` with no launcher starts two rank processes that join one
+    process group (the rank wiring is exercised with gloo, no GPU); a --gpus / WORLD_SIZE
+    disagreement exits non-zero before any rank starts."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-selftest"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec == {"world": 2, "rank_sum": 1, "ranks": 2, "local_ranks": "0"}
+    bad = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--launch-selftest"],
+                         env=dict(env, WORLD_SIZE="2"), capture_output=True, text=True, timeout=120)
+    assert bad.returncode != 0 and "disagrees" in bad.stderr

@@ -686,3 +686,31 @@ def test_model_switch_across_streams_is_ordered(engine, model, scene):
             assert torch.equal(b[k], ref_b[k]), ("model B", k)
     finally:
         e2.close()
+
+
+@pytest.mark.timeout(300)
+def test_c4_global_batch_equals_eight_shards(engine, model):
+    """BASELINE configs[3] (C4): 32768 envs = 8 ranks x 4096.  The whole global batch stepped on
+    one GPU (reset distribution, 250 settle sub-steps, then 2 launches of 25 sub-steps with random
+    ctrl) equals, bit for bit, the 8 rank shards (env_offset r * 4096) each prepared and stepped on
+    their own -- what the 8-GPU run computes, since no env's trajectory depends on another env or
+    on the shard it sits in.  Finite state, no warning bits."""
+    import bench
+    G, R = 32768, 8
+    B = G // R
+    gst, gctrl = bench.step_inputs(engine, model, 0, G)
+    for i in range(2):
+        gst["ctrl"] = gctrl[i]
+        engine.step(gst, bench.NSUB)
+    torch.cuda.synchronize()
+    assert torch.isfinite(gst["qpos"]).all() and torch.isfinite(gst["qvel"]).all()
+    assert not bool(gst["warn"].ne(0).any())
+    for r in range(R):
+        st, ctrl = bench.step_inputs(engine, model, r, B)
+        assert torch.equal(ctrl, gctrl[:, r * B:(r + 1) * B])
+        for i in range(2):
+            st["ctrl"] = ctrl[i]
+            engine.step(st, bench.NSUB)
+        torch.cuda.synchronize()
+        for k in ("qpos", "qvel", "qacc_warmstart", "time", "warn"):
+            assert torch.equal(st[k], gst[k][r * B:(r + 1) * B]), (r, k)
