@@ -313,12 +313,22 @@ def run_tqc(engine, B, rank, world, dist, steps=3, warmup=2, learner_reps=20):
     learner_ms = (time.perf_counter() - t0) / learner_reps * 1e3
     sub = env.cfg.n_substeps * env.cfg.n_calls
     step_ms = elapsed / steps * 1e3
-    # the reference's update-to-data ratio (one gradient step per 4 transitions: sb3 defaults over
-    # 4 SubprocVecEnv workers) would add (B / 4 - 1) more gradient steps per vector step
-    ref_utd_ms = step_ms + (B / 4 - 1) * learner_ms
+    # the reference's update-to-data ratio (train.py: one gradient step per 4 transitions, sb3's
+    # defaults over 4 SubprocVecEnv workers), measured: one vector step + B / 4 gradient steps
+    utd = max(1, B // 4)
+
+    def fn_utd(i):
+        agent.collect_step()
+        agent.train(utd)
+
+    utd_elapsed, _ = _timed(fn_utd, 1, 0, dist)
     return {"gym_steps_per_s": B * world * steps / elapsed, "env_steps_per_s": B * world * steps * sub / elapsed,
             "ms_per_step": step_ms, "learner_ms_per_update": learner_ms,
-            "transitions_per_s_at_reference_utd": B * world / (ref_utd_ms * 1e-3),
+            "learner": "one gradient step captured in a HIP graph, replayed (fused Adam)" if agent._graph is not None
+                       else "eager",
+            "transitions_per_s_at_reference_utd": B * world / utd_elapsed,
+            "reference_utd": {"gradient_steps_per_vector_step": utd, "ms_per_vector_step": utd_elapsed * 1e3,
+                              "measured": True},
             "workload": f"C5: TQC (train.py hyper-parameters) on {B} FrankaShelfPNPDense envs per GPU, "
                         f"one gym step + one gradient step per step"}
 

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 8
+#define PNP_ABI_VERSION 9
 
 #define PNP_OK 0
 #define PNP_ERR_ARG -1
@@ -44,6 +44,10 @@ typedef struct pnp_model_desc {
   int32_t noslip_iterations, iterations;
   double tolerance;
   int32_t cone_pyramidal, multiccd, warmstart, integrator_euler;
+  /* mjOption noslip_tolerance (default 1e-6) and mjStatistic meaninertia (mj_setConst: mean of
+   * diag(M) at qpos0, armature included): mj_solNewton / mj_solNoSlip scale their improvement and
+   * gradient tests by 1 / (meaninertia * max(1, nv)) */
+  double noslip_tolerance, stat_meaninertia;
   /* bodies [nbody] */
   const int32_t* body_parentid;
   const int32_t* body_rootid;
@@ -257,7 +261,8 @@ int32_t pnp_step_f64(pnp_model* model, const pnp_state_f64* state, int32_t B, in
 #define PNP_DBG_EFC_TYPE 3044
 #define PNP_DBG_EFC_J 3252      /* nefc x nv dense */
 #define PNP_DBG_QACC_NEWTON 10740 /* Newton result before no-slip */
-#define PNP_DBG_SIZE 10776
+#define PNP_DBG_NOSLIP_ITER 10776 /* no-slip sweeps run (mj_solNoSlip's early exit) */
+#define PNP_DBG_SIZE 10780
 int32_t pnp_forward_debug(pnp_model* model, const pnp_state* state, int32_t B, double* dbg, void* stream);
 int32_t pnp_forward_debug_f64(pnp_model* model, const pnp_state_f64* state, int32_t B, double* dbg,
                               void* stream);
@@ -271,10 +276,10 @@ int32_t pnp_forward_debug_f64(pnp_model* model, const pnp_state_f64* state, int3
  * kinematics inertial/geom frames, Newton gradient, Newton convergence test, Newton Hessian; then per-sub-step counts summed over the sub-steps (not
  * cycles): ncon, nefc, Newton iterations, live convex pairs, islands, noslip sweep length,
  * broadphase survivors; then 8 ad-hoc sub-stage timers (aux0..aux7, cycles; what each brackets is
- * stated at its sub_lap call in csrc/step.hip); then two more counts: noslip sub-steps on the
- * dense long-list path and on the streaming path.  Separate instantiation: the product kernel
- * carries no timers. */
-#define PNP_NSTAGE 44
+ * stated at its sub_lap call in csrc/step.hip); then three more counts: noslip sub-steps on the
+ * dense long-list path and on the streaming path, noslip sweeps run.  Separate instantiation: the
+ * product kernel carries no timers. */
+#define PNP_NSTAGE 45
 #define PNP_NSTAGE_CYCLES 27
 int32_t pnp_step_profile(pnp_model* model, const pnp_state* state, int32_t B, int32_t nsub,
                          unsigned long long* stage_cycles, void* stream);

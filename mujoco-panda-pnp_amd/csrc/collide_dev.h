@@ -336,8 +336,14 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
 // mju_makeFrame: complete the contact frame from its normal (colliders set the normal only)
 // ---------------------------------------------------------------- convex pairs (MPR)
 // oracle/convex.c restated on the device (MuJoCo 2.3.3 mjc_Convex = libccd ccdMPRPenetration):
-// same control flow, tolerances scaled to T's epsilon; the portal lives in registers (every
-// index below is a compile-time constant).
+// same control flow and constants; the portal lives in registers (every index below is a
+// compile-time constant).  The arithmetic is fp64 in every build (CT), the fp32 product kernels
+// included (round 4): where the penetration direction is not unique (a hull corner on a board,
+// two faces multiccd tilts 2e-3 rad apart) MPR's path decides the normal, and fp32 rounding of the
+// Minkowski differences, portal sign tests and support gains took the other branch on a third of
+// the convex-contact fixture's envs.  Inputs (geom frames, hull vertices) stay the build's T and are
+// widened exactly; the contact leaves rounded to T.  MPR runs only in the full and wide tiers
+// (the compact tier hands any live convex pair over), so C3's compact kernel carries none of it.
 //
 // Wave-cooperative: the whole wave runs MPR on ONE pair (every lane holds the same portal, so
 // all branches are uniform) and splits each mesh support map over its 64 lanes.  Lane l keeps
@@ -346,15 +352,15 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
 // for the first vertex inside the tie band -- instead of 2 x nvert dependent global loads on a
 // single lane.
 constexpr int C_WV = 3;
+typedef double CT;   // MPR arithmetic (every build)
 template <typename T>
 struct CShape {
   int type, mesh, vadr, nvert;
-  T pos[3], R[9], size[3], margin;
-  T wv[C_WV][3];   // mesh: vertices lane + 64 j (local frame)
+  CT pos[3], R[9], size[3], margin;
+  T wv[C_WV][3];   // mesh: vertices lane + 64 j (local frame, the image's precision)
 };
-template <typename T>
 struct SVert {
-  T v[3], v1[3], v2[3];
+  CT v[3], v1[3], v2[3];
 };
 template <typename T> __device__ __forceinline__ T ccd_eps() { return PM<T>::eps(); }
 template <typename T> __device__ __forceinline__ bool ccd_zero(T x) { return fabs(x) < ccd_eps<T>(); }
@@ -401,21 +407,21 @@ __device__ void c_load_shape(const DevPhys<T>& /*image: phys<T>()*/, CShape<T>& 
 }
 // first vertex within the tie band of the maximum (oracle/convex.c support), wave-cooperative
 template <typename T>
-__device__ int c_mesh_argmax(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& s, const T* ld) {
+__device__ int c_mesh_argmax(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& s, const CT* ld) {
   const DevPhys<T>& m = phys<T>();
   const int l = threadIdx.x & 63, n = s.nvert;
-  T dv[C_WV], bd = T(-1e30);
+  CT dv[C_WV], bd = CT(-1e30);
 #pragma unroll
   for (int j = 0; j < C_WV; j++) {
-    dv[j] = 64 * j + l < n ? s.wv[j][0] * ld[0] + s.wv[j][1] * ld[1] + s.wv[j][2] * ld[2] : T(-1e30);
+    dv[j] = 64 * j + l < n ? CT(s.wv[j][0]) * ld[0] + CT(s.wv[j][1]) * ld[1] + CT(s.wv[j][2]) * ld[2] : CT(-1e30);
     bd = fmax(bd, dv[j]);
   }
   for (int i = 64 * C_WV + l; i < n; i += 64) {
     const T* V = m.mesh_vert[s.vadr + i];
-    bd = fmax(bd, V[0] * ld[0] + V[1] * ld[1] + V[2] * ld[2]);
+    bd = fmax(bd, CT(V[0]) * ld[0] + CT(V[1]) * ld[1] + CT(V[2]) * ld[2]);
   }
   bd = c_wave_max(bd);
-  const T lo = bd - T(1e-9);
+  const CT lo = bd - CT(1e-9);
 #pragma unroll
   for (int j = 0; j < C_WV; j++) {
     const uint64_t b = __ballot(64 * j + l < n && dv[j] >= lo);
@@ -426,7 +432,7 @@ __device__ int c_mesh_argmax(const DevPhys<T>& /*image: phys<T>()*/, const CShap
     bool ok = false;
     if (i < n) {
       const T* V = m.mesh_vert[s.vadr + i];
-      ok = V[0] * ld[0] + V[1] * ld[1] + V[2] * ld[2] >= lo;
+      ok = CT(V[0]) * ld[0] + CT(V[1]) * ld[1] + CT(V[2]) * ld[2] >= lo;
     }
     const uint64_t b = __ballot(ok);
     if (b) return base + __ffsll((unsigned long long)b) - 1;
@@ -434,50 +440,47 @@ __device__ int c_mesh_argmax(const DevPhys<T>& /*image: phys<T>()*/, const CShap
   return 0;
 }
 template <typename T>
-__device__ void c_support(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& s, const T* d, T* out) {
+__device__ void c_support(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& s, const CT* d, CT* out) {
   const DevPhys<T>& m = phys<T>();
-  T ld[3];
+  CT ld[3];
   for (int k = 0; k < 3; k++) ld[k] = s.R[k] * d[0] + s.R[3 + k] * d[1] + s.R[6 + k] * d[2];
-  T lp[3];
+  CT lp[3];
   if (s.type == 2) {
     for (int k = 0; k < 3; k++) lp[k] = ld[k] * s.size[0];
   } else if (s.type == 6) {
-    for (int k = 0; k < 3; k++) lp[k] = ld[k] >= T(-1e-12) ? s.size[k] : -s.size[k];
+    for (int k = 0; k < 3; k++) lp[k] = ld[k] >= CT(-1e-12) ? s.size[k] : -s.size[k];
   } else {
     const T* V = m.mesh_vert[s.vadr + c_mesh_argmax(m, s, ld)];
     lp[0] = V[0]; lp[1] = V[1]; lp[2] = V[2];
   }
   for (int k = 0; k < 3; k++)
-    out[k] = s.pos[k] + s.R[3 * k] * lp[0] + s.R[3 * k + 1] * lp[1] + s.R[3 * k + 2] * lp[2] + T(0.5) * s.margin * d[k];
+    out[k] = s.pos[k] + s.R[3 * k] * lp[0] + s.R[3 * k + 1] * lp[1] + s.R[3 * k + 2] * lp[2] + CT(0.5) * s.margin * d[k];
 }
 template <typename T>
-__device__ __forceinline__ void c_mksupport(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& a, const CShape<T>& b, const T* d, SVert<T>& v) {
+__device__ __forceinline__ void c_mksupport(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& a, const CShape<T>& b, const CT* d, SVert& v) {
   const DevPhys<T>& m = phys<T>();
-  const T nd[3] = {-d[0], -d[1], -d[2]};
+  const CT nd[3] = {-d[0], -d[1], -d[2]};
   c_support(m, a, d, v.v1);
   c_support(m, b, nd, v.v2);
   cs3(v.v, v.v1, v.v2);
 }
-template <typename T>
-__device__ __forceinline__ void c_portal_dir(const SVert<T>& p1, const SVert<T>& p2, const SVert<T>& p3, T* dir) {
-  T a[3], b[3];
+__device__ __forceinline__ void c_portal_dir(const SVert& p1, const SVert& p2, const SVert& p3, CT* dir) {
+  CT a[3], b[3];
   cs3(a, p2.v, p1.v);
   cs3(b, p3.v, p1.v);
   cc3(dir, a, b);
   cnorm(dir);
 }
-template <typename T>
-__device__ __forceinline__ bool c_reach_tol(const SVert<T>& p1, const SVert<T>& p2, const SVert<T>& p3, const SVert<T>& v4,
-                                            const T* dir, T tol) {
-  const T dv4 = cd3(v4.v, dir);
-  T t1 = dv4 - cd3(p1.v, dir), t2 = dv4 - cd3(p2.v, dir), t3 = dv4 - cd3(p3.v, dir);
+__device__ __forceinline__ bool c_reach_tol(const SVert& p1, const SVert& p2, const SVert& p3, const SVert& v4,
+                                            const CT* dir, CT tol) {
+  const CT dv4 = cd3(v4.v, dir);
+  CT t1 = dv4 - cd3(p1.v, dir), t2 = dv4 - cd3(p2.v, dir), t3 = dv4 - cd3(p3.v, dir);
   t1 = t1 < t2 ? t1 : t2;
   t1 = t1 < t3 ? t1 : t3;
   return ccd_eq(t1, tol) || t1 < tol;
 }
-template <typename T>
-__device__ __forceinline__ void c_expand(SVert<T>& p0, SVert<T>& p1, SVert<T>& p2, SVert<T>& p3, const SVert<T>& v4) {
-  T v4v0[3];
+__device__ __forceinline__ void c_expand(SVert& p0, SVert& p1, SVert& p2, SVert& p3, const SVert& v4) {
+  CT v4v0[3];
   cc3(v4v0, v4.v, p0.v);
   if (cd3(p1.v, v4v0) > 0) {
     if (cd3(p2.v, v4v0) > 0) p1 = v4;
@@ -537,15 +540,15 @@ __device__ T c_tri_dist2(const T* P, const T* x0, const T* B, const T* C, T* w) 
 
 // ccdMPRPenetration: true and (depth, dir, pos) on intersection
 template <typename T>
-__device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A, const CShape<T>& Bs, T& depth, T* dir, T* pos) {
+__device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A, const CShape<T>& Bs, CT& depth, CT* dir, CT* pos) {
   const DevPhys<T>& m = phys<T>();
-  const T tol = T(1e-6);   // mjOption mpr_tolerance
-  SVert<T> p0, p1, p2, p3, v4;
-  T d[3], va[3], vb[3], dot;
+  const CT tol = CT(1e-6);   // mjOption mpr_tolerance
+  SVert p0, p1, p2, p3, v4;
+  CT d[3], va[3], vb[3], dot;
   // ---- discover portal
   for (int k = 0; k < 3; k++) { p0.v1[k] = A.pos[k]; p0.v2[k] = Bs.pos[k]; }
   cs3(p0.v, p0.v1, p0.v2);
-  if (p0.v[0] == 0 && p0.v[1] == 0 && p0.v[2] == 0) p0.v[0] += ccd_eps<T>() * T(10);
+  if (p0.v[0] == 0 && p0.v[1] == 0 && p0.v[2] == 0) p0.v[0] += ccd_eps<CT>() * CT(10);
   d[0] = -p0.v[0]; d[1] = -p0.v[1]; d[2] = -p0.v[2];
   cnorm(d);
   c_mksupport(m, A, Bs, d, p1);
@@ -553,14 +556,14 @@ __device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A
   if (ccd_zero(dot) || dot < 0) return false;
   cc3(d, p0.v, p1.v);
   if (ccd_zero(cd3(d, d))) {
-    for (int k = 0; k < 3; k++) pos[k] = T(0.5) * (p1.v1[k] + p1.v2[k]);
+    for (int k = 0; k < 3; k++) pos[k] = CT(0.5) * (p1.v1[k] + p1.v2[k]);
     if (p1.v[0] == 0 && p1.v[1] == 0 && p1.v[2] == 0) {   // touching on v1
       depth = 0;
       dir[0] = dir[1] = dir[2] = 0;
       return true;
     }
     for (int k = 0; k < 3; k++) dir[k] = p1.v[k];          // origin on the segment v0-v1
-    depth = PM<T>::sqrt_(cd3(dir, dir));
+    depth = PM<CT>::sqrt_(cd3(dir, dir));
     cnorm(dir);
     return true;
   }
@@ -573,7 +576,7 @@ __device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A
   cc3(d, va, vb);
   cnorm(d);
   if (cd3(d, p0.v) > 0) {
-    const SVert<T> t = p1;
+    const SVert t = p1;
     p1 = p2;
     p2 = t;
     d[0] = -d[0]; d[1] = -d[1]; d[2] = -d[2];
@@ -619,18 +622,18 @@ __device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A
     c_portal_dir(p1, p2, p3, d);
     c_mksupport(m, A, Bs, d, v4);
     if (c_reach_tol(p1, p2, p3, v4, d, tol) || it > 50) {
-      const T O[3] = {0, 0, 0};
-      depth = PM<T>::sqrt_(c_tri_dist2(O, p1.v, p2.v, p3.v, dir));
+      const CT O[3] = {0, 0, 0};
+      depth = PM<CT>::sqrt_(c_tri_dist2(O, p1.v, p2.v, p3.v, dir));
       if (ccd_zero(depth)) dir[0] = dir[1] = dir[2] = 0;
       else cnorm(dir);
       // contact position: barycentric mix of the supports (findPos)
-      T vec[3], b0, b1, b2, b3;
+      CT vec[3], b0, b1, b2, b3;
       c_portal_dir(p1, p2, p3, d);
       cc3(vec, p1.v, p2.v); b0 = cd3(vec, p3.v);
       cc3(vec, p3.v, p2.v); b1 = cd3(vec, p0.v);
       cc3(vec, p0.v, p1.v); b2 = cd3(vec, p3.v);
       cc3(vec, p2.v, p1.v); b3 = cd3(vec, p0.v);
-      T sum = b0 + b1 + b2 + b3;
+      CT sum = b0 + b1 + b2 + b3;
       if (ccd_zero(sum) || sum < 0) {
         b0 = 0;
         cc3(vec, p2.v, p3.v); b1 = cd3(vec, d);
@@ -638,11 +641,11 @@ __device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A
         cc3(vec, p1.v, p2.v); b3 = cd3(vec, d);
         sum = b1 + b2 + b3;
       }
-      const T inv = T(1) / sum;
+      const CT inv = CT(1) / sum;
       for (int k = 0; k < 3; k++) {
-        const T q1 = b0 * p0.v1[k] + b1 * p1.v1[k] + b2 * p2.v1[k] + b3 * p3.v1[k];
-        const T q2 = b0 * p0.v2[k] + b1 * p1.v2[k] + b2 * p2.v2[k] + b3 * p3.v2[k];
-        pos[k] = T(0.5) * (q1 * inv + q2 * inv);
+        const CT q1 = b0 * p0.v1[k] + b1 * p1.v1[k] + b2 * p2.v1[k] + b3 * p3.v1[k];
+        const CT q2 = b0 * p0.v2[k] + b1 * p1.v2[k] + b2 * p2.v2[k] + b3 * p3.v2[k];
+        pos[k] = CT(0.5) * (q1 * inv + q2 * inv);
       }
       return true;
     }
@@ -788,18 +791,18 @@ template <typename T>
 __device__ __forceinline__ bool c_mpr_contact(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>* sh, T margin,
                                               T* c) {
   const DevPhys<T>& m = phys<T>();
-  T depth, nrm[3], pos[3];
+  CT depth, nrm[3], pos[3];
   if (!c_mpr(m, sh[0], sh[1], depth, nrm, pos)) return false;
   if (nrm[0] == 0 && nrm[1] == 0 && nrm[2] == 0) return false;   // normal undefined
   if (sh[0].type == 2) {   // mjc_fixNormal: the sphere's normal at the contact point (g1 of its pairs)
-    T n[3];
+    CT n[3];
     cs3(n, pos, sh[0].pos);
-    const T len = PM<T>::sqrt_(cd3(n, n));
-    if (len < T(1e-15)) { nrm[0] = 1; nrm[1] = 0; nrm[2] = 0; }
+    const CT len = PM<CT>::sqrt_(cd3(n, n));
+    if (len < CT(1e-15)) { nrm[0] = 1; nrm[1] = 0; nrm[2] = 0; }
     else { nrm[0] = n[0] / len; nrm[1] = n[1] / len; nrm[2] = n[2] / len; }
   }
-  c[0] = margin - depth;
-  for (int k = 0; k < 3; k++) { c[1 + k] = pos[k]; c[4 + k] = nrm[k]; }
+  c[0] = T(CT(margin) - depth);
+  for (int k = 0; k < 3; k++) { c[1 + k] = T(pos[k]); c[4 + k] = T(nrm[k]); }
   return true;
 }
 // the pair's two shapes, origin at geom 1's centre (oracle/convex.c): centimetre-scale support
@@ -815,26 +818,28 @@ __device__ __forceinline__ void c_convex_shapes(const DevPhys<T>& /*image: phys<
     sh[i].type = m.geom_type[g];
     sh[i].mesh = m.geom_dataid[g];
     sh[i].margin = margin;
-    for (int k = 0; k < 3; k++) { sh[i].pos[k] = s.gpos[g][k] - s.gpos[g1][k]; sh[i].size[k] = m.geom_size[g][k]; }
+    for (int k = 0; k < 3; k++) { sh[i].pos[k] = CT(s.gpos[g][k]) - CT(s.gpos[g1][k]); sh[i].size[k] = m.geom_size[g][k]; }
     for (int k = 0; k < 9; k++) sh[i].R[k] = s.gmat[g][k];
     c_load_shape(m, sh[i]);
   }
 }
-// multiccd trial t (0..3): geom 1 rotated by q, geom 2 by q^-1 about their centres, q the rotation
-// by a = -+1e-3 rad about the first contact's tangent axis t >> 1 (frame f = mju_makeFrame of its
+// multiccd trial t (0..3): geom 1 rotated by q, geom 2 by q^-1, both about the first contact's
+// position o (mjc_rotateFrame; an unverified assumption, oracle/convex.c), q the rotation by
+// a = -+1e-3 rad about the first contact's tangent axis t >> 1 (frame f = mju_makeFrame of its
 // normal): q = (cos(a/2), axis sin(a/2)) (oracle: sp_axisangle2quat), R(q^-1) = R(q)^T.  Ra, Rb:
-// the unperturbed frames (the Env's geom frames: nothing extra held in registers across MPR).
+// the unperturbed frames (the Env's geom frames: nothing extra held in registers across MPR);
+// sh[].pos holds the unperturbed centres on entry.
 // (One function for the serial and the multi-wave convex passes: same bits.)
 template <typename T>
-__device__ __forceinline__ void c_fan_rotate(CShape<T>* sh, const T* Ra, const T* Rb, const T* f, int t) {
+__device__ __forceinline__ void c_fan_rotate(CShape<T>* sh, const T* Ra, const T* Rb, const CT* f, const CT* o, int t) {
   const bool second = (t >> 1) != 0;   // (selects, not an index: f stays in registers)
-  const T ax[3] = {second ? f[6] : f[3], second ? f[7] : f[4], second ? f[8] : f[5]};
-  const T sh_ = (t & 1) ? T(0.0004999999791666669) : T(-0.0004999999791666669), q0 = T(0.9999998750000026);
-  const T q[4] = {q0, ax[0] * sh_, ax[1] * sh_, ax[2] * sh_};
-  T Rq[9];
-  const T q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
-  const T q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
-  const T q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
+  const CT ax[3] = {second ? f[6] : f[3], second ? f[7] : f[4], second ? f[8] : f[5]};
+  const CT sh_ = (t & 1) ? CT(0.0004999999791666669) : CT(-0.0004999999791666669), q0 = CT(0.9999998750000026);
+  const CT q[4] = {q0, ax[0] * sh_, ax[1] * sh_, ax[2] * sh_};
+  CT Rq[9];
+  const CT q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
+  const CT q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
+  const CT q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
   Rq[0] = q00 + q11 - q22 - q33; Rq[4] = q00 - q11 + q22 - q33; Rq[8] = q00 - q11 - q22 + q33;
   Rq[1] = 2 * (q12 - q03); Rq[2] = 2 * (q13 + q02); Rq[3] = 2 * (q12 + q03);
   Rq[5] = 2 * (q23 - q01); Rq[6] = 2 * (q13 - q02); Rq[7] = 2 * (q23 + q01);
@@ -842,13 +847,21 @@ __device__ __forceinline__ void c_fan_rotate(CShape<T>* sh, const T* Ra, const T
   for (int i = 0; i < 3; i++)
 #pragma unroll
     for (int j = 0; j < 3; j++) {
-      sh[0].R[3 * i + j] = Rq[3 * i] * Ra[j] + Rq[3 * i + 1] * Ra[3 + j] + Rq[3 * i + 2] * Ra[6 + j];
-      sh[1].R[3 * i + j] = Rq[i] * Rb[j] + Rq[3 + i] * Rb[3 + j] + Rq[6 + i] * Rb[6 + j];
+      sh[0].R[3 * i + j] = Rq[3 * i] * CT(Ra[j]) + Rq[3 * i + 1] * CT(Ra[3 + j]) + Rq[3 * i + 2] * CT(Ra[6 + j]);
+      sh[1].R[3 * i + j] = Rq[i] * CT(Rb[j]) + Rq[3 + i] * CT(Rb[3 + j]) + Rq[6 + i] * CT(Rb[6 + j]);
     }
+  CT r0[3], r1[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) { r0[k] = sh[0].pos[k] - o[k]; r1[k] = sh[1].pos[k] - o[k]; }
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    sh[0].pos[k] = o[k] + (Rq[3 * k] * r0[0] + Rq[3 * k + 1] * r0[1] + Rq[3 * k + 2] * r0[2]);
+    sh[1].pos[k] = o[k] + (Rq[k] * r1[0] + Rq[3 + k] * r1[1] + Rq[6 + k] * r1[2]);
+  }
 }
 // the perturbation frame from the first contact's normal n0
 template <typename T>
-__device__ __forceinline__ void c_fan_frame(const T* n0, T* f) {
+__device__ __forceinline__ void c_fan_frame(const T* n0, CT* f) {
   f[0] = n0[0]; f[1] = n0[1]; f[2] = n0[2];
   for (int k = 3; k < 9; k++) f[k] = 0;
   t_makeframe(f);
@@ -870,7 +883,7 @@ __device__ __forceinline__ bool c_fan_close(const T* a, const T* b, T tol) {
 // the first run and the trials at two call sites, the convex stage's spills grew the compact
 // build's scratch 304 -> 896 B per lane and cost C3 2 % although C3 never runs the stage (392 B and
 // -1.0 % with one).  The serial and the multi-wave convex passes both call it: the same bits.
-#if PNP_WIDE
+#if PNP_MW
 #define C_RUN_INLINE __attribute__((noinline))   // two call sites (serial and multi-wave passes)
 #else
 #define C_RUN_INLINE __forceinline__              // one call site (c_convex's loop)
@@ -881,9 +894,10 @@ __device__ C_RUN_INLINE bool c_convex_run(const Env<T>& s, int g1, int g2, T mar
   CShape<T> sh[2];
   c_convex_shapes(m, s, g1, g2, margin, sh);
   if (t >= 0) {
-    T f[9];
+    CT f[9];
     c_fan_frame(val[0] + 4, f);
-    c_fan_rotate(sh, s.gmat[g1], s.gmat[g2], f, t);
+    const CT o[3] = {CT(val[0][1]), CT(val[0][2]), CT(val[0][3])};   // first contact (geom-1-centred)
+    c_fan_rotate(sh, s.gmat[g1], s.gmat[g2], f, o, t);
   }
   T c[7];
   const bool hit = c_mpr_contact(m, sh, margin, c);
@@ -896,7 +910,9 @@ __device__ __forceinline__ int c_convex(const DevPhys<T>& /*image: phys<T>()*/, 
                                         T (*val)[7]) {
   const DevPhys<T>& m = phys<T>();
   const int l = threadIdx.x & 63;
-  const int trips = (!PNP_COMPACT && m.multiccd) ? 4 : 0;   // (the compact build hands fans over: step.hip)
+  // (the compact build runs no MPR: step.hip); smooth geoms (the sphere, always g1 of its pairs) make
+  // no fan (oracle/convex.c mpr_fan)
+  const int trips = (!PNP_COMPACT && m.multiccd && m.geom_type[g1] != 2 && m.geom_type[g2] != 2) ? 4 : 0;
   int n = 0;
   for (int t = -1; t < trips; t++) {   // t = -1: the first run; then the multiccd trials
     wsync();

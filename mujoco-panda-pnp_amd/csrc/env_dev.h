@@ -393,8 +393,9 @@ __device__ __forceinline__ int tier_need(const DevPhys<T>& m, const Env<T>& s) {
   const int l = lane_id();
   const bool big = __ballot(l < nis && s.isl_roff[l + 1] - s.isl_roff[l] > PNP_BIG_ROWS - 4) != 0;
   const int jt = nis ? s.isl_joff[nis] : 0, he = nis ? s.isl_eoff[nis] : 0;
+  // (the compact tier runs no MPR: an env with a live convex pair starts in the full tier)
   if (5 * nc <= 4 * PNP_GC_MAXCON && 5 * ne <= 4 * PNP_GC_MAXEFC && 5 * slots <= 4 * PNP_GC_MAXJSLOT && !big &&
-      5 * jt <= 4 * PNP_GC_JTCAP && 5 * he <= 4 * PNP_GC_HCAP)
+      5 * jt <= 4 * PNP_GC_JTCAP && 5 * he <= 4 * PNP_GC_HCAP && s.nconvex == 0)
     return 0;
   if (6 * nc <= 5 * PNP_GF_MAXCON && 6 * ne <= 5 * PNP_GF_MAXEFC && 6 * slots <= 5 * PNP_GF_MAXJSLOT &&
       6 * jt <= 5 * PNP_GF_JTCAP)

@@ -33,7 +33,8 @@ int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
   }
   for (int g = 0; g < s->ngeom; g++)
     if (s->geom_bodyid[g] < 0 || s->geom_bodyid[g] >= s->nbody ||
-        ((s->geom_contype[g] || s->geom_conaffinity[g]) && s->geom_type[g] == 7 && s->geom_dataid[g] >= s->nmesh)) {
+        ((s->geom_contype[g] || s->geom_conaffinity[g]) && s->geom_type[g] == 7 &&
+         (s->geom_dataid[g] < 0 || s->geom_dataid[g] >= s->nmesh))) {
       snprintf(err, errlen, "geom %d: body or mesh id out of range", g);
       return -1;
     }
@@ -43,17 +44,29 @@ int build_phys(const pnp_model_desc* s, DevPhys<T>* d, char* err, int errlen) {
       snprintf(err, errlen, "body %d: parent / joint / dof ids out of range", b);
       return -1;
     }
-  for (int j = 0; j < s->njnt; j++)
-    if (s->jnt_qposadr[j] < 0 || s->jnt_qposadr[j] >= s->nq || s->jnt_dofadr[j] < 0 || s->jnt_dofadr[j] >= s->nv) {
+  for (int j = 0; j < s->njnt; j++) {
+    // qpos / dof widths of the joint type (mjtJoint: free 7 / 6, ball 4 / 3, slide and hinge 1 / 1)
+    const int t = s->jnt_type[j];
+    const int nqj = t == 0 ? 7 : (t == 1 ? 4 : 1), nvj = t == 0 ? 6 : (t == 1 ? 3 : 1);
+    if (t < 0 || t > 3 || s->jnt_qposadr[j] < 0 || s->jnt_qposadr[j] + nqj > s->nq || s->jnt_dofadr[j] < 0 ||
+        s->jnt_dofadr[j] + nvj > s->nv) {
       snprintf(err, errlen, "joint %d: qpos / dof address out of range", j);
       return -1;
     }
+  }
   d->nq = s->nq; d->nv = s->nv; d->nu = s->nu; d->nbody = s->nbody; d->njnt = s->njnt;
   d->nmocap = s->nmocap; d->neq = s->neq;
   d->timestep = (T)s->timestep;
   for (int k = 0; k < 3; k++) d->gravity[k] = (T)s->gravity[k];
   d->noslip_iterations = s->noslip_iterations;
   d->iterations = s->iterations;
+  d->tolerance = (T)s->tolerance;
+  d->noslip_tolerance = (T)s->noslip_tolerance;
+  d->meaninertia = (T)s->stat_meaninertia;
+  if (!(s->stat_meaninertia > 0)) {
+    snprintf(err, errlen, "stat_meaninertia must be > 0 (mj_setConst: mean of diag(M) at qpos0)");
+    return -1;
+  }
   d->multiccd = s->multiccd;
   // ---- bodies
   for (int b = 0; b < s->nbody; b++) {

@@ -54,6 +54,9 @@ struct DevPhys {
   int nq, nv, nu, nbody, njnt, ngeom, npair, nmocap, neq, ntree, nmentry;
   T timestep, gravity[3];
   int noslip_iterations, iterations;
+  // termination of mj_solNewton / mj_solNoSlip: mjOption tolerance / noslip_tolerance, both tested
+  // on values scaled by 1 / (stat.meaninertia * max(1, nv))
+  T tolerance, noslip_tolerance, meaninertia;
   // bodies
   int body_parentid[PH_MAXB], body_rootid[PH_MAXB], body_weldid[PH_MAXB], body_mocapid[PH_MAXB];
   int body_jntadr[PH_MAXB], body_jntnum[PH_MAXB], body_dofadr[PH_MAXB], body_dofnum[PH_MAXB];

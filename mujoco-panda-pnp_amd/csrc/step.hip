@@ -134,7 +134,7 @@ struct Env {
   T qpos[PH_MAXQ], qvel[PH_MAXV], ctrl[PH_MAXU], mocap_pos[6], mocap_quat[8], qacc_ws[PH_MAXV];
   T time;
   uint32_t warn;
-  int ncon, nefc, ne, nisland, solver_iter;
+  int ncon, nefc, ne, nisland, solver_iter, noslip_iter;
   int nlive, ncon_raw;     // collision: broadphase survivors, contacts before the capacity cap
   int nconvex;             // collision: live convex (MPR) pairs
   double wpose[2][7];      // fp32 builds: the first weld's two body poses in fp64 (pos, quat)
@@ -328,7 +328,7 @@ enum {
   SC_N_CONV, SC_N_HESS,
   SN_CON = 27, SN_EFC, SN_ITER, SN_CONVEX, SN_ISLAND, SN_NS_SWEEP, SN_LIVE,
   SC_AUX0 = 34,  // 8 ad-hoc sub-stage timers, SC_AUX0 .. SC_AUX0 + 7
-  SN_NS_DENSE = 42, SN_NS_STREAM
+  SN_NS_DENSE = 42, SN_NS_STREAM, SN_NS_ITER
 };
 
 // ============================================================================ small helpers
@@ -1406,9 +1406,14 @@ __device__ __attribute__((noinline)) void st_collision_convex_mw(Env<float>& s) 
     wsync();
     mw_run(s, MW_MPR | (n << 8));
     const bool first = l < n && s.mw_hit[per * l];
-    if (per > 1) {   // the trials of the pairs with a first contact
-      const uint64_t hb = __ballot(first);
-      if (first) s.mw_fan[__popcll(hb & ((1ull << l) - 1ull))] = (unsigned char)l;
+    if (per > 1) {   // the trials of the pairs with a first contact (no fan for a sphere: c_convex)
+      bool fan = first;
+      if (first) {
+        const int p = s.cst_key[l];
+        fan = m.geom_type[m.pair_g1[p]] != 2 && m.geom_type[m.pair_g2[p]] != 2;
+      }
+      const uint64_t hb = __ballot(fan);
+      if (fan) s.mw_fan[__popcll(hb & ((1ull << l) - 1ull))] = (unsigned char)l;
       wsync();
       const int nh = __popcll(hb);
       if (nh) mw_run(s, MW_FAN | ((4 * nh) << 8));
@@ -1480,18 +1485,6 @@ __device__ __attribute__((noinline)) void st_collision_convex(const DevPhys<T>& 
       const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
       // the pair's contacts (up to C_MULTI with multiccd) staged in cst_val, then lanes 0.. append
       const int n = c_convex(m, s, g1, g2, fmax(m.geom_margin[g1], m.geom_margin[g2]), s.cst_val);
-#if PNP_COMPACT
-      // The compact build carries no multiccd fan (c_convex stops after the first run): a convex
-      // pair in contact hands the sub-step to the full tier, like a capacity overflow.  The fan's
-      // code in this build grew its frames (forward 48 -> 64, the stage 180 -> 284 B per lane),
-      // its scratch footprint and write-back (PMC 760 -> 989 MB per launch), and cost C3 1 %,
-      // although C3's settled envs never make a convex contact.
-      if (n && m.multiccd) {
-        if (l == 0) CAP_FULL(8u);
-        wsync();
-        return;
-      }
-#endif
       if (l < n && ncon + l < PH_MAXCON) {
         const T pos[3] = {s.cst_val[l][1], s.cst_val[l][2], s.cst_val[l][3]};
         const T nrm[3] = {s.cst_val[l][4], s.cst_val[l][5], s.cst_val[l][6]};
@@ -2392,7 +2385,15 @@ __device__ __attribute__((noinline)) void island_newton_dir_wave(Env<T>& s, int 
 // rounding level of the step length (|a_new - a| <= 4 eps |a|) or its bracket has collapsed.
 // Islands with isl_flag set (done) keep a = 0.  Leaves the step lengths in s.isl_alpha.
 template <typename T, class CLK>
-__device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
+__device__ T line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
+  // MuJoCo 2.3.3 PrimalLineSearch: one step length for the whole problem (2.3.3 has no islands),
+  // along the Newton direction p of every island.  Its two early exits are kept: |p| < mjMINVAL,
+  // and phi'(0) >= -gtol with gtol = tolerance * ls_tolerance (0.01) * |p| / scale (p not a descent
+  // direction to within the tolerance); then the exact minimiser of the convex piecewise quadratic
+  // phi(a) = cost(x + a p) by Newton steps on phi' with bracketing (MuJoCo stops its own iterate at
+  // |phi'| < gtol; the exact minimiser is the oracle's).  Lane l holds rows l + 64 k
+  // (k < 2) in registers; larger row counts stream the rest from LDS (the wide tier's 200-700
+  // rows).  Returns the step (wave-uniform).
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
@@ -2400,119 +2401,76 @@ __device__ void line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, C
     s.efc_Jp[r] = row_dot(s, r, s.p, T(0));
   }
   wsync();
+  T pp = 0, A0 = 0, B0 = 0;
   if (l < m.nv) {
     const T mp = mulM_row(m, s, l, s.p);
-    s.v2[l] = mp * s.p[l];
-    s.grad[l] = mp * s.v1[l];   // the gradient is no longer needed this iteration
+    A0 = mp * s.p[l];
+    B0 = mp * s.v1[l];
+    pp = s.p[l] * s.p[l];
   }
-  wsync();
+  A0 = wsum(A0);
+  B0 = wsum(B0);
+  const T snorm = PM<T>::sqrt_(wsum(pp));
   clk.aux_lap(SC_AUX0 + 5);   // aux5: line search J p, M p
-  const int q = l & 7;
-  int itc = 0;   // bracketing iterations of the lane's island (stage profile count)
-  // Islands with more rows than a group's register cache (closed fingers pressed together put
-  // 200-400 rows on the arm island): bracketed on the whole wave, one after the other, each
-  // row read once per bracketing iteration by 64 lanes (the group path below would walk it 8
-  // rows at a time, ~35 dependent LDS rounds per iteration).  Same bracketing; the row sums
-  // reduce over 64 lanes instead of 8 (rounding only).
-  constexpr int RK = PNP_BIG_ROWS / 8;
-  const uint32_t big = PNP_BIG_ISLANDS ? (uint32_t)__ballot(l < s.nisland && !s.isl_flag[l] &&
-                                                            s.isl_roff[l + 1] - s.isl_roff[l] > 8 * RK)
-                                       : 0u;
-  for (uint32_t bm = big; bm; bm &= bm - 1) {
-    const int I = __builtin_ctz(bm);
-    const int n = s.isl_n[I];
-    const T A0 = wsum(l < n ? s.v2[s.isl_dof[I][l]] : T(0)), B0 = wsum(l < n ? s.grad[s.isl_dof[I][l]] : T(0));
-    const int r0 = s.isl_roff[I], r1 = s.isl_roff[I + 1];
-    T lo = 0, hi = T(-1), a = 1;
-    int it = 0;
-    for (; it < 60; it++) {
-      T d1 = 0, d2 = 0;
-      for (int rr = r0 + l; rr < r1; rr += NT) {
-        const int r = s.isl_row[rr];
-        const T jp = s.efc_Jp[r], v = s.efc_jar[r] + a * jp;
-        if (r < s.ne || v < 0) { d1 += s.efc_D[r] * v * jp; d2 += s.efc_D[r] * jp * jp; }
+  const int n = s.nefc, ne = s.ne;
+  T rjp[2], rjar[2], rD[2];
+  bool req[2], rin[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int r = l + NT * k;
+    rin[k] = r < n;
+    const int rc = rin[k] ? r : 0;
+    rjp[k] = s.efc_Jp[rc];
+    rjar[k] = s.efc_jar[rc];
+    rD[k] = s.efc_D[rc];
+    req[k] = r < ne;
+  }
+  // phi'(a) - (A0 a + B0) and phi''(a) - A0 over the rows active at a (equality rows always)
+  auto deriv = [&](T a, T& d1, T& d2) {
+    d1 = 0;
+    d2 = 0;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const T jp = rjp[k], v = rjar[k] + a * jp;
+      const bool on = rin[k] && (req[k] || v < 0);
+      d1 = on ? d1 + rD[k] * v * jp : d1;
+      d2 = on ? d2 + rD[k] * jp * jp : d2;
+    }
+    for (int r = l + 2 * NT; r < n; r += NT) {
+      const T jp = s.efc_Jp[r], v = s.efc_jar[r] + a * jp;
+      if (r < ne || v < 0) { d1 += s.efc_D[r] * v * jp; d2 += s.efc_D[r] * jp * jp; }
+    }
+    d1 = wsum(d1) + A0 * a + B0;
+    d2 = wsum(d2) + A0;
+  };
+  const T scale = T(1) / (m.meaninertia * T(m.nv > 1 ? m.nv : 1));
+  const T gtol = m.tolerance * T(0.01) * snorm / scale;
+  T a = 0;
+  int it = 0;
+  if (snorm >= T(1e-15)) {
+    T d1, d2;
+    deriv(T(0), d1, d2);
+    if (d1 < -gtol) {
+      T lo = 0, hi = T(-1);
+      a = 1;
+      for (; it < 60; it++) {
+        deriv(a, d1, d2);
+        if (!(d2 > T(0))) { a = 0; break; }
+        if (d1 == T(0)) break;
+        if (d1 > 0) hi = a; else lo = a;
+        T an = a - d1 / d2;
+        if (!(an > lo) || (hi >= T(0) && !(an < hi))) an = hi >= T(0) ? T(0.5) * (lo + hi) : T(2) * a;
+        // converged once the Newton step is at the rounding level of a (waiting for an == a bit
+        // for bit costs extra rounds of last-bit oscillation), or the bracket has collapsed
+        const bool fin = fabs(an - a) <= T(4) * PM<T>::eps() * fabs(a) || (hi >= T(0) && hi - lo <= PM<T>::eps() * hi);
+        a = an;
+        if (fin) break;
       }
-      d1 = wsum(d1) + A0 * a + B0;
-      d2 = wsum(d2) + A0;
-      if (!(d2 > T(0))) { a = 0; break; }
-      if (d1 == T(0)) break;
-      if (d1 > 0) hi = a; else lo = a;
-      T an = a - d1 / d2;
-      if (!(an > lo) || (hi >= T(0) && !(an < hi))) an = hi >= T(0) ? T(0.5) * (lo + hi) : T(2) * a;
-      const bool fin = fabs(an - a) <= T(4) * PM<T>::eps() * fabs(a) || (hi >= T(0) && hi - lo <= PM<T>::eps() * hi);
-      a = an;
-      if (fin) break;
     }
-    if (l == 0) s.isl_alpha[I] = a;
-    if ((l >> 3) == I) itc = it + 1;
   }
-  {
-    const int I = l >> 3;
-    if (I >= s.nisland || (big >> I & 1u)) goto ls_done;
-    if (s.isl_flag[I]) {
-      if (q == 0) s.isl_alpha[I] = 0;
-      goto ls_done;
-    }
-    const T A0 = group_sum(s, I, s.v2, (const T*)nullptr), B0 = group_sum(s, I, s.grad, (const T*)nullptr);
-    const int r0 = s.isl_roff[I], r1 = s.isl_roff[I + 1];
-    // the lane's rows (rr = r0 + q + 8 k) are fixed over the iterations: islands of up to 32
-    // rows keep (Jp, jar, D, equality) in registers (larger ones took the wave path above)
-    T rjp[RK], rjar[RK], rD[RK];
-    bool req[RK], rin[RK];
-#pragma unroll
-    for (int k = 0; k < RK; k++) {
-      const int rr = r0 + q + 8 * k;
-      rin[k] = rr < r1;
-      const int r = s.isl_row[rin[k] ? rr : r0];
-      rjp[k] = s.efc_Jp[r];
-      rjar[k] = s.efc_jar[r];
-      rD[k] = s.efc_D[r];
-      req[k] = r < s.ne;
-    }
-    const bool small = r1 - r0 <= 8 * RK;
-    T lo = 0, hi = T(-1), a = 1;
-    for (int it = 0; it < 60; it++) {
-      itc++;
-      T d1 = 0, d2 = 0;
-      if (small) {
-#pragma unroll
-        for (int k = 0; k < RK; k++) {
-          const T jp = rjp[k], v = rjar[k] + a * jp;
-          const bool on = rin[k] && (req[k] || v < 0);
-          d1 = on ? d1 + rD[k] * v * jp : d1;
-          d2 = on ? d2 + rD[k] * jp * jp : d2;
-        }
-      } else {
-        for (int rr = r0 + q; rr < r1; rr += 8) {
-          const int r = s.isl_row[rr];
-          const T jp = s.efc_Jp[r], v = s.efc_jar[r] + a * jp;
-          if (r < s.ne || v < 0) { d1 += s.efc_D[r] * v * jp; d2 += s.efc_D[r] * jp * jp; }
-        }
-      }
-      d1 = rowsum8(d1) + A0 * a + B0;
-      d2 = rowsum8(d2) + A0;
-      if (!(d2 > T(0))) { a = 0; break; }
-      if (d1 == T(0)) break;
-      if (d1 > 0) hi = a; else lo = a;
-      T an = a - d1 / d2;
-      if (!(an > lo) || (hi >= T(0) && !(an < hi))) an = hi >= T(0) ? T(0.5) * (lo + hi) : T(2) * a;
-      // converged once the Newton step is at the rounding level of a (waiting for an == a bit
-      // for bit cost extra rounds of last-bit oscillation), or the bracket has collapsed
-      const bool fin = fabs(an - a) <= T(4) * PM<T>::eps() * fabs(a) || (hi >= T(0) && hi - lo <= PM<T>::eps() * hi);
-      a = an;
-      if (fin) break;
-    }
-    if (q == 0) s.isl_alpha[I] = a;
-  }
-ls_done:
-  wsync();
-  clk.aux_lap(SC_AUX0 + 6);   // aux6: line search bracketing per island
-  {
-    int mx = 0;
-#pragma unroll
-    for (int g = 0; g < 8; g++) mx = max(mx, __builtin_amdgcn_readlane(itc, 8 * g));
-    clk.count(SC_AUX0 + 7, mx);   // aux7: line-search bracketing iterations (max over islands)
-  }
+  clk.aux_lap(SC_AUX0 + 6);   // aux6: line search bracketing
+  clk.count(SC_AUX0 + 7, it + 1);   // aux7: line-search bracketing iterations
+  return a;
 }
 
 // Newton direction of every island on its own 9-lane group (see st_newton); out of line so that
@@ -2628,10 +2586,12 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   clk.aux_start();
   build_islands(m, s, clk);
   if (PNP_HANDS && s.ovf) return;
-  // warm start per island: the better of qacc_warmstart and qacc_smooth (MuJoCo chooses for the
-  // whole problem; per island the minimiser is the same and the start is better).  One pass:
-  // cost(qacc_smooth) has no dof term and its jar is efc_bb (= J qacc_smooth - aref, same
-  // arithmetic), and the chosen start's jar / active set are kept instead of re-evaluated.
+  // warm start (mj_fwdConstraint): qacc_warmstart unless its cost exceeds qacc_smooth's, for the
+  // whole problem.  One pass: cost(qacc_smooth) has no dof term and its jar is efc_bb (= J
+  // qacc_smooth - aref, same arithmetic), and the chosen start's jar / active set are kept instead
+  // of re-evaluated.  The costs are kept per island (island I's dofs and rows; they sum to the
+  // problem's cost): the improvement test below sums per-island differences, so a small island's
+  // progress does not cancel against the arm's cost in fp32.
   if (l < m.nv) s.v1[l] = s.qacc_ws[l] - s.qacc_smooth[l];
   wsync();
   if (l < m.nv) s.v2[l] = T(0.5) * s.v1[l] * mulM_row(m, s, l, s.v1);
@@ -2644,38 +2604,41 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   }
   wsync();
   island_sums2(s, s.v2, s.ntmp, s.isl_val, s.efc_Jp, s.isl_cost);
+  const int nisl = s.nisland;
+  const bool ws = !(wsum(l < nisl ? s.isl_val[l] : T(0)) > wsum(l < nisl ? s.isl_cost[l] : T(0)));
   if (l < PH_MAXT) {
-    const bool ws = l < s.nisland && s.isl_val[l] < s.isl_cost[l];
-    s.isl_alpha[l] = ws ? T(1) : T(0);
-    if (ws) s.isl_cost[l] = s.isl_val[l];
+    if (ws && l < nisl) s.isl_cost[l] = s.isl_val[l];
     s.isl_flag[l] = 0;
     s.isl_hvalid[l] = 0;
   }
   wsync();
-  if (l < m.nv) s.x[l] = s.isl_alpha[s.tree_island[s.c_dof_tree[l]]] != T(0) ? s.qacc_ws[l] : s.qacc_smooth[l];
+  if (l < m.nv) s.x[l] = ws ? s.qacc_ws[l] : s.qacc_smooth[l];
   for (int r = l; r < s.nefc; r += NT) {
-    const T v = s.isl_alpha[s.tree_island[s.efc_t0[r]]] != T(0) ? s.efc_jar[r] : s.efc_bb[r];
+    const T v = ws ? s.efc_jar[r] : s.efc_bb[r];
     s.efc_jar[r] = v;
     s.efc_act[r] = r < s.ne || v < 0;
   }
   wsync();
   clk.lap(8);
-  // lane I (< nisland) keeps island I's convergence state
-  T cost = l < s.nisland ? s.isl_cost[l] : T(0);
-  bool done = l >= s.nisland;
-  int unchanged = 0;                      // consecutive steps that kept the island's active set
-  // gradient floor of a converged island, scaled like the oracle: 1 / (meaninertia * nv) with
-  // meaninertia = mean of diag(M) of this step
-  const T meaninertia = wsum(l < m.nv ? s.M[mblk(m, l, l)] : T(0)) / T(m.nv);
-  const T gscale = T(1) / (meaninertia * T(m.nv > 1 ? m.nv : 1));
-  const T gtol = T(100) * PM<T>::eps();
+  // MuJoCo 2.3.3 mj_solNewton's iteration and exits (oracle/physics.c solve_newton): direction
+  // -H^-1 g per island (H is block-diagonal over islands, so this is the problem's Newton
+  // direction), one line search for the whole problem, stop at a zero step, then after each step
+  // once scale (cost_old - cost) < tolerance or scale |g| < tolerance (scale = 1 / (meaninertia
+  // nv), the model statistic), or after `iterations` steps.  fp32 cannot resolve tolerance 1e-8
+  // in these sums, so the fp32 builds also stop at the rounding floor: the last step kept the
+  // active set (x at that quadratic's minimiser) and the scaled gradient is at fp32 rounding, or two
+  // steps in a row kept it.
+  T cost = l < nisl ? s.isl_cost[l] : T(0);   // lane I: island I's cost
+  const bool idle = l >= nisl;                 // lane I: no island I
+  int unchanged = 0;                           // consecutive steps that kept the active set
+  const T scale = T(1) / (m.meaninertia * T(m.nv > 1 ? m.nv : 1));
+  T improvement = 0;
   int it = 0;
   const int nent = s.isl_eoff[s.nisland];
   const bool jt = s.jt_ok;
   // group-parallel island factorisation when every island fits a 9-lane group
   const bool gch = s.nisland <= GCH_GROUPS && !__ballot(l < s.nisland && s.isl_n[l] > GCH_N);
-  const int nisl = s.nisland;
-  for (; it < m.iterations; it++) {
+  for (;;) {
     clk.sub_start();
     // gradient g = M (x - x_smooth) + J^T (D jar) over the dof's island rows
     if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
@@ -2714,6 +2677,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       }
       wsync();
     }
+    T g2 = 0;
     if (l < m.nv) {
       const int t = s.c_dof_tree[l], I = s.tree_island[t];
       const T mv = mulM_row(m, s, l, s.v1);
@@ -2721,27 +2685,26 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
                 : jt ? jt_dof_sum(s, I, s.dof_ipos[l], mv, s.rr_f)
                      : dof_row_sum(mv, s, I, t, l - s.c_tree_dofadr[t], s.efc_D, s.efc_jar, true);
       s.grad[l] = g;
-      s.v2[l] = g * g;
+      g2 = g * g;
     }
     wsync();
     clk.sub_lap(SC_N_GRAD);
-    // an island whose last step kept its active set is at that quadratic's minimiser up to the
-    // rounding of one Cholesky solve (cond(H) eps): done once its gradient is at the floor,
-    // otherwise it takes one more (refining) Newton step
-    island_sums(s, s.v2, (const T*)nullptr, s.isl_val);
-    if (!done && unchanged >= 1 && PM<T>::sqrt_(s.isl_val[l]) * gscale < gtol) done = true;
-    if (l < PH_MAXT) s.isl_flag[l] = done;
-    wsync();
+    if (it > 0) {
+      const T gradient = scale * PM<T>::sqrt_(wsum(g2));
+      bool stop = improvement < m.tolerance || gradient < m.tolerance;
+      if constexpr (sizeof(T) == 4) stop = stop || (unchanged >= 1 && gradient < T(100) * PM<T>::eps());
+      if (stop) { clk.sub_lap(SC_N_CONV); clk.lap(9); break; }
+    }
     clk.sub_lap(SC_N_CONV);
-    if (!__ballot(!done)) { clk.lap(9); break; }
+    if (it >= m.iterations) { clk.lap(9); break; }
     // Hessian island blocks (lower triangle, lane per entry): M + sum_active D J J^T; blocks of
     // islands whose active set is unchanged since their last assembly are reused as they are;
     // fp32 islands with many rows on the matrix cores (hess_mfma)
     uint32_t bigh = 0;
     if constexpr (sizeof(T) == 4 && PNP_BIG_ISLANDS) {
       if (jt)
-        bigh = (uint32_t)__ballot(l < nisl && !s.isl_flag[l] && !s.isl_hvalid[l] &&
-                                  s.isl_roff[l + 1] - s.isl_roff[l] > NT && s.isl_n[l] <= 16);
+        bigh = (uint32_t)__ballot(l < nisl && !s.isl_hvalid[l] && s.isl_roff[l + 1] - s.isl_roff[l] > NT &&
+                                  s.isl_n[l] <= 16);
       for (uint32_t bm = bigh; bm; bm &= bm - 1) hess_mfma(s, __builtin_ctz(bm));
     }
     for (int e = l; e < nent; e += NT) {
@@ -2752,7 +2715,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       for (int J = 1; J <= PH_MAXT; J++) I += J < nisl && e >= s.isl_eoff[J] ? 1 : 0;
       const int eI = s.isl_eoff[I], nI = s.isl_n[I], r0I = s.isl_roff[I], e1I = s.isl_roff[I + 1],
                 joI = s.isl_joff[I];
-      if (s.isl_flag[I] || s.isl_hvalid[I] || (bigh >> I & 1u)) continue;
+      if (s.isl_hvalid[I] || (bigh >> I & 1u)) continue;
       const int le = e - eI;
       int a = (int)((PM<float>::sqrt_(8.0f * le + 1.0f) - 1.0f) * 0.5f);
       while (a * (a + 1) / 2 > le) a--;
@@ -2789,14 +2752,14 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     // Newton direction per island (lane per island); the register path leaves H intact, the
     // in-place LDS path (merged islands > 9 dofs) consumes it
     if (gch) {
-      newton_dir_groups(s, done);
+      newton_dir_groups(s, false);
     } else {
       // one unrolled register variant (islands of <= 9 dofs padded with identity): lanes holding
       // 6- and 9-dof islands run the same code instead of two divergent copies; larger (merged)
       // islands one after the other on the whole wave
-      const int n = !done ? s.isl_n[l] : 0;
-      if (!done && n <= 9) island_newton_dir_reg<T, 9>(s, l, n);
-      if (!done) s.isl_hvalid[l] = n <= 9;
+      const int n = !idle ? s.isl_n[l] : 0;
+      if (!idle && n <= 9) island_newton_dir_reg<T, 9>(s, l, n);
+      if (!idle) s.isl_hvalid[l] = n <= 9;
       wsync();
       for (uint32_t bm = (uint32_t)__ballot(n > 9); bm; bm &= bm - 1) {
         const int I = __builtin_ctz(bm), nI = s.isl_n[I];
@@ -2806,9 +2769,11 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     wsync();
     clk.lap(10);
     clk.aux_start();
-    line_search(m, s, clk);
+    const T alpha = line_search(m, s, clk);
     clk.lap(11);
-    if (l < m.nv) s.x[l] += s.isl_alpha[s.tree_island[s.c_dof_tree[l]]] * s.p[l];
+    if (alpha == T(0)) { clk.lap(12); break; }
+    if (l < m.nv) s.x[l] += alpha * s.p[l];
+    it++;
     // remember the active set the step was computed with
     for (int r = l; r < s.nefc; r += NT) s.efc_Jp[r] = (T)s.efc_act[r];
     wsync();
@@ -2826,21 +2791,19 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       if (I < s.nisland && q == 0) s.isl_val[I] = any ? T(1) : T(0);
     }
     wsync();
-    // island converged: two consecutive steps kept its active set (then its piecewise quadratic
-    // is a single quadratic there and x its minimiser, refined once), or its cost stopped
-    // decreasing
-    if (!done) {
-      const bool changed = s.isl_val[l] != T(0);
-      const T nc = s.isl_cost[l];
-      const T impr = cost - nc;
-      unchanged = changed ? 0 : unchanged + 1;
+    // improvement = scale (cost_old - cost), summed over the islands' own differences
+    {
+      const bool changed = !idle && s.isl_val[l] != T(0);
+      const T nc = !idle ? s.isl_cost[l] : T(0);
       if (changed) s.isl_hvalid[l] = 0;
-      if (unchanged >= 2 || !(impr > 0) || !(s.isl_alpha[l] > T(0))) done = true;
+      improvement = scale * wsum(cost - nc);
       cost = nc;
+      unchanged = __ballot(changed) ? 0 : unchanged + 1;
     }
     wsync();
     clk.lap(12);
-    if (!__ballot(!done)) { it++; break; }
+    if constexpr (sizeof(T) == 4)
+      if (unchanged >= 2) break;
   }
   clk.lap(12);
   if (l == 0) s.solver_iter = it;
@@ -2917,35 +2880,46 @@ __device__ __attribute__((noinline)) void st_noslip_dense_sweep(const DevPhys<T>
     }
   }
   wsync();
-  for (int si = 0; si < 2; si++) {
+  // the group's (<= 2) islands: I = grp and grp + 4
+  struct DSet {
+    int k0, cnt, maxc, n, r0, jo, qq, d;
+    bool lane_on;
+  };
+  auto mkset = [&](int si) {
+    DSet z;
     const int I = grp + 4 * si;
     const bool has = I < s.nisland;
-    const int k0 = si ? iend0 : 0;
-    const int cnt = has ? (si ? iend1 : iend0) - k0 : 0;
-    const int maxc = max(max(__builtin_amdgcn_readlane(cnt, 0), __builtin_amdgcn_readlane(cnt, 16)),
-                         max(__builtin_amdgcn_readlane(cnt, 32), __builtin_amdgcn_readlane(cnt, 48)));
-    if (maxc == 0) continue;
-    const int n = has ? s.isl_n[I] : 0;
-    const int r0 = has ? s.isl_roff[I] : 0;
-    const bool lane_on = q < n;
-    const int qq = lane_on ? q : 0;
-    const int d = lane_on ? s.isl_dof[I][q] : 0;
-    const int jo = has ? s.isl_joff[I] - r0 * n : 0;   // (row position p, island dof c) at jo + p n + c
-    T v = lane_on ? s.v2[d] : T(0);
-    struct DRow {   // stage 2
-      int p, j;
-      bool act;
-    };
-    struct DRaw {   // stage 1
-      int j;
-      bool act;
-      T Jd, W0, W1, bd, f0, f1, pc, u, w, iK1;
-    };
-    auto dlist = [&](int k) { return k < cnt ? (int)s.ns_list[grp][k0 + k] : -1; };
+    z.k0 = si ? iend0 : 0;
+    z.cnt = has ? (si ? iend1 : iend0) - z.k0 : 0;
+    z.maxc = max(max(__builtin_amdgcn_readlane(z.cnt, 0), __builtin_amdgcn_readlane(z.cnt, 16)),
+                 max(__builtin_amdgcn_readlane(z.cnt, 32), __builtin_amdgcn_readlane(z.cnt, 48)));
+    z.n = has ? s.isl_n[I] : 0;
+    z.r0 = has ? s.isl_roff[I] : 0;
+    z.lane_on = q < z.n;
+    z.qq = z.lane_on ? q : 0;
+    z.d = z.lane_on ? s.isl_dof[I][q] : 0;
+    z.jo = has ? s.isl_joff[I] - z.r0 * z.n : 0;   // (row position p, island dof c) at jo + p n + c
+    return z;
+  };
+  const DSet S0 = mkset(0), S1 = mkset(1);
+  T v0 = S0.lane_on ? s.v2[S0.d] : T(0), v1 = S1.lane_on ? s.v2[S1.d] : T(0);
+  struct DRow {   // stage 2
+    int p, j;
+    bool act;
+  };
+  struct DRaw {   // stage 1
+    int j;
+    bool act;
+    T Jd, W0, W1, bd, f0, f1, pc, u, w, iK1;
+  };
+  // one Gauss-Seidel sweep over the set's island; returns the group's improvement (MuJoCo
+  // costChange summed over the pair updates; uniform in the group's 16 lanes)
+  auto sweep = [&](const DSet& z, T& v) -> T {
+    auto dlist = [&](int k) { return k < z.cnt ? (int)s.ns_list[grp][z.k0 + k] : -1; };
     auto drow = [&](int p) {
       DRow x;
       x.act = p >= 0;
-      x.p = x.act ? p : r0;   // (an inactive slot reads the island's first row, masked below)
+      x.p = x.act ? p : z.r0;   // (an inactive slot reads the island's first row, masked below)
       x.j = s.isl_row[x.p];
       return x;
     };
@@ -2953,9 +2927,9 @@ __device__ __attribute__((noinline)) void st_noslip_dense_sweep(const DevPhys<T>
       DRaw w;
       w.j = x.j;
       w.act = x.act;
-      const int o = jo + x.p * n + qq;
-      const T J0 = s.jt[o], J1 = s.jt[o + n], W0 = s.efc_Wv[o], W1 = s.efc_Wv[o + n];
-      const bool on = x.act && lane_on;
+      const int o = z.jo + x.p * z.n + z.qq;
+      const T J0 = s.jt[o], J1 = s.jt[o + z.n], W0 = s.efc_Wv[o], W1 = s.efc_Wv[o + z.n];
+      const bool on = x.act && z.lane_on;
       w.Jd = on ? J0 - J1 : T(0);
       w.W0 = on ? W0 : T(0);
       w.W1 = on ? W1 : T(0);
@@ -2968,11 +2942,13 @@ __device__ __attribute__((noinline)) void st_noslip_dense_sweep(const DevPhys<T>
       w.iK1 = s.efc_Jp[x.p + 1];
       return w;
     };
+    T impr = 0;
     // The pair's 2 x 2 projection (the streaming path's, rearranged): with r = J v + b and
     // A the Delassus block, K0 = mid (a00 - a11) + (r0 - r1) - (a00 - a10) f0 - (a01 - a11) f1,
     // y = clamp(-K0 / K1, +-mid) -- only r0 - r1 = (J0 - J1) v + b0 - b1 is needed, one row sum
     // instead of two, and the per-pair coefficients come from the table.  An inactive slot has
-    // zero J and W, so v does not move.
+    // zero J and W, so v does not move.  The update moves the forces along (1, -1) by dl, so
+    // MuJoCo's costChange 0.5 d^T A d + d^T r is dl (0.5 dl K1 + (r0 - r1)), K1 = u - w.
     auto update = [&](const DRaw& cur) {
       const T rd = rowsum16(cur.Jd * v) + cur.bd;
       const T f0 = cur.f0, f1 = cur.f1;
@@ -2981,32 +2957,48 @@ __device__ __attribute__((noinline)) void st_noslip_dense_sweep(const DevPhys<T>
       T y = -K0 * cur.iK1;
       y = y < -mid ? -mid : (y > mid ? mid : y);
       const T n0 = mid + y, n1 = mid - y;
+      const T dl = T(0.5) * ((n0 - f0) - (n1 - f1));
+      impr = cur.act ? impr - dl * (T(0.5) * dl * (cur.u - cur.w) + rd) : impr;
       v += cur.W0 * (n0 - f0) + cur.W1 * (n1 - f1);
       if (cur.act && q == 0) { s.efc_force[cur.j] = n0; s.efc_force[cur.j + 1] = n1; }
     };
-    for (int iter = 0; iter < m.noslip_iterations; iter++) {
-      // unrolled by two with the stage registers alternating (ra / rb), so that the loop carries
-      // no register moves and no wait on the loads it has just issued
-      DRaw ra = draw(drow(dlist(0)));
-      DRow x1 = drow(dlist(1));
-      int p2 = dlist(2);
-      for (int k = 0; k < maxc; k += 2) {
-        const int p3 = dlist(k + 3);
-        const DRow x2 = drow(p2);
-        const DRaw rb = draw(x1);
-        update(ra);
-        if (k + 1 >= maxc) break;
-        const int p4 = dlist(k + 4);
-        const DRow x3 = drow(p3);
-        ra = draw(x2);
-        update(rb);
-        x1 = x3;
-        p2 = p4;
-      }
-      wsync();   // the next sweep reads the forces this one wrote
+    // unrolled by two with the stage registers alternating (ra / rb), so that the loop carries
+    // no register moves and no wait on the loads it has just issued
+    DRaw ra = draw(drow(dlist(0)));
+    DRow x1 = drow(dlist(1));
+    int p2 = dlist(2);
+    for (int k = 0; k < z.maxc; k += 2) {
+      const int p3 = dlist(k + 3);
+      const DRow x2 = drow(p2);
+      const DRaw rb = draw(x1);
+      update(ra);
+      if (k + 1 >= z.maxc) break;
+      const int p4 = dlist(k + 4);
+      const DRow x3 = drow(p3);
+      ra = draw(x2);
+      update(rb);
+      x1 = x3;
+      p2 = p4;
     }
-    if (lane_on) s.v2[d] = v;
+    wsync();   // the next sweep reads the forces this one wrote
+    return impr;
+  };
+  // mj_solNoSlip's loop: a sweep over every island, then stop once the problem's scaled
+  // improvement is below noslip_tolerance (islands are independent under Gauss-Seidel, so one
+  // sweep of each in turn is one sweep of the problem)
+  const T scale = T(1) / (m.meaninertia * T(m.nv > 1 ? m.nv : 1));
+  int iter = 0;
+  while (iter < m.noslip_iterations) {
+    T impr = 0;
+    if (S0.maxc) impr += sweep(S0, v0);
+    if (S1.maxc) impr += sweep(S1, v1);
+    impr = (rdlane(impr, 0) + rdlane(impr, 16)) + (rdlane(impr, 32) + rdlane(impr, 48));
+    iter++;
+    if (impr * scale < m.noslip_tolerance) break;
   }
+  if (S0.lane_on) s.v2[S0.d] = v0;
+  if (S1.lane_on) s.v2[S1.d] = v1;
+  if (l == 0) s.noslip_iter = iter;
   wsync();
 }
 
@@ -3014,8 +3006,17 @@ template <typename T, class CLK>
 __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
+  if (l == 0) s.noslip_iter = 0;
   if (m.noslip_iterations <= 0 || s.nefc == 0) return;
   clk.sub_start();
+  // mj_solNoSlip's exit: after each sweep, stop once the sweep's improvement (MuJoCo costChange
+  // summed over the pair updates) scaled by 1 / (meaninertia nv) is below noslip_tolerance.  Every
+  // path below reduces its per-group improvement (uniform in the group's 16 lanes) over the four
+  // groups after a sweep.  costChange's restore of a pair whose cost rose by more than 1e-10 is not
+  // applied: the projection is the exact minimiser of the pair's 2 x 2 problem over an interval
+  // that holds the old forces, so the change is <= 0 but for rounding (oracle: applied).
+  const T ns_scale = T(1) / (m.meaninertia * T(m.nv > 1 ? m.nv : 1));
+  auto ns_total = [](T g) { return (rdlane(g, 0) + rdlane(g, 16)) + (rdlane(g, 32) + rdlane(g, 48)); };
   constexpr int NSR = 8;   // short lists (see the force-space path below)
   // Pair lists: islands are independent under Gauss-Seidel (block-diagonal M, rows inside one
   // island), so island I runs on DPP row (I mod 4) — 16 lanes, one slot per lane — in its own
@@ -3271,7 +3272,9 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       }
       NS_BC(0) NS_BC(1) NS_BC(2) NS_BC(3) NS_BC(4) NS_BC(5) NS_BC(6) NS_BC(7)
 #undef NS_BC
-      for (int iter = 0; iter < m.noslip_iterations; iter++) {
+      int iter = 0;
+      while (iter < m.noslip_iterations) {
+        T impr = 0;
       // the 2 x 2 projection rearranged as in st_noslip_dense_sweep: K0 = mid (a00 - a11) +
       // (r0 - r1) - (a00 - a10) f0 - (a01 - a11) f1, y = clamp(-K0 / K1, +-mid), 1 / K1 = 0 for
       // a flat pair (its forces stay at their mean)
@@ -3287,11 +3290,16 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
           const bool act = K < glen;                                                      \
           const T d0 = act ? n0 - f0 : T(0), d1 = act ? n1 - f1 : T(0);                   \
           r += A[2 * K] * d0 + A[2 * K + 1] * d1;                                         \
+          const T dl = T(0.5) * (d0 - d1);                                                \
+          impr -= dl * (T(0.5) * dl * (PU[K] - PW[K]) + rd);                              \
           if (act) { F0[K] = n0; F1[K] = n1; }                                            \
         }
         NS_UPD(0) NS_UPD(1) NS_UPD(2) NS_UPD(3) NS_UPD(4) NS_UPD(5) NS_UPD(6) NS_UPD(7)
 #undef NS_UPD
+        iter++;
+        if (ns_total(impr) * ns_scale < m.noslip_tolerance) break;
       }
+      if (l == 0) s.noslip_iter = iter;
 #pragma unroll
       for (int k = 0; k < NSR; k++)
         if (k < glen && q == 0) { s.efc_force[s.ns_list[grp][k]] = F0[k]; s.efc_force[s.ns_list[grp][k] + 1] = F1[k]; }
@@ -3310,41 +3318,51 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   // the streaming path (row sums in island-dof lane order).
   if (maxlen > NSR) {
     if (!__ballot(!small)) {
-      for (int si = 0; si < 2; si++) {
+      // tree sizes packed 4 bits each (dofnum - 1, <= PH_MAXTDOF = 16): a row's first-tree width
+      // is one bit-field extract, not a select chain over the trees
+      static_assert(PH_MAXT <= 8 && PH_MAXTDOF <= 16, "tree sizes must pack into 4-bit fields");
+      uint32_t tdn_pack = 0;
+#pragma unroll
+      for (int t = 0; t < PH_MAXT; t++)
+        tdn_pack |= (uint32_t)((t < m.ntree ? s.c_tree_dofnum[t] : 1) - 1) << (4 * t);
+      struct LSet {
+        int k0, cnt, maxc, d, td, dloc;
+        bool lane_on;
+      };
+      auto mkset = [&](int si) {
+        LSet z;
         const int I = grp + 4 * si;
         const bool has = I < s.nisland;
-        const int k0 = si ? iend0 : 0;
-        const int cnt = has ? (si ? iend1 : iend0) - k0 : 0;
-        const int maxc = max(max(__builtin_amdgcn_readlane(cnt, 0), __builtin_amdgcn_readlane(cnt, 16)),
-                             max(__builtin_amdgcn_readlane(cnt, 32), __builtin_amdgcn_readlane(cnt, 48)));
-        if (maxc == 0) continue;
+        z.k0 = si ? iend0 : 0;
+        z.cnt = has ? (si ? iend1 : iend0) - z.k0 : 0;
+        z.maxc = max(max(__builtin_amdgcn_readlane(z.cnt, 0), __builtin_amdgcn_readlane(z.cnt, 16)),
+                     max(__builtin_amdgcn_readlane(z.cnt, 32), __builtin_amdgcn_readlane(z.cnt, 48)));
         const int n = has ? s.isl_n[I] : 0;
-        const bool lane_on = q < n;
-        const int d = lane_on ? s.isl_dof[I][q] : 0;
-        const int td = s.c_dof_tree[d], dloc = d - s.c_tree_dofadr[td];
-        T v = lane_on ? s.v2[d] : T(0);
-        // software pipeline over the pairs, one LDS level per stage, so that no wait inside the
-        // loop covers a load issued in the same iteration: list entry 3 pairs ahead, the row's
-        // trees and offsets 2 ahead, its J / W / b / f entries 1 ahead; the Delassus block of a
-        // pair is formed at its own update (off the chain through v).  Tree sizes come from
-        // registers.
-        // tree sizes packed 4 bits each (dofnum - 1, <= PH_MAXTDOF = 16): a row's first-tree width
-        // is one bit-field extract, not a select chain over the trees
-        static_assert(PH_MAXT <= 8 && PH_MAXTDOF <= 16, "tree sizes must pack into 4-bit fields");
-        uint32_t tdn_pack = 0;
-#pragma unroll
-        for (int t = 0; t < PH_MAXT; t++)
-          tdn_pack |= (uint32_t)((t < m.ntree ? s.c_tree_dofnum[t] : 1) - 1) << (4 * t);
-        struct DRow {   // stage 2
-          int j, t0, t1, off0, off1;
-          bool act;
-        };
-        struct DRaw {   // stage 3
-          int j;
-          bool act;
-          T J0, J1, W0, W1, b0, b1, f0, f1;
-        };
-        auto dlist = [&](int k) { return k < cnt ? (int)s.ns_list[grp][k0 + k] : -1; };
+        z.lane_on = q < n;
+        z.d = z.lane_on ? s.isl_dof[I][q] : 0;
+        z.td = s.c_dof_tree[z.d];
+        z.dloc = z.d - s.c_tree_dofadr[z.td];
+        return z;
+      };
+      const LSet S0 = mkset(0), S1 = mkset(1);
+      T v0 = S0.lane_on ? s.v2[S0.d] : T(0), v1 = S1.lane_on ? s.v2[S1.d] : T(0);
+      struct DRow {   // stage 2
+        int j, t0, t1, off0, off1;
+        bool act;
+      };
+      struct DRaw {   // stage 3
+        int j;
+        bool act;
+        T J0, J1, W0, W1, b0, b1, f0, f1;
+      };
+      // one sweep of the set's island, v in registers (lane q = island dof q); returns the group's
+      // improvement.  Software pipeline over the pairs, one LDS level per stage, so that no wait
+      // inside the loop covers a load issued in the same iteration: list entry 3 pairs ahead, the
+      // row's trees and offsets 2 ahead, its J / W / b / f entries 1 ahead; the Delassus block of
+      // a pair is formed at its own update (off the chain through v).  Tree sizes come from
+      // registers.
+      auto sweep = [&](const LSet& z, T& v) -> T {
+        auto dlist = [&](int k) { return k < z.cnt ? (int)s.ns_list[grp][z.k0 + k] : -1; };
         auto drow = [&](int jj) {
           DRow x;
           x.act = jj >= 0;
@@ -3357,8 +3375,8 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
         };
         auto draw = [&](const DRow& x) {
           const int n0 = x.t0 >= 0 ? (int)((tdn_pack >> (4 * x.t0)) & 15u) + 1 : 0;
-          const int slot = td == x.t0 ? dloc : (td == x.t1 ? n0 + dloc : -1);
-          const bool on = x.act && lane_on && slot >= 0;
+          const int slot = z.td == x.t0 ? z.dloc : (z.td == x.t1 ? n0 + z.dloc : -1);
+          const bool on = x.act && z.lane_on && slot >= 0;
           const int sl = on ? slot : 0;                 // unconditional, in-range loads; masked below
           DRaw p;
           p.j = x.j;
@@ -3375,37 +3393,49 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
           p.f1 = s.efc_force[x.j + 1];
           return p;
         };
-        for (int iter = 0; iter < m.noslip_iterations; iter++) {
-          DRaw cur = draw(drow(dlist(0)));
-          DRow x1 = drow(dlist(1));
-          int j2 = dlist(2);
-          for (int k = 0; k < maxc; k++) {
-            const int j3 = dlist(k + 3);
-            const DRow x2 = drow(j2);
-            const DRaw nxt = draw(x1);
-            const T a00 = rowsum16(cur.J0 * cur.W0), a01 = rowsum16(cur.J0 * cur.W1);
-            const T a10 = rowsum16(cur.J1 * cur.W0), a11 = rowsum16(cur.J1 * cur.W1);
-            const T r0 = rowsum16(cur.J0 * v) + cur.b0;
-            const T r1 = rowsum16(cur.J1 * v) + cur.b1;
-            const T f0 = cur.f0, f1 = cur.f1;
-            const T bc0 = r0 - (a00 * f0 + a01 * f1), bc1 = r1 - (a10 * f0 + a11 * f1);
-            const T mid = T(0.5) * (f0 + f1);
-            const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;
-            T y = -K0 / K1;
-            y = y < -mid ? -mid : (y > mid ? mid : y);
-            const bool flat = K1 < T(1e-15);
-            const T n0 = flat ? mid : mid + y, n1 = flat ? mid : mid - y;
-            const T d0 = cur.act ? n0 - f0 : T(0), d1 = cur.act ? n1 - f1 : T(0);
-            v += cur.W0 * d0 + cur.W1 * d1;
-            if (cur.act && q == 0) { s.efc_force[cur.j] = n0; s.efc_force[cur.j + 1] = n1; }
-            cur = nxt;
-            x1 = x2;
-            j2 = j3;
-          }
-          wsync();   // the next sweep reads the forces this one wrote
+        T impr = 0;
+        DRaw cur = draw(drow(dlist(0)));
+        DRow x1 = drow(dlist(1));
+        int j2 = dlist(2);
+        for (int k = 0; k < z.maxc; k++) {
+          const int j3 = dlist(k + 3);
+          const DRow x2 = drow(j2);
+          const DRaw nxt = draw(x1);
+          const T a00 = rowsum16(cur.J0 * cur.W0), a01 = rowsum16(cur.J0 * cur.W1);
+          const T a10 = rowsum16(cur.J1 * cur.W0), a11 = rowsum16(cur.J1 * cur.W1);
+          const T r0 = rowsum16(cur.J0 * v) + cur.b0;
+          const T r1 = rowsum16(cur.J1 * v) + cur.b1;
+          const T f0 = cur.f0, f1 = cur.f1;
+          const T bc0 = r0 - (a00 * f0 + a01 * f1), bc1 = r1 - (a10 * f0 + a11 * f1);
+          const T mid = T(0.5) * (f0 + f1);
+          const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;
+          T y = -K0 / K1;
+          y = y < -mid ? -mid : (y > mid ? mid : y);
+          const bool flat = K1 < T(1e-15);
+          const T n0 = flat ? mid : mid + y, n1 = flat ? mid : mid - y;
+          const T d0 = cur.act ? n0 - f0 : T(0), d1 = cur.act ? n1 - f1 : T(0);
+          const T dl = T(0.5) * (d0 - d1);
+          impr -= dl * (T(0.5) * dl * K1 + (r0 - r1));
+          v += cur.W0 * d0 + cur.W1 * d1;
+          if (cur.act && q == 0) { s.efc_force[cur.j] = n0; s.efc_force[cur.j + 1] = n1; }
+          cur = nxt;
+          x1 = x2;
+          j2 = j3;
         }
-        if (lane_on) s.v2[d] = v;
+        wsync();   // the next sweep reads the forces this one wrote
+        return impr;
+      };
+      int iter = 0;
+      while (iter < m.noslip_iterations) {
+        T impr = 0;
+        if (S0.maxc) impr += sweep(S0, v0);
+        if (S1.maxc) impr += sweep(S1, v1);
+        iter++;
+        if (ns_total(impr) * ns_scale < m.noslip_tolerance) break;
       }
+      if (S0.lane_on) s.v2[S0.d] = v0;
+      if (S1.lane_on) s.v2[S1.d] = v1;
+      if (l == 0) s.noslip_iter = iter;
       wsync();
       return;
     }
@@ -3423,7 +3453,9 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       F0[k] = s.efc_force[P[k].j];
       F1[k] = s.efc_force[P[k].j + 1];
     }
-    for (int iter = 0; iter < m.noslip_iterations; iter++) {
+    int iter = 0;
+    while (iter < m.noslip_iterations) {
+      T impr = 0;
 #pragma unroll
       for (int k = 0; k < NSR; k++) {
         if (k >= maxlen) break;
@@ -3444,10 +3476,15 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
           n0 = mid + y; n1 = mid - y;
         }
         if (cur.on) s.v2[cur.d] = vd + (cur.W0 * (n0 - f0) + cur.W1 * (n1 - f1));
+        const T dl = T(0.5) * ((n0 - f0) - (n1 - f1));
+        impr = cur.act ? impr - dl * (T(0.5) * dl * K1 + (r0 - r1)) : impr;
         if (cur.act) { F0[k] = n0; F1[k] = n1; }
         wsync();
       }
+      iter++;
+      if (ns_total(impr) * ns_scale < m.noslip_tolerance) break;
     }
+    if (l == 0) s.noslip_iter = iter;
 #pragma unroll
     for (int k = 0; k < NSR; k++)
       if (P[k].act && q == 0) { s.efc_force[P[k].j] = F0[k]; s.efc_force[P[k].j + 1] = F1[k]; }
@@ -3455,7 +3492,9 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     return;
   }
   clk.count(SN_NS_STREAM, 1);
-  for (int iter = 0; iter < m.noslip_iterations; iter++) {
+  int iter = 0;
+  while (iter < m.noslip_iterations) {
+    T impr = 0;
     NsPair cur = fetch(0);
     for (int k = 0; k < maxlen; k++) {
       const NsPair nxt = fetch(k + 1 < maxlen ? k + 1 : k);
@@ -3476,11 +3515,17 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
         n0 = mid + y; n1 = mid - y;
       }
       if (cur.on) s.v2[cur.d] += cur.W0 * (n0 - f0) + cur.W1 * (n1 - f1);
+      const T dl = T(0.5) * ((n0 - f0) - (n1 - f1));
+      impr = cur.act ? impr - dl * (T(0.5) * dl * K1 + (r0 - r1)) : impr;
       if (cur.act && q == 0) { s.efc_force[cur.j] = n0; s.efc_force[cur.j + 1] = n1; }
       wsync();
       cur = nxt;
     }
+    iter++;
+    if (ns_total(impr) * ns_scale < m.noslip_tolerance) break;
   }
+  if (l == 0) s.noslip_iter = iter;
+  wsync();
 }
 
 template <typename T>
@@ -3624,7 +3669,14 @@ __device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& 
   st_collision(m, s, clk);
   if (s.nconvex) {
     clk.sub_start();
-#if PNP_MW
+#if PNP_COMPACT
+    // The compact build runs no MPR: a live convex pair hands the sub-step to the full tier, like
+    // a capacity overflow (C3's settled envs keep none).  MPR is fp64 in every build (collide_dev.h)
+    // and the tiers' results must be the same bits; its code in this build grew the frames and
+    // the write-back of every launch (round 3: a convex contact's multiccd fan alone cost C3 1 %).
+    if (lane_id() == 0) CAP_FULL(8u);
+    wsync();
+#elif PNP_MW
     if constexpr (sizeof(T) == 4) {
       if (s.mw > 1) st_collision_convex_mw(s);
       else st_collision_convex(m, s);
@@ -3652,6 +3704,7 @@ __device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& 
   clk.count(SN_ITER, s.solver_iter);
   clk.count(SN_ISLAND, s.nefc ? s.nisland : 0);
   st_noslip(m, s, clk);     clk.lap(13);
+  clk.count(SN_NS_ITER, s.noslip_iter);
   st_finish_accel(m, s);    clk.lap(14);
 }
 
@@ -3805,6 +3858,7 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) forwa
     o[PNP_DBG_COUNTS + 1] = s.nefc;
     o[PNP_DBG_COUNTS + 2] = s.solver_iter;
     o[PNP_DBG_COUNTS + 3] = s.warn;
+    o[PNP_DBG_NOSLIP_ITER] = s.noslip_iter;
   }
   for (int r = l; r < s.nefc; r += NT) {
     o[PNP_DBG_EFC_FORCE + r] = s.efc_force[r];

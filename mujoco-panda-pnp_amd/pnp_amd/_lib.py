@@ -10,7 +10,7 @@ from .model import PnpIKParams, PnpModelDesc
 # PNP_LIB: another build of the same sources (tools/asan_cpu_tests.sh: the host-sanitizer build)
 LIB_PATH = os.environ.get("PNP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpnp.so")
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # every symbol include/pnp.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -64,7 +64,7 @@ class PnpEnvOut(C.Structure):
 # debug record layout (include/pnp.h PNP_DBG_*)
 DBG = dict(QM=0, BIAS=1296, ACT=1332, QACC_SMOOTH=1368, QACC=1404, COUNTS=1440, CON=1444, CON_STRIDE=16,
            EFC_FORCE=2212, EFC_POS=2420, EFC_D=2628, EFC_AREF=2836, EFC_TYPE=3044, EFC_J=3252,
-           QACC_NEWTON=10740, SIZE=10776)
+           QACC_NEWTON=10740, NOSLIP_ITER=10776, SIZE=10780)
 
 _lib = None
 

@@ -351,5 +351,6 @@ def run_batched(num_envs, env_id="FrankaShelfPNPDense-v0", max_tick=3000, sim_st
 
     server.run([program(b) for b in range(num_envs)])
     objects = {n: server.site_xpos[:, server.model.site_id(f"{n}_site")].copy() for n in seq}
+    warn = (server.env.state["warn"].to(torch.int64) & 0xFFFF).cpu().numpy()   # sticky warning bits per env
     return {"success": success, "ticks": ticks, "rounds": server.rounds, "launches": dict(server.launches),
-            "objects": objects}
+            "objects": objects, "warn": warn}

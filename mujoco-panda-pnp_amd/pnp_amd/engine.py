@@ -150,7 +150,9 @@ class Engine:
               # ad-hoc sub-stage timers (cycles; see the sub_lap calls in csrc/step.hip)
               "aux0", "aux1", "aux2", "aux3", "aux4", "aux5", "aux6", "aux7",
               # noslip path counts (sub-steps on the dense long-list / the streaming path)
-              "n_ns_dense", "n_ns_stream")
+              "n_ns_dense", "n_ns_stream",
+              # noslip sweeps run (mj_solNoSlip's early exit on noslip_tolerance)
+              "n_noslip_iter")
     N_STAGE_CYCLES = 27
 
     def step_profile(self, st, nsub=1):

@@ -101,9 +101,12 @@ def run(env_id="FrankaShelfPNPDense-v0", max_tick=3000, sim_steps=5, task_sequen
         for n in u.task_sequence:
             print(f"    {n}: at {np.round(obj[n], 3)}, target {np.round(tgt[n], 3)}, "
                   f"distance {np.linalg.norm(obj[n] - tgt[n]):.3f} m")
+    # the env's sticky warning bits (MuJoCo's data.warning): bad-state resets (1, 2, 4) and a full
+    # contact / constraint buffer (8, 16: the physics dropped contacts MuJoCo would keep)
+    warn = int(u.data.warn) & 0xFFFF
     env.close()
     return {"success": success, "ticks": ticks, "wall_s": wall, "objects": obj, "targets": tgt,
-            "rewards": rewards}
+            "rewards": rewards, "warn": warn}
 
 
 def main(argv=None):

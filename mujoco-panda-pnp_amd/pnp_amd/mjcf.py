@@ -156,7 +156,7 @@ class MJCFCompiler:
         self.meshdir = ""
         self.option = {"timestep": 0.002, "integrator": "Euler", "noslip_iterations": 0,
                        "cone": "pyramidal", "gravity": [0, 0, -9.81], "multiccd": 0, "warmstart": 1,
-                       "iterations": 100, "tolerance": 1e-8, "solver": "Newton"}
+                       "iterations": 100, "tolerance": 1e-8, "solver": "Newton", "noslip_tolerance": 1e-6}
         self.autolimits = True
         root = self._expand(ET.parse(self.xml_path).getroot(), self.dir)
         self.root = root
@@ -197,11 +197,12 @@ class MJCFCompiler:
             self.autolimits = c.get("autolimits", "true") == "true"
             assert c.get("angle", "radian") == "radian"
         for o in r.findall("option"):
-            for k in ("timestep",):
+            for k in ("timestep", "tolerance", "noslip_tolerance"):
                 if o.get(k):
                     self.option[k] = float(o.get(k))
-            if o.get("noslip_iterations"):
-                self.option["noslip_iterations"] = int(o.get("noslip_iterations"))
+            for k in ("noslip_iterations", "iterations"):
+                if o.get(k):
+                    self.option[k] = int(o.get(k))
             for k in ("integrator", "cone", "solver"):
                 if o.get(k):
                     self.option[k] = o.get(k)
@@ -569,7 +570,7 @@ class _ModelBuilder:
             opt_noslip_iterations=opt["noslip_iterations"], opt_iterations=opt["iterations"],
             opt_tolerance=opt["tolerance"], opt_multiccd=opt.get("multiccd", 0),
             opt_warmstart=opt.get("warmstart", 1), opt_cone_pyramidal=int(opt["cone"] == "pyramidal"),
-            opt_integrator_euler=int(opt["integrator"] == "Euler"),
+            opt_integrator_euler=int(opt["integrator"] == "Euler"), opt_noslip_tolerance=opt["noslip_tolerance"],
             body_parentid=body_parentid, body_rootid=body_rootid, body_weldid=body_weldid,
             body_mocapid=body_mocapid, body_jntadr=body_jntadr, body_jntnum=body_jntnum,
             body_dofadr=body_dofadr, body_dofnum=body_dofnum, body_pos=body_pos, body_quat=body_quat,

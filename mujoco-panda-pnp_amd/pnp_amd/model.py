@@ -24,7 +24,7 @@ _DESC_FIELDS = [
     ("nsite", "i"), ("nmocap", "i"), ("neq", "i"), ("nmesh", "i"), ("nmeshvert", "i"),
     ("timestep", "d"), ("gravity", "g"), ("noslip_iterations", "i"), ("iterations", "i"),
     ("tolerance", "d"), ("cone_pyramidal", "i"), ("multiccd", "i"), ("warmstart", "i"),
-    ("integrator_euler", "i"),
+    ("integrator_euler", "i"), ("noslip_tolerance", "d"), ("stat_meaninertia", "d"),
     ("body_parentid", "I"), ("body_rootid", "I"), ("body_weldid", "I"), ("body_mocapid", "I"),
     ("body_jntadr", "I"), ("body_jntnum", "I"), ("body_dofadr", "I"), ("body_dofnum", "I"),
     ("body_pos", "D"), ("body_quat", "D"), ("body_ipos", "D"), ("body_iquat", "D"),
@@ -67,7 +67,7 @@ _SCALAR_SRC = {"timestep": "opt_timestep", "gravity": "opt_gravity",
                "noslip_iterations": "opt_noslip_iterations", "iterations": "opt_iterations",
                "tolerance": "opt_tolerance", "cone_pyramidal": "opt_cone_pyramidal",
                "multiccd": "opt_multiccd", "warmstart": "opt_warmstart",
-               "integrator_euler": "opt_integrator_euler"}
+               "integrator_euler": "opt_integrator_euler", "noslip_tolerance": "opt_noslip_tolerance"}
 
 
 class PandaModel:

@@ -6,6 +6,8 @@
 * ``body_invweight0``: mean diagonal of J M^-1 J^T for the body's COM (translational and
   rotational 3x3 blocks separately) at qpos0, 0 for static bodies — used for equality and
   contact rows' ``efc_diagApprox`` (reference call sites: every mj_step).
+* ``stat_meaninertia``: mjStatistic.meaninertia, the mean of diag(M) at qpos0 (armature
+  included), which scales the Newton and no-slip termination tests.
 
 M here is assembled independently of the engine's CRBA, as the Jacobian sum
 ``M = sum_b Jp_b^T m_b Jp_b + Jr_b^T I_b Jr_b + diag(armature)`` over body COMs, in numpy.
@@ -110,7 +112,7 @@ def mass_matrix(m, qpos):
 
 def compute(m):
     """Returns the extra arrays (dof_parentid, dof_invweight0, body_invweight0, body_subtreemass,
-    body_treedepth)."""
+    body_treedepth) and the model statistic stat_meaninertia."""
     nv, nb, nj = int(m["nv"]), int(m["nbody"]), int(m["njnt"])
     # dof_parentid: previous dof of the same joint, else last dof of the nearest ancestor body
     dof_parentid = -np.ones(nv, np.int32)
@@ -151,5 +153,8 @@ def compute(m):
     depth = np.zeros(nb, np.int32)
     for b in range(1, nb):
         depth[b] = depth[int(m["body_parentid"][b])] + 1
+    # mjStatistic.meaninertia: the mean diagonal of M at qpos0 (armature included); mj_solNewton and
+    # mj_solNoSlip scale their termination tests by 1 / (meaninertia * max(1, nv))
+    stat_meaninertia = float(np.mean(np.diag(M))) if nv else 1.0
     return dict(dof_parentid=dof_parentid, dof_invweight0=dof_invweight0, body_invweight0=body_invweight0,
-                body_subtreemass=subtreemass, body_treedepth=depth)
+                body_subtreemass=subtreemass, body_treedepth=depth, stat_meaninertia=stat_meaninertia)

@@ -64,6 +64,9 @@ class TQCConfig:
     clip_obs: float = 10.0               # VecNormalize
     norm_eps: float = 1e-8
     seed: int = 0
+    # one gradient step captured in a HIP graph and replayed gradient_steps times per train() (single
+    # process only; the data-parallel learner all-reduces eagerly)
+    graph: bool = True
 
 
 def _world():
@@ -95,19 +98,20 @@ class RunningMeanStd:
         self.update_from_moments(bmean, bvar, n)
 
     def update_from_moments(self, bmean, bvar, bcount):
+        # in place: the captured learner step (TQC._capture) reads mean / var at fixed addresses
         delta = bmean - self.mean
         tot = self.count + bcount
-        self.mean = self.mean + delta * bcount / tot
         m2 = self.var * self.count + bvar * bcount + delta * delta * self.count * bcount / tot
-        self.var = m2 / tot
+        self.mean.copy_(self.mean + delta * bcount / tot)
+        self.var.copy_(m2 / tot)
         self.count = tot
 
     def state_dict(self):
         return {"mean": self.mean, "var": self.var, "count": torch.tensor(self.count, dtype=torch.float64)}
 
     def load_state_dict(self, d):
-        self.mean = d["mean"].to(self.mean)
-        self.var = d["var"].to(self.var)
+        self.mean.copy_(d["mean"].to(self.mean))
+        self.var.copy_(d["var"].to(self.var))
         self.count = float(d["count"])
 
 
@@ -160,6 +164,9 @@ class DictReplayBuffer:
         self.dones = z(self.size, n_envs)
         self.pos, self.full = 0, False
         self.device = device
+        # rows filled so far, on the device: sample() draws indices from it without a host value,
+        # so the captured learner step samples the buffer as it grows
+        self.upper = torch.zeros((), dtype=torch.float32, device=device)
 
     def add(self, obs, next_obs, action, reward, done):
         self.obs[self.pos].copy_(obs)
@@ -170,11 +177,14 @@ class DictReplayBuffer:
         self.pos += 1
         if self.pos == self.size:
             self.full, self.pos = True, 0
+        self.upper.fill_(float(self.size if self.full else self.pos))
 
     def sample(self, batch_size, generator=None):
-        upper = self.size if self.full else self.pos
-        bi = torch.randint(0, upper, (batch_size,), device=self.device, generator=generator)
-        ei = torch.randint(0, self.n_envs, (batch_size,), device=self.device, generator=generator)
+        """Uniform (row, env) pairs over the filled rows: floor(U[0, 1) * upper), the row count read
+        on the device (sb3 samples the same distribution with randint on the host's upper bound)."""
+        u = torch.rand(2, batch_size, device=self.device, generator=generator)
+        bi = torch.clamp((u[0] * self.upper).long(), max=self.size - 1)
+        ei = torch.clamp((u[1] * self.n_envs).long(), max=self.n_envs - 1)
         return (self.obs[bi, ei], self.actions[bi, ei], self.next_obs[bi, ei], self.dones[bi, ei, None],
                 self.rewards[bi, ei, None])
 
@@ -286,9 +296,17 @@ class TQC:
         self.critic_target.load_state_dict(self.critic.state_dict())
         self.critic_target.requires_grad_(False)
         self.target_entropy = -float(self.act_dim)
-        self.actor_opt = torch.optim.Adam(self.actor.parameters(), lr=c.learning_rate)
-        self.critic_opt = torch.optim.Adam(self.critic.parameters(), lr=c.learning_rate)
-        self.ent_opt = torch.optim.Adam([self.log_ent_coef], lr=c.learning_rate)
+        # fused Adam with the learning rate as a device tensor (the linear schedule writes it in place,
+        # so a captured step follows it); capturable: step counts on the device
+        cuda = self.device.type == "cuda"
+        self._lr = torch.full((), c.learning_rate, dtype=torch.float32, device=self.device) if cuda else c.learning_rate
+        kw = dict(lr=self._lr, fused=True, capturable=True) if cuda else dict(lr=c.learning_rate)
+        self.actor_opt = torch.optim.Adam(self.actor.parameters(), **kw)
+        self.critic_opt = torch.optim.Adam(self.critic.parameters(), **kw)
+        self.ent_opt = torch.optim.Adam([self.log_ent_coef], **kw)
+        self._graph = None          # the captured gradient step (TQC._capture)
+        self._graph_out = None
+        self._eager_updates = 0     # steps run eagerly before the capture (allocator / optimiser state)
         self.vecnorm = VecNormalize(dims, self.device, c.clip_obs, c.norm_eps)
         self.buffer = DictReplayBuffer(c.buffer_size, self.n_envs, self.obs_dim, self.act_dim, self.device)
         # per-rank sampling streams (exploration, replay indices); identical init weights
@@ -309,9 +327,12 @@ class TQC:
 
     def _update_lr(self):
         lr = self.cfg.learning_rate * self._progress_remaining()
-        for opt in (self.actor_opt, self.critic_opt, self.ent_opt):
-            for g in opt.param_groups:
-                g["lr"] = lr
+        if isinstance(self._lr, torch.Tensor):
+            self._lr.fill_(lr)      # shared by the three optimisers' param groups
+        else:
+            for opt in (self.actor_opt, self.critic_opt, self.ent_opt):
+                for g in opt.param_groups:
+                    g["lr"] = lr
         return lr
 
     @staticmethod
@@ -386,38 +407,89 @@ class TQC:
             return flat_obs(self.vecnorm.normalize(dict(zip(OBS_KEYS, parts))))
         return norm(o), a, norm(no), d, r
 
+    def _update(self):
+        """One gradient step (sb3-contrib tqc.py train() order) on device tensors, no host sync:
+        entropy coefficient, critics, actor, Polyak target update.  Returns the logged values as
+        device scalars."""
+        c = self.cfg
+        obs, act, nobs, done, rew = self._sample_norm()
+        a_pi, lp = self.actor.action_log_prob(obs, self.gen)
+        lp = lp.reshape(-1, 1)
+        ent_coef = torch.exp(self.log_ent_coef.detach())
+        ent_loss = -(self.log_ent_coef * (lp + self.target_entropy).detach()).mean()
+        self._step_opt(self.ent_opt, ent_loss, [self.log_ent_coef])
+        with torch.no_grad():
+            na, nlp = self.actor.action_log_prob(nobs, self.gen)
+            nq = self.critic_target(nobs, na)
+            keep = c.n_quantiles * c.n_critics - c.top_quantiles_to_drop_per_net * c.n_critics
+            nq, _ = torch.sort(nq.reshape(c.batch_size, -1))
+            nq = nq[:, :keep]
+            tq = nq - ent_coef * nlp.reshape(-1, 1)
+            tq = rew + (1 - done) * c.gamma * tq
+            tq = tq.unsqueeze(1)
+        cq = self.critic(obs, act)
+        critic_loss = quantile_huber_loss(cq, tq, sum_over_quantiles=False)
+        self._step_opt(self.critic_opt, critic_loss, self.critic.parameters())
+        qpi = self.critic(obs, a_pi).mean(dim=2).mean(dim=1, keepdim=True)
+        actor_loss = (ent_coef * lp - qpi).mean()
+        self._step_opt(self.actor_opt, actor_loss, self.actor.parameters())
+        if (self.n_updates + 1) % c.target_update_interval == 0:
+            with torch.no_grad():
+                tps, ps = list(self.critic_target.parameters()), list(self.critic.parameters())
+                torch._foreach_mul_(tps, 1 - c.tau)
+                torch._foreach_add_(tps, ps, alpha=c.tau)
+        self.n_updates += 1
+        return ent_coef, critic_loss.detach(), actor_loss.detach(), ent_loss.detach()
+
+    def _graph_ok(self):
+        return (self.cfg.graph and _world() == 1 and self.device.type == "cuda"
+                and self.cfg.target_update_interval == 1)
+
+    def _capture(self):
+        """Capture one gradient step in a HIP graph (torch.cuda.graph): every kernel of the step
+        -- replay sampling, the three losses' forward and backward passes, fused Adam, the Polyak
+        update -- replayed with one launch instead of ~400 (the eager step is launch-bound: batch
+        512, 256-wide layers).  The exploration / replay generator is registered with the graph,
+        so each replay draws the numbers the eager step would at that point of the stream.  Called
+        after 3 eager steps (autograd / allocator / optimiser state exist); gradients are dropped
+        first so the captured backward passes allocate them in the graph's pool, as set_to_none
+        does eagerly.  The capture itself runs nothing."""
+        for opt in (self.actor_opt, self.critic_opt, self.ent_opt):
+            opt.zero_grad(set_to_none=True)
+        g = torch.cuda.CUDAGraph()
+        g.register_generator_state(self.gen)
+        n0 = self.n_updates
+        with torch.cuda.graph(g):
+            self._graph_out = self._update()
+        self.n_updates = n0
+        self._graph = g
+
     def train(self, gradient_steps=None):
+        """gradient_steps (default cfg.gradient_steps) gradient steps; with a captured step each
+        is one graph replay.  Results are the eager steps' bit for bit (tests/test_tqc_gpu.py)."""
         c = self.cfg
         lr = self._update_lr()
-        for _ in range(gradient_steps or c.gradient_steps):
-            obs, act, nobs, done, rew = self._sample_norm()
-            a_pi, lp = self.actor.action_log_prob(obs, self.gen)
-            lp = lp.reshape(-1, 1)
-            ent_coef = torch.exp(self.log_ent_coef.detach())
-            ent_loss = -(self.log_ent_coef * (lp + self.target_entropy).detach()).mean()
-            self._step_opt(self.ent_opt, ent_loss, [self.log_ent_coef])
-            with torch.no_grad():
-                na, nlp = self.actor.action_log_prob(nobs, self.gen)
-                nq = self.critic_target(nobs, na)
-                keep = c.n_quantiles * c.n_critics - c.top_quantiles_to_drop_per_net * c.n_critics
-                nq, _ = torch.sort(nq.reshape(c.batch_size, -1))
-                nq = nq[:, :keep]
-                tq = nq - ent_coef * nlp.reshape(-1, 1)
-                tq = rew + (1 - done) * c.gamma * tq
-                tq = tq.unsqueeze(1)
-            cq = self.critic(obs, act)
-            critic_loss = quantile_huber_loss(cq, tq, sum_over_quantiles=False)
-            self._step_opt(self.critic_opt, critic_loss, self.critic.parameters())
-            qpi = self.critic(obs, a_pi).mean(dim=2).mean(dim=1, keepdim=True)
-            actor_loss = (ent_coef * lp - qpi).mean()
-            self._step_opt(self.actor_opt, actor_loss, self.actor.parameters())
+        n = gradient_steps or c.gradient_steps
+        out = None
+        for _ in range(n):
+            if not self._graph_ok():
+                out = self._update()
+                continue
+            if self._graph is None and self._eager_updates < 3:
+                side = torch.cuda.Stream(device=self.device)
+                side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(side):
+                    out = self._update()
+                torch.cuda.current_stream(self.device).wait_stream(side)
+                self._eager_updates += 1
+                continue
+            if self._graph is None:
+                self._capture()
+            self._graph.replay()
             self.n_updates += 1
-            if self.n_updates % c.target_update_interval == 0:
-                with torch.no_grad():
-                    for p, tp in zip(self.critic.parameters(), self.critic_target.parameters()):
-                        tp.mul_(1 - c.tau).add_(p, alpha=c.tau)
-        self.logs = {"lr": lr, "ent_coef": ent_coef.item(), "critic_loss": critic_loss.item(),
-                     "actor_loss": actor_loss.item(), "ent_coef_loss": ent_loss.item()}
+            out = self._graph_out
+        self.logs = {"lr": lr, "ent_coef": out[0], "critic_loss": out[1], "actor_loss": out[2],
+                     "ent_coef_loss": out[3]}
         return self.logs
 
     def learn(self, total_timesteps, callback=None, log_every=0):
@@ -440,7 +512,7 @@ class TQC:
                 n = max(s["episodes"], 1)
                 print(f"steps {self.num_timesteps * _world()}  {self.num_timesteps * _world() / (time.perf_counter() - t0):.0f} "
                       f"transitions/s  episodes {s['episodes']}  ep_rew {s['ep_reward_sum'] / n:.2f}  "
-                      f"success {s['success_sum'] / n:.3f}  {self.logs}", flush=True)
+                      f"success {s['success_sum'] / n:.3f}  {({k: float(v) for k, v in self.logs.items()})}", flush=True)
         return self
 
     # ------------------------------------------------------------------ checkpoints
@@ -462,6 +534,13 @@ class TQC:
         self.ent_opt.load_state_dict(d["ent_opt"])
         self.vecnorm.load_state_dict(d["vecnormalize"])
         self.num_timesteps, self.n_updates = int(d["num_timesteps"]), int(d["n_updates"])
+        # the optimisers now hold new state tensors: the schedule's shared lr tensor back in their
+        # groups, and a captured step (which read the old ones) is re-captured
+        if isinstance(self._lr, torch.Tensor):
+            for opt in (self.actor_opt, self.critic_opt, self.ent_opt):
+                for g in opt.param_groups:
+                    g["lr"] = self._lr
+        self._graph, self._graph_out, self._eager_updates = None, None, 0
 
     def save(self, path):
         torch.save(self.state_dict(), path)

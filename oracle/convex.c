@@ -17,15 +17,16 @@
  * replaces the normal by the analytic one for smooth geoms (here: the sphere, the only smooth
  * type in a convex pair of this scene).
  * multiccd (shelf_pnp.xml:5 enables it; mjENBL_MULTICCD in mjc_Convex): after the first contact,
- * MPR is re-run four times with the two geoms rotated in opposite senses about their own centres
- * by +-perturbation_angle (1e-3 rad) about the two tangent axes of the first contact's frame
- * (mju_makeFrame of its normal): (t1, -a), (t1, +a), (t2, -a), (t2, +a), geom 1 by q and geom 2
- * by q^-1.  A contact found this way is appended when its position is farther than
- * relative_tolerance (1e-3) x min(rbound1, rbound2) from every contact the pair already has
- * (up to 5 per pair).  MuJoCo applies the rotation inside the support function (direction
- * rotated in, support point rotated out); rotating the geom frame once per run is the same map.
- * Restated from MuJoCo 2.3.3's published engine_collision_convex.c (not present here, so the
- * constants and the trial order are unverified: parity unpinned).
+ * MPR is re-run four times with the two geoms rotated in opposite senses ABOUT THE FIRST CONTACT'S
+ * POSITION (mjc_rotateFrame) by +-perturbation_angle (1e-3 rad) about the two tangent axes of the
+ * first contact's frame (mju_makeFrame of its normal): (t1, -a), (t1, +a), (t2, -a), (t2, +a),
+ * geom 1 by q and geom 2 by q^-1.  A contact found this way is appended when its position is
+ * farther than relative_tolerance (1e-3) x min(rbound1, rbound2) from every contact the pair
+ * already has (up to 5 per pair).  Pairs with a smooth geom (the sphere) make no fan.
+ * UNVERIFIED ASSUMPTIONS (MuJoCo 2.3.3's engine_collision_convex.c is not present here; the two
+ * choices below follow two independent recollections of it -- round 3 rotated about the geoms'
+ * own centres and fanned sphere pairs too): the rotation centre (the first contact point), the
+ * sphere exclusion, the constants and the trial order.  Parity unpinned, DESIGN.md section 2.
  * Pairs whose oriented bounding boxes are disjoint cannot touch; they skip MPR (result-neutral).
  */
 #include <float.h>
@@ -433,6 +434,9 @@ static int mpr_fan(Mdl* m, shape* s, int g1, int g2, double margin, orc_contact*
   if (!mpr_contact(s, margin, &out[0])) return 0;
   int n = 1;
   if (!m->multiccd) return n;
+  /* smooth geoms (the sphere) make no fan: assumed from MuJoCo's mjc_Convex (unverified, see the
+     header) -- rotating a sphere about the contact point only slides it along its own surface */
+  if (s[0].type == C_SPHERE || s[1].type == C_SPHERE) return n;
   /* multiccd: perturbed runs about the first contact's tangent axes */
   const double relative_tolerance = 1e-3, perturbation_angle = 1e-3;
   double frame[9];
@@ -444,6 +448,8 @@ static int mpr_fan(Mdl* m, shape* s, int g1, int g2, double margin, orc_contact*
   const double R0[2][9] = {
       {s[0].R[0], s[0].R[1], s[0].R[2], s[0].R[3], s[0].R[4], s[0].R[5], s[0].R[6], s[0].R[7], s[0].R[8]},
       {s[1].R[0], s[1].R[1], s[1].R[2], s[1].R[3], s[1].R[4], s[1].R[5], s[1].R[6], s[1].R[7], s[1].R[8]}};
+  const double P0[2][3] = {{s[0].pos[0], s[0].pos[1], s[0].pos[2]}, {s[1].pos[0], s[1].pos[1], s[1].pos[2]}};
+  const double* org = out[0].pos;   /* the rotations' centre: the first contact's position */
   for (int ax = 0; ax < 2; ax++)
     for (int sg = 0; sg < 2; sg++) {
       const double ang = sg ? perturbation_angle : -perturbation_angle;
@@ -452,8 +458,15 @@ static int mpr_fan(Mdl* m, shape* s, int g1, int g2, double margin, orc_contact*
       sp_negquat(qi, q);
       sp_quat2mat(Rq, q);
       sp_quat2mat(Rqi, qi);
-      mulmat3(s[0].R, Rq, R0[0]);    /* geom 1 rotated by q about its centre */
-      mulmat3(s[1].R, Rqi, R0[1]);   /* geom 2 by q^-1 */
+      /* (mjc_rotateFrame) geom 1 rotated by q, geom 2 by q^-1, both about the first contact */
+      const double* Rs[2] = {Rq, Rqi};
+      for (int i = 0; i < 2; i++) {
+        double rel[3], rot[3];
+        mulmat3(s[i].R, Rs[i], R0[i]);
+        sub3(rel, P0[i], org);
+        for (int k = 0; k < 3; k++) rot[k] = Rs[i][3 * k] * rel[0] + Rs[i][3 * k + 1] * rel[1] + Rs[i][3 * k + 2] * rel[2];
+        for (int k = 0; k < 3; k++) s[i].pos[k] = org[k] + rot[k];
+      }
       orc_contact c;
       if (!mpr_contact(s, margin, &c)) continue;
       int distinct = 1;

@@ -17,7 +17,9 @@
  *   primal soft-constraint problem, mj_solNoSlip (pyramidal pairs), mj_checkPos/Vel/Acc with
  *   auto-reset, mj_Euler with implicit joint damping and quaternion integration.
  * Parity with real MuJoCo is UNPINNED for dynamics and contacts (no reference test pins them,
- * SURVEY §8c); the solver here converges to the exact optimum of the same convex problem.
+ * SURVEY §8c).  The solvers stop by MuJoCo 2.3.3's rules (round 4): Newton on scaled improvement /
+ * gradient < tolerance, noslip on scaled sweep improvement < noslip_tolerance with costChange's
+ * restore, both scaled by 1 / (stat.meaninertia * nv); the line search is exact (see line_search).
  */
 #include "physics.h"
 
@@ -492,10 +494,28 @@ static double cost_eval(Mdl* m, orc_data* d, const double* x, double* jar, int* 
   return c;
 }
 
-/* exact minimiser of the convex piecewise-quadratic phi(alpha) = cost(x + alpha p) */
+/* mj_solNewton's termination scale (engine_solver.c, mj_solPrimal): improvement and gradient are
+   tested against mjOption.tolerance after scaling by 1 / (mjStatistic.meaninertia * max(1, nv)),
+   meaninertia the model constant (mean of diag(M) at qpos0, pnp_amd/setconst.py) */
+static double solver_scale(Mdl* m) {
+  return 1.0 / (m->stat_meaninertia * (m->nv > 1 ? m->nv : 1));
+}
+
+/* Line search along p from x.  MuJoCo 2.3.3 PrimalLineSearch first returns 0 when the search
+   vector is below mjMINVAL or p is not a descent direction to within
+   gtol = tolerance * ls_tolerance * |p| / scale (ls_tolerance = 0.01, the mjOption default); then
+   it runs Newton steps on phi'(alpha) with bracketing until |phi'| < gtol.  Restated: the same two
+   exits, then the EXACT minimiser of the convex piecewise-quadratic phi(alpha) = cost(x + alpha p)
+   (breakpoints sorted; MuJoCo's iterate stops within gtol of it -- a declared deviation at the
+   1e-10 level) */
 static double line_search(Mdl* m, orc_data* d, const double* x, const double* p, const double* jar) {
   int nv = m->nv, ne = d->ne, n = d->nefc;
   double Mp[ORC_MAXV], dx[ORC_MAXV], Jp[ORC_MAXEFC];
+  double snorm = 0;
+  for (int i = 0; i < nv; i++) snorm += p[i] * p[i];
+  snorm = sqrt(snorm);
+  if (snorm < ORC_MINVAL) return 0;
+  const double gtol = m->tolerance * 0.01 * snorm / solver_scale(m);
   for (int i = 0; i < nv; i++) dx[i] = x[i] - d->qacc_smooth[i];
   mulM(m, d, Mp, p);
   double A = 0, B = 0;
@@ -523,7 +543,7 @@ static double line_search(Mdl* m, orc_data* d, const double* x, const double* p,
     while (j >= 0 && brk[order[j]] > brk[t]) { order[j + 1] = order[j]; j--; }
     order[j + 1] = t;
   }
-  if (B >= 0) return 0;
+  if (B >= -gtol) return 0;   /* phi'(0) = B: not a descent direction */
   for (int i = 0; i < nb; i++) {
     int r = order[i];
     double a = brk[r];
@@ -536,6 +556,32 @@ static double line_search(Mdl* m, orc_data* d, const double* x, const double* p,
   return A > 0 ? -B / A : 0;
 }
 
+/* gradient M (x - qacc_smooth) + J^T D jar over the active rows, Hessian M + J^T D J */
+static void grad_hess(Mdl* m, orc_data* d, const double* x, const double* jar, const int* act, double* grad,
+                      double* H) {
+  int nv = m->nv, n = d->nefc;
+  double Mdx[ORC_MAXV], dx[ORC_MAXV];
+  for (int i = 0; i < nv; i++) dx[i] = x[i] - d->qacc_smooth[i];
+  mulM(m, d, Mdx, dx);
+  memcpy(grad, Mdx, nv * sizeof(double));
+  memcpy(H, d->qM, nv * nv * sizeof(double));
+  for (int r = 0; r < n; r++) {
+    if (!act[r]) continue;
+    const double* Jr = d->efc_J + r * nv;
+    double Dr = d->efc_D[r];
+    for (int i = 0; i < nv; i++) {
+      if (Jr[i] == 0) continue;
+      grad[i] += Jr[i] * Dr * jar[r];
+      for (int k = 0; k < nv; k++) H[i * nv + k] += Jr[i] * Dr * Jr[k];
+    }
+  }
+}
+
+/* mj_solNewton (MuJoCo 2.3.3 engine_solver.c mj_solPrimal, flg_Newton): one problem over all dofs
+   (2.3.3 has no constraint islands), one step length per iteration.  Warm start as
+   mj_fwdConstraint: qacc_warmstart unless its cost exceeds qacc_smooth's.  Each iteration: Newton
+   direction -H^-1 g, line search (above), alpha == 0 -> stop; step; then stop once
+   scale (cost_old - cost) < tolerance or scale |g| < tolerance, or after `iterations` steps. */
 static void solve_newton(Mdl* m, orc_data* d) {
   int nv = m->nv, n = d->nefc;
   double x[ORC_MAXV], grad[ORC_MAXV], pdir[ORC_MAXV], H[ORC_MAXV * ORC_MAXV], L[ORC_MAXV * ORC_MAXV];
@@ -543,47 +589,31 @@ static void solve_newton(Mdl* m, orc_data* d) {
   int act[ORC_MAXEFC];
   double c_ws = cost_eval(m, d, d->qacc_warmstart, NULL, NULL);
   double c_sm = cost_eval(m, d, d->qacc_smooth, NULL, NULL);
-  memcpy(x, c_ws < c_sm ? d->qacc_warmstart : d->qacc_smooth, nv * sizeof(double));
+  memcpy(x, c_ws > c_sm ? d->qacc_smooth : d->qacc_warmstart, nv * sizeof(double));
   double cost = cost_eval(m, d, x, jar, act);
-  double meaninertia = 0;
-  for (int i = 0; i < nv; i++) meaninertia += d->qM[i * nv + i];
-  meaninertia /= nv;
-  double scale = 1.0 / (meaninertia * (nv > 1 ? nv : 1));
+  const double scale = solver_scale(m);
   int it = 0;
-  double gnorm = 0, improvement = 0;
-  for (; it < 200; it++) {
-    double Mdx[ORC_MAXV], dx[ORC_MAXV];
-    for (int i = 0; i < nv; i++) dx[i] = x[i] - d->qacc_smooth[i];
-    mulM(m, d, Mdx, dx);
-    memcpy(grad, Mdx, nv * sizeof(double));
-    memcpy(H, d->qM, nv * nv * sizeof(double));
-    for (int r = 0; r < n; r++) {
-      if (!act[r]) continue;
-      const double* Jr = d->efc_J + r * nv;
-      double Dr = d->efc_D[r];
-      for (int i = 0; i < nv; i++) {
-        if (Jr[i] == 0) continue;
-        grad[i] += Jr[i] * Dr * jar[r];
-        for (int k = 0; k < nv; k++) H[i * nv + k] += Jr[i] * Dr * Jr[k];
-      }
-    }
-    gnorm = 0;
-    for (int i = 0; i < nv; i++) gnorm += grad[i] * grad[i];
-    gnorm = sqrt(gnorm) * scale;
-    if (gnorm < 1e-14) break;
+  double gradient = 0, improvement = 0;
+  grad_hess(m, d, x, jar, act, grad, H);
+  while (it < m->iterations) {
     if (chol(L, H, nv)) break;
     chol_solve(pdir, L, grad, nv);
     for (int i = 0; i < nv; i++) pdir[i] = -pdir[i];
     double alpha = line_search(m, d, x, pdir, jar);
-    if (alpha <= 0) break;
+    if (alpha == 0) break;
     for (int i = 0; i < nv; i++) x[i] += alpha * pdir[i];
+    it++;
     double nc = cost_eval(m, d, x, jar, act);
-    improvement = (cost - nc) * scale;
+    improvement = scale * (cost - nc);
     cost = nc;
-    if (improvement < 1e-18 && it > 0) { it++; break; }
+    grad_hess(m, d, x, jar, act, grad, H);
+    double g2 = 0;
+    for (int i = 0; i < nv; i++) g2 += grad[i] * grad[i];
+    gradient = scale * sqrt(g2);
+    if (improvement < m->tolerance || gradient < m->tolerance) break;
   }
   d->solver_iter = it;
-  d->solver_gradient = gnorm;
+  d->solver_gradient = gradient;
   d->solver_improvement = improvement;
   /* forces, constraint force, acceleration */
   for (int r = 0; r < n; r++) d->efc_force[r] = act[r] ? -d->efc_D[r] * jar[r] : 0;
@@ -591,8 +621,28 @@ static void solve_newton(Mdl* m, orc_data* d) {
 }
 
 /* ------------------------------------------------------------------ no-slip (pyramidal) */
+/* MuJoCo 2.3.3 costChange: the 2 x 2 block's cost change 0.5 dT A d + dT res of an update; a
+   change above 1e-10 (an increase) restores the old forces and counts as 0.  Returns -change. */
+static double cost_change(const double* Ac, double* f, const double* old, const double* res) {
+  const double dl[2] = {f[0] - old[0], f[1] - old[1]};
+  double change = 0.5 * (dl[0] * (Ac[0] * dl[0] + Ac[1] * dl[1]) + dl[1] * (Ac[2] * dl[0] + Ac[3] * dl[1])) +
+                  dl[0] * res[0] + dl[1] * res[1];
+  if (change > 1e-10) {
+    f[0] = old[0];
+    f[1] = old[1];
+    change = 0;
+  }
+  return -change;
+}
+
+/* mj_solNoSlip (MuJoCo 2.3.3), pyramidal contacts: Gauss-Seidel over the pairs of opposing
+   pyramid edges on A = J M^-1 J^T without regularisation, at most `maxiter` sweeps; a sweep's
+   improvement (the sum of cost_change) is scaled like Newton's, and the solver stops once it is
+   below noslip_tolerance.  d->noslip_iter = sweeps run, noslip_improvement[k] = sweep k's. */
 static void solve_noslip(Mdl* m, orc_data* d, int maxiter) {
   int nv = m->nv, n = d->nefc;
+  d->noslip_iter = 0;
+  for (int k = 0; k < 8; k++) d->noslip_improvement[k] = -1;
   if (maxiter <= 0 || n == 0) return;
   /* A = J M^-1 J^T */
   double* MinvJt = (double*)malloc(sizeof(double) * n * nv);
@@ -606,14 +656,9 @@ static void solve_noslip(Mdl* m, orc_data* d, int maxiter) {
       A[r * n + c] = s;
     }
   double* f = d->efc_force;
-  /* diagnostic: the per-sweep improvement MuJoCo's mj_solNoSlip tests against noslip_tolerance
-     (the cost decrease 0.5 dT A d + dT res of every pair update, scaled by 1 / (meaninertia nv));
-     recorded only -- this oracle always runs maxiter sweeps (not restated) */
-  double mi = 0;
-  for (int i = 0; i < nv; i++) mi += d->qM[i * nv + i];
-  const double nscale = 1.0 / ((mi / nv) * (nv > 1 ? nv : 1));
-  for (int k = 0; k < 8; k++) d->noslip_improvement[k] = -1;
-  for (int iter = 0; iter < maxiter; iter++) {
+  const double scale = solver_scale(m);
+  int iter = 0;
+  while (iter < maxiter) {
     double impr = 0;
     for (int i = d->ne; i < n; i++) {
       if (d->efc_type[i] != ORC_CNSTR_CONTACT_PYRAMIDAL) continue;
@@ -640,14 +685,16 @@ static void solve_noslip(Mdl* m, orc_data* d, int maxiter) {
           f[j] = mid + y;
           f[j + 1] = mid - y;
         }
-        const double dl[2] = {f[j] - old[0], f[j + 1] - old[1]};
-        impr -= 0.5 * (dl[0] * (Ac[0] * dl[0] + Ac[1] * dl[1]) + dl[1] * (Ac[2] * dl[0] + Ac[3] * dl[1])) +
-                dl[0] * res[0] + dl[1] * res[1];
+        impr += cost_change(Ac, f + j, old, res);
       }
       i += 2 * (dim - 1) - 1;
     }
-    if (iter < 8) d->noslip_improvement[iter] = impr * nscale;
+    impr *= scale;
+    if (iter < 8) d->noslip_improvement[iter] = impr;
+    iter++;
+    if (impr < m->noslip_tolerance) break;
   }
+  d->noslip_iter = iter;
   free(MinvJt);
   free(A);
 }
@@ -868,6 +915,9 @@ int orc_field(Mdl* m, const orc_data* d, const char* name, double* out, int cap)
   else if (!strcmp(name, "nefc")) { tmp[0] = d->nefc; src = tmp; n = 1; }
   else if (!strcmp(name, "solver_iter")) { tmp[0] = d->solver_iter; src = tmp; n = 1; }
   else if (!strcmp(name, "noslip_improvement")) { src = d->noslip_improvement; n = 8; }
+  else if (!strcmp(name, "noslip_iter")) { tmp[0] = d->noslip_iter; src = tmp; n = 1; }
+  else if (!strcmp(name, "solver_improvement")) { src = &d->solver_improvement; n = 1; }
+  else if (!strcmp(name, "solver_gradient")) { src = &d->solver_gradient; n = 1; }
   else if (!strcmp(name, "warn")) { tmp[0] = d->warn; src = tmp; n = 1; }
   else if (!strcmp(name, "contact")) {
     /* per contact: pos3 frame9 dist includemargin friction5 solref2 solimp5 dim geom1 geom2 = 30 */

@@ -73,7 +73,8 @@ typedef struct {
   double qfrc_constraint[ORC_MAXV], qacc[ORC_MAXV], qacc_newton[ORC_MAXV];
   int solver_iter;
   double solver_improvement, solver_gradient;
-  double noslip_improvement[8];   /* diagnostic: MuJoCo's scaled noslip improvement per sweep (not used to stop) */
+  double noslip_improvement[8];   /* MuJoCo's scaled noslip improvement of sweep k (-1: not run) */
+  int noslip_iter;                /* noslip sweeps run (mj_solNoSlip's early exit) */
 } orc_data;
 
 #endif

@@ -31,6 +31,9 @@ def test_execute_pnp_three_cubes():
     obj, tgt = r["objects"]["cube1"], r["targets"]["cube1"]
     shelf_z = 0.73                                   # cube1 rests on the middle board (shelf_pnp.xml)
     assert abs(obj[2] - shelf_z) > 0.05 or np.linalg.norm(obj - tgt) < 0.2, (obj, tgt)
+    # no contact / constraint buffer ever filled (CONTACTFULL 8, CNSTRFULL 16) and no bad-state
+    # reset: the fp64 facade's physics kept every contact MuJoCo would
+    assert r["warn"] == 0, r["warn"]
 
 
 @pytest.mark.timeout(900)
@@ -49,6 +52,7 @@ def test_batched_bt_equals_sequential_facade_runs():
         r = run(task_sequence=["cube1"], max_tick=1500, verbose=False, env_index=b)
         assert (r["success"], r["ticks"]) == (bool(res["success"][b]), int(res["ticks"][b])), (b, r["ticks"], res["ticks"][b])
     assert res["success"].mean() >= 0.5
+    assert not res["warn"].any(), np.nonzero(res["warn"])   # no full contact / row buffer, no bad state
     # batching really happened: the 128 RotateSkill resets (2 per env) took fewer than B slerp
     # launches, and the planners' IK solves one launch per round at most
     assert res["launches"]["ik"] < res["rounds"] and res["launches"]["slerp"] < B

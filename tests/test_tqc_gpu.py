@@ -97,3 +97,42 @@ def test_c5_config_8192_envs():
     w = env.state["warn"].to(torch.int64) & 0xFFFFFFFF
     assert int((w & 0x1F).max()) == 0, "bad-state reset or contact / row truncation"
     assert int((w >> 16).max()) == 0, "a tier hand-over bit leaked out of the call"
+
+
+def test_captured_learner_step_equals_eager():
+    """The HIP-graph gradient step (TQC._capture: one captured update replayed gradient_steps
+    times) gives the eager steps' results bit for bit -- same replay samples, same exploration
+    noise (the generator is registered with the graph), fused Adam either way -- over 12 updates
+    across two train() calls, and its learner step is faster than the eager one."""
+    import time
+    from pnp_amd.envs import BatchedFrankaShelfPNPEnv, EnvConfig
+    from pnp_amd.tqc import TQC, TQCConfig
+    B = 64
+    agents = []
+    for graph in (False, True):
+        env = BatchedFrankaShelfPNPEnv(B, config=EnvConfig(**SHORT))
+        a = TQC(env, TQCConfig(learning_starts=0, graph=graph))
+        a.total_timesteps = 10 ** 6
+        a.reset()
+        for _ in range(3):
+            a.collect_step()
+        agents.append(a)
+    eager, graphed = agents
+    for n in (5, 7):
+        le, lg = eager.train(n), graphed.train(n)
+        for k in ("critic_loss", "actor_loss", "ent_coef_loss", "ent_coef"):
+            assert torch.equal(le[k], lg[k]), k
+    assert graphed._graph is not None and eager._graph is None
+    for name in ("actor", "critic", "critic_target"):
+        for (kp, p), (_, q) in zip(getattr(eager, name).state_dict().items(), getattr(graphed, name).state_dict().items()):
+            assert torch.equal(p, q), (name, kp)
+    assert torch.equal(eager.log_ent_coef, graphed.log_ent_coef)
+    ms = []
+    for a in agents:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        a.train(50)
+        torch.cuda.synchronize()
+        ms.append((time.perf_counter() - t0) / 50 * 1e3)
+    print(f"learner step: eager {ms[0]:.3f} ms, captured {ms[1]:.3f} ms")
+    assert ms[1] < ms[0]
