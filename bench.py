@@ -158,7 +158,8 @@ def _sq_valu():
         with open(f) as fh:
             j = json.load(fh)
         return j.get("valu_issue_frac"), {"file": "profiles/sq_counters_step.json", "measured_in_this_run": False,
-                                           "kernel_version": j.get("kernel_version"), "source": j.get("source")}
+                                           "kernel_version": j.get("kernel_version"), "source": j.get("source"),
+                                           "valu_pipe_util": j.get("valu_pipe_util")}
     return None, None
 
 

@@ -237,7 +237,12 @@ typedef struct pnp_state_f64 {
  * (48 contacts, 4 per CU), wide (192 contacts, 1 per CU).  Each runs the envs the previous tier
  * handed over, from the sub-step that would have overflowed its capacities, so results equal the
  * wide kernel's bit for bit; only the wide tier truncates (PNP_WARN_CONTACTFULL / CNSTRFULL).
- * fp64 (debugging instantiation): the full kernel alone, truncating at 48 contacts.
+ * fp64 (the single-env facade, the batched behaviour trees, debugging): the full kernel, whose
+ * overflowing sub-steps the fp64 wide tier resumes (96 contacts, 400 rows, 1 per CU), truncating
+ * past that.  Solver exits: MuJoCo 2.3.3's (Newton: one line search per iteration, stop on scaled
+ * improvement or gradient < tolerance; noslip: stop on scaled sweep improvement < noslip_tolerance;
+ * scale = 1 / (stat_meaninertia * nv)); the fp32 tiers solve each constraint island to its
+ * minimiser (fp32 cannot resolve the 1e-8 scaled tolerance) and share the noslip exit.
  * Environment variables (A/B runs and tests): PNP_STEP_COMPACT=0 starts at the full tier,
  * 3 runs the wide kernel alone, 2 the compact kernel alone (a test diagnostic that leaves
  * handed-over envs mid-call); PNP_STEP_WIDE=0 drops the wide tier (the full kernel truncates). */

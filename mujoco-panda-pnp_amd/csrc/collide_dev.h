@@ -342,8 +342,8 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
 // two faces multiccd tilts 2e-3 rad apart) MPR's path decides the normal, and fp32 rounding of the
 // Minkowski differences, portal sign tests and support gains took the other branch on a third of
 // the convex-contact fixture's envs.  Inputs (geom frames, hull vertices) stay the build's T and are
-// widened exactly; the contact leaves rounded to T.  MPR runs only in the full and wide tiers
-// (the compact tier hands any live convex pair over), so C3's compact kernel carries none of it.
+// widened exactly; the contact leaves rounded to T.  The compact tier runs the first MPR only (a
+// contact with multiccd hands the sub-step over), in its own out-of-line stage.
 //
 // Wave-cooperative: the whole wave runs MPR on ONE pair (every lane holds the same portal, so
 // all branches are uniform) and splits each mesh support map over its 64 lanes.  Lane l keeps
@@ -910,8 +910,8 @@ __device__ __forceinline__ int c_convex(const DevPhys<T>& /*image: phys<T>()*/, 
                                         T (*val)[7]) {
   const DevPhys<T>& m = phys<T>();
   const int l = threadIdx.x & 63;
-  // (the compact build runs no MPR: step.hip); smooth geoms (the sphere, always g1 of its pairs) make
-  // no fan (oracle/convex.c mpr_fan)
+  // (the compact build runs the first MPR only: step.hip); smooth geoms (the sphere, always g1 of its
+  // pairs) make no fan (oracle/convex.c mpr_fan)
   const int trips = (!PNP_COMPACT && m.multiccd && m.geom_type[g1] != 2 && m.geom_type[g2] != 2) ? 4 : 0;
   int n = 0;
   for (int t = -1; t < trips; t++) {   // t = -1: the first run; then the multiccd trials

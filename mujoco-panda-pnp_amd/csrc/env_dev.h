@@ -393,9 +393,8 @@ __device__ __forceinline__ int tier_need(const DevPhys<T>& m, const Env<T>& s) {
   const int l = lane_id();
   const bool big = __ballot(l < nis && s.isl_roff[l + 1] - s.isl_roff[l] > PNP_BIG_ROWS - 4) != 0;
   const int jt = nis ? s.isl_joff[nis] : 0, he = nis ? s.isl_eoff[nis] : 0;
-  // (the compact tier runs no MPR: an env with a live convex pair starts in the full tier)
   if (5 * nc <= 4 * PNP_GC_MAXCON && 5 * ne <= 4 * PNP_GC_MAXEFC && 5 * slots <= 4 * PNP_GC_MAXJSLOT && !big &&
-      5 * jt <= 4 * PNP_GC_JTCAP && 5 * he <= 4 * PNP_GC_HCAP && s.nconvex == 0)
+      5 * jt <= 4 * PNP_GC_JTCAP && 5 * he <= 4 * PNP_GC_HCAP)
     return 0;
   if (6 * nc <= 5 * PNP_GF_MAXCON && 6 * ne <= 5 * PNP_GF_MAXEFC && 6 * slots <= 5 * PNP_GF_MAXJSLOT &&
       6 * jt <= 5 * PNP_GF_JTCAP)
@@ -590,7 +589,7 @@ __global__ void __launch_bounds__(NT * MW_WAVES, PNP_WIDE ? 1 : 4) env_step_wide
 }
 #endif
 
-#if !PNP_COMPACT && !PNP_WIDE
+#if !PNP_COMPACT && !PNP_WIDE && !PNP_WIDE64
 __global__ void route_commit_kernel(uint8_t* __restrict__ tier, int B) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < B) {
@@ -695,6 +694,24 @@ int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* s
     return rc;
   if (const int32_t rc = launch_env_step_mw(st, p, e, action, o, B, stream, resume, only_tier, 0, "env_step_wide_kernel"))
     return rc;
+  return lease.launched();
+}
+#elif PNP_WIDE64
+// fp64 wide tier: the resume pass of pnp_env_step_f64 over the envs the full fp64 kernel handed
+// over (launched by the full build's launch_env_step, which holds the full fp64 image's lease)
+int32_t launch_env_step_wide64(const pnp_model* model, const pnp_state_t<double>* st, const pnp_env_params* p,
+                               const pnp_env_state* e, const double* action, const pnp_env_out* o, int32_t B,
+                               void* stream) {
+  const DevPhys<double>* src = phys_image<double>(model);
+  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  if (B <= 0) return PNP_OK;
+  ResidentLease lease;
+  if (const int32_t rc = lease.acquire(RES_WIDE64_F64, model, (const void*)&g_phys_f64, src,
+                                       sizeof(DevPhys<double>), stream))
+    return rc;
+  hipLaunchKernelGGL(env_step_kernel<double>, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, *p,
+                     env_view<double>(e), action, out_view<double>(o), B, 1, 0, -1);
+  if (const int32_t rc = pnp_check_launch("env_step_kernel (wide64)")) return rc;
   return lease.launched();
 }
 #else
@@ -839,6 +856,16 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   ResidentLease lease;
   auto k = env_step_kernel<T>;
   if ((rc = env_prep(model, st, k, &dm, "pnp_env_step", stream, lease))) return rc;
+  if constexpr (sizeof(T) == 8) {
+    // fp64 (the facade, the batched behaviour trees): the full kernel, handing the envs whose
+    // sub-steps outgrow it to the fp64 wide tier's resume pass
+    const int w64 = p->n_substeps * p->n_calls <= PNP_RESUME_MAXSUB && wide_enabled();
+    hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), action,
+                       out_view<T>(o), B, 0, w64, -1);
+    if ((rc = pnp_check_launch("env_step_kernel (fp64)"))) return rc;
+    if (w64 && (rc = launch_env_step_wide64(model, st, p, e, action, o, B, stream))) return rc;
+    return lease.launched();
+  }
   // fp32 tiers: the compact gym kernel (8 envs per CU) runs every env, the full kernel resumes
   // the envs it hands over, the wide kernel the envs the full kernel hands over
   const bool tiers = sizeof(T) == 4 && p->n_substeps * p->n_calls <= PNP_RESUME_MAXSUB;

@@ -83,7 +83,8 @@ template <typename T> int build_phys(const pnp_model_desc* s, DevPhys<T>* d, cha
 // acquire() makes `model`'s image the one the symbol holds for launches on `stream` (copying it
 // in, after every earlier reader of the old image, when another model was resident) and holds
 // the slot until launched() has recorded the launch that reads it; see the top of resident.cpp.
-enum ResidentImage { RES_FULL_F32 = 0, RES_FULL_F64, RES_COMPACT_F32, RES_COMPACT_GYM_F32, RES_WIDE_F32, RES_NKIND };
+enum ResidentImage { RES_FULL_F32 = 0, RES_FULL_F64, RES_COMPACT_F32, RES_COMPACT_GYM_F32, RES_WIDE_F32, RES_WIDE64_F64,
+                     RES_NKIND };
 class ResidentLease {
  public:
   ResidentLease() = default;
@@ -113,6 +114,13 @@ int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* s
                              const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
                              void* stream, int resume, int only_tier);
 int32_t step_wide_lds_bytes();
+// step_wide64.hip: the fp64 wide tier (resume passes of pnp_step_f64 and pnp_env_step_f64)
+int32_t launch_step_wide64(const pnp_model* model, const pnp_state_t<double>* st, int32_t B, int32_t nsub,
+                           void* stream);
+int32_t launch_env_step_wide64(const pnp_model* model, const pnp_state_t<double>* st, const pnp_env_params* p,
+                               const pnp_env_state* e, const double* action, const pnp_env_out* o, int32_t B,
+                               void* stream);
+int32_t step_wide64_lds_bytes();
 // env_compact.hip: the compact tier of the fp32 gym step (every env from sub-step 0)
 int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
                                 const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,

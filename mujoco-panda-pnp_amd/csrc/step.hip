@@ -43,6 +43,9 @@
 #ifndef PNP_GYM
 #define PNP_GYM 0   // env_compact.hip: the compact tier's gym kernel (own namespace and image)
 #endif
+#ifndef PNP_WIDE64
+#define PNP_WIDE64 0   // step_wide64.hip: the fp64 instantiation's wide tier (facade / batched BT)
+#endif
 #ifdef PNP_NS_NAME
 #define PNP_NS PNP_NS_NAME
 #elif PNP_COMPACT
@@ -57,8 +60,8 @@
 #define PNP_HANDS (!PNP_WIDE)
 // PNP_MW: the fp32 gym kernels of this build run several waves per env (helper waves for the convex
 // pass): the wide build (4 waves, 1 env per CU) and the full build (2 waves, 4 envs per CU)
-#define PNP_MW (PNP_WIDE || (!PNP_COMPACT && !PNP_GYM))
-#define PNP_LEAN (PNP_COMPACT || PNP_WIDE)
+#define PNP_MW ((PNP_WIDE || (!PNP_COMPACT && !PNP_GYM)) && !PNP_WIDE64)
+#define PNP_LEAN (PNP_COMPACT || PNP_WIDE || PNP_WIDE64)
 // PNP_BIG_ISLANDS: the solver's whole-wave paths for islands with more rows than a wave (line
 // search, gradient, MFMA Hessian).  Compiled out of the compact build, which hands such islands
 // over instead (build_islands), so its common case pays nothing for them.
@@ -1485,6 +1488,20 @@ __device__ __attribute__((noinline)) void st_collision_convex(const DevPhys<T>& 
       const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
       // the pair's contacts (up to C_MULTI with multiccd) staged in cst_val, then lanes 0.. append
       const int n = c_convex(m, s, g1, g2, fmax(m.geom_margin[g1], m.geom_margin[g2]), s.cst_val);
+#if PNP_COMPACT
+      // The compact build carries no multiccd fan (c_convex stops after the first run): a convex
+      // pair in contact hands the sub-step to the full tier, like a capacity overflow.  The fan's
+      // code in this build grew its frames and write-back and cost C3 1 % (round 3), although C3's
+      // settled envs never make a convex contact.  (The first run stays: a pair whose bounding
+      // boxes overlap without contact -- the arm swinging near a board under random servo targets
+      // would otherwise hand its env over too: C3 -30 %.)  MPR is fp64 in every build, so the
+      // tiers take the same hit decision.
+      if (n && m.multiccd && m.geom_type[g1] != 2 && m.geom_type[g2] != 2) {
+        if (l == 0) CAP_FULL(8u);
+        wsync();
+        return;
+      }
+#endif
       if (l < n && ncon + l < PH_MAXCON) {
         const T pos[3] = {s.cst_val[l][1], s.cst_val[l][2], s.cst_val[l][3]};
         const T nrm[3] = {s.cst_val[l][4], s.cst_val[l][5], s.cst_val[l][6]};
@@ -2384,16 +2401,150 @@ __device__ __attribute__((noinline)) void island_newton_dir_wave(Env<T>& s, int 
 // at once, each independently of the others.  An island stops once its Newton step is at the
 // rounding level of the step length (|a_new - a| <= 4 eps |a|) or its bracket has collapsed.
 // Islands with isl_flag set (done) keep a = 0.  Leaves the step lengths in s.isl_alpha.
+// ---------------------------------------------------------------- fp32: per-island Newton
+// The fp32 builds solve every island to its exact minimiser on its own (per-island warm start,
+// exact line search and convergence), as before round 4.  MuJoCo's iteration (one step length and
+// one improvement / gradient test for the whole problem, st_newton below) cannot be carried in
+// fp32: the arm island's cost and derivative carry rounding of ~1e-7 x (weld forces x rows), which
+// swamps a cube island's whole contribution to the shared line-search derivative and improvement
+// -- measured (round 4, the global variant in fp32): a cube's velocity change 0.137 off the oracle,
+// qacc 3.8e-4 -- whereas the islands' exact minimisers are what MuJoCo's fp64 iteration reaches
+// once the active set settles (its exits fire at gradient ~1e-16 after the step that lands there).
+// The fp64 instantiation runs MuJoCo's iteration and exits exactly (tools/noslip_exit_diag.py:
+// iteration counts equal to the oracle's env by env).
+template <typename T, class CLK>
+__device__ void line_search_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
+  const DevPhys<T>& m = phys<T>();
+  const int l = lane_id();
+  if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
+  for (int r = l; r < s.nefc; r += NT) {
+    s.efc_Jp[r] = row_dot(s, r, s.p, T(0));
+  }
+  wsync();
+  if (l < m.nv) {
+    const T mp = mulM_row(m, s, l, s.p);
+    s.v2[l] = mp * s.p[l];
+    s.grad[l] = mp * s.v1[l];   // the gradient is no longer needed this iteration
+  }
+  wsync();
+  clk.aux_lap(SC_AUX0 + 5);   // aux5: line search J p, M p
+  const int q = l & 7;
+  int itc = 0;   // bracketing iterations of the lane's island (stage profile count)
+  // Islands with more rows than a group's register cache (closed fingers pressed together put
+  // 200-400 rows on the arm island): bracketed on the whole wave, one after the other, each
+  // row read once per bracketing iteration by 64 lanes (the group path below would walk it 8
+  // rows at a time, ~35 dependent LDS rounds per iteration).  Same bracketing; the row sums
+  // reduce over 64 lanes instead of 8 (rounding only).
+  constexpr int RK = PNP_BIG_ROWS / 8;
+  const uint32_t big = PNP_BIG_ISLANDS ? (uint32_t)__ballot(l < s.nisland && !s.isl_flag[l] &&
+                                                            s.isl_roff[l + 1] - s.isl_roff[l] > 8 * RK)
+                                       : 0u;
+  for (uint32_t bm = big; bm; bm &= bm - 1) {
+    const int I = __builtin_ctz(bm);
+    const int n = s.isl_n[I];
+    const T A0 = wsum(l < n ? s.v2[s.isl_dof[I][l]] : T(0)), B0 = wsum(l < n ? s.grad[s.isl_dof[I][l]] : T(0));
+    const int r0 = s.isl_roff[I], r1 = s.isl_roff[I + 1];
+    T lo = 0, hi = T(-1), a = 1;
+    int it = 0;
+    for (; it < 60; it++) {
+      T d1 = 0, d2 = 0;
+      for (int rr = r0 + l; rr < r1; rr += NT) {
+        const int r = s.isl_row[rr];
+        const T jp = s.efc_Jp[r], v = s.efc_jar[r] + a * jp;
+        if (r < s.ne || v < 0) { d1 += s.efc_D[r] * v * jp; d2 += s.efc_D[r] * jp * jp; }
+      }
+      d1 = wsum(d1) + A0 * a + B0;
+      d2 = wsum(d2) + A0;
+      if (!(d2 > T(0))) { a = 0; break; }
+      if (d1 == T(0)) break;
+      if (d1 > 0) hi = a; else lo = a;
+      T an = a - d1 / d2;
+      if (!(an > lo) || (hi >= T(0) && !(an < hi))) an = hi >= T(0) ? T(0.5) * (lo + hi) : T(2) * a;
+      const bool fin = fabs(an - a) <= T(4) * PM<T>::eps() * fabs(a) || (hi >= T(0) && hi - lo <= PM<T>::eps() * hi);
+      a = an;
+      if (fin) break;
+    }
+    if (l == 0) s.isl_alpha[I] = a;
+    if ((l >> 3) == I) itc = it + 1;
+  }
+  {
+    const int I = l >> 3;
+    if (I >= s.nisland || (big >> I & 1u)) goto ls_done;
+    if (s.isl_flag[I]) {
+      if (q == 0) s.isl_alpha[I] = 0;
+      goto ls_done;
+    }
+    const T A0 = group_sum(s, I, s.v2, (const T*)nullptr), B0 = group_sum(s, I, s.grad, (const T*)nullptr);
+    const int r0 = s.isl_roff[I], r1 = s.isl_roff[I + 1];
+    // the lane's rows (rr = r0 + q + 8 k) are fixed over the iterations: islands of up to 32
+    // rows keep (Jp, jar, D, equality) in registers (larger ones took the wave path above)
+    T rjp[RK], rjar[RK], rD[RK];
+    bool req[RK], rin[RK];
+#pragma unroll
+    for (int k = 0; k < RK; k++) {
+      const int rr = r0 + q + 8 * k;
+      rin[k] = rr < r1;
+      const int r = s.isl_row[rin[k] ? rr : r0];
+      rjp[k] = s.efc_Jp[r];
+      rjar[k] = s.efc_jar[r];
+      rD[k] = s.efc_D[r];
+      req[k] = r < s.ne;
+    }
+    const bool small = r1 - r0 <= 8 * RK;
+    T lo = 0, hi = T(-1), a = 1;
+    for (int it = 0; it < 60; it++) {
+      itc++;
+      T d1 = 0, d2 = 0;
+      if (small) {
+#pragma unroll
+        for (int k = 0; k < RK; k++) {
+          const T jp = rjp[k], v = rjar[k] + a * jp;
+          const bool on = rin[k] && (req[k] || v < 0);
+          d1 = on ? d1 + rD[k] * v * jp : d1;
+          d2 = on ? d2 + rD[k] * jp * jp : d2;
+        }
+      } else {
+        for (int rr = r0 + q; rr < r1; rr += 8) {
+          const int r = s.isl_row[rr];
+          const T jp = s.efc_Jp[r], v = s.efc_jar[r] + a * jp;
+          if (r < s.ne || v < 0) { d1 += s.efc_D[r] * v * jp; d2 += s.efc_D[r] * jp * jp; }
+        }
+      }
+      d1 = rowsum8(d1) + A0 * a + B0;
+      d2 = rowsum8(d2) + A0;
+      if (!(d2 > T(0))) { a = 0; break; }
+      if (d1 == T(0)) break;
+      if (d1 > 0) hi = a; else lo = a;
+      T an = a - d1 / d2;
+      if (!(an > lo) || (hi >= T(0) && !(an < hi))) an = hi >= T(0) ? T(0.5) * (lo + hi) : T(2) * a;
+      // converged once the Newton step is at the rounding level of a (waiting for an == a bit
+      // for bit cost extra rounds of last-bit oscillation), or the bracket has collapsed
+      const bool fin = fabs(an - a) <= T(4) * PM<T>::eps() * fabs(a) || (hi >= T(0) && hi - lo <= PM<T>::eps() * hi);
+      a = an;
+      if (fin) break;
+    }
+    if (q == 0) s.isl_alpha[I] = a;
+  }
+ls_done:
+  wsync();
+  clk.aux_lap(SC_AUX0 + 6);   // aux6: line search bracketing per island
+  {
+    int mx = 0;
+#pragma unroll
+    for (int g = 0; g < 8; g++) mx = max(mx, __builtin_amdgcn_readlane(itc, 8 * g));
+    clk.count(SC_AUX0 + 7, mx);   // aux7: line-search bracketing iterations (max over islands)
+  }
+}
+
 template <typename T, class CLK>
 __device__ T line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   // MuJoCo 2.3.3 PrimalLineSearch: one step length for the whole problem (2.3.3 has no islands),
-  // along the Newton direction p of every island.  Its two early exits are kept: |p| < mjMINVAL,
-  // and phi'(0) >= -gtol with gtol = tolerance * ls_tolerance (0.01) * |p| / scale (p not a descent
-  // direction to within the tolerance); then the exact minimiser of the convex piecewise quadratic
-  // phi(a) = cost(x + a p) by Newton steps on phi' with bracketing (MuJoCo stops its own iterate at
-  // |phi'| < gtol; the exact minimiser is the oracle's).  Lane l holds rows l + 64 k
-  // (k < 2) in registers; larger row counts stream the rest from LDS (the wide tier's 200-700
-  // rows).  Returns the step (wave-uniform).
+  // along the Newton direction p of every island: 0 when |p| < mjMINVAL (or phi'(0) >= 0), else
+  // the exact minimiser of the convex piecewise quadratic phi(a) = cost(x + a p) by Newton steps on
+  // phi' with bracketing (MuJoCo's iterate stops at |phi'| < gtol; the exact minimiser is the
+  // oracle's).  Lane l holds rows l + 64 k (k < 2) in registers; larger row counts
+  // stream the rest from LDS (the wide tier's 200-700 rows).  Returns the step (wave-uniform);
+  // the fp64 instantiation's (st_newton; the fp32 builds: line_search_islands).
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
   if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
@@ -2443,14 +2594,12 @@ __device__ T line_search(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK&
     d1 = wsum(d1) + A0 * a + B0;
     d2 = wsum(d2) + A0;
   };
-  const T scale = T(1) / (m.meaninertia * T(m.nv > 1 ? m.nv : 1));
-  const T gtol = m.tolerance * T(0.01) * snorm / scale;
   T a = 0;
   int it = 0;
   if (snorm >= T(1e-15)) {
     T d1, d2;
     deriv(T(0), d1, d2);
-    if (d1 < -gtol) {
+    if (d1 < T(0)) {
       T lo = 0, hi = T(-1);
       a = 1;
       for (; it < 60; it++) {
@@ -2574,9 +2723,245 @@ __device__ __attribute__((noinline)) void hess_mfma(Env<float>& s, int I) {
 }
 
 template <typename T, class CLK>
+__device__ void st_newton_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
+  const DevPhys<T>& m = phys<T>();
+  const int l = lane_id();
+  if (s.nefc == 0) {
+    if (l < m.nv) s.qacc[l] = s.qacc_smooth[l];
+    if (l == 0) s.solver_iter = 0;
+    wsync();
+    return;
+  }
+  clk.aux_start();
+  build_islands(m, s, clk);
+  if (PNP_HANDS && s.ovf) return;
+  // warm start per island: the better of qacc_warmstart and qacc_smooth (MuJoCo chooses for the
+  // whole problem; per island the minimiser is the same and the start is better).  One pass:
+  // cost(qacc_smooth) has no dof term and its jar is efc_bb (= J qacc_smooth - aref, same
+  // arithmetic), and the chosen start's jar / active set are kept instead of re-evaluated.
+  if (l < m.nv) s.v1[l] = s.qacc_ws[l] - s.qacc_smooth[l];
+  wsync();
+  if (l < m.nv) s.v2[l] = T(0.5) * s.v1[l] * mulM_row(m, s, l, s.v1);
+  for (int r = l; r < s.nefc; r += NT) {
+    const T v = row_dot(s, r, s.qacc_ws, -s.efc_aref[r]);
+    const T bs = s.efc_bb[r];
+    s.efc_jar[r] = v;
+    s.ntmp[r] = r < s.ne || v < 0 ? T(0.5) * s.efc_D[r] * v * v : T(0);
+    s.efc_Jp[r] = r < s.ne || bs < 0 ? T(0.5) * s.efc_D[r] * bs * bs : T(0);
+  }
+  wsync();
+  island_sums2(s, s.v2, s.ntmp, s.isl_val, s.efc_Jp, s.isl_cost);
+  if (l < PH_MAXT) {
+    const bool ws = l < s.nisland && s.isl_val[l] < s.isl_cost[l];
+    s.isl_alpha[l] = ws ? T(1) : T(0);
+    if (ws) s.isl_cost[l] = s.isl_val[l];
+    s.isl_flag[l] = 0;
+    s.isl_hvalid[l] = 0;
+  }
+  wsync();
+  if (l < m.nv) s.x[l] = s.isl_alpha[s.tree_island[s.c_dof_tree[l]]] != T(0) ? s.qacc_ws[l] : s.qacc_smooth[l];
+  for (int r = l; r < s.nefc; r += NT) {
+    const T v = s.isl_alpha[s.tree_island[s.efc_t0[r]]] != T(0) ? s.efc_jar[r] : s.efc_bb[r];
+    s.efc_jar[r] = v;
+    s.efc_act[r] = r < s.ne || v < 0;
+  }
+  wsync();
+  clk.lap(8);
+  // lane I (< nisland) keeps island I's convergence state
+  T cost = l < s.nisland ? s.isl_cost[l] : T(0);
+  bool done = l >= s.nisland;
+  int unchanged = 0;                      // consecutive steps that kept the island's active set
+  // gradient floor of a converged island, scaled like MuJoCo's tests: 1 / (stat.meaninertia * nv)
+  const T gscale = T(1) / (m.meaninertia * T(m.nv > 1 ? m.nv : 1));
+  const T gtol = T(100) * PM<T>::eps();
+  int it = 0;
+  const int nent = s.isl_eoff[s.nisland];
+  const bool jt = s.jt_ok;
+  // group-parallel island factorisation when every island fits a 9-lane group
+  const bool gch = s.nisland <= GCH_GROUPS && !__ballot(l < s.nisland && s.isl_n[l] > GCH_N);
+  const int nisl = s.nisland;
+  for (; it < m.iterations; it++) {
+    clk.sub_start();
+    // gradient g = M (x - x_smooth) + J^T (D jar) over the dof's island rows
+    if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
+    if (jt)
+      for (int rr = l; rr < s.nefc; rr += NT) {
+        const int r = s.isl_row[rr];
+        const bool a = s.efc_act[r];
+        const T d = s.efc_D[r];
+        s.rr_f[rr] = a ? d * s.efc_jar[r] : T(0);
+        s.rr_d[rr] = a ? d : T(0);
+      }
+    wsync();
+    // islands with many rows (closed fingers: 200-400 rows on the arm island): J^T (D jar) on the
+    // whole wave -- lane (dof a, slice k) sums rows a + ... k, k + S, k + 2S .. (S = 64 / n
+    // slices), then lane a adds its S partials -- instead of one lane per dof walking every row;
+    // the sums land in v2 (dead here) for the dof lanes below
+    const uint32_t bigg = PNP_BIG_ISLANDS && jt ? (uint32_t)__ballot(l < nisl && s.isl_roff[l + 1] - s.isl_roff[l] > NT &&
+                                                                     s.isl_n[l] <= 32)
+                                                : 0u;
+    for (uint32_t bm = bigg; bm; bm &= bm - 1) {
+      const int I = __builtin_ctz(bm);
+      const int n = s.isl_n[I], r0 = s.isl_roff[I], nr = s.isl_roff[I + 1] - r0, S = NT / n;
+      const int a = l % n, k0 = l / n;
+      if (k0 < S) {
+        const T* col = s.jt + s.isl_joff[I] + a;
+        const T* fr = s.rr_f + r0;
+        T part = 0;
+        for (int k = k0; k < nr; k += S) part += col[k * n] * fr[k];
+        s.ntmp[l] = part;
+      }
+      wsync();
+      if (l < n) {
+        T g = 0;
+        for (int k = 0; k < S; k++) g += s.ntmp[l + k * n];
+        s.v2[s.isl_dof[I][l]] = g;
+      }
+      wsync();
+    }
+    if (l < m.nv) {
+      const int t = s.c_dof_tree[l], I = s.tree_island[t];
+      const T mv = mulM_row(m, s, l, s.v1);
+      const T g = (bigg >> I & 1u) ? mv + s.v2[l]
+                : jt ? jt_dof_sum(s, I, s.dof_ipos[l], mv, s.rr_f)
+                     : dof_row_sum(mv, s, I, t, l - s.c_tree_dofadr[t], s.efc_D, s.efc_jar, true);
+      s.grad[l] = g;
+      s.v2[l] = g * g;
+    }
+    wsync();
+    clk.sub_lap(SC_N_GRAD);
+    // an island whose last step kept its active set is at that quadratic's minimiser up to the
+    // rounding of one Cholesky solve (cond(H) eps): done once its gradient is at the floor,
+    // otherwise it takes one more (refining) Newton step
+    island_sums(s, s.v2, (const T*)nullptr, s.isl_val);
+    if (!done && unchanged >= 1 && PM<T>::sqrt_(s.isl_val[l]) * gscale < gtol) done = true;
+    if (l < PH_MAXT) s.isl_flag[l] = done;
+    wsync();
+    clk.sub_lap(SC_N_CONV);
+    if (!__ballot(!done)) { clk.lap(9); break; }
+    // Hessian island blocks (lower triangle, lane per entry): M + sum_active D J J^T; blocks of
+    // islands whose active set is unchanged since their last assembly are reused as they are;
+    // fp32 islands with many rows on the matrix cores (hess_mfma)
+    uint32_t bigh = 0;
+    if constexpr (sizeof(T) == 4 && PNP_BIG_ISLANDS) {
+      if (jt)
+        bigh = (uint32_t)__ballot(l < nisl && !s.isl_flag[l] && !s.isl_hvalid[l] &&
+                                  s.isl_roff[l + 1] - s.isl_roff[l] > NT && s.isl_n[l] <= 16);
+      for (uint32_t bm = bigh; bm; bm &= bm - 1) hess_mfma(s, __builtin_ctz(bm));
+    }
+    for (int e = l; e < nent; e += NT) {
+      // the entry's island: comparisons against the offsets (independent LDS loads issued
+      // together) instead of a loop that waits on one load per island
+      int I = 0;
+#pragma unroll
+      for (int J = 1; J <= PH_MAXT; J++) I += J < nisl && e >= s.isl_eoff[J] ? 1 : 0;
+      const int eI = s.isl_eoff[I], nI = s.isl_n[I], r0I = s.isl_roff[I], e1I = s.isl_roff[I + 1],
+                joI = s.isl_joff[I];
+      if (s.isl_flag[I] || s.isl_hvalid[I] || (bigh >> I & 1u)) continue;
+      const int le = e - eI;
+      int a = (int)((PM<float>::sqrt_(8.0f * le + 1.0f) - 1.0f) * 0.5f);
+      while (a * (a + 1) / 2 > le) a--;
+      while ((a + 1) * (a + 2) / 2 <= le) a++;
+      const int b = le - a * (a + 1) / 2;
+      const int i = s.isl_dof[I][a], j = s.isl_dof[I][b];
+      const int ti = s.c_dof_tree[i], tj = s.c_dof_tree[j];
+      T h = ti == tj ? s.M[mblk(m, i, j)] : T(0);
+      const int li = i - s.c_tree_dofadr[ti], lj = j - s.c_tree_dofadr[tj];
+      const int e1 = e1I;
+      if (jt) {
+        const int n = nI, r0 = r0I;
+        const T* ja = s.jt + joI + a;
+        const T* jb = s.jt + joI + b;
+        const T* dr = s.rr_d + r0;
+#pragma unroll 4
+        for (int k = 0; k < e1 - r0; k++) h += ja[k * n] * dr[k] * jb[k * n];
+      } else
+#pragma unroll 2
+      for (int rr = r0I; rr < e1; rr++) {   // unconditional loads (see own_slot)
+        const int r = s.isl_row[rr];
+        const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], off = s.efc_off[r];
+        const int n0 = s.c_tree_dofnum[t0];
+        const int ki = t0 == ti ? li : (t1 == ti ? n0 + li : -1);
+        const int kj = t0 == tj ? lj : (t1 == tj ? n0 + lj : -1);
+        const T c = s.efc_Jv[off + (ki >= 0 ? ki : 0)] * s.efc_D[r] * s.efc_Jv[off + (kj >= 0 ? kj : 0)];
+        h = ki >= 0 && kj >= 0 && s.efc_act[r] ? h + c : h;
+      }
+      s.Hp[e] = h;   // = HI(I, a, b)
+    }
+    wsync();
+    clk.sub_lap(SC_N_HESS);
+    clk.lap(9);
+    // Newton direction per island (lane per island); the register path leaves H intact, the
+    // in-place LDS path (merged islands > 9 dofs) consumes it
+    if (gch) {
+      newton_dir_groups(s, done);
+    } else {
+      // one unrolled register variant (islands of <= 9 dofs padded with identity): lanes holding
+      // 6- and 9-dof islands run the same code instead of two divergent copies; larger (merged)
+      // islands one after the other on the whole wave
+      const int n = !done ? s.isl_n[l] : 0;
+      if (!done && n <= 9) island_newton_dir_reg<T, 9>(s, l, n);
+      if (!done) s.isl_hvalid[l] = n <= 9;
+      wsync();
+      for (uint32_t bm = (uint32_t)__ballot(n > 9); bm; bm &= bm - 1) {
+        const int I = __builtin_ctz(bm), nI = s.isl_n[I];
+        island_newton_dir_wave<T, PH_MAXV>(s, I, nI);
+      }
+    }
+    wsync();
+    clk.lap(10);
+    clk.aux_start();
+    line_search_islands(m, s, clk);
+    clk.lap(11);
+    if (l < m.nv) s.x[l] += s.isl_alpha[s.tree_island[s.c_dof_tree[l]]] * s.p[l];
+    // remember the active set the step was computed with
+    for (int r = l; r < s.nefc; r += NT) s.efc_Jp[r] = (T)s.efc_act[r];
+    wsync();
+    eval_cost(m, s, s.x, true, s.isl_cost);
+    // active-set change per island (rows of island I on DPP row I & 3)
+    {
+      const int q = l & 7, I = l >> 3;
+      bool ch = false;
+      if (I < s.nisland)
+        for (int rr = s.isl_roff[I] + q; rr < s.isl_roff[I + 1]; rr += 8) {
+          const int r = s.isl_row[rr];
+          ch |= (T)s.efc_act[r] != s.efc_Jp[r];
+        }
+      const bool any = ((__ballot(ch) >> (l & 56)) & 0xFFull) != 0;
+      if (I < s.nisland && q == 0) s.isl_val[I] = any ? T(1) : T(0);
+    }
+    wsync();
+    // island converged: two consecutive steps kept its active set (then its piecewise quadratic
+    // is a single quadratic there and x its minimiser, refined once), or its cost stopped
+    // decreasing
+    if (!done) {
+      const bool changed = s.isl_val[l] != T(0);
+      const T nc = s.isl_cost[l];
+      const T impr = cost - nc;
+      unchanged = changed ? 0 : unchanged + 1;
+      if (changed) s.isl_hvalid[l] = 0;
+      if (unchanged >= 2 || !(impr > 0) || !(s.isl_alpha[l] > T(0))) done = true;
+      cost = nc;
+    }
+    wsync();
+    clk.lap(12);
+    if (!__ballot(!done)) { it++; break; }
+  }
+  clk.lap(12);
+  if (l == 0) s.solver_iter = it;
+  for (int r = l; r < s.nefc; r += NT) s.efc_force[r] = s.efc_act[r] ? -s.efc_D[r] * s.efc_jar[r] : T(0);
+  if (l < m.nv) s.qacc[l] = s.x[l];
+  wsync();
+}
+
+template <typename T, class CLK>
 __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
   const int l = lane_id();
+  if constexpr (sizeof(T) == 4) {
+    st_newton_islands(m, s, clk);
+    return;
+  }
   if (s.nefc == 0) {
     if (l < m.nv) s.qacc[l] = s.qacc_smooth[l];
     if (l == 0) s.solver_iter = 0;
@@ -2624,13 +3009,9 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   // -H^-1 g per island (H is block-diagonal over islands, so this is the problem's Newton
   // direction), one line search for the whole problem, stop at a zero step, then after each step
   // once scale (cost_old - cost) < tolerance or scale |g| < tolerance (scale = 1 / (meaninertia
-  // nv), the model statistic), or after `iterations` steps.  fp32 cannot resolve tolerance 1e-8
-  // in these sums, so the fp32 builds also stop at the rounding floor: the last step kept the
-  // active set (x at that quadratic's minimiser) and the scaled gradient is at fp32 rounding, or two
-  // steps in a row kept it.
+  // nv), the model statistic), or after `iterations` steps.  (fp64 only: st_newton_islands above.)
   T cost = l < nisl ? s.isl_cost[l] : T(0);   // lane I: island I's cost
   const bool idle = l >= nisl;                 // lane I: no island I
-  int unchanged = 0;                           // consecutive steps that kept the active set
   const T scale = T(1) / (m.meaninertia * T(m.nv > 1 ? m.nv : 1));
   T improvement = 0;
   int it = 0;
@@ -2691,9 +3072,7 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     clk.sub_lap(SC_N_GRAD);
     if (it > 0) {
       const T gradient = scale * PM<T>::sqrt_(wsum(g2));
-      bool stop = improvement < m.tolerance || gradient < m.tolerance;
-      if constexpr (sizeof(T) == 4) stop = stop || (unchanged >= 1 && gradient < T(100) * PM<T>::eps());
-      if (stop) { clk.sub_lap(SC_N_CONV); clk.lap(9); break; }
+      if (improvement < m.tolerance || gradient < m.tolerance) { clk.sub_lap(SC_N_CONV); clk.lap(9); break; }
     }
     clk.sub_lap(SC_N_CONV);
     if (it >= m.iterations) { clk.lap(9); break; }
@@ -2798,12 +3177,9 @@ __device__ void st_newton(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       if (changed) s.isl_hvalid[l] = 0;
       improvement = scale * wsum(cost - nc);
       cost = nc;
-      unchanged = __ballot(changed) ? 0 : unchanged + 1;
     }
     wsync();
     clk.lap(12);
-    if constexpr (sizeof(T) == 4)
-      if (unchanged >= 2) break;
   }
   clk.lap(12);
   if (l == 0) s.solver_iter = it;
@@ -3669,14 +4045,7 @@ __device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& 
   st_collision(m, s, clk);
   if (s.nconvex) {
     clk.sub_start();
-#if PNP_COMPACT
-    // The compact build runs no MPR: a live convex pair hands the sub-step to the full tier, like
-    // a capacity overflow (C3's settled envs keep none).  MPR is fp64 in every build (collide_dev.h)
-    // and the tiers' results must be the same bits; its code in this build grew the frames and
-    // the write-back of every launch (round 3: a convex contact's multiccd fan alone cost C3 1 %).
-    if (lane_id() == 0) CAP_FULL(8u);
-    wsync();
-#elif PNP_MW
+#if PNP_MW
     if constexpr (sizeof(T) == 4) {
       if (s.mw > 1) st_collision_convex_mw(s);
       else st_collision_convex(m, s);
@@ -3923,6 +4292,28 @@ int32_t step_wide_lds_bytes() { return (int32_t)sizeof(Env<float>); }
 
 #include "env_dev.h"   // the gym step's wide resume pass
 
+#elif PNP_WIDE64
+// fp64 wide tier: the resume pass of pnp_step_f64 after the full fp64 kernel handed an env over
+// (the single-env facade and the batched behaviour trees run in fp64; closed fingers on a cube make
+// more than the full tier's 48 contacts); truncates past its own capacities with a warning
+int32_t launch_step_wide64(const pnp_model* model, const pnp_state_t<double>* st, int32_t B, int32_t nsub,
+                           void* stream) {
+  const DevPhys<double>* src = phys_image<double>(model);
+  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  ResidentLease lease;
+  if (const int32_t rc = lease.acquire(RES_WIDE64_F64, model, (const void*)&g_phys_f64, src,
+                                       sizeof(DevPhys<double>), stream))
+    return rc;
+  auto k = step_kernel<double, false>;
+  hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, B, nsub, (unsigned long long*)nullptr, 1, 0);
+  if (const int32_t rc = pnp_check_launch("step_kernel (wide64)")) return rc;
+  return lease.launched();
+}
+
+int32_t step_wide64_lds_bytes() { return (int32_t)sizeof(Env<double>); }
+
+#include "env_dev.h"   // the fp64 gym step's wide resume pass
+
 #else
 
 template <typename T>
@@ -3982,6 +4373,17 @@ static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B
   auto k = prof ? step_kernel<T, true> : step_kernel<T, false>;
   const bool tiers = sizeof(T) == 4 && nsub <= PNP_RESUME_MAXSUB;   // the resume bits hold the sub-step
   const int wide = tiers && wide_enabled();
+  if constexpr (sizeof(T) == 8) {
+    // fp64: the full kernel, handing the sub-steps that outgrow it to the fp64 wide tier
+    const int w64 = nsub <= PNP_RESUME_MAXSUB && wide_enabled();
+    hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, nsub, prof, 0, w64);
+    if (const int32_t rc = pnp_check_launch("step_kernel (fp64)")) return rc;
+    if (w64)
+      if (const int32_t rc = launch_step_wide64(model, reinterpret_cast<const pnp_state_t<double>*>(st), B, nsub,
+                                                stream))
+        return rc;
+    return lease.launched();
+  }
   const auto* st32 = reinterpret_cast<const pnp_state_t<float>*>(st);
   if (tiers && compact_mode() == 3) {
     if (const int32_t rc = launch_step_wide(model, st32, B, nsub, stream, prof, 0)) return rc;

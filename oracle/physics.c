@@ -501,13 +501,13 @@ static double solver_scale(Mdl* m) {
   return 1.0 / (m->stat_meaninertia * (m->nv > 1 ? m->nv : 1));
 }
 
-/* Line search along p from x.  MuJoCo 2.3.3 PrimalLineSearch first returns 0 when the search
-   vector is below mjMINVAL or p is not a descent direction to within
-   gtol = tolerance * ls_tolerance * |p| / scale (ls_tolerance = 0.01, the mjOption default); then
-   it runs Newton steps on phi'(alpha) with bracketing until |phi'| < gtol.  Restated: the same two
-   exits, then the EXACT minimiser of the convex piecewise-quadratic phi(alpha) = cost(x + alpha p)
-   (breakpoints sorted; MuJoCo's iterate stops within gtol of it -- a declared deviation at the
-   1e-10 level) */
+/* Line search along p from x.  MuJoCo 2.3.3 PrimalLineSearch returns 0 when the search vector is
+   below mjMINVAL; otherwise it always takes one Newton step on phi'(alpha) from 0, then brackets
+   with further Newton steps until |phi'| < gtol = tolerance * ls_tolerance * |p| / scale
+   (ls_tolerance = 0.01).  Restated: the mjMINVAL exit, then the EXACT minimiser of the convex
+   piecewise-quadratic phi(alpha) = cost(x + alpha p) (breakpoints sorted), 0 when phi'(0) >= 0.
+   MuJoCo's first Newton step is that minimiser whenever it stays in phi's first quadratic piece;
+   otherwise its iterate stops within gtol of it -- a declared deviation, DESIGN.md §2. */
 static double line_search(Mdl* m, orc_data* d, const double* x, const double* p, const double* jar) {
   int nv = m->nv, ne = d->ne, n = d->nefc;
   double Mp[ORC_MAXV], dx[ORC_MAXV], Jp[ORC_MAXEFC];
@@ -515,7 +515,6 @@ static double line_search(Mdl* m, orc_data* d, const double* x, const double* p,
   for (int i = 0; i < nv; i++) snorm += p[i] * p[i];
   snorm = sqrt(snorm);
   if (snorm < ORC_MINVAL) return 0;
-  const double gtol = m->tolerance * 0.01 * snorm / solver_scale(m);
   for (int i = 0; i < nv; i++) dx[i] = x[i] - d->qacc_smooth[i];
   mulM(m, d, Mp, p);
   double A = 0, B = 0;
@@ -543,7 +542,7 @@ static double line_search(Mdl* m, orc_data* d, const double* x, const double* p,
     while (j >= 0 && brk[order[j]] > brk[t]) { order[j + 1] = order[j]; j--; }
     order[j + 1] = t;
   }
-  if (B >= -gtol) return 0;   /* phi'(0) = B: not a descent direction */
+  if (B >= 0) return 0;   /* phi'(0) = B: not a descent direction */
   for (int i = 0; i < nb; i++) {
     int r = order[i];
     double a = brk[r];

@@ -195,6 +195,23 @@ def _conditioning_floor(model, st, nsub=1, trials=3, per_env=False):
     return fv, fa
 
 
+def _knife_edge_envs(model, st, trials=3):
+    """Per env: the oracle's contact count is not the same on the state and on one-ulp fp32
+    perturbations of its qpos (the perturbations of _conditioning_floor)."""
+    rng = np.random.default_rng(2024)
+    cnt = lambda s, b: int(O.forward_fields({k: s[k][b] for k in O.STATE_KEYS}, ["ncon"], model=model)["ncon"][0])
+    B = st["qpos"].shape[0]
+    base = [cnt(st, b) for b in range(B)]
+    out = np.zeros(B, bool)
+    for _ in range(trials):
+        p = PS.copy_state(st)
+        x = p["qpos"].astype(np.float32)
+        up = rng.random(x.shape) < 0.5
+        p["qpos"] = np.where(up, np.nextafter(x, np.float32(np.inf)), np.nextafter(x, np.float32(-np.inf))).astype(np.float64)
+        out |= np.array([cnt(p, b) != base[b] for b in range(B)])
+    return out
+
+
 def _f32_tree_errors(engine, model, st, nsub=1, per_env=False):
     """Per tree: (dqvel M-norm relative error, M dqacc relative error) of the fp32 kernel against
     the oracle on identical (fp32-rounded) inputs; see the module docstring."""
@@ -213,11 +230,17 @@ def _f32_tree_errors(engine, model, st, nsub=1, per_env=False):
         ncon = [O.forward_fields({k: st[k][b] for k in O.STATE_KEYS}, ["ncon"], model=model)["ncon"][0]
                 for b in range(st["qpos"].shape[0])]
         # forward_debug runs the full tier alone (48 contacts, truncating like MuJoCo at a full
-        # buffer): only envs beyond that capacity are left out of M dqacc (their dqvel is checked)
-        qa_got = []
+        # buffer): envs beyond that capacity are left out of M dqacc (their dqvel is checked), and
+        # so are envs at a contact knife edge (the oracle's own contact count changes under a one-ulp
+        # perturbation of the state: pads touching at distance ~0); any other count difference fails
+        qa_got, knife = [], None
         for b in range(st["qpos"].shape[0]):
             same = int(dbg[b, D["COUNTS"]]) == int(ncon[b])
-            assert same or int(ncon[b]) > 48, f"env {b}: contact count {int(dbg[b, D['COUNTS']])} != oracle {int(ncon[b])}"
+            if not same and int(ncon[b]) <= 48:
+                knife = _knife_edge_envs(model, st) if knife is None else knife
+                assert knife[b], f"env {b}: contact count {int(dbg[b, D['COUNTS']])} != oracle {int(ncon[b])}"
+                print(f"env {b}: contact knife edge (kernel {int(dbg[b, D['COUNTS']])}, oracle {int(ncon[b])}): "
+                      f"M dqacc not compared")
             qa_got.append(dbg[b, D["QACC"]:D["QACC"] + nv] if same else None)
     return _tree_metrics(model, st, ref, got, qa_ref, qa_got, nsub, per_env)
 
@@ -456,7 +479,9 @@ def test_mesh_contacts_f64_match_oracle(engine, model, mesh_scene):
     mesh contacts and pairs with several contacts, and the fp64 kernel's contact list (order,
     positions, frames, depths), rows and solver outputs match the oracle's restatement."""
     n, fan = _mesh_contacts(engine, model, mesh_scene)
-    assert n >= 4 and fan >= 3, (n, fan)      # the fixture exercises MPR and the multiccd fan
+    # the fixture exercises MPR and the multiccd fan (trials rotate about the first contact since
+    # round 4: a face contact's fan adds the patch's other side, 2 contacts per pair here)
+    assert n >= 4 and fan >= 2, (n, fan)
     w = _forward_compare(engine, model, mesh_scene, torch.float64)
     assert max(w.values()) < 1e-9, w
 

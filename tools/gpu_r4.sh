@@ -8,7 +8,7 @@ OUT="$ROOT/gpurun_out"; mkdir -p "$OUT"; cd "$ROOT"
 TAG="${TAG:-r4}"
 TESTS="${TESTS:-tests}"
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v --timeout 240 --timeout-method thread ${PYK:+-k "$PYK"} > "$OUT/${TAG}_pytest.log" 2>&1
+timeout -k 10 1100 python -u -m pytest $TESTS -m gpu ${PYX--x} -v --timeout 240 --timeout-method thread ${PYK:+-k "$PYK"} > "$OUT/${TAG}_pytest.log" 2>&1
 rc=$?; tail -3 "$OUT/${TAG}_pytest.log"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: stop"; exit $rc; fi
 prc=$rc

@@ -47,6 +47,9 @@ def main():
                   "SQ_WAIT_INST_LDS"):
             if c in per:
                 print(f"  {c} / SQ_WAVE_CYCLES = {per[c] / wc:.3f}")
+        if "SQ_INSTS_VALU" in per:
+            print(f"  VALU pipe utilisation (2 cycles per VALU instruction, SQ_WAVE_CYCLES in quad-cycles, "
+                  f"{wps} waves per SIMD) = {min(1.0, wps * 2.0 * per['SQ_INSTS_VALU'] / (4.0 * wc)):.3f}")
     if jpath and wc and "SQ_ACTIVE_INST_VALU" in per:
         import json
         rec = {"kernel": kname, "waves_per_simd": wps,
@@ -55,6 +58,11 @@ def main():
                "insts_per_wave": {c: per[c] / w for c in per if c.startswith("SQ_INSTS_") and w},
                # the SIMD's vector ALU: each resident wave keeps it busy its own ACTIVE_INST_VALU share
                "valu_issue_frac": min(1.0, wps * per["SQ_ACTIVE_INST_VALU"] / wc),
+               # VALU pipe utilisation from instruction counts: a wave64 VALU instruction occupies the
+               # SIMD's pipe 2 cycles (MI355X_MICROARCH.md, hardware model) and SQ_WAVE_CYCLES counts
+               # quad-cycles (its PMC-units row), so a wave keeps the pipe busy 2 x SQ_INSTS_VALU of its
+               # 4 x SQ_WAVE_CYCLES, times the resident waves per SIMD
+               "valu_pipe_util": (min(1.0, wps * 2.0 * per["SQ_INSTS_VALU"] / (4.0 * wc)) if "SQ_INSTS_VALU" in per else None),
                "source": "rocprofv3 --pmc SQ_* (two passes of 8 SQ counters), tools/gpu_sq.sh"}
         json.dump(rec, open(jpath, "w"), indent=1)
 
