@@ -228,3 +228,64 @@ def test_multiccd_contact_fan(model):
     f_on = O.forward_fields(row, ["ncon"], model=model)["ncon"][0]
     f_off = O.forward_fields(row, ["ncon"], model=off)["ncon"][0]
     assert f_on > f_off
+
+
+def test_meaninertia_is_the_mean_diagonal_of_M_at_qpos0(model):
+    """stat.meaninertia (mj_setConst; scales the solvers' termination tests) = mean of diag(M) at
+    qpos0 with armature -- the compiler's value (Jacobian-sum M, setconst.py) against the oracle's
+    own CRBA at qpos0."""
+    st = PS.reset_states(1, seed=0, model=model)
+    st["qpos"][0] = model.qpos0
+    M = O.forward_fields(_row(st, 0), ["qM"], model=model)["qM"].reshape(model.nv, model.nv)
+    assert abs(model.stat_meaninertia - np.mean(np.diag(M))) <= 1e-12 * model.stat_meaninertia
+    assert model.opt_noslip_tolerance == 1e-6 and model.opt_tolerance == 1e-8 and model.opt_iterations == 100
+
+
+def _scale(model):
+    return 1.0 / (model.stat_meaninertia * max(1, model.nv))
+
+
+@pytest.mark.parametrize("kind", ["settled", "mesh"])
+def test_noslip_stops_by_mujoco_rule(model, kind):
+    """mj_solNoSlip's exit: sweep k ran only if sweep k-1's scaled improvement was >= noslip_tolerance,
+    and the solver stopped after the first sweep below it (or at noslip_iterations)."""
+    if kind == "settled":
+        st = PS.settled_states(8, seed=0, nsettle=60, model=model)
+    else:
+        import test_step_gpu as T
+        st = T.mesh_states(model)
+    tol, cap = model.opt_noslip_tolerance, model.opt_noslip_iterations
+    counts = []
+    for b in range(st["qpos"].shape[0]):
+        f = O.forward_fields(_row(st, b), ["noslip_improvement", "noslip_iter", "nefc"], model=model)
+        n, imp = int(f["noslip_iter"][0]), f["noslip_improvement"]
+        if int(f["nefc"][0]) == 0:
+            assert n == 0
+            continue
+        assert 1 <= n <= cap
+        assert all(imp[k] >= tol for k in range(n - 1))          # earlier sweeps did not stop it
+        assert imp[n - 1] < tol or n == cap                       # the last one did, or the cap
+        assert all(imp[k] == -1 for k in range(n, 8))             # no sweep past the exit
+        counts.append(n)
+    if kind == "settled":
+        assert set(counts) == {1}      # settled contacts: the first sweep's improvement is ~1e-20
+    else:
+        assert max(counts) == cap and min(counts) == 1
+
+
+def test_newton_stops_by_mujoco_rule(model):
+    """mj_solNewton's exits on the mesh fixture: after the last step the scaled improvement or the
+    scaled gradient is below tolerance (or the iteration cap); the scaled values are reported."""
+    import test_step_gpu as T
+    st = T.mesh_states(model)
+    tol = model.opt_tolerance
+    its = []
+    for b in range(st["qpos"].shape[0]):
+        f = O.forward_fields(_row(st, b), ["solver_iter", "solver_improvement", "solver_gradient", "nefc"],
+                             model=model)
+        it = int(f["solver_iter"][0])
+        its.append(it)
+        if it == 0 or it == model.opt_iterations:
+            continue
+        assert f["solver_improvement"][0] < tol or f["solver_gradient"][0] < tol, (b, f)
+    assert max(its) >= 2      # the fixture makes Newton iterate
