@@ -29,8 +29,13 @@ def test_execute_pnp_three_cubes():
     assert rw.min() >= -0.003 - 0.05 - 1e-6 and rw.max() <= 2 + 1 + 4 + 10 + 0.5 + 1e-6
     assert -300 < rw.sum() < 0.5 * 17.5 * len(rw)
     obj, tgt = r["objects"]["cube1"], r["targets"]["cube1"]
-    shelf_z = 0.73                                   # cube1 rests on the middle board (shelf_pnp.xml)
-    assert abs(obj[2] - shelf_z) > 0.05 or np.linalg.norm(obj - tgt) < 0.2, (obj, tgt)
+    # cube1 is placed: within the env's own success distance of its target (distance_threshold
+    # 0.05, shelf_pnp.py:22 / panda_env.py:303-306); measured 0.022 m.  Cubes 2 and 3 are knocked
+    # off their boards on the way (as in the reference's own runs: its VecNormalize pickle's last
+    # observations have the cubes at z = 0.02) -- printed, not pinned
+    assert np.linalg.norm(obj - tgt) < 0.05, (obj, tgt)
+    for n in ("cube2", "cube3"):
+        print(f"{n}: at {np.round(r['objects'][n], 3)}, target {r['targets'][n]}")
     # no contact / constraint buffer ever filled (CONTACTFULL 8, CNSTRFULL 16) and no bad-state
     # reset: the fp64 facade's physics kept every contact MuJoCo would
     assert r["warn"] == 0, r["warn"]
