@@ -221,6 +221,7 @@ struct Env {
   T efc_force[PH_MAXEFC], efc_jar[PH_MAXEFC], efc_Jp[PH_MAXEFC];
   int con_rbase[PH_MAXCON], con_sbase[PH_MAXCON], con_t[PH_MAXCON][2];
   unsigned char con_dim[PH_MAXCON];
+  T con_b[PH_MAXCON];          // contact: the reference acceleration's damping b (st_noslip's pair rows)
   int tree_island[PH_MAXT], isl_n[PH_MAXT];
   unsigned char isl_dof[PH_MAXT][PH_MAXV];
   int isl_eoff[PH_MAXT + 1], isl_roff[PH_MAXT + 1];
@@ -1828,6 +1829,7 @@ __device__ void st_constraints(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s
     s.efc_t0[r] = t0; s.efc_t1[r] = t1;
     s.efc_type[r] = 6; s.efc_id[r] = c;
     row_imp(m, s, r, con.dist, con.includemargin, tran + fri * fri * (k < 3 ? tran : rot), con.solref, con.solimp);
+    if (q == 0) s.con_b[c] = s.efc_Jp[r];   // (row_imp parks b there; the same for every row of c)
   }
   if (l == 0) {
     s.nefc = kept_rows;
@@ -3215,12 +3217,12 @@ __device__ __forceinline__ void tree_solve_fixed(const T* L, const T* j, T* x_ou
 }
 
 // Dense long-list sweep (st_noslip): the group's island v in registers, lane q = island dof q;
-// each pair's J and W rows are read at the lane's island position straight from the dense
-// blocks (jt, and W in jt's layout), its 2 x 2 Delassus block from the per-call table (efc_jar /
-// efc_Jp at the pair's island row position, both dead after the Newton stage), so an update is
-// two row sums of J v, the projection and a lane-local v += W df.  List entries are island row
-// positions.  Software pipeline: list entry 3 pairs ahead, the row's efc index 2 ahead, its
-// J / W / b / f / Delassus entries 1 ahead.  Islands are independent under Gauss-Seidel: a group
+// each pair's difference rows Jd, Wd are formed at the lane's island position straight from the
+// dense blocks (jt, and W in jt's layout), its K1 and 1 / K1 from the per-call table (efc_jar at
+// the pair's island row positions, dead after the Newton stage), so an update is one row sum of
+// Jd v, the projection and a lane-local v += Wd dl.  List entries are island row positions.
+// Software pipeline: list entry 3 pairs ahead, the row's efc index 2 ahead, its
+// J / W / bd / f / K1 entries 1 ahead.  Islands are independent under Gauss-Seidel: a group
 // sweeps its (<= 2) islands one after the other, each in its own row order.
 template <typename T>
 __device__ __attribute__((noinline)) void st_noslip_dense_sweep(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
@@ -3238,21 +3240,11 @@ __device__ __attribute__((noinline)) void st_noslip_dense_sweep(const DevPhys<T>
       const int o = s.isl_joff[I] + (p - s.isl_roff[I]) * n;
       const T* J = s.jt + o;
       const T* W = s.efc_Wv + o;
-      T a00 = 0, a01 = 0, a10 = 0, a11 = 0;
-      for (int c = 0; c < n; c++) {
-        const T j0 = J[c], j1 = J[n + c], w0 = W[c], w1 = W[n + c];
-        a00 += j0 * w0;
-        a01 += j0 * w1;
-        a10 += j1 * w0;
-        a11 += j1 * w1;
-      }
-      // the projection's coefficients (see update below); 1 / K1 = 0 for a flat pair (K1 < 1e-15),
-      // whose forces then stay at their mean
-      const T K1 = a00 + a11 - a01 - a10;
-      s.efc_jar[p] = a00 - a11;
-      s.efc_jar[p + 1] = a00 - a10;
-      s.efc_Jp[p] = a01 - a11;
-      s.efc_Jp[p + 1] = K1 < T(1e-15) ? T(0) : T(1) / K1;
+      T K1 = 0;   // Jd . Wd (st_noslip)
+      for (int c = 0; c < n; c++) K1 += (J[c] - J[n + c]) * (W[c] - W[n + c]);
+      // 1 / K1 = 0 for a flat pair (K1 < 1e-15), whose forces then stay at their mean
+      s.efc_jar[p] = K1;
+      s.efc_jar[p + 1] = K1 < T(1e-15) ? T(0) : T(1) / K1;
     }
   }
   wsync();
@@ -3286,7 +3278,7 @@ __device__ __attribute__((noinline)) void st_noslip_dense_sweep(const DevPhys<T>
   struct DRaw {   // stage 1
     int j;
     bool act;
-    T Jd, W0, W1, bd, f0, f1, pc, u, w, iK1;
+    T Jd, Wd, bd, f0, f1, K1, iK1;
   };
   // one Gauss-Seidel sweep over the set's island; returns the group's improvement (MuJoCo
   // costChange summed over the pair updates; uniform in the group's 16 lanes)
@@ -3307,35 +3299,30 @@ __device__ __attribute__((noinline)) void st_noslip_dense_sweep(const DevPhys<T>
       const T J0 = s.jt[o], J1 = s.jt[o + z.n], W0 = s.efc_Wv[o], W1 = s.efc_Wv[o + z.n];
       const bool on = x.act && z.lane_on;
       w.Jd = on ? J0 - J1 : T(0);
-      w.W0 = on ? W0 : T(0);
-      w.W1 = on ? W1 : T(0);
-      w.bd = s.efc_bb[x.j] - s.efc_bb[x.j + 1];
+      w.Wd = on ? W0 - W1 : T(0);
+      w.bd = s.efc_bb[x.j];
       w.f0 = s.efc_force[x.j];
       w.f1 = s.efc_force[x.j + 1];
-      w.pc = s.efc_jar[x.p];
-      w.u = s.efc_jar[x.p + 1];
-      w.w = s.efc_Jp[x.p];
-      w.iK1 = s.efc_Jp[x.p + 1];
+      w.K1 = s.efc_jar[x.p];
+      w.iK1 = s.efc_jar[x.p + 1];
       return w;
     };
     T impr = 0;
-    // The pair's 2 x 2 projection (the streaming path's, rearranged): with r = J v + b and
-    // A the Delassus block, K0 = mid (a00 - a11) + (r0 - r1) - (a00 - a10) f0 - (a01 - a11) f1,
-    // y = clamp(-K0 / K1, +-mid) -- only r0 - r1 = (J0 - J1) v + b0 - b1 is needed, one row sum
-    // instead of two, and the per-pair coefficients come from the table.  An inactive slot has
-    // zero J and W, so v does not move.  The update moves the forces along (1, -1) by dl, so
-    // MuJoCo's costChange 0.5 d^T A d + d^T r is dl (0.5 dl K1 + (r0 - r1)), K1 = u - w.
+    // The pair's 2 x 2 projection on its difference row (st_noslip): r0 - r1 = Jd v + bd (one
+    // row sum), y = clamp((f0 - mid) - (r0 - r1) / K1, +-mid) (= -K0 / K1), K1 and 1 / K1 from
+    // the table.  An inactive slot has zero Jd and Wd, so v does not move.  The update moves the
+    // forces along (1, -1) by dl, so MuJoCo's costChange 0.5 d^T A d + d^T r is
+    // dl (0.5 dl K1 + (r0 - r1)), and v moves by Wd dl.
     auto update = [&](const DRaw& cur) {
       const T rd = rowsum16(cur.Jd * v) + cur.bd;
       const T f0 = cur.f0, f1 = cur.f1;
       const T mid = T(0.5) * (f0 + f1);
-      const T K0 = mid * cur.pc + rd - cur.u * f0 - cur.w * f1;
-      T y = -K0 * cur.iK1;
+      T y = cur.iK1 != T(0) ? (f0 - mid) - rd * cur.iK1 : T(0);
       y = y < -mid ? -mid : (y > mid ? mid : y);
       const T n0 = mid + y, n1 = mid - y;
       const T dl = T(0.5) * ((n0 - f0) - (n1 - f1));
-      impr = cur.act ? impr - dl * (T(0.5) * dl * (cur.u - cur.w) + rd) : impr;
-      v += cur.W0 * (n0 - f0) + cur.W1 * (n1 - f1);
+      impr = cur.act ? impr - dl * (T(0.5) * dl * cur.K1 + rd) : impr;
+      v += cur.Wd * dl;
       if (cur.act && q == 0) { s.efc_force[cur.j] = n0; s.efc_force[cur.j + 1] = n1; }
     };
     // unrolled by two with the stage registers alternating (ra / rb), so that the loop carries
@@ -3421,6 +3408,29 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       else iend1 = len;
     }
     if (q == 0) s.ns_len[grp] = len;
+  }
+  // Every path below updates a pair (rows j, j + 1 = J_n +- mu J_t of one contact) through its
+  // difference row Jd = J_j - J_j+1 (= 2 mu J_t) and Wd = W_j - W_j+1 = M^-1 Jd^T: with r = J v + b
+  // and A = J W (symmetric), MuJoCo's K1 = a00 + a11 - a01 - a10 is Jd . Wd and its
+  // K0 = mid (a00 - a11) + bc0 - bc1 is (r0 - r1) + K1 (mid - f0) -- the same projection, without
+  // forming K1 and K0 as differences of Delassus entries: between two bodies of one tree (closed
+  // fingers pressed together) J_t is small against J_n, K1 ~ 1e-6 beside entries ~20, and the
+  // differences of fp32 entries are rounding (the fp32 kernel then left pairs at their mean
+  // that MuJoCo saturates: fingers 0.07 m/s^2 off).  r0 - r1 = Jd . v + (b0 - b1), and b0 - b1 =
+  // Jd . qacc_smooth - (aref0 - aref1) with aref0 - aref1 = -b Jd . qvel (the two rows share the
+  // contact's position term): bd = Jd . (qacc_smooth + b qvel), replacing efc_bb[j] (dead after
+  // Newton) for the sweeps.
+  for (int r = l; r < s.nefc; r += NT) {
+    if (s.efc_type[r] != 6 || ((r - s.con_rbase[s.efc_id[r]]) & 1) != 0) continue;
+    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
+    const int o0 = s.efc_off[r], o1 = s.efc_off[r + 1];
+    const T b = s.con_b[s.efc_id[r]];
+    T bd = 0;
+    for (int k = 0; k < w; k++) {
+      const int d = slot_dof(m, t0, t1, k);
+      bd += (s.efc_Jv[o0 + k] - s.efc_Jv[o1 + k]) * (s.qacc_smooth[d] + b * s.qvel[d]);
+    }
+    s.efc_bb[r] = bd;
   }
   wsync();
   const int maxlen = max(max(s.ns_len[0], s.ns_len[1]), max(s.ns_len[2], s.ns_len[3]));
@@ -3540,7 +3550,7 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   struct NsPair {
     int j, d;
     bool act, on;
-    T J0, J1, W0, W1, b0, b1;
+    T Jd, Wd, bd;   // the pair's difference row (see above)
   };
   auto fetch = [&](int k) {
     NsPair p;
@@ -3553,121 +3563,111 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     p.d = p.on ? slot_dof(m, t0, t1, qq) : 0;
     const T J0 = s.efc_Jv[o0 + qq], J1 = s.efc_Jv[o1 + qq];
     const T W0 = s.efc_Wv[o0 + qq], W1 = s.efc_Wv[o1 + qq];
-    p.J0 = p.on ? J0 : T(0);
-    p.J1 = p.on ? J1 : T(0);
-    p.W0 = p.on ? W0 : T(0);
-    p.W1 = p.on ? W1 : T(0);
-    p.b0 = s.efc_bb[p.j];
-    p.b1 = s.efc_bb[p.j + 1];
+    p.Jd = p.on ? J0 - J1 : T(0);
+    p.Wd = p.on ? W0 - W1 : T(0);
+    p.bd = s.efc_bb[p.j];
     return p;
   };
   // Short sweeps (every group's list <= NSR pairs, the common case: an island of a box resting on
-  // a board has 8) keep the whole sweep in registers: each pair's J / W slots, its 2 x 2 Delassus
-  // block (fixed over the iterations), b and its two forces (only this pair writes them).  An
-  // update is then one LDS read of v at the slot's dof, two row sums, the 2 x 2 projection and
-  // the write back of v; the forces return to LDS once, after the last iteration.  Same
-  // arithmetic in the same order as the streaming path below.
+  // a board has 8) keep the whole sweep in registers.
   // Force space (the common case: every group's pairs act on the same trees, so their packed
-  // slots address the same dofs): lane q of a group owns pair-row q (pair q / 2, edge q & 1) of
-  // the group's list and keeps its residual r_q = J_q v + b_q and its row of the Delassus block
-  // A_qj = J_q W_j (j over the group's pair rows) in registers.  A pair update reads its two
-  // residuals and A entries by DPP row broadcasts, projects as below, and adds A(:, pair) df to
-  // every lane's residual -- r = J (v0 + W df) + b without the v round trip through LDS and
-  // the two row sums per update.  Same projection arithmetic; residuals differ from the
-  // v-space sweep by rounding only.
+  // slots address the same dofs): lane q of a group owns pair q of the group's list and keeps its
+  // difference residual rd_q = Jd_q v + bd_q and its row of the difference Delassus block
+  // Ad_qj = Jd_q . Wd_j (j over the group's pairs; Ad_qq = K1_q) in registers.  A pair update
+  // reads its residual and K1 by DPP row broadcasts, projects as below, and adds Ad(:, pair) dl to
+  // every lane's residual -- rd = Jd (v0 + Wd dl) + bd without the v round trip through LDS and
+  // the row sum per update.  Same projection; residuals differ from the v-space sweep by rounding.
   {
     bool uni = true;
-    int jr = 0, off = 0, w = 0;
-    const bool mine = q < 2 * glen && q < 2 * NSR;
+    int jr = 0, o0 = 0, o1 = 0, w = 0;
+    const bool mine = q < glen && q < NSR;
     if (mine) {
-      jr = s.ns_list[grp][q >> 1] + (q & 1);
+      jr = s.ns_list[grp][q];
       const int j0 = s.ns_list[grp][0];
       uni = s.efc_t0[jr] == s.efc_t0[j0] && s.efc_t1[jr] == s.efc_t1[j0];
-      off = s.efc_off[jr];
+      o0 = s.efc_off[jr];
+      o1 = s.efc_off[jr + 1];
       w = row_width(m, s.efc_t0[jr], s.efc_t1[jr]);
     }
     if (maxlen <= NSR && !__ballot(!uni)) {
-      T r = 0, A[2 * NSR];
+      T rd = 0, Ad[NSR];
       if (!__ballot(mine && w > 8)) {
         // rows of <= 8 slots (a free body against the world): fully unrolled, every load of a
         // row issued back to back
         const int t0 = s.efc_t0[jr], t1 = s.efc_t1[jr];
         const int n0 = s.c_tree_dofnum[t0], d0 = s.c_tree_dofadr[t0];
         const int d1 = t1 >= 0 ? s.c_tree_dofadr[t1] - n0 : 0;
-        // 8 slots read per row with no masking of the loads: Jq is zero past the row's width and
+        // 8 slots read per row with no masking of the loads: Jd is zero past the row's width and
         // the W slots past a contact row are the next contact row's or the zeroed tail
-        T Jq[8];
-        r = mine ? s.efc_bb[jr] : T(0);
+        T Jd[8];
+        rd = mine ? s.efc_bb[jr] : T(0);
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-          const T jv = s.efc_Jv[off + k];
+          const T jd = s.efc_Jv[o0 + k] - s.efc_Jv[o1 + k];
           const T vd = s.v2[k < n0 ? d0 + k : (d1 + k < PH_MAXV ? d1 + k : 0)];
-          Jq[k] = mine && k < w ? jv : T(0);
-          r += Jq[k] * vd;
+          Jd[k] = mine && k < w ? jd : T(0);
+          rd += Jd[k] * vd;
         }
 #pragma unroll
-        for (int j = 0; j < 2 * NSR; j++) {
-          const int oj = s.efc_off[s.ns_list[grp][j < 2 * glen ? j >> 1 : 0] + (j & 1)];
-          const T* W = s.efc_Wv + oj;
+        for (int j = 0; j < NSR; j++) {
+          const int jj = s.ns_list[grp][j < glen ? j : 0];
+          const T* W0 = s.efc_Wv + s.efc_off[jj];
+          const T* W1 = s.efc_Wv + s.efc_off[jj + 1];
           T a = 0;
 #pragma unroll
-          for (int k = 0; k < 8; k++) a += Jq[k] * W[k];
-          A[j] = j < 2 * glen ? a : T(0);
+          for (int k = 0; k < 8; k++) a += Jd[k] * (W0[k] - W1[k]);
+          Ad[j] = j < glen ? a : T(0);
         }
       } else {
         if (mine) {
           const int t0 = s.efc_t0[jr], t1 = s.efc_t1[jr];
-          r = s.efc_bb[jr];
-          for (int k = 0; k < w; k++) r += s.efc_Jv[off + k] * s.v2[slot_dof(m, t0, t1, k)];
+          rd = s.efc_bb[jr];
+          for (int k = 0; k < w; k++) rd += (s.efc_Jv[o0 + k] - s.efc_Jv[o1 + k]) * s.v2[slot_dof(m, t0, t1, k)];
         }
 #pragma unroll
-        for (int j = 0; j < 2 * NSR; j++) {
+        for (int j = 0; j < NSR; j++) {
           T a = 0;
-          if (mine && j < 2 * glen) {
-            const int oj = s.efc_off[s.ns_list[grp][j >> 1] + (j & 1)];
-            for (int k = 0; k < w; k++) a += s.efc_Jv[off + k] * s.efc_Wv[oj + k];
+          if (mine && j < glen) {
+            const int jj = s.ns_list[grp][j];
+            const int p0 = s.efc_off[jj], p1 = s.efc_off[jj + 1];
+            for (int k = 0; k < w; k++)
+              a += (s.efc_Jv[o0 + k] - s.efc_Jv[o1 + k]) * (s.efc_Wv[p0 + k] - s.efc_Wv[p1 + k]);
           }
-          A[j] = a;
+          Ad[j] = a;
         }
       }
-      // per pair: the projection's coefficients from its 2 x 2 Delassus block (see NS_UPD)
-      T F0[NSR], F1[NSR], PC[NSR], PU[NSR], PW[NSR], IK[NSR];
+      // per pair: K1 (its own Ad diagonal) and 1 / K1 (0 for a flat pair: forces stay at their mean)
+      T F0[NSR], F1[NSR], KK[NSR], IK[NSR];
 #pragma unroll
       for (int k = 0; k < NSR; k++) {
         const int jk = k < glen ? s.ns_list[grp][k] : 0;
         F0[k] = s.efc_force[jk];
         F1[k] = s.efc_force[jk + 1];
       }
-#define NS_BC(K)                                                                          \
-      {                                                                                   \
-        const T a00 = rowbcast<2 * K>(A[2 * K]), a01 = rowbcast<2 * K>(A[2 * K + 1]);     \
-        const T a10 = rowbcast<2 * K + 1>(A[2 * K]), a11 = rowbcast<2 * K + 1>(A[2 * K + 1]); \
-        const T K1 = a00 + a11 - a01 - a10;                                               \
-        PC[K] = a00 - a11; PU[K] = a00 - a10; PW[K] = a01 - a11;                          \
-        IK[K] = K1 < T(1e-15) ? T(0) : T(1) / K1;                                         \
+#define NS_BC(K)                                  \
+      {                                           \
+        const T k1 = rowbcast<K>(Ad[K]);          \
+        KK[K] = k1;                               \
+        IK[K] = k1 < T(1e-15) ? T(0) : T(1) / k1; \
       }
       NS_BC(0) NS_BC(1) NS_BC(2) NS_BC(3) NS_BC(4) NS_BC(5) NS_BC(6) NS_BC(7)
 #undef NS_BC
       int iter = 0;
       while (iter < m.noslip_iterations) {
         T impr = 0;
-      // the 2 x 2 projection rearranged as in st_noslip_dense_sweep: K0 = mid (a00 - a11) +
-      // (r0 - r1) - (a00 - a10) f0 - (a01 - a11) f1, y = clamp(-K0 / K1, +-mid), 1 / K1 = 0 for
-      // a flat pair (its forces stay at their mean)
+      // the 2 x 2 projection on the difference row (st_noslip_dense_sweep's update)
 #define NS_UPD(K)                                                                          \
         if (K < maxlen) {                                                                 \
-          const T rd = rowbcast<2 * K>(r) - rowbcast<2 * K + 1>(r);                      \
+          const T rdk = rowbcast<K>(rd);                                                  \
           const T f0 = F0[K], f1 = F1[K];                                                 \
           const T mid = T(0.5) * (f0 + f1);                                               \
-          const T K0 = mid * PC[K] + rd - PU[K] * f0 - PW[K] * f1;                         \
-          T y = -K0 * IK[K];                                                              \
+          T y = IK[K] != T(0) ? (f0 - mid) - rdk * IK[K] : T(0);                          \
           y = y < -mid ? -mid : (y > mid ? mid : y);                                      \
           const T n0 = mid + y, n1 = mid - y;                                             \
           const bool act = K < glen;                                                      \
-          const T d0 = act ? n0 - f0 : T(0), d1 = act ? n1 - f1 : T(0);                   \
-          r += A[2 * K] * d0 + A[2 * K + 1] * d1;                                         \
-          const T dl = T(0.5) * (d0 - d1);                                                \
-          impr -= dl * (T(0.5) * dl * (PU[K] - PW[K]) + rd);                              \
+          const T dl = act ? T(0.5) * ((n0 - f0) - (n1 - f1)) : T(0);                     \
+          rd += Ad[K] * dl;                                                               \
+          impr -= dl * (T(0.5) * dl * KK[K] + rdk);                                       \
           if (act) { F0[K] = n0; F1[K] = n1; }                                            \
         }
         NS_UPD(0) NS_UPD(1) NS_UPD(2) NS_UPD(3) NS_UPD(4) NS_UPD(5) NS_UPD(6) NS_UPD(7)
@@ -3729,7 +3729,7 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
       struct DRaw {   // stage 3
         int j;
         bool act;
-        T J0, J1, W0, W1, b0, b1, f0, f1;
+        T Jd, Wd, bd, f0, f1;
       };
       // one sweep of the set's island, v in registers (lane q = island dof q); returns the group's
       // improvement.  Software pipeline over the pairs, one LDS level per stage, so that no wait
@@ -3759,12 +3759,9 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
           p.act = x.act;
           const T J0 = s.efc_Jv[x.off0 + sl], J1 = s.efc_Jv[x.off1 + sl];
           const T W0 = s.efc_Wv[x.off0 + sl], W1 = s.efc_Wv[x.off1 + sl];
-          p.J0 = on ? J0 : T(0);
-          p.J1 = on ? J1 : T(0);
-          p.W0 = on ? W0 : T(0);
-          p.W1 = on ? W1 : T(0);
-          p.b0 = s.efc_bb[x.j];
-          p.b1 = s.efc_bb[x.j + 1];
+          p.Jd = on ? J0 - J1 : T(0);
+          p.Wd = on ? W0 - W1 : T(0);
+          p.bd = s.efc_bb[x.j];
           p.f0 = s.efc_force[x.j];
           p.f1 = s.efc_force[x.j + 1];
           return p;
@@ -3777,22 +3774,18 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
           const int j3 = dlist(k + 3);
           const DRow x2 = drow(j2);
           const DRaw nxt = draw(x1);
-          const T a00 = rowsum16(cur.J0 * cur.W0), a01 = rowsum16(cur.J0 * cur.W1);
-          const T a10 = rowsum16(cur.J1 * cur.W0), a11 = rowsum16(cur.J1 * cur.W1);
-          const T r0 = rowsum16(cur.J0 * v) + cur.b0;
-          const T r1 = rowsum16(cur.J1 * v) + cur.b1;
+          // the projection on the pair's difference row (st_noslip_dense_sweep's update)
+          const T K1 = rowsum16(cur.Jd * cur.Wd);
+          const T rd = rowsum16(cur.Jd * v) + cur.bd;
           const T f0 = cur.f0, f1 = cur.f1;
-          const T bc0 = r0 - (a00 * f0 + a01 * f1), bc1 = r1 - (a10 * f0 + a11 * f1);
           const T mid = T(0.5) * (f0 + f1);
-          const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;
-          T y = -K0 / K1;
-          y = y < -mid ? -mid : (y > mid ? mid : y);
           const bool flat = K1 < T(1e-15);
-          const T n0 = flat ? mid : mid + y, n1 = flat ? mid : mid - y;
-          const T d0 = cur.act ? n0 - f0 : T(0), d1 = cur.act ? n1 - f1 : T(0);
-          const T dl = T(0.5) * (d0 - d1);
-          impr -= dl * (T(0.5) * dl * K1 + (r0 - r1));
-          v += cur.W0 * d0 + cur.W1 * d1;
+          T y = flat ? T(0) : (f0 - mid) - rd / K1;
+          y = y < -mid ? -mid : (y > mid ? mid : y);
+          const T n0 = mid + y, n1 = mid - y;
+          const T dl = cur.act ? T(0.5) * ((n0 - f0) - (n1 - f1)) : T(0);
+          impr -= dl * (T(0.5) * dl * K1 + rd);
+          v += cur.Wd * dl;
           if (cur.act && q == 0) { s.efc_force[cur.j] = n0; s.efc_force[cur.j + 1] = n1; }
           cur = nxt;
           x1 = x2;
@@ -3818,14 +3811,13 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   }
   if (maxlen <= NSR) {
     NsPair P[NSR];
-    T A00[NSR], A01[NSR], A10[NSR], A11[NSR], F0[NSR], F1[NSR];
+    T K1s[NSR], F0[NSR], F1[NSR];
 #pragma unroll
     for (int k = 0; k < NSR; k++) {
       P[k] = fetch(k < maxlen ? k : 0);
       P[k].act = P[k].act && k < maxlen;
       P[k].on = P[k].on && k < maxlen;
-      A00[k] = rowsum16(P[k].J0 * P[k].W0); A01[k] = rowsum16(P[k].J0 * P[k].W1);
-      A10[k] = rowsum16(P[k].J1 * P[k].W0); A11[k] = rowsum16(P[k].J1 * P[k].W1);
+      K1s[k] = rowsum16(P[k].Jd * P[k].Wd);
       F0[k] = s.efc_force[P[k].j];
       F1[k] = s.efc_force[P[k].j + 1];
     }
@@ -3837,23 +3829,16 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
         if (k >= maxlen) break;
         const NsPair& cur = P[k];
         const T vd = cur.on ? s.v2[cur.d] : T(0);
-        const T r0 = rowsum16(cur.J0 * vd) + cur.b0;
-        const T r1 = rowsum16(cur.J1 * vd) + cur.b1;
+        const T rd = rowsum16(cur.Jd * vd) + cur.bd;
         const T f0 = F0[k], f1 = F1[k];
-        const T a00 = A00[k], a01 = A01[k], a10 = A10[k], a11 = A11[k];
-        const T bc0 = r0 - (a00 * f0 + a01 * f1), bc1 = r1 - (a10 * f0 + a11 * f1);
         const T mid = T(0.5) * (f0 + f1);
-        const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;
-        T n0, n1;
-        if (K1 < T(1e-15)) { n0 = n1 = mid; }
-        else {
-          T y = -K0 / K1;
-          if (y < -mid) y = -mid; else if (y > mid) y = mid;
-          n0 = mid + y; n1 = mid - y;
-        }
-        if (cur.on) s.v2[cur.d] = vd + (cur.W0 * (n0 - f0) + cur.W1 * (n1 - f1));
+        const T K1 = K1s[k];
+        T y = K1 < T(1e-15) ? T(0) : (f0 - mid) - rd / K1;
+        if (y < -mid) y = -mid; else if (y > mid) y = mid;
+        const T n0 = mid + y, n1 = mid - y;
         const T dl = T(0.5) * ((n0 - f0) - (n1 - f1));
-        impr = cur.act ? impr - dl * (T(0.5) * dl * K1 + (r0 - r1)) : impr;
+        if (cur.on) s.v2[cur.d] = vd + cur.Wd * dl;
+        impr = cur.act ? impr - dl * (T(0.5) * dl * K1 + rd) : impr;
         if (cur.act) { F0[k] = n0; F1[k] = n1; }
         wsync();
       }
@@ -3875,24 +3860,16 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     for (int k = 0; k < maxlen; k++) {
       const NsPair nxt = fetch(k + 1 < maxlen ? k + 1 : k);
       const T vd = cur.on ? s.v2[cur.d] : T(0);
-      const T a00 = rowsum16(cur.J0 * cur.W0), a01 = rowsum16(cur.J0 * cur.W1);
-      const T a10 = rowsum16(cur.J1 * cur.W0), a11 = rowsum16(cur.J1 * cur.W1);
-      const T r0 = rowsum16(cur.J0 * vd) + cur.b0;
-      const T r1 = rowsum16(cur.J1 * vd) + cur.b1;
+      const T K1 = rowsum16(cur.Jd * cur.Wd);
+      const T rd = rowsum16(cur.Jd * vd) + cur.bd;
       const T f0 = s.efc_force[cur.j], f1 = s.efc_force[cur.j + 1];
-      const T bc0 = r0 - (a00 * f0 + a01 * f1), bc1 = r1 - (a10 * f0 + a11 * f1);
       const T mid = T(0.5) * (f0 + f1);
-      const T K1 = a00 + a11 - a01 - a10, K0 = mid * (a00 - a11) + bc0 - bc1;
-      T n0, n1;
-      if (K1 < T(1e-15)) { n0 = n1 = mid; }
-      else {
-        T y = -K0 / K1;
-        if (y < -mid) y = -mid; else if (y > mid) y = mid;
-        n0 = mid + y; n1 = mid - y;
-      }
-      if (cur.on) s.v2[cur.d] += cur.W0 * (n0 - f0) + cur.W1 * (n1 - f1);
+      T y = K1 < T(1e-15) ? T(0) : (f0 - mid) - rd / K1;
+      if (y < -mid) y = -mid; else if (y > mid) y = mid;
+      const T n0 = mid + y, n1 = mid - y;
       const T dl = T(0.5) * ((n0 - f0) - (n1 - f1));
-      impr = cur.act ? impr - dl * (T(0.5) * dl * K1 + (r0 - r1)) : impr;
+      if (cur.on) s.v2[cur.d] += cur.Wd * dl;
+      impr = cur.act ? impr - dl * (T(0.5) * dl * K1 + rd) : impr;
       if (cur.act && q == 0) { s.efc_force[cur.j] = n0; s.efc_force[cur.j + 1] = n1; }
       wsync();
       cur = nxt;

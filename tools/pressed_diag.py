@@ -81,3 +81,107 @@ def variants():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "variants":
     variants()
+
+
+def fingers_only():
+    """The pressed states with the pad boxes out of collision (contype = conaffinity = 0 on both
+    sides): only the finger meshes' pair (72, 80) and the hand pair remain, within the full tier's
+    48 contacts, so forward_debug's contact list (full tier) compares with the oracle's contact by
+    contact; then the per-tree fp32 step error."""
+    from pnp_amd import _lib
+    from pnp_amd.engine import Engine
+    from pnp_amd.model import PandaModel
+    D = _lib.DBG
+    m = PandaModel()
+    for g in list(range(73, 78)) + list(range(81, 86)):
+        m.geom_contype[g] = 0
+        m.geom_conaffinity[g] = 0
+    m._desc = None
+    eng = Engine(model=m, device=get_engine().device)
+    st = T._round32(pressed(m))
+    dbg = eng.forward_debug(T._dev(st, torch.float32)).cpu().numpy()
+    np.set_printoptions(precision=7, suppress=False, linewidth=200)
+    for b in range(st["qpos"].shape[0]):
+        f = O.forward_fields({k: st[k][b] for k in O.STATE_KEYS}, ["contact", "ncon", "solver_iter"], model=m)
+        n = int(f["ncon"][0])
+        c = f["contact"].reshape(n, 30)
+        kn = int(dbg[b, D["COUNTS"]])
+        kc = dbg[b, D["CON"]:D["CON"] + 16 * kn].reshape(kn, 16)
+        print(f"env {b}: oracle {n} contacts, kernel {kn}; newton oracle {int(f['solver_iter'][0])} kernel {int(dbg[b, D['COUNTS'] + 2])}")
+        if b in (6, 8):
+            print("  oracle (dist pos normal g1 g2):")
+            for r in c:
+                print("   ", r[0], r[1:4], r[4:7], int(r[27]), int(r[28]))
+            print("  kernel:")
+            for r in kc:
+                print("   ", r[12], r[0:3], r[3:6], int(r[13]), int(r[14]))
+    ref = PS.copy_state(st)
+    O.step(ref, nsub=1, nthreads=8, model=m)
+    g32 = T._host(eng.step(T._dev(st, torch.float32), 1))
+    ev32, _ = T._tree_metrics(m, st, ref, g32, per_env=True)
+    print("fingers only: arm dqvel errors", np.array2string(ev32[:, 0], precision=2), flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "fingers":
+    fingers_only()
+
+
+def _cost(f, x):
+    """MuJoCo's primal cost at qacc x from the oracle's forward fields (fp64): 0.5 (x - xs)' M (x - xs)
+    + sum over active rows of 0.5 D (J x - aref)^2 (equality rows always, the rest when negative)."""
+    nv = f["qacc_smooth"].size
+    M = f["qM"].reshape(nv, nv)
+    J = f["efc_J"].reshape(-1, nv)
+    jar = J @ x - f["efc_aref"]
+    act = (f["efc_type"] == 0) | (jar < 0)
+    d = x - f["qacc_smooth"]
+    return 0.5 * d @ M @ d + 0.5 * np.sum(f["efc_D"][act] * jar[act] ** 2), act
+
+
+def fingers_cost():
+    """Fingers-only model (see fingers_only): per env, the fp64 primal cost at the oracle's Newton
+    result and at the fp32 kernel's (forward_debug QACC_NEWTON), their finger qacc, and whether the
+    active sets agree; the kernel's rows (J, D, aref) against the oracle's."""
+    from pnp_amd import _lib
+    from pnp_amd.engine import Engine
+    from pnp_amd.model import PandaModel
+    D = _lib.DBG
+    m = PandaModel()
+    for g in list(range(73, 78)) + list(range(81, 86)):
+        m.geom_contype[g] = 0
+        m.geom_conaffinity[g] = 0
+    m._desc = None
+    eng = Engine(model=m, device=get_engine().device)
+    st = T._round32(pressed(m))
+    dbg = eng.forward_debug(T._dev(st, torch.float32)).cpu().numpy()
+    nv = m.nv
+    for b in range(st["qpos"].shape[0]):
+        f = O.forward_fields({k: st[k][b] for k in O.STATE_KEYS},
+                             ["qM", "efc_J", "efc_D", "efc_aref", "efc_type", "qacc_smooth", "qacc_newton", "nefc", "qacc",
+                              "noslip_iter", "efc_force"], model=m)
+        ne = int(f["nefc"][0])
+        xo = f["qacc_newton"]
+        xk = dbg[b, D["QACC_NEWTON"]:D["QACC_NEWTON"] + nv]
+        co, ao = _cost(f, xo)
+        ck, ak = _cost(f, xk)
+        kne = int(dbg[b, D["COUNTS"] + 1])
+        kJ = dbg[b, D["EFC_J"]:D["EFC_J"] + kne * nv].reshape(kne, nv)
+        kD = dbg[b, D["EFC_D"]:D["EFC_D"] + kne]
+        kA = dbg[b, D["EFC_AREF"]:D["EFC_AREF"] + kne]
+        rows = ""
+        if kne == ne:
+            rows = (f"; rows |dJ| {np.abs(kJ - f['efc_J'].reshape(ne, nv)).max():.1e} |dD|/D {np.max(np.abs(kD - f['efc_D']) / f['efc_D']):.1e} "
+                    f"|daref| {np.abs(kA - f['efc_aref']).max():.1e} (|aref| {np.abs(f['efc_aref']).max():.1e})")
+        print(f"env {b}: cost oracle {co:.10e} kernel {ck:.10e} (diff {ck - co:.2e}); finger qacc oracle {xo[7:9]} "
+              f"kernel {xk[7:9]}; active sets equal {np.array_equal(ao, ak)} (nefc {ne}, kernel {kne}){rows}", flush=True)
+        qk = dbg[b, D["QACC"]:D["QACC"] + nv]
+        print(f"   after noslip: finger qacc oracle {f['qacc'][7:9]} kernel {qk[7:9]} (diff {qk[7:9] - f['qacc'][7:9]}); "
+              f"sweeps oracle {int(f['noslip_iter'][0])} kernel {int(dbg[b, D['NOSLIP_ITER']])}", flush=True)
+        if b in (6, 8) and kne == ne:
+            kf = dbg[b, D["EFC_FORCE"]:D["EFC_FORCE"] + kne]
+            print("   efc_force oracle", np.array2string(f["efc_force"], precision=4), flush=True)
+            print("   efc_force kernel", np.array2string(kf, precision=4), flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "cost":
+    fingers_cost()
