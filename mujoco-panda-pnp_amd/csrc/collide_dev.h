@@ -297,9 +297,17 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
       }
     }
   }
+  // rows A[bi], Bm[bj] by selects: a runtime index into the register arrays would put A and Bm in
+  // scratch (six 12-byte spills and reloads per lane and box pair, every sub-step)
+  T ua[3], ub[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    ua[k] = bi == 0 ? A[0][k] : (bi == 1 ? A[1][k] : A[2][k]);
+    ub[k] = bj == 0 ? Bm[0][k] : (bj == 1 ? Bm[1][k] : Bm[2][k]);
+  }
   if (btype == 2) {
     T L[3];
-    t_cross(L, A[bi], Bm[bj]);
+    t_cross(L, ua, ub);
     const T len = PM<T>::sqrt_(t_dot3(L, L));
     for (int k = 0; k < 3; k++) bestn[k] = btl >= 0 ? L[k] / len : -L[k] / len;
   }
@@ -312,6 +320,7 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
   }
   // edge-edge: the closest points of the two edges, relative to p1
   T pa[3] = {0, 0, 0}, pb[3] = {Tv[0], Tv[1], Tv[2]};
+#pragma unroll
   for (int t = 0; t < 3; t++) {
     if (t != bi) {
       const T sg = t_dot3(A[t], bestn) > 0 ? T(1) : T(-1);
@@ -322,7 +331,6 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
       for (int k = 0; k < 3; k++) pb[k] += sg * s2[t] * Bm[t][k];
     }
   }
-  const T ua[3] = {A[bi][0], A[bi][1], A[bi][2]}, ub[3] = {Bm[bj][0], Bm[bj][1], Bm[bj][2]};
   const T w[3] = {pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]};
   const T a = t_dot3(ua, ub), dd = t_dot3(ua, w), e = t_dot3(ub, w), den = 1 - a * a;
   T ta = 0, tb = 0;
