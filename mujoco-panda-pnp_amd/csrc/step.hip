@@ -2773,8 +2773,13 @@ __device__ void st_newton_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>
   T cost = l < s.nisland ? s.isl_cost[l] : T(0);
   bool done = l >= s.nisland;
   int unchanged = 0;                      // consecutive steps that kept the island's active set
-  // gradient floor of a converged island, scaled like MuJoCo's tests: 1 / (stat.meaninertia * nv)
-  const T gscale = T(1) / (m.meaninertia * T(m.nv > 1 ? m.nv : 1));
+  // gradient floor of a converged island (this solver's own test, not MuJoCo's exit: 100 eps of
+  // the gradient scaled by 1 / (meaninertia nv) with meaninertia the mean of this step's diag(M),
+  // as tuned in round 3; the model constant stat.meaninertia (0.16, about half of it on C3 states)
+  // made the floor twice as strict and cost 0.18 Newton iterations per env-sub-step for nothing
+  // the per-tree bar sees)
+  const T meaninertia = wsum(l < m.nv ? s.M[mblk(m, l, l)] : T(0)) / T(m.nv);
+  const T gscale = T(1) / (meaninertia * T(m.nv > 1 ? m.nv : 1));
   const T gtol = T(100) * PM<T>::eps();
   int it = 0;
   const int nent = s.isl_eoff[s.nisland];
@@ -3216,6 +3221,36 @@ __device__ __forceinline__ void tree_solve_fixed(const T* L, const T* j, T* x_ou
   for (int i = 0; i < N; i++) x_out[i] = x[i];
 }
 
+// bd of the pair starting at contact row r (st_noslip): Jd . (qacc_smooth + b qvel) over the
+// row's <= 2 trees, tree by tree (9- and 6-dof trees unrolled: independent loads issued together)
+template <int N, typename T>
+__device__ __forceinline__ T pair_bd_tree(const T* J0, const T* J1, const T* qs, const T* qv, T b) {
+  T a = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) a += (J0[i] - J1[i]) * (qs[i] + b * qv[i]);
+  return a;
+}
+template <typename T>
+__device__ __forceinline__ void pair_bd(Env<T>& s, int r) {
+  const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
+  const T* J0 = s.efc_Jv + s.efc_off[r];
+  const T* J1 = s.efc_Jv + s.efc_off[r + 1];
+  const T b = s.con_b[s.efc_id[r]];
+  T bd = 0;
+  int base = 0;
+  for (int h = 0; h < 2; h++) {
+    const int t = h ? t1 : t0;
+    if (t < 0) continue;
+    const int n = s.c_tree_dofnum[t], d0 = s.c_tree_dofadr[t];
+    if (n == 9) bd += pair_bd_tree<9>(J0 + base, J1 + base, s.qacc_smooth + d0, s.qvel + d0, b);
+    else if (n == 6) bd += pair_bd_tree<6>(J0 + base, J1 + base, s.qacc_smooth + d0, s.qvel + d0, b);
+    else
+      for (int i = 0; i < n; i++) bd += (J0[base + i] - J1[base + i]) * (s.qacc_smooth[d0 + i] + b * s.qvel[d0 + i]);
+    base += n;
+  }
+  s.efc_bb[r] = bd;
+}
+
 // Dense long-list sweep (st_noslip): the group's island v in registers, lane q = island dof q;
 // each pair's difference rows Jd, Wd are formed at the lane's island position straight from the
 // dense blocks (jt, and W in jt's layout), its K1 and 1 / K1 from the per-call table (efc_jar at
@@ -3419,19 +3454,7 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
   // that MuJoCo saturates: fingers 0.07 m/s^2 off).  r0 - r1 = Jd . v + (b0 - b1), and b0 - b1 =
   // Jd . qacc_smooth - (aref0 - aref1) with aref0 - aref1 = -b Jd . qvel (the two rows share the
   // contact's position term): bd = Jd . (qacc_smooth + b qvel), replacing efc_bb[j] (dead after
-  // Newton) for the sweeps.
-  for (int r = l; r < s.nefc; r += NT) {
-    if (s.efc_type[r] != 6 || ((r - s.con_rbase[s.efc_id[r]]) & 1) != 0) continue;
-    const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
-    const int o0 = s.efc_off[r], o1 = s.efc_off[r + 1];
-    const T b = s.con_b[s.efc_id[r]];
-    T bd = 0;
-    for (int k = 0; k < w; k++) {
-      const int d = slot_dof(m, t0, t1, k);
-      bd += (s.efc_Jv[o0 + k] - s.efc_Jv[o1 + k]) * (s.qacc_smooth[d] + b * s.qvel[d]);
-    }
-    s.efc_bb[r] = bd;
-  }
+  // Newton) for the sweeps -- formed by the pair's first row in the W loops below (pair_bd).
   wsync();
   const int maxlen = max(max(s.ns_len[0], s.ns_len[1]), max(s.ns_len[2], s.ns_len[3]));
   bool small = true;
@@ -3453,6 +3476,7 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     for (int rr = l; rr < s.nefc; rr += NT) {
       const int r = s.isl_row[rr];
       if (s.efc_type[r] != 6) continue;
+      if (((r - s.con_rbase[s.efc_id[r]]) & 1) == 0) pair_bd(s, r);
       const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
       const int I = s.tree_island[t0], n = s.isl_n[I];
       T* row = s.efc_Wv + s.isl_joff[I] + (rr - s.isl_roff[I]) * n;
@@ -3491,6 +3515,7 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     // W_r = M^-1 J_r^T for contact rows (block-diagonal M: solve per tree of the row)
     for (int r = l; r < s.nefc; r += NT) {
       if (s.efc_type[r] != 6) continue;
+      if (((r - s.con_rbase[s.efc_id[r]]) & 1) == 0) pair_bd(s, r);
       const int t0 = s.efc_t0[r], t1 = s.efc_t1[r];
       int base = 0;
       for (int h = 0; h < 2; h++) {
