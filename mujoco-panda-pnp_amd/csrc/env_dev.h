@@ -510,25 +510,80 @@ __device__ __forceinline__ void env_step_one(const DevPhys<T>& m, Env<T>& s, con
   }
 }
 
+// ---- hand-over queue of the fp32 gym step (the full-tier passes -> the wide tier's resume pass)
+// The wide resume pass used to start after the full resume pass had finished every env, so an env
+// handed compact -> full -> wide waited for the slowest env of the full pass before its wide
+// sub-steps began (the gym step's span was the sum of three passes' slowest envs).  With the
+// queue, each full-tier workgroup that hands its env over publishes it at once, and a persistent
+// wide consumer grid (on a few CUs, launched after the producers in host order) resumes it while
+// the full passes still run.  Layout (ints): count of entries, producer workgroups done, the
+// consumers' claim counter, a timeout flag, then the entries (-1 until published).  Every env's
+// computation is unchanged: only when its wide sub-steps start.
+#define PNP_HQ_COUNT 0
+#define PNP_HQ_DONE 1
+#define PNP_HQ_NEXT 2
+#define PNP_HQ_ERR 3
+#define PNP_HQ_ENTRY 8
+// a consumer that waits longer than this for a producer gives up (flag PNP_HQ_ERR; the env keeps
+// its resume bits) instead of holding the GPU: 20 s of the 100 MHz constant clock
+#define PNP_HQ_TIMEOUT 2000000000ll
+// producer side: after the workgroup's last state store, publish its env if it handed over, and
+// count the workgroup done (every workgroup of the grid, so the consumers know when to stop)
+__device__ __forceinline__ void hq_publish(int* hq, int b, bool handed) {
+  wsync();           // every lane's state stores issued ...
+  __threadfence();   // ... and visible device-wide before the entry and the done count
+  if (lane_id() == 0) {
+    if (handed) {
+      const int i = __hip_atomic_fetch_add(&hq[PNP_HQ_COUNT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&hq[PNP_HQ_ENTRY + i], b, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __hip_atomic_fetch_add(&hq[PNP_HQ_DONE], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// consumer side: entry i (claimed by this workgroup) once published, or -1 once every producer
+// workgroup is done and fewer than i + 1 entries exist (or on the timeout); wave-uniform
+__device__ __forceinline__ int hq_take(int* hq, int i, int target, int cap) {
+  if (i >= cap) return -1;   // (at most one entry per env)
+  int b = -1;
+  if (lane_id() == 0) {
+    const long long t0 = wall_clock64();
+    for (;;) {
+      b = __hip_atomic_load(&hq[PNP_HQ_ENTRY + i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      if (b >= 0) break;
+      if (__hip_atomic_load(&hq[PNP_HQ_DONE], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= target &&
+          __hip_atomic_load(&hq[PNP_HQ_COUNT], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) <= i)
+        break;
+      if (wall_clock64() - t0 > PNP_HQ_TIMEOUT) {
+        __hip_atomic_store(&hq[PNP_HQ_ERR], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  return __builtin_amdgcn_readfirstlane(__shfl(b, 0));
+}
+
 template <typename T>
 __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
                                                       pnp_env_params prm, EnvSoA<T> es, const T* __restrict__ action,
-                                                      EnvOutT<T> out, int B, int resume, int hand, int only_tier) {
+                                                      EnvOutT<T> out, int B, int resume, int hand, int only_tier,
+                                                      int* __restrict__ hq) {
   __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
   Env<T>& s = s_env;
   const DevPhys<T>& m = phys<T>();
   (void)mp;
   const int b = blockIdx.x;
-  if (b >= B) return;
+  if (b >= B) return;   // (grid = B)
   const int cur = es.tier ? (es.tier[b] & 3) : 0;
-  if (only_tier >= 0 && es.tier && cur != only_tier) return;   // routed to another tier's pass
+  bool run = !(only_tier >= 0 && es.tier && cur != only_tier);   // else routed to another tier's pass
   int k0 = 0;
-  if (resume) {
+  if (run && resume) {
     const uint32_t w = st.warn[b];
-    if (!(w & PNP_RESUME_FLAG)) return;
+    run = (w & PNP_RESUME_FLAG) != 0;
     k0 = (int)((w >> PNP_RESUME_SHIFT) & PNP_RESUME_MAXSUB);
   }
-  env_step_one(m, s, st, prm, es, action, out, b, cur, k0, resume, hand, 1);
+  if (run) env_step_one(m, s, st, prm, es, action, out, b, cur, k0, resume, hand, 1);
+  if (hq) hq_publish(hq, b, run && PNP_HANDS && s.ovf);
 }
 
 #if PNP_MW
@@ -566,10 +621,14 @@ __global__ void __launch_bounds__(1024) wide_select_kernel(const uint8_t* __rest
   }
   if (t == 0) list[0] = base;
 }
+// hq (resume passes of the gym step): consume the hand-over queue instead of the list -- claim
+// entries one at a time until hq_take reports the producers done (hq_target workgroups) and
+// the queue drained; B bounds the entries
 __global__ void __launch_bounds__(NT * MW_WAVES, PNP_WIDE ? 1 : 4) env_step_wide_kernel(pnp_state_t<float> st, pnp_env_params prm,
                                                                           EnvSoA<float> es, const float* __restrict__ action,
                                                                           EnvOutT<float> out, const int* __restrict__ list,
-                                                                          int resume, int hand) {
+                                                                          int resume, int hand, int* __restrict__ hq,
+                                                                          int hq_target, int B) {
   __shared__ __attribute__((aligned(16))) Env<float> s_env;   // static LDS: see env_lds_note
   Env<float>& s = s_env;
   const DevPhys<float>& m = phys<float>();
@@ -577,12 +636,23 @@ __global__ void __launch_bounds__(NT * MW_WAVES, PNP_WIDE ? 1 : 4) env_step_wide
     mw_helper(s);
     return;
   }
-  const int count = list[0];
-  for (int i = blockIdx.x; i < count; i += gridDim.x) {
-    const int b = list[1 + i];
+  auto one = [&](int b) {
     const int cur = es.tier ? (es.tier[b] & 3) : 0;
     const int k0 = resume ? (int)((st.warn[b] >> PNP_RESUME_SHIFT) & PNP_RESUME_MAXSUB) : 0;
     env_step_one(m, s, st, prm, es, action, out, b, cur, k0, resume, hand, MW_WAVES);
+  };
+  if (hq) {
+    for (;;) {
+      int i = 0;
+      if (lane_id() == 0) i = __hip_atomic_fetch_add(&hq[PNP_HQ_NEXT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      i = __builtin_amdgcn_readfirstlane(__shfl(i, 0));
+      const int b = hq_take(hq, i, hq_target, B);
+      if (b < 0) break;
+      one(b);
+    }
+  } else {
+    const int count = list[0];
+    for (int i = blockIdx.x; i < count; i += gridDim.x) one(list[1 + i]);
   }
   if (lane_id() == 0) s.mw_cmd = MW_EXIT;   // every path of wave 0 ends here
   __syncthreads();
@@ -644,18 +714,26 @@ static int32_t wide_list(int kind, int32_t B, int** out, int* ncu) {
 // persistent multi-wave gym pass of this build's tier over the envs the selection kernel lists
 static int32_t launch_env_step_mw(const pnp_state_t<float>* st, const pnp_env_params* p, const pnp_env_state* e,
                                   const float* action, const pnp_env_out* o, int32_t B, void* stream, int resume,
-                                  int only_tier, int hand, const char* what) {
+                                  int only_tier, int hand, const char* what, int* hq = nullptr, int hq_target = 0,
+                                  int hq_grid = 0) {
   if (B <= 0) return PNP_OK;
   int* list = nullptr;
   int ncu = 0;
   if (const int32_t rc = wide_list(resume ? 1 : 0, B, &list, &ncu)) return rc;
-  hipLaunchKernelGGL(wide_select_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, e->tier, st->warn, B, resume,
-                     only_tier, list);
-  if (const int32_t rc = pnp_check_launch("wide_select_kernel")) return rc;
   const int per_cu = (int)(163840 / sizeof(Env<float>)) > 0 ? (int)(163840 / sizeof(Env<float>)) : 1;   // envs per CU (LDS)
-  const int grid = B < per_cu * ncu ? B : per_cu * ncu;
+  int grid = B < per_cu * ncu ? B : per_cu * ncu;
+  if (hq) {
+    // the consumer grid leaves the other CUs to the producers it waits for (no deadlock: they
+    // always have room, and they are enqueued before it on any shared hardware queue)
+    grid = hq_grid < grid ? hq_grid : grid;
+    if (grid < 1 || grid >= per_cu * ncu) { pnp_set_error("pnp_env_step: hand-over queue grid %d", grid); return PNP_ERR_ARG; }
+  } else {
+    hipLaunchKernelGGL(wide_select_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, e->tier, st->warn, B, resume,
+                       only_tier, list);
+    if (const int32_t rc = pnp_check_launch("wide_select_kernel")) return rc;
+  }
   hipLaunchKernelGGL(env_step_wide_kernel, dim3(grid), dim3(NT * MW_WAVES), 0, (hipStream_t)stream, *st, *p,
-                     env_view<float>(e), action, out_view<float>(o), (const int*)list, resume, hand);
+                     env_view<float>(e), action, out_view<float>(o), (const int*)list, resume, hand, hq, hq_target, B);
   return pnp_check_launch(what);
 }
 #endif
@@ -670,7 +748,7 @@ int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>
                                        sizeof(DevPhys<float>), stream))
     return rc;
   hipLaunchKernelGGL(env_step_kernel<float>, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, *p,
-                     env_view<float>(e), action, out_view<float>(o), B, 0, 1, only_tier);
+                     env_view<float>(e), action, out_view<float>(o), B, 0, 1, only_tier, (int*)nullptr);
   if (const int32_t rc = pnp_check_launch("env_step_kernel (compact)")) return rc;
   return lease.launched();
 }
@@ -684,7 +762,7 @@ int32_t env_compact_lds_bytes() { return (int32_t)sizeof(Env<float>); }
 // the full image's lease like the route streams.
 int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
                              const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
-                             void* stream, int resume, int only_tier) {
+                             void* stream, int resume, int only_tier, int* hq, int hq_target, int hq_grid) {
   const DevPhys<float>* src = phys_image<float>(model);
   if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
   if (B <= 0) return PNP_OK;
@@ -692,7 +770,9 @@ int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* s
   if (const int32_t rc = lease.acquire(RES_WIDE_F32, model, (const void*)&g_phys_f32, src, sizeof(DevPhys<float>),
                                        stream))
     return rc;
-  if (const int32_t rc = launch_env_step_mw(st, p, e, action, o, B, stream, resume, only_tier, 0, "env_step_wide_kernel"))
+  if (const int32_t rc = launch_env_step_mw(st, p, e, action, o, B, stream, resume, only_tier, 0,
+                                            hq ? "env_step_wide_kernel (hand-over queue)" : "env_step_wide_kernel",
+                                            hq, hq_target, hq_grid))
     return rc;
   return lease.launched();
 }
@@ -710,7 +790,7 @@ int32_t launch_env_step_wide64(const pnp_model* model, const pnp_state_t<double>
                                        sizeof(DevPhys<double>), stream))
     return rc;
   hipLaunchKernelGGL(env_step_kernel<double>, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, *p,
-                     env_view<double>(e), action, out_view<double>(o), B, 1, 0, -1);
+                     env_view<double>(e), action, out_view<double>(o), B, 1, 0, -1, (int*)nullptr);
   if (const int32_t rc = pnp_check_launch("env_step_kernel (wide64)")) return rc;
   return lease.launched();
 }
@@ -818,12 +898,49 @@ static bool gym_full_mw_enabled() {
   const char* e = getenv("PNP_GYM_FULL_MW");
   return e && e[0] == '1';
 }
-// Two side streams per device for the routed passes, forked from and joined back into the
-// caller's stream.  Used only while the full image's lease is held (launch_env_step), which
-// serialises their users per device; creation has its own lock.
+// PNP_GYM_QUEUE: unset / 1 = routed fp32 gym steps hand the full tier's hand-overs to the wide
+// tier through the device queue (hq_publish / hq_take), consumed concurrently with the full passes
+// (default); 0 = the wide resume pass starts after the full passes (A/B runs).  PNP_GYM_QUEUE_CU:
+// the consumer grid, one wide workgroup per CU (default 192 of 256: leaves a quarter of the CUs
+// to the producers).  Measured (4096 envs, random actions, gym-steps/s; profiles/r04/gym_queue_ab.log):
+// queue off 18.5 k; consumers 32: 9.5 k, 64: 15.2 k, 128: 19.5 k, 160-255: 19.9-20.4 k -- a step
+// hands hundreds of envs to the wide tier, so the consumer grid must stay wide
+static bool gym_queue_enabled() {
+  const char* e = getenv("PNP_GYM_QUEUE");
+  return !(e && e[0] == '0');
+}
+static int gym_queue_grid() {
+  const char* e = getenv("PNP_GYM_QUEUE_CU");
+  const int g = e ? atoi(e) : 192;
+  return g > 0 ? g : 192;
+}
+// the hand-over queue buffer per device (PNP_HQ_ENTRY header ints + one entry per env); its users
+// are serialised by the full image's lease like the route streams
+static int32_t hand_queue(int32_t B, int** out) {
+  static std::mutex mu;
+  static int* buf[64] = {};
+  static int cap[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { pnp_set_error("pnp_env_step: bad device"); return PNP_ERR_HIP; }
+  std::lock_guard<std::mutex> lk(mu);
+  hipError_t e = hipSuccess;
+  if (cap[dev] < B + PNP_HQ_ENTRY) {
+    if (buf[dev]) e = hipFree(buf[dev]);   // (synchronises: only when a larger batch arrives)
+    buf[dev] = nullptr;
+    cap[dev] = 0;
+    if (e == hipSuccess) e = hipMalloc((void**)&buf[dev], sizeof(int) * (size_t)(B + PNP_HQ_ENTRY));
+    if (e == hipSuccess) cap[dev] = B + PNP_HQ_ENTRY;
+  }
+  if (e != hipSuccess) { pnp_set_error("pnp_env_step: hand-over queue: %s", hipGetErrorString(e)); return PNP_ERR_HIP; }
+  *out = buf[dev];
+  return PNP_OK;
+}
+// Three side streams per device for the routed passes and the hand-over queue's consumer, forked
+// from and joined back into the caller's stream.  Used only while the full image's lease is held
+// (launch_env_step), which serialises their users per device; creation has its own lock.
 struct RouteStreams {
-  hipStream_t side[2] = {nullptr, nullptr};
-  hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+  hipStream_t side[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr}, cdone = nullptr;
 };
 static int32_t route_streams(RouteStreams** out) {
   static std::mutex mu;
@@ -835,11 +952,12 @@ static int32_t route_streams(RouteStreams** out) {
   hipError_t e = hipSuccess;
   // (neither wave priority, s_setprio, for the routed passes nor the highest stream priority
   // shortened the routed wide pass: its span is the heaviest env's own chain of sub-steps)
-  for (int i = 0; i < 2 && e == hipSuccess; i++) {
+  for (int i = 0; i < 3 && e == hipSuccess; i++) {
     if (!r.side[i]) e = hipStreamCreateWithFlags(&r.side[i], hipStreamNonBlocking);
     if (e == hipSuccess && !r.join[i]) e = hipEventCreateWithFlags(&r.join[i], hipEventDisableTiming);
   }
   if (e == hipSuccess && !r.fork) e = hipEventCreateWithFlags(&r.fork, hipEventDisableTiming);
+  if (e == hipSuccess && !r.cdone) e = hipEventCreateWithFlags(&r.cdone, hipEventDisableTiming);
   if (e != hipSuccess) { pnp_set_error("pnp_env_step: route streams: %s", hipGetErrorString(e)); return PNP_ERR_HIP; }
   *out = &r;
   return PNP_OK;
@@ -861,7 +979,7 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
     // sub-steps outgrow it to the fp64 wide tier's resume pass
     const int w64 = p->n_substeps * p->n_calls <= PNP_RESUME_MAXSUB && wide_enabled();
     hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), action,
-                       out_view<T>(o), B, 0, w64, -1);
+                       out_view<T>(o), B, 0, w64, -1, (int*)nullptr);
     if ((rc = pnp_check_launch("env_step_kernel (fp64)"))) return rc;
     if (w64 && (rc = launch_env_step_wide64(model, st, p, e, action, o, B, stream))) return rc;
     return lease.launched();
@@ -879,6 +997,9 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   const bool route = compact && wide && gym_compact_mode() == 1 && e->tier && gym_route_enabled();
   // fp32 full-tier passes: persistent, two waves per env (helper wave for the convex pass)
   const bool full_mw = tiers && gym_full_mw_enabled();
+  // the full passes' hand-overs reach the wide tier through the device queue (routed steps)
+  const bool queue = route && !full_mw && gym_full_resume_enabled() && gym_queue_enabled();
+  int* hq = nullptr;
   RouteStreams* rs = nullptr;
   // join side stream i back into the caller's stream (its kernels read the full image and write
   // the state: later work on s0, and the next model switch, must be ordered after them)
@@ -890,18 +1011,24 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   // an error after the fork still joins both side streams and records the lease's use on s0
   // before it is reported (the routed passes already enqueued keep running)
   bool forked = false;
+  const int nside = queue ? 3 : 2;
   auto fail = [&](int32_t code) -> int32_t {
     if (forked) {
-      join_side(0);
-      join_side(1);
+      for (int i = 0; i < nside; i++) join_side(i);
       lease.launched();
     }
     return code;
   };
   if (route) {
     if ((rc = route_streams(&rs))) return rc;
-    hipError_t he = hipEventRecord(rs->fork, s0);   // after the full image's copy and the last step
-    for (int i = 0; i < 2 && he == hipSuccess; i++) he = hipStreamWaitEvent(rs->side[i], rs->fork, 0);
+    hipError_t he = hipSuccess;
+    if (queue) {   // a fresh queue, ordered before every pass of this step
+      if ((rc = hand_queue(B, &hq))) return rc;
+      he = hipMemsetAsync(hq, 0, sizeof(int) * PNP_HQ_ENTRY, s0);
+      if (he == hipSuccess) he = hipMemsetAsync(hq + PNP_HQ_ENTRY, 0xFF, sizeof(int) * (size_t)B, s0);
+    }
+    if (he == hipSuccess) he = hipEventRecord(rs->fork, s0);   // after the full image's copy and the last step
+    for (int i = 0; i < nside && he == hipSuccess; i++) he = hipStreamWaitEvent(rs->side[i], rs->fork, 0);
     if (he != hipSuccess) { pnp_set_error("pnp_env_step: fork: %s", hipGetErrorString(he)); return PNP_ERR_HIP; }
     forked = true;
     if ((rc = launch_env_step_wide(model, st32, p, e, a32, o, B, rs->side[1], 0, 2))) return fail(rc);
@@ -909,18 +1036,22 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
       rc = launch_env_step_mw(st32, p, e, a32, o, B, rs->side[0], 0, 1, wide, "env_step_wide_kernel (full, routed)");
     } else {
       hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, rs->side[0], dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
-                         0, wide, 1);
+                         0, wide, 1, hq);
       rc = pnp_check_launch("env_step_kernel (full, routed)");
     }
     if (rc) return fail(rc);
   }
   if (compact && (rc = launch_env_step_compact(model, st32, p, e, a32, o, B, stream, route ? 0 : -1))) return fail(rc);
   if (compact && gym_compact_mode() == 2) {
-    if (forked) {
-      join_side(0);
-      join_side(1);
-    }
+    if (forked)
+      for (int i = 0; i < nside; i++) join_side(i);
     return lease.launched();
+  }
+  if (queue) {   // the consumer starts once the compact pass is done (it does not take its CUs)
+    if (const hipError_t he = hipEventRecord(rs->cdone, s0)) {
+      pnp_set_error("pnp_env_step: compact event: %s", hipGetErrorString(he));
+      return fail(PNP_ERR_HIP);
+    }
   }
   if (!route || gym_full_resume_enabled()) {
     if (full_mw) {
@@ -928,22 +1059,38 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
                               "env_step_wide_kernel (full)");
     } else {
       hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, s0, dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
-                         compact ? 1 : 0, wide, route ? 0 : -1);
+                         compact ? 1 : 0, wide, route ? 0 : -1, hq);
       rc = pnp_check_launch("env_step_kernel");
     }
     if (rc) return fail(rc);
   }
-  if (route) {   // the wide resume pass also takes the routed full pass's hand-overs
-    if (const hipError_t he = join_side(0)) {
-      pnp_set_error("pnp_env_step: join: %s", hipGetErrorString(he));
+  if (queue) {
+    // the wide consumer of both full passes' hand-overs (2 B producer workgroups), enqueued after
+    // both of them in host order
+    if (const hipError_t he = hipStreamWaitEvent(rs->side[2], rs->cdone, 0)) {
+      pnp_set_error("pnp_env_step: consumer wait: %s", hipGetErrorString(he));
       return fail(PNP_ERR_HIP);
     }
-  }
-  if (wide && (rc = launch_env_step_wide(model, st32, p, e, a32, o, B, stream, 1, -1))) return fail(rc);
-  if (route) {
-    if (const hipError_t he = join_side(1)) {
-      pnp_set_error("pnp_env_step: join: %s", hipGetErrorString(he));
-      return fail(PNP_ERR_HIP);
+    if ((rc = launch_env_step_wide(model, st32, p, e, a32, o, B, rs->side[2], 1, -1, hq, 2 * B, gym_queue_grid())))
+      return fail(rc);
+    for (int i = 0; i < 3; i++)
+      if (const hipError_t he = join_side(i)) {
+        pnp_set_error("pnp_env_step: join: %s", hipGetErrorString(he));
+        return fail(PNP_ERR_HIP);
+      }
+  } else {
+    if (route) {   // the wide resume pass also takes the routed full pass's hand-overs
+      if (const hipError_t he = join_side(0)) {
+        pnp_set_error("pnp_env_step: join: %s", hipGetErrorString(he));
+        return fail(PNP_ERR_HIP);
+      }
+    }
+    if (wide && (rc = launch_env_step_wide(model, st32, p, e, a32, o, B, stream, 1, -1))) return fail(rc);
+    if (route) {
+      if (const hipError_t he = join_side(1)) {
+        pnp_set_error("pnp_env_step: join: %s", hipGetErrorString(he));
+        return fail(PNP_ERR_HIP);
+      }
     }
   }
   if (e->tier) {   // every pass has run: the next step's tiers become current

@@ -110,9 +110,12 @@ int32_t step_compact_lds_bytes();
 // step_wide.hip: the wide-capacity fp32 tier (resume passes of pnp_step and pnp_env_step)
 int32_t launch_step_wide(const pnp_model* model, const pnp_state_t<float>* st, int32_t B, int32_t nsub,
                          void* stream, unsigned long long* prof, int resume);
+// hq / hq_target: the gym step's hand-over queue (env_dev.h, PNP_HQ_*): the resume pass then
+// consumes the envs the full-tier passes publish, concurrently with them, on hq_grid workgroups
 int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
                              const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
-                             void* stream, int resume, int only_tier);
+                             void* stream, int resume, int only_tier, int* hq = nullptr, int hq_target = 0,
+                             int hq_grid = 0);
 int32_t step_wide_lds_bytes();
 // step_wide64.hip: the fp64 wide tier (resume passes of pnp_step_f64 and pnp_env_step_f64)
 int32_t launch_step_wide64(const pnp_model* model, const pnp_state_t<double>* st, int32_t B, int32_t nsub,

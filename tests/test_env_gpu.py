@@ -138,12 +138,12 @@ def test_gym_step_wide_tier_pressed_fingers(model):
     assert int((g.state["warn"] & 0xFFFF).max()) == 0 and not o.st["warn"].any()
 
 
-def _gym_run(mode, B, nsteps, pressed=False, route="1", tiers=None):
+def _gym_run(mode, B, nsteps, pressed=False, route="1", tiers=None, **extra_env):
     import os
     from pnp_amd.envs import BatchedFrankaShelfPNPEnv
-    old = {k: os.environ.get(k) for k in ("PNP_GYM_COMPACT", "PNP_GYM_ROUTE")}
-    os.environ["PNP_GYM_COMPACT"] = mode
-    os.environ["PNP_GYM_ROUTE"] = route
+    env = {"PNP_GYM_COMPACT": mode, "PNP_GYM_ROUTE": route, **extra_env}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         g = BatchedFrankaShelfPNPEnv(B, autoreset=True)
         g.reset()
@@ -203,6 +203,26 @@ def test_gym_routing_is_exact():
     for t in tiers:
         assert int(t.max()) <= 2                        # committed: no pending bits left
     assert any(bool((t[::3] > 0).any()) for t in tiers[:-1])   # pressed envs routed past compact
+    w = a.state["warn"].to(torch.int64) & 0xFFFFFFFF
+    assert not bool((w >> 16).any()) and int((w & 0xFFFF).max()) == 0
+
+
+@pytest.mark.parametrize("grid", ["2", "192"])
+def test_gym_hand_over_queue_is_exact(grid):
+    """The hand-over queue (env_dev.h hq_publish / hq_take: the full-tier passes publish the envs
+    they hand to the wide tier, a persistent wide consumer grid resumes them concurrently) gives
+    the bits of the wide resume pass that starts after the full passes -- with 2 consumer
+    workgroups (each waits for and drains many entries) and with the default grid; no env is left
+    with resume bits (a consumer that timed out would leave them)."""
+    a, oa = _gym_run("1", 96, 3, pressed=True, route="1", PNP_GYM_QUEUE="1", PNP_GYM_QUEUE_CU=grid)
+    b, ob = _gym_run("1", 96, 3, pressed=True, route="1", PNP_GYM_QUEUE="0")
+    for x, y in zip(oa, ob):
+        for u, v in zip(x, y):
+            assert torch.equal(u, v)
+    for k in a.state:
+        assert torch.equal(a.state[k], b.state[k]), k
+    for k in a.env:
+        assert torch.equal(a.env[k], b.env[k]), k
     w = a.state["warn"].to(torch.int64) & 0xFFFFFFFF
     assert not bool((w >> 16).any()) and int((w & 0xFFFF).max()) == 0
 
