@@ -384,7 +384,7 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_e
 #define PNP_GF_MAXCON 48
 #define PNP_GF_MAXEFC 208
 #define PNP_GF_MAXJSLOT 2048
-#define PNP_GF_JTCAP 1536
+#define PNP_GF_JTCAP 1792
 template <typename T>
 __device__ __forceinline__ int tier_need(const DevPhys<T>& m, const Env<T>& s) {
   const int ne = s.nefc, nc = s.ncon_raw;
@@ -409,12 +409,14 @@ __device__ __forceinline__ int tier_need(const DevPhys<T>& m, const Env<T>& s) {
 // One env's gym step on its workgroup's wave 0 (env_step_kernel: one env per workgroup; the wide
 // build's env_step_wide_kernel: a persistent loop over the selected envs).  k0: the sub-step to
 // resume from (resume passes); cur: the env's current tier; mw: the workgroup's waves.
+// hand_pct: bit 0 = hand overflowing sub-steps over, bits 8.. = the routing's wide share (below).
 template <typename T>
 __device__ __forceinline__ void env_step_one(const DevPhys<T>& m, Env<T>& s, const pnp_state_t<T>& st,
                                              const pnp_env_params& prm, const EnvSoA<T>& es, const T* __restrict__ action,
-                                             const EnvOutT<T>& out, int b, int cur, int k0, int resume, int hand, int mw) {
+                                             const EnvOutT<T>& out, int b, int cur, int k0, int resume, int hand_pct, int mw) {
   (void)mw;
   const int l = lane_id();
+  const int hand = hand_pct & 1, wide_pct = hand_pct >> 8;
   load_env(m, s, st, b, hand);
 #if PNP_MW
   if (l == 0) s.mw = mw;
@@ -453,11 +455,21 @@ __device__ __forceinline__ void env_step_one(const DevPhys<T>& m, Env<T>& s, con
   const int nsub = prm.n_substeps * prm.n_calls;
   int k = k0;
   const bool track = !PNP_COMPACT && es.tier;
-  int need_tier = 0;
+  int need_tier = 0, nwide = 0, nrun = 0;
   for (; k < nsub && !(PNP_HANDS && s.ovf); k++) {
     mj_step_dev(m, s, clk, k == nsub - 1 ? s.qpos_pre : nullptr);
-    if (track && !(PNP_HANDS && s.ovf)) need_tier = max(need_tier, tier_need(m, s));
+    if (track && !(PNP_HANDS && s.ovf)) {
+      const int t = tier_need(m, s);
+      need_tier = max(need_tier, t);
+      nwide += t == 2;
+      nrun++;
+    }
   }
+  // an env that needed the wide tier on fewer than wide_pct % of the sub-steps it ran here starts
+  // its next step in the full tier (4 envs per CU instead of 1) and is handed over -- through the
+  // hand-over queue, at once -- when a sub-step needs it (closed fingers: pad contacts flicker in
+  // and out, most sub-steps light)
+  if (need_tier == 2 && 100 * nwide < wide_pct * nrun) need_tier = 1;
   if (PNP_HANDS && s.ovf) {   // sub-step k - 1 overflowed before changing the state: hand over
     if (l == 0)
       s.warn |= PNP_RESUME_FLAG | ((uint32_t)s.ovf << PNP_RESUME_WHY_SHIFT) | ((uint32_t)(k - 1) << PNP_RESUME_SHIFT);
@@ -737,6 +749,17 @@ static int32_t launch_env_step_mw(const pnp_state_t<float>* st, const pnp_env_pa
   return pnp_check_launch(what);
 }
 #endif
+// PNP_GYM_WIDE_PCT: the routing sends an env to the wide tier for its next step only if at least
+// this share (%) of its sub-steps needed it (see env_step_one; 0: any one sub-step, round 3's
+// rule).  Random-action gym workload (4096 envs, profiles/r04/gym_route_pct_ab.log): 0: 20.1-20.2 k
+// gym-steps/s (~600 envs a step started in the wide tier, one env per CU, most of them closed
+// grippers whose pad contacts overflow the full tier on a few sub-steps); 10 .. 100: 22.4-22.8 k.
+// Default 50.
+static int gym_wide_pct() {
+  const char* e = getenv("PNP_GYM_WIDE_PCT");
+  const int v = e ? atoi(e) : 50;
+  return v < 0 ? 0 : (v > 100 ? 100 : v);
+}
 #if PNP_COMPACT
 int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
                                 const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
@@ -770,7 +793,7 @@ int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* s
   if (const int32_t rc = lease.acquire(RES_WIDE_F32, model, (const void*)&g_phys_f32, src, sizeof(DevPhys<float>),
                                        stream))
     return rc;
-  if (const int32_t rc = launch_env_step_mw(st, p, e, action, o, B, stream, resume, only_tier, 0,
+  if (const int32_t rc = launch_env_step_mw(st, p, e, action, o, B, stream, resume, only_tier, gym_wide_pct() << 8,
                                             hq ? "env_step_wide_kernel (hand-over queue)" : "env_step_wide_kernel",
                                             hq, hq_target, hq_grid))
     return rc;
@@ -988,6 +1011,7 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   // the envs it hands over, the wide kernel the envs the full kernel hands over
   const bool tiers = sizeof(T) == 4 && p->n_substeps * p->n_calls <= PNP_RESUME_MAXSUB;
   const int wide = tiers && wide_enabled();
+  const int hand_pct = wide | gym_wide_pct() << 8;   // the full passes' hand flag + routing share
   const bool compact = tiers && gym_compact_enabled();
   const auto* st32 = reinterpret_cast<const pnp_state_t<float>*>(st);
   const float* a32 = reinterpret_cast<const float*>(action);
@@ -1033,10 +1057,10 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
     forked = true;
     if ((rc = launch_env_step_wide(model, st32, p, e, a32, o, B, rs->side[1], 0, 2))) return fail(rc);
     if (full_mw) {
-      rc = launch_env_step_mw(st32, p, e, a32, o, B, rs->side[0], 0, 1, wide, "env_step_wide_kernel (full, routed)");
+      rc = launch_env_step_mw(st32, p, e, a32, o, B, rs->side[0], 0, 1, hand_pct, "env_step_wide_kernel (full, routed)");
     } else {
       hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, rs->side[0], dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
-                         0, wide, 1, hq);
+                         0, hand_pct, 1, hq);
       rc = pnp_check_launch("env_step_kernel (full, routed)");
     }
     if (rc) return fail(rc);
@@ -1055,11 +1079,11 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   }
   if (!route || gym_full_resume_enabled()) {
     if (full_mw) {
-      rc = launch_env_step_mw(st32, p, e, a32, o, B, stream, compact ? 1 : 0, route ? 0 : -1, wide,
+      rc = launch_env_step_mw(st32, p, e, a32, o, B, stream, compact ? 1 : 0, route ? 0 : -1, hand_pct,
                               "env_step_wide_kernel (full)");
     } else {
       hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, s0, dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
-                         compact ? 1 : 0, wide, route ? 0 : -1, hq);
+                         compact ? 1 : 0, hand_pct, route ? 0 : -1, hq);
       rc = pnp_check_launch("env_step_kernel");
     }
     if (rc) return fail(rc);

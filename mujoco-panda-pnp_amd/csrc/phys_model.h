@@ -43,7 +43,7 @@
 #define PH_MAXJSLOT 2048  // packed constraint-Jacobian slots (sum of row widths)
 #endif
 #ifndef PH_JTCAP
-#define PH_JTCAP 1536    // dense island Jacobian entries (sum over islands of rows x dofs; larger: slot path)
+#define PH_JTCAP 1792    // dense island Jacobian entries (sum over islands of rows x dofs; larger: slot path)
 #endif
 #define PH_ROWW 16        // sparse row width: dofs of <= 2 trees (arm 9 + cube 6)
 #define PH_MAXMENTRY 160  // (i, j in ancestors(i)) entries of M

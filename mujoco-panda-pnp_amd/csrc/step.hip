@@ -2683,7 +2683,6 @@ __device__ __attribute__((noinline)) void newton_dir_groups(Env<T>& s, bool done
 // per entry) walks every row once per entry.  fp32 MFMA is exact f32 (an fmaf chain per
 // element); the sums associate differently from the scalar loop (rounding only).
 __device__ __attribute__((noinline)) void hess_mfma(Env<float>& s, int I) {
-  const DevPhys<float>& m = phys<float>();
   const int l = lane_id();
   const int n = s.isl_n[I], r0 = s.isl_roff[I], nr = s.isl_roff[I + 1] - r0;
   const float* J = s.jt + s.isl_joff[I];
