@@ -416,7 +416,7 @@ __device__ __forceinline__ void env_step_one(const DevPhys<T>& m, Env<T>& s, con
                                              const EnvOutT<T>& out, int b, int cur, int k0, int resume, int hand_pct, int mw) {
   (void)mw;
   const int l = lane_id();
-  const int hand = hand_pct & 1, wide_pct = hand_pct >> 8;
+  const int hand = hand_pct & 1, wide_pct = (hand_pct >> 8) & 255, full_pct = hand_pct >> 16;
   load_env(m, s, st, b, hand);
 #if PNP_MW
   if (l == 0) s.mw = mw;
@@ -455,13 +455,14 @@ __device__ __forceinline__ void env_step_one(const DevPhys<T>& m, Env<T>& s, con
   const int nsub = prm.n_substeps * prm.n_calls;
   int k = k0;
   const bool track = !PNP_COMPACT && es.tier;
-  int need_tier = 0, nwide = 0, nrun = 0;
+  int need_tier = 0, nwide = 0, nfull = 0, nrun = 0;
   for (; k < nsub && !(PNP_HANDS && s.ovf); k++) {
     mj_step_dev(m, s, clk, k == nsub - 1 ? s.qpos_pre : nullptr);
     if (track && !(PNP_HANDS && s.ovf)) {
       const int t = tier_need(m, s);
       need_tier = max(need_tier, t);
       nwide += t == 2;
+      nfull += t >= 1;
       nrun++;
     }
   }
@@ -470,6 +471,8 @@ __device__ __forceinline__ void env_step_one(const DevPhys<T>& m, Env<T>& s, con
   // hand-over queue, at once -- when a sub-step needs it (closed fingers: pad contacts flicker in
   // and out, most sub-steps light)
   if (need_tier == 2 && 100 * nwide < wide_pct * nrun) need_tier = 1;
+  // likewise compact -> full (PNP_GYM_FULL_PCT; the compact pass's hand-overs wait for it to end)
+  if (need_tier == 1 && 100 * nfull < full_pct * nrun) need_tier = 0;
   if (PNP_HANDS && s.ovf) {   // sub-step k - 1 overflowed before changing the state: hand over
     if (l == 0)
       s.warn |= PNP_RESUME_FLAG | ((uint32_t)s.ovf << PNP_RESUME_WHY_SHIFT) | ((uint32_t)(k - 1) << PNP_RESUME_SHIFT);
@@ -755,6 +758,14 @@ static int32_t launch_env_step_mw(const pnp_state_t<float>* st, const pnp_env_pa
 // gym-steps/s (~600 envs a step started in the wide tier, one env per CU, most of them closed
 // grippers whose pad contacts overflow the full tier on a few sub-steps); 10 .. 100: 22.4-22.8 k.
 // Default 50.
+// PNP_GYM_FULL_PCT: the same share for starting in the full tier instead of the compact one
+// (0: any one sub-step).  Measured on top of the wide share (profiles/r04/gym_route_pct_ab.log):
+// 0: 22.1 k gym-steps/s; 20 .. 80: 22.7-23.1 k.  Default 50.
+static int gym_full_pct() {
+  const char* e = getenv("PNP_GYM_FULL_PCT");
+  const int v = e ? atoi(e) : 50;
+  return v < 0 ? 0 : (v > 100 ? 100 : v);
+}
 static int gym_wide_pct() {
   const char* e = getenv("PNP_GYM_WIDE_PCT");
   const int v = e ? atoi(e) : 50;
@@ -793,7 +804,7 @@ int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* s
   if (const int32_t rc = lease.acquire(RES_WIDE_F32, model, (const void*)&g_phys_f32, src, sizeof(DevPhys<float>),
                                        stream))
     return rc;
-  if (const int32_t rc = launch_env_step_mw(st, p, e, action, o, B, stream, resume, only_tier, gym_wide_pct() << 8,
+  if (const int32_t rc = launch_env_step_mw(st, p, e, action, o, B, stream, resume, only_tier, gym_wide_pct() << 8 | gym_full_pct() << 16,
                                             hq ? "env_step_wide_kernel (hand-over queue)" : "env_step_wide_kernel",
                                             hq, hq_target, hq_grid))
     return rc;
@@ -1011,7 +1022,7 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   // the envs it hands over, the wide kernel the envs the full kernel hands over
   const bool tiers = sizeof(T) == 4 && p->n_substeps * p->n_calls <= PNP_RESUME_MAXSUB;
   const int wide = tiers && wide_enabled();
-  const int hand_pct = wide | gym_wide_pct() << 8;   // the full passes' hand flag + routing share
+  const int hand_pct = wide | gym_wide_pct() << 8 | gym_full_pct() << 16;   // hand flag + routing shares
   const bool compact = tiers && gym_compact_enabled();
   const auto* st32 = reinterpret_cast<const pnp_state_t<float>*>(st);
   const float* a32 = reinterpret_cast<const float*>(action);
