@@ -185,13 +185,17 @@ def test_gym_compact_tier_is_exact():
     assert not bool((w >> 16).any()) and int((w & 0xFFFF).max()) == 0
 
 
-def test_gym_routing_is_exact():
+@pytest.mark.parametrize("share", ["0", "50"])
+def test_gym_routing_is_exact(share):
     """Routed gym steps (env_dev.h: envs whose last step finished in the full / wide tier start
     there, on side streams concurrent with the compact pass) are bit-identical to every env
-    starting in the compact tier, and the routing engages on a batch with pressed pads."""
+    starting in the compact tier; with the routing shares at 0 (a tier any one sub-step needed:
+    round 3's rule) the routing engages on a batch with pressed pads, and with the default shares
+    (50 %: PNP_GYM_WIDE_PCT / PNP_GYM_FULL_PCT) the results are the same bits."""
     tiers = []
-    a, oa = _gym_run("1", 96, 4, pressed=True, route="1", tiers=tiers)
-    b, ob = _gym_run("1", 96, 4, pressed=True, route="0")
+    shares = dict(PNP_GYM_WIDE_PCT=share, PNP_GYM_FULL_PCT=share)
+    a, oa = _gym_run("1", 96, 4, pressed=True, route="1", tiers=tiers, **shares)
+    b, ob = _gym_run("1", 96, 4, pressed=True, route="0", **shares)
     for x, y in zip(oa, ob):
         for u, v in zip(x, y):
             assert torch.equal(u, v)
@@ -202,7 +206,8 @@ def test_gym_routing_is_exact():
             assert torch.equal(a.env[k], b.env[k]), k
     for t in tiers:
         assert int(t.max()) <= 2                        # committed: no pending bits left
-    assert any(bool((t[::3] > 0).any()) for t in tiers[:-1])   # pressed envs routed past compact
+    if share == "0":
+        assert any(bool((t[::3] > 0).any()) for t in tiers[:-1])   # pressed envs routed past compact
     w = a.state["warn"].to(torch.int64) & 0xFFFFFFFF
     assert not bool((w >> 16).any()) and int((w & 0xFFFF).max()) == 0
 
