@@ -935,18 +935,20 @@ static bool gym_full_mw_enabled() {
 // PNP_GYM_QUEUE: unset / 1 = routed fp32 gym steps hand the full tier's hand-overs to the wide
 // tier through the device queue (hq_publish / hq_take), consumed concurrently with the full passes
 // (default); 0 = the wide resume pass starts after the full passes (A/B runs).  PNP_GYM_QUEUE_CU:
-// the consumer grid, one wide workgroup per CU (default 192 of 256: leaves a quarter of the CUs
-// to the producers).  Measured (4096 envs, random actions, gym-steps/s; profiles/r04/gym_queue_ab.log):
-// queue off 18.5 k; consumers 32: 9.5 k, 64: 15.2 k, 128: 19.5 k, 160-255: 19.9-20.4 k -- a step
-// hands hundreds of envs to the wide tier, so the consumer grid must stay wide
+// the consumer grid, one wide workgroup per CU (default 224 of 256: leaves 32 CUs to the producers,
+// whose progress is all the consumers wait for).  Measured (4096 envs, random actions,
+// gym-steps/s; profiles/r04/gym_queue_ab.log), with round 3's routing: queue off 18.5 k; consumers
+// 32: 9.5 k, 64: 15.2 k, 128: 19.5 k, 160-255: 19.9-20.4 k; with the routing shares (50 %): off
+// 18.8 k, 96: 18.8 k, 160: 22.3 k, 192: 22.9 k, 240: 23.2 k -- the full passes hand envs to the
+// wide tier at every point of the step, and each needs a free consumer then
 static bool gym_queue_enabled() {
   const char* e = getenv("PNP_GYM_QUEUE");
   return !(e && e[0] == '0');
 }
 static int gym_queue_grid() {
   const char* e = getenv("PNP_GYM_QUEUE_CU");
-  const int g = e ? atoi(e) : 192;
-  return g > 0 ? g : 192;
+  const int g = e ? atoi(e) : 224;
+  return g > 0 ? g : 224;
 }
 // the hand-over queue buffer per device (PNP_HQ_ENTRY header ints + one entry per env); its users
 // are serialised by the full image's lease like the route streams

@@ -212,7 +212,7 @@ def test_gym_routing_is_exact(share):
     assert not bool((w >> 16).any()) and int((w & 0xFFFF).max()) == 0
 
 
-@pytest.mark.parametrize("grid", ["2", "192"])
+@pytest.mark.parametrize("grid", ["2", "224"])
 def test_gym_hand_over_queue_is_exact(grid):
     """The hand-over queue (env_dev.h hq_publish / hq_take: the full-tier passes publish the envs
     they hand to the wide tier, a persistent wide consumer grid resumes them concurrently) gives
