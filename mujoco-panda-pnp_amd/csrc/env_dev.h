@@ -974,9 +974,13 @@ static int32_t hand_queue(int32_t B, int** out) {
 // Three side streams per device for the routed passes and the hand-over queue's consumer, forked
 // from and joined back into the caller's stream.  Used only while the full image's lease is held
 // (launch_env_step), which serialises their users per device; creation has its own lock.
+// `last`: recorded on the caller's stream when a routed step is complete; the next routed step
+// (possibly on another stream) waits for it, so two steps never share the per-device selection
+// lists and hand-over queue on the GPU at the same time.
 struct RouteStreams {
   hipStream_t side[3] = {nullptr, nullptr, nullptr};
-  hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr}, cdone = nullptr;
+  hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr}, cdone = nullptr, last = nullptr;
+  bool last_valid = false;
 };
 static int32_t route_streams(RouteStreams** out) {
   static std::mutex mu;
@@ -994,6 +998,7 @@ static int32_t route_streams(RouteStreams** out) {
   }
   if (e == hipSuccess && !r.fork) e = hipEventCreateWithFlags(&r.fork, hipEventDisableTiming);
   if (e == hipSuccess && !r.cdone) e = hipEventCreateWithFlags(&r.cdone, hipEventDisableTiming);
+  if (e == hipSuccess && !r.last) e = hipEventCreateWithFlags(&r.last, hipEventDisableTiming);
   if (e != hipSuccess) { pnp_set_error("pnp_env_step: route streams: %s", hipGetErrorString(e)); return PNP_ERR_HIP; }
   *out = &r;
   return PNP_OK;
@@ -1058,8 +1063,8 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   };
   if (route) {
     if ((rc = route_streams(&rs))) return rc;
-    hipError_t he = hipSuccess;
-    if (queue) {   // a fresh queue, ordered before every pass of this step
+    hipError_t he = rs->last_valid ? hipStreamWaitEvent(s0, rs->last, 0) : hipSuccess;
+    if (queue && he == hipSuccess) {   // a fresh queue, ordered before every pass of this step
       if ((rc = hand_queue(B, &hq))) return rc;
       he = hipMemsetAsync(hq, 0, sizeof(int) * PNP_HQ_ENTRY, s0);
       if (he == hipSuccess) he = hipMemsetAsync(hq + PNP_HQ_ENTRY, 0xFF, sizeof(int) * (size_t)B, s0);
@@ -1133,6 +1138,13 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   if (e->tier) {   // every pass has run: the next step's tiers become current
     hipLaunchKernelGGL(route_commit_kernel, dim3((B + 255) / 256), dim3(256), 0, s0, e->tier, B);
     if ((rc = pnp_check_launch("route_commit_kernel"))) return fail(rc);
+  }
+  if (route) {
+    if (const hipError_t he = hipEventRecord(rs->last, s0)) {
+      pnp_set_error("pnp_env_step: step event: %s", hipGetErrorString(he));
+      return fail(PNP_ERR_HIP);
+    }
+    rs->last_valid = true;
   }
   return lease.launched();   // recorded on the caller's stream, after both joins
 }
