@@ -1487,21 +1487,22 @@ __device__ __attribute__((noinline)) void st_collision_convex(const DevPhys<T>& 
       todo &= todo - 1;
       const int p = __builtin_amdgcn_readlane(pair, src);
       const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
-      // the pair's contacts (up to C_MULTI with multiccd) staged in cst_val, then lanes 0.. append
-      const int n = c_convex(m, s, g1, g2, fmax(m.geom_margin[g1], m.geom_margin[g2]), s.cst_val);
 #if PNP_COMPACT
-      // The compact build carries no multiccd fan (c_convex stops after the first run): a convex
-      // pair in contact hands the sub-step to the full tier, like a capacity overflow.  The fan's
-      // code in this build grew its frames and write-back and cost C3 1 % (round 3), although C3's
-      // settled envs never make a convex contact.  (The first run stays: a pair whose bounding
-      // boxes overlap without contact -- the arm swinging near a board under random servo targets
-      // would otherwise hand its env over too: C3 -30 %.)  MPR is fp64 in every build, so the
-      // tiers take the same hit decision.
-      if (n && m.multiccd && m.geom_type[g1] != 2 && m.geom_type[g2] != 2) {
+      // The compact build runs no MPR: a convex pair it cannot prove separated (c_convex_screen)
+      // hands the sub-step to the full tier, like a capacity overflow, and the full tier's fp64
+      // MPR decides (the same contacts: a proven pair has none).  Round 3 ran the first MPR here
+      // (handing over only pairs in contact: every overlap of bounding boxes handed over had cost
+      // C3 30 %, the arm swinging near a board); in fp64 (round 4) its frame grew the kernel's
+      // scratch 292 -> 704 B per lane and cost C3 2 % although C3's envs rarely run it.
+      if (!c_convex_screen(m, s, g1, g2, fmax(m.geom_margin[g1], m.geom_margin[g2]))) {
         if (l == 0) CAP_FULL(8u);
         wsync();
         return;
       }
+      const int n = 0;
+#else
+      // the pair's contacts (up to C_MULTI with multiccd) staged in cst_val, then lanes 0.. append
+      const int n = c_convex(m, s, g1, g2, fmax(m.geom_margin[g1], m.geom_margin[g2]), s.cst_val);
 #endif
       if (l < n && ncon + l < PH_MAXCON) {
         const T pos[3] = {s.cst_val[l][1], s.cst_val[l][2], s.cst_val[l][3]};

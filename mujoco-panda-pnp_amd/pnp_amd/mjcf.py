@@ -128,6 +128,21 @@ def _convex_hull(verts):
     return hv
 
 
+def _hull_centroid(hv):
+    """Volume centroid of the convex hull of hv: tetrahedra from an interior point (the vertex
+    mean) to every hull facet."""
+    from scipy.spatial import ConvexHull
+    hull = ConvexHull(hv)
+    c0 = hv.mean(0)
+    vol, cen = 0.0, np.zeros(3)
+    for tri in hull.simplices:
+        a, b, c = hv[tri]
+        w = abs(np.dot(a - c0, np.cross(b - c0, c - c0))) / 6.0
+        vol += w
+        cen += w * (a + b + c + c0) / 4.0
+    return cen / vol
+
+
 # ----------------------------------------------------------------------------- parser
 @dataclass
 class _Class:
@@ -476,7 +491,7 @@ class _ModelBuilder:
         geom_dataid = -np.ones(ng, np.int32)
         geom_solmix = np.ones(ng)
         geom_rbound = np.zeros(ng)
-        mesh_names, mesh_vert, mesh_vertadr, mesh_vertnum = [], [], [], []
+        mesh_names, mesh_vert, mesh_vertadr, mesh_vertnum, mesh_center = [], [], [], [], []
         for k, g in enumerate(geoms):
             t = _GEOM_TYPES[g.get("type", "sphere")]
             geom_type[k] = t
@@ -500,14 +515,25 @@ class _ModelBuilder:
             geom_solmix[k] = float(g.get("solmix", 1))
             collidable = geom_contype[k] != 0 or geom_conaffinity[k] != 0
             if t == GEOM_MESH and collidable:
+                # MuJoCo's mesh compiler moves a mesh into its own frame at the mesh's centre of mass
+                # and shifts the geom frame by the same offset (mjCMesh / mjCGeom: geom pos += quat
+                # * mesh pos): the geom centre -- MPR's interior point -- then lies inside the hull.
+                # Here the centre is the hull's volume centroid (the collision shape is the hull;
+                # for a convex mesh the two coincide).  Without it the finger meshes' frames sit
+                # outside their hulls, and MPR reported ~5 cm of phantom penetration between two
+                # closed fingers whose hulls are 3 mm apart.
                 mname = g["mesh"]
                 if mname not in mesh_names:
                     hv = _convex_hull(_load_mesh_vertices(self.c.meshes[mname]))
+                    cen = _hull_centroid(hv)
+                    hv = hv - cen
                     mesh_vertadr.append(sum(len(v) for v in mesh_vert))
                     mesh_vertnum.append(len(hv))
                     mesh_vert.append(hv)
                     mesh_names.append(mname)
+                    mesh_center.append(cen)
                 geom_dataid[k] = mesh_names.index(mname)
+                geom_pos[k] = geom_pos[k] + quat2mat(geom_quat[k]) @ mesh_center[geom_dataid[k]]
                 geom_rbound[k] = np.linalg.norm(mesh_vert[geom_dataid[k]], axis=1).max()
             elif t == GEOM_BOX:
                 geom_rbound[k] = np.linalg.norm(geom_size[k])

@@ -58,10 +58,16 @@ def _screen(m, gx, gmat, g1, g2, margin):
 
 
 def _states(model):
-    st = PS.reset_states(6, seed=3, model=model)
+    """Arm poses swung through the scene, plus states with convex contacts: the hand pushed into
+    cube1 and the fingers closed past each other (pads pressed)."""
+    st = PS.reset_states(8, seed=3, model=model)
     rng = np.random.default_rng(4)
-    st["qpos"][:, :7] += rng.normal(size=(6, 7)) * 0.6     # arm swung through the scene
-    st["qpos"][:, 7:9] = rng.uniform(-0.002, 0.04, size=(6, 2))
+    st["qpos"][:4, :7] += rng.normal(size=(4, 7)) * 0.6     # arm swung through the scene
+    st["qpos"][:, 7:9] = rng.uniform(-0.002, 0.04, size=(8, 2))
+    sx, _ = O.site_kinematics(st["qpos"][4:6], model=model)
+    a = int(model.jnt_qposadr[model.joint_id("cube1_joint")])
+    st["qpos"][4:6, a:a + 3] = sx[:, model.site_id("ee_center_site")] + [0.0, 0.0, 0.075]
+    st["qpos"][6:, 7:9] = -0.003
     return st
 
 
@@ -86,19 +92,22 @@ def test_screen_never_hides_an_mpr_contact(model):
         p1, p2 = weld[par[w1]], weld[par[w2]]
         return not (w1 != 0 and w2 != 0 and (w1 == p2 or w2 == p1))
     margin = 0.0
-    proven = checked = 0
+    proven = checked = hits = 0
     for b in range(st["qpos"].shape[0]):
         row = {k: st[k][b] for k in O.STATE_KEYS}
         _, gx, gmat = O.convex_probe(row, int(meshes[0]), int(meshes[1]), model=model)
         gx32, gm32 = gx.astype(np.float32).astype(np.float64), gmat.astype(np.float32).astype(np.float64)
         for g2 in meshes:
-            for g1 in others[::2]:
-                if g1 >= g2 or not is_pair(int(g1), int(g2)):
+            for g1 in others:
+                # (the engine's convex pairs put the mesh second: any index order)
+                if g1 == g2 or (int(model.geom_type[g1]) == 7 and g1 > g2) or not is_pair(int(g1), int(g2)):
                     continue
                 if not _screen(model, gx32, gm32, int(g1), int(g2), margin):
+                    hits += O.convex_probe(row, int(g1), int(g2), model=model)[0] is not None
                     continue
                 proven += 1
                 hit, _, _ = O.convex_probe(row, int(g1), int(g2), model=model)
                 checked += 1
                 assert hit is None, (b, g1, g2, hit)
     assert checked > 50, (proven, checked)
+    assert hits > 0, hits   # the states do hold convex contacts the screen must not hide
