@@ -174,19 +174,28 @@ def _oracle_qacc(model, st):
 
 def _conditioning_floor(model, st, nsub=1, trials=3, per_env=False):
     """How far the exact (fp64) step itself moves, per tree and in the same metrics, when qpos and
-    qvel are perturbed by one fp32 ulp (random directions, fixed seed): the accuracy an fp32
-    computation can be asked for (a backward-stable fp32 step is within a small multiple of it)."""
+    qvel are perturbed at fp32 resolution (random directions, fixed seed): the accuracy an fp32
+    computation can be asked for (a backward-stable fp32 step is within a small multiple of it).
+    Two kinds of trials: `trials` of one fp32 ulp of each coordinate, and as many of half an fp32
+    ulp of 1.0 (6e-8) on every coordinate -- fp32 kinematics rounds world-frame positions at ~1 m
+    whatever the joint's own magnitude, which one ulp of a slide joint at 3 mm (2e-10) does not
+    model (round 4: two finger hulls in face contact, their MPR normal not unique, moved 1.6e-4
+    in fp32 against a one-ulp floor of 5.1e-5 and a world-scale floor of 6.2e-5)."""
     rng = np.random.default_rng(2024)
     ref = PS.copy_state(st)
     O.step(ref, nsub=nsub, nthreads=8, model=model)
     qa_ref = _oracle_qacc(model, st)
     fv, fa = 0.0, 0.0
-    for _ in range(trials):
+    for t in range(2 * trials):
         p = PS.copy_state(st)
         for k in ("qpos", "qvel"):
             x = p[k].astype(np.float32)
             up = rng.random(x.shape) < 0.5
-            p[k] = np.where(up, np.nextafter(x, np.float32(np.inf)), np.nextafter(x, np.float32(-np.inf))).astype(np.float64)
+            if t < trials:
+                p[k] = np.where(up, np.nextafter(x, np.float32(np.inf)), np.nextafter(x, np.float32(-np.inf))).astype(np.float64)
+            else:
+                step = np.maximum(np.spacing(np.abs(x)), np.spacing(np.float32(1.0)) / 2).astype(np.float64)
+                p[k] = x.astype(np.float64) + np.where(up, step, -step)
         q = PS.copy_state(p)
         O.step(q, nsub=nsub, nthreads=8, model=model)
         q["qvel0"] = p["qvel"]
