@@ -596,8 +596,9 @@ def _step_f32_mode(engine, st, nsub, mode):
 @pytest.fixture(scope="module")
 def pressed(model):
     """Closed fingers pressed into each other (pad boxes interpenetrating 1-4 mm, finger servos
-    closing): 52-61 contacts, more than the full tier's 48 -- the closed-gripper states of the
-    random-action gym workload (tools/contact_census.py, tools/gym_profile.py)."""
+    closing; past -2.5 mm per finger the two finger hulls touch face to face too): 47-63 contacts,
+    mostly more than the full tier's 48 -- the closed-gripper states of the random-action gym
+    workload (tools/contact_census.py, tools/gym_profile.py)."""
     n = 12
     st = PS.reset_states(n, seed=11, model=model)
     st["qpos"][:, 7:9] = -np.linspace(0.001, 0.004, n)[:, None]
