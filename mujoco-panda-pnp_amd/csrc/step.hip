@@ -936,14 +936,16 @@ __device__ void chol_block(const T* A, T* Lb, int n, int ld) {
 // x = (L L^T)^-1 b on one block; x, b are indexed through dof lists (idx) of a global vector
 template <typename T>
 __device__ void chol_solve_block(const T* Lb, int n, int ld, const int* idx, int adr, T* x, const T* b) {
-  T y[PH_MAXV];
+  // the forward substitution's y lives in x itself (step i reads b[i] before writing y[i] there,
+  // so x may alias b): no private array, whose frame (PH_MAXV floats) every caller of the solves
+  // would carry although the scene's trees never take this path (<= 9 dofs: registers)
   for (int i = 0; i < n; i++) {
     T v = b[idx ? idx[i] : adr + i];
-    for (int k = 0; k < i; k++) v -= Lb[i * ld + k] * y[k];
-    y[i] = v / Lb[i * ld + i];
+    for (int k = 0; k < i; k++) v -= Lb[i * ld + k] * x[idx ? idx[k] : adr + k];
+    x[idx ? idx[i] : adr + i] = v / Lb[i * ld + i];
   }
   for (int i = n - 1; i >= 0; i--) {
-    T v = y[i];
+    T v = x[idx ? idx[i] : adr + i];
     for (int k = i + 1; k < n; k++) v -= Lb[k * ld + i] * x[idx ? idx[k] : adr + k];
     x[idx ? idx[i] : adr + i] = v / Lb[i * ld + i];
   }
@@ -3491,14 +3493,13 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
         if (nt == 9) tree_solve_fixed<9>(s.L + o, Jr, Wr);
         else if (nt == 6) tree_solve_fixed<6>(s.L + o, Jr, Wr);
         else {
-          T y[PH_MAXTDOF];
-          for (int i = 0; i < nt; i++) {
+          for (int i = 0; i < nt; i++) {   // forward substitution into Wr (no private array)
             T v = Jr[i];
-            for (int k = 0; k < i; k++) v -= s.L[o + i * nt + k] * y[k];
-            y[i] = v / s.L[o + i * nt + i];
+            for (int k = 0; k < i; k++) v -= s.L[o + i * nt + k] * Wr[k];
+            Wr[i] = v / s.L[o + i * nt + i];
           }
           for (int i = nt - 1; i >= 0; i--) {
-            T v = y[i];
+            T v = Wr[i];
             for (int k = i + 1; k < nt; k++) v -= s.L[o + k * nt + i] * Wr[k];
             Wr[i] = v / s.L[o + i * nt + i];
           }
@@ -3530,14 +3531,13 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
           base += n;
           continue;
         }
-        T y[PH_MAXTDOF];
-        for (int i = 0; i < n; i++) {
+        for (int i = 0; i < n; i++) {   // forward substitution into the W row (no private array)
           T v = EJ(r, base + i);
-          for (int k = 0; k < i; k++) v -= s.L[o + i * n + k] * y[k];
-          y[i] = v / s.L[o + i * n + i];
+          for (int k = 0; k < i; k++) v -= s.L[o + i * n + k] * EW(r, base + k);
+          EW(r, base + i) = v / s.L[o + i * n + i];
         }
         for (int i = n - 1; i >= 0; i--) {
-          T v = y[i];
+          T v = EW(r, base + i);
           for (int k = i + 1; k < n; k++) v -= s.L[o + k * n + i] * EW(r, base + k);
           EW(r, base + i) = v / s.L[o + i * n + i];
         }
