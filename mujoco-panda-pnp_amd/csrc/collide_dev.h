@@ -475,14 +475,48 @@ __device__ __forceinline__ void c_mksupport(const DevPhys<T>& /*image: phys<T>()
   c_support(m, b, nd, v.v2);
   cs3(v.v, v.v1, v.v2);
 }
-__device__ __forceinline__ void c_portal_dir(const SVert& p1, const SVert& p2, const SVert& p3, CT* dir) {
+// Portal vertices in registers (SVert) or, in the wide build, with their two support points in
+// a per-wave LDS slot (SVertL: v in registers; v1 / v2 are read only by the touching case and
+// findPos): 48 fewer fp64 VGPRs live across MPR's portal loops.  Slot ids are wave-uniform; a new
+// support takes the slot no portal vertex holds.  Every lane writes the same values.
+struct SVertL {
+  CT v[3];
+  int id;
+};
+template <typename T>
+__device__ __forceinline__ void c_mks(const DevPhys<T>& m, const CShape<T>& a, const CShape<T>& b, const CT* d, SVert& v,
+                                      double (*)[6], int) {
+  c_mksupport(m, a, b, d, v);
+}
+template <typename T>
+__device__ __forceinline__ void c_mks(const DevPhys<T>& m, const CShape<T>& a, const CShape<T>& b, const CT* d, SVertL& v,
+                                      double (*sv)[6], int id) {
+  SVert t;
+  c_mksupport(m, a, b, d, t);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    v.v[k] = t.v[k];
+    sv[id][k] = t.v1[k];
+    sv[id][3 + k] = t.v2[k];
+  }
+  v.id = id;
+}
+__device__ __forceinline__ CT c_sv1(const SVert& p, double (*)[6], int k) { return p.v1[k]; }
+__device__ __forceinline__ CT c_sv2(const SVert& p, double (*)[6], int k) { return p.v2[k]; }
+__device__ __forceinline__ CT c_sv1(const SVertL& p, double (*sv)[6], int k) { return CT(sv[p.id][k]); }
+__device__ __forceinline__ CT c_sv2(const SVertL& p, double (*sv)[6], int k) { return CT(sv[p.id][3 + k]); }
+__device__ __forceinline__ int c_svid(const SVert&) { return 0; }
+__device__ __forceinline__ int c_svid(const SVertL& p) { return p.id; }
+template <typename V>
+__device__ __forceinline__ void c_portal_dir(const V& p1, const V& p2, const V& p3, CT* dir) {
   CT a[3], b[3];
   cs3(a, p2.v, p1.v);
   cs3(b, p3.v, p1.v);
   cc3(dir, a, b);
   cnorm(dir);
 }
-__device__ __forceinline__ bool c_reach_tol(const SVert& p1, const SVert& p2, const SVert& p3, const SVert& v4,
+template <typename V>
+__device__ __forceinline__ bool c_reach_tol(const V& p1, const V& p2, const V& p3, const V& v4,
                                             const CT* dir, CT tol) {
   const CT dv4 = cd3(v4.v, dir);
   CT t1 = dv4 - cd3(p1.v, dir), t2 = dv4 - cd3(p2.v, dir), t3 = dv4 - cd3(p3.v, dir);
@@ -490,7 +524,8 @@ __device__ __forceinline__ bool c_reach_tol(const SVert& p1, const SVert& p2, co
   t1 = t1 < t3 ? t1 : t3;
   return ccd_eq(t1, tol) || t1 < tol;
 }
-__device__ __forceinline__ void c_expand(SVert& p0, SVert& p1, SVert& p2, SVert& p3, const SVert& v4) {
+template <typename V>
+__device__ __forceinline__ void c_expand(const SVert& p0, V& p1, V& p2, V& p3, const V& v4) {
   CT v4v0[3];
   cc3(v4v0, v4.v, p0.v);
   if (cd3(p1.v, v4v0) > 0) {
@@ -550,11 +585,13 @@ __device__ T c_tri_dist2(const T* P, const T* x0, const T* B, const T* C, T* w) 
 }
 
 // ccdMPRPenetration: true and (depth, dir, pos) on intersection
-template <typename T>
-__device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A, const CShape<T>& Bs, CT& depth, CT* dir, CT* pos) {
+template <typename T, typename V = SVert>
+__device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A, const CShape<T>& Bs, CT& depth, CT* dir, CT* pos,
+                      double (*sv)[6] = nullptr) {
   const DevPhys<T>& m = phys<T>();
   const CT tol = CT(1e-6);   // mjOption mpr_tolerance
-  SVert p0, p1, p2, p3, v4;
+  SVert p0;
+  V p1, p2, p3, v4;
   CT d[3], va[3], vb[3], dot;
   // ---- discover portal
   for (int k = 0; k < 3; k++) { p0.v1[k] = A.pos[k]; p0.v2[k] = Bs.pos[k]; }
@@ -562,12 +599,12 @@ __device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A
   if (p0.v[0] == 0 && p0.v[1] == 0 && p0.v[2] == 0) p0.v[0] += ccd_eps<CT>() * CT(10);
   d[0] = -p0.v[0]; d[1] = -p0.v[1]; d[2] = -p0.v[2];
   cnorm(d);
-  c_mksupport(m, A, Bs, d, p1);
+  c_mks(m, A, Bs, d, p1, sv, 0);
   dot = cd3(p1.v, d);
   if (ccd_zero(dot) || dot < 0) return false;
   cc3(d, p0.v, p1.v);
   if (ccd_zero(cd3(d, d))) {
-    for (int k = 0; k < 3; k++) pos[k] = CT(0.5) * (p1.v1[k] + p1.v2[k]);
+    for (int k = 0; k < 3; k++) pos[k] = CT(0.5) * (c_sv1(p1, sv, k) + c_sv2(p1, sv, k));
     if (p1.v[0] == 0 && p1.v[1] == 0 && p1.v[2] == 0) {   // touching on v1
       depth = 0;
       dir[0] = dir[1] = dir[2] = 0;
@@ -579,7 +616,7 @@ __device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A
     return true;
   }
   cnorm(d);
-  c_mksupport(m, A, Bs, d, p2);
+  c_mks(m, A, Bs, d, p2, sv, 1);
   dot = cd3(p2.v, d);
   if (ccd_zero(dot) || dot < 0) return false;
   cs3(va, p1.v, p0.v);
@@ -587,14 +624,14 @@ __device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A
   cc3(d, va, vb);
   cnorm(d);
   if (cd3(d, p0.v) > 0) {
-    const SVert t = p1;
+    const V t = p1;
     p1 = p2;
     p2 = t;
     d[0] = -d[0]; d[1] = -d[1]; d[2] = -d[2];
   }
   bool found = false;
   for (int guard = 0; guard < 1000 && !found; guard++) {
-    c_mksupport(m, A, Bs, d, p3);
+    c_mks(m, A, Bs, d, p3, sv, 3 - c_svid(p1) - c_svid(p2));
     dot = cd3(p3.v, d);
     if (ccd_zero(dot) || dot < 0) return false;
     bool cont = false;
@@ -622,7 +659,7 @@ __device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A
     c_portal_dir(p1, p2, p3, d);
     dot = cd3(d, p1.v);
     if (ccd_zero(dot) || dot > 0) { inside = true; break; }
-    c_mksupport(m, A, Bs, d, v4);
+    c_mks(m, A, Bs, d, v4, sv, 6 - c_svid(p1) - c_svid(p2) - c_svid(p3));
     dot = cd3(v4.v, d);
     if (!(ccd_zero(dot) || dot > 0) || c_reach_tol(p1, p2, p3, v4, d, tol)) return false;
     c_expand(p0, p1, p2, p3, v4);
@@ -631,7 +668,7 @@ __device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A
   // ---- penetration: refine towards the surface
   for (int it = 0;; it++) {
     c_portal_dir(p1, p2, p3, d);
-    c_mksupport(m, A, Bs, d, v4);
+    c_mks(m, A, Bs, d, v4, sv, 6 - c_svid(p1) - c_svid(p2) - c_svid(p3));
     if (c_reach_tol(p1, p2, p3, v4, d, tol) || it > 50) {
       const CT O[3] = {0, 0, 0};
       depth = PM<CT>::sqrt_(c_tri_dist2(O, p1.v, p2.v, p3.v, dir));
@@ -654,8 +691,8 @@ __device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A
       }
       const CT inv = CT(1) / sum;
       for (int k = 0; k < 3; k++) {
-        const CT q1 = b0 * p0.v1[k] + b1 * p1.v1[k] + b2 * p2.v1[k] + b3 * p3.v1[k];
-        const CT q2 = b0 * p0.v2[k] + b1 * p1.v2[k] + b2 * p2.v2[k] + b3 * p3.v2[k];
+        const CT q1 = b0 * p0.v1[k] + b1 * c_sv1(p1, sv, k) + b2 * c_sv1(p2, sv, k) + b3 * c_sv1(p3, sv, k);
+        const CT q2 = b0 * p0.v2[k] + b1 * c_sv2(p1, sv, k) + b2 * c_sv2(p2, sv, k) + b3 * c_sv2(p3, sv, k);
         pos[k] = CT(0.5) * (q1 * inv + q2 * inv);
       }
       return true;
@@ -870,10 +907,15 @@ __device__ void t_makeframe(T f[9]) {
 constexpr int C_MULTI = 5;
 template <typename T>
 __device__ __forceinline__ bool c_mpr_contact(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>* sh, T margin,
-                                              T* c) {
+                                              T* c, double (*sv)[6]) {
   const DevPhys<T>& m = phys<T>();
   CT depth, nrm[3], pos[3];
+#if PNP_WIDE
+  if (!c_mpr<T, SVertL>(m, sh[0], sh[1], depth, nrm, pos, sv)) return false;
+#else
+  (void)sv;
   if (!c_mpr(m, sh[0], sh[1], depth, nrm, pos)) return false;
+#endif
   if (nrm[0] == 0 && nrm[1] == 0 && nrm[2] == 0) return false;   // normal undefined
   if (sh[0].type == 2) {   // mjc_fixNormal: the sphere's normal at the contact point (g1 of its pairs)
     CT n[3];
@@ -981,7 +1023,12 @@ __device__ C_RUN_INLINE bool c_convex_run(const Env<T>& s, int g1, int g2, T mar
     c_fan_rotate(sh, s.gmat[g1], s.gmat[g2], f, o, t);
   }
   T c[7];
-  const bool hit = c_mpr_contact(m, sh, margin, c);
+#if PNP_WIDE
+  double (*sv)[6] = const_cast<Env<T>&>(s).mpr_sv[threadIdx.x >> 6];   // this wave's portal slots
+#else
+  double (*sv)[6] = nullptr;
+#endif
+  const bool hit = c_mpr_contact(m, sh, margin, c, sv);
   if (hit && (threadIdx.x & 63) == 0)
     for (int k = 0; k < 7; k++) val[slot][k] = c[k];
   return hit;

@@ -244,6 +244,9 @@ struct Env {
   unsigned char mw_hit[NT];    // the convex pass: staging slot holds a contact
   unsigned char mw_fan[NT];    // the convex pass: round-local pairs whose multiccd trials run
 #endif
+#if PNP_WIDE
+  double mpr_sv[4][4][6];      // per wave: MPR's portal support points (collide_dev.h SVertL)
+#endif
 };
 static_assert(sizeof(((Env<float>*)0)->efc_Jv) >= 7 * 4 * NT + 2 * NT + 4 + 2 * PH_MAXLIVE,
               "collision staging + broadphase survivors must fit the efc_Jv union");
