@@ -475,7 +475,7 @@ __device__ __forceinline__ void c_mksupport(const DevPhys<T>& /*image: phys<T>()
   c_support(m, b, nd, v.v2);
   cs3(v.v, v.v1, v.v2);
 }
-// Portal vertices in registers (SVert) or, in the wide build, with their two support points in
+// Portal vertices in registers (SVert) or, in the full / wide builds, with their two support points in
 // a per-wave LDS slot (SVertL: v in registers; v1 / v2 are read only by the touching case and
 // findPos): 48 fewer fp64 VGPRs live across MPR's portal loops.  Slot ids are wave-uniform; a new
 // support takes the slot no portal vertex holds.  Every lane writes the same values.
@@ -910,7 +910,7 @@ __device__ __forceinline__ bool c_mpr_contact(const DevPhys<T>& /*image: phys<T>
                                               T* c, double (*sv)[6]) {
   const DevPhys<T>& m = phys<T>();
   CT depth, nrm[3], pos[3];
-#if PNP_WIDE
+#if PNP_MPR_SLOTS
   if (!c_mpr<T, SVertL>(m, sh[0], sh[1], depth, nrm, pos, sv)) return false;
 #else
   (void)sv;
@@ -1023,7 +1023,7 @@ __device__ C_RUN_INLINE bool c_convex_run(const Env<T>& s, int g1, int g2, T mar
     c_fan_rotate(sh, s.gmat[g1], s.gmat[g2], f, o, t);
   }
   T c[7];
-#if PNP_WIDE
+#if PNP_MPR_SLOTS
   double (*sv)[6] = const_cast<Env<T>&>(s).mpr_sv[threadIdx.x >> 6];   // this wave's portal slots
 #else
   double (*sv)[6] = nullptr;

@@ -61,6 +61,9 @@
 // PNP_MW: the fp32 gym kernels of this build run several waves per env (helper waves for the convex
 // pass): the wide build (4 waves, 1 env per CU) and the full build (2 waves, 4 envs per CU)
 #define PNP_MW ((PNP_WIDE || (!PNP_COMPACT && !PNP_GYM)) && !PNP_WIDE64)
+// MPR's portal support points in per-wave LDS slots (collide_dev.h SVertL): the full and wide
+// builds (the compact builds run no MPR; the fp64 wide build keeps registers)
+#define PNP_MPR_SLOTS (!PNP_COMPACT && !PNP_WIDE64)
 #define PNP_LEAN (PNP_COMPACT || PNP_WIDE || PNP_WIDE64)
 // PNP_BIG_ISLANDS: the solver's whole-wave paths for islands with more rows than a wave (line
 // search, gradient, MFMA Hessian).  Compiled out of the compact build, which hands such islands
@@ -244,8 +247,8 @@ struct Env {
   unsigned char mw_hit[NT];    // the convex pass: staging slot holds a contact
   unsigned char mw_fan[NT];    // the convex pass: round-local pairs whose multiccd trials run
 #endif
-#if PNP_WIDE
-  double mpr_sv[4][4][6];      // per wave: MPR's portal support points (collide_dev.h SVertL)
+#if PNP_MPR_SLOTS
+  double mpr_sv[PNP_WIDE ? 4 : 2][4][6];   // per wave: MPR's portal support points (collide_dev.h SVertL)
 #endif
 };
 static_assert(sizeof(((Env<float>*)0)->efc_Jv) >= 7 * 4 * NT + 2 * NT + 4 + 2 * PH_MAXLIVE,
