@@ -51,6 +51,7 @@ STEP_BYTES_PER_ENV = 4 * (37 + 33 + 9 + 3 + 4 + 33 + 1 + 1) + 4 * (37 + 33 + 33 
 NSUB = 25                       # panda_env.py n_substeps
 NSETTLE = 250                   # _env_setup settle sub-steps (panda_env.py:124-141)
 NCTRL = 64                      # distinct per-step ctrl draws, cycled
+RANK_LEGS = {}                  # leg -> every rank's [wall s, kernel ms] (dist_record)
 
 
 def host_threads():
@@ -80,11 +81,13 @@ def _oracle():
     return O
 
 
-def _timed(fn, steps, warmup, dist, per_call_events=True):
+def _timed(fn, steps, warmup, dist, per_call_events=True, ranks_out=None):
     """W untimed + K timed calls bracketed by barrier + synchronize; returns (wall s, avg event ms).
     per_call_events: an event pair around every call (the average launch duration of long
     kernels); off, one pair around the K calls (average = region / K): for kernels of tens of
-    microseconds, where event markers between the launches cost ~8 us per call (IK leg)."""
+    microseconds, where event markers between the launches cost ~8 us per call (IK leg).
+    ranks_out (a list): receives every rank's own (wall s, kernel ms), gathered, in rank order --
+    the job's figures are their max."""
     for i in range(warmup):
         fn(i)
     torch.cuda.synchronize()
@@ -112,6 +115,8 @@ def _timed(fn, steps, warmup, dist, per_call_events=True):
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
     if not per_call_events:
         kern_ms /= steps
+    if ranks_out is not None:
+        ranks_out[:] = gather_ranks([elapsed, kern_ms]) if dist else [[elapsed, kern_ms]]
     if dist:
         elapsed, kern_ms = reduce_max([elapsed, kern_ms], "cuda")
     return elapsed, kern_ms
@@ -122,6 +127,59 @@ def reduce_max(values, device):
     t = torch.tensor(values, device=device, dtype=torch.float64)
     torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     return [float(v) for v in t]
+
+
+def gather_ranks(obj):
+    """Every rank's `obj`, in rank order (all_gather_object: gloo or RCCL)."""
+    out = [None] * torch.distributed.get_world_size()
+    torch.distributed.all_gather_object(out, obj)
+    return out
+
+
+def rank_identity(local, device):
+    """What this rank ran on: its rank / local rank and, on a GPU, the device index, name and PCI
+    bus (one MI355X per rank under RCCL -- the record shows it instead of assuming it)."""
+    me = {"rank": int(os.environ.get("RANK", "0")), "local_rank": local,
+          "visible_devices": os.environ.get("HIP_VISIBLE_DEVICES", os.environ.get("CUDA_VISIBLE_DEVICES"))}
+    if device == "cuda":
+        d = torch.cuda.current_device()
+        pr = torch.cuda.get_device_properties(d)
+        me.update(device=d, device_name=pr.name, arch=getattr(pr, "gcnArchName", None),
+                  pci=f"{getattr(pr, 'pci_domain_id', 0):04x}:{getattr(pr, 'pci_bus_id', 0):02x}:"
+                      f"{getattr(pr, 'pci_device_id', 0):02x}")
+    else:
+        me.update(device="cpu")
+    return me
+
+
+def dist_record(expected, world, dist, ident, legs):
+    """The job as torch.distributed saw it -- world size and backend from the process group (not
+    the launcher's environment), each rank's device and its own timings per leg -- and the check
+    that it is the job --gpus asked for (rank 0 raises otherwise: a record that is not N ranks on N
+    distinct GPUs is never printed).  ident: every rank's rank_identity; legs: {leg: every rank's
+    [wall s, kernel ms]}."""
+    ws = torch.distributed.get_world_size() if dist else 1
+    backend = str(torch.distributed.get_backend()) if dist else None
+    ranks = []
+    for r, me in enumerate(ident):
+        row = dict(me)
+        for leg, vals in legs.items():
+            if vals:
+                row[f"{leg}_wall_s"], row[f"{leg}_kernel_ms"] = float(vals[r][0]), float(vals[r][1])
+        ranks.append(row)
+    rec = {"world_size": ws, "backend": backend, "gpus_flag": expected, "ranks": ranks}
+    problems = []
+    if ws != expected or world != expected:
+        problems.append(f"process group world size {ws} (launcher {world}) != --gpus {expected}")
+    if [r["rank"] for r in ranks] != list(range(ws)):
+        problems.append(f"ranks {[r['rank'] for r in ranks]} are not 0..{ws - 1}")
+    if backend == "nccl":
+        pcis = [r.get("pci") for r in ranks]
+        if len(set(pcis)) != len(pcis):
+            problems.append(f"ranks share GPUs: {pcis}")
+    if problems:
+        raise SystemExit("bench.py: " + "; ".join(problems))
+    return rec
 
 
 def _progress(rank, msg):
@@ -213,7 +271,7 @@ def run_step(args, engine, model, rank, world, dist):
         st["ctrl"] = ctrl[i % NCTRL]
         engine.step(st, NSUB)
 
-    elapsed, kern_ms = _timed(fn, args.steps, args.warmup, dist)
+    elapsed, kern_ms = _timed(fn, args.steps, args.warmup, dist, ranks_out=RANK_LEGS.setdefault("step", []))
     _progress(rank, f"step leg done: {total_steps(B, world, args.steps) / elapsed / 1e6:.2f} M env-steps/s")
     warn = int((st["warn"].to(torch.int64) & 0xFFFFFFFF).max())   # warn is int32: bit 31 reads negative
     finite = bool(torch.isfinite(st["qpos"]).all())
@@ -281,7 +339,8 @@ def run_gym(engine, B, rank, world, dist, steps=3, warmup=1):
     env.reset()
     acts = torch.as_tensor(np.random.default_rng(7 + rank).uniform(-1, 1, size=(4, B, 7)), dtype=torch.float32,
                            device=engine.device)
-    elapsed, kern_ms = _timed(lambda i: env.step(acts[i % 4]), steps, warmup, dist)
+    elapsed, kern_ms = _timed(lambda i: env.step(acts[i % 4]), steps, warmup, dist,
+                              ranks_out=RANK_LEGS.setdefault("gym", []))
     sub = env.cfg.n_substeps * env.cfg.n_calls
     return {"gym_steps_per_s": B * world * steps / elapsed, "env_steps_per_s": B * world * steps * sub / elapsed,
             "ms_per_gym_step": elapsed / steps * 1e3, "kernel_avg_ms": kern_ms, "sub_steps_per_gym_step": sub,
@@ -305,7 +364,7 @@ def run_tqc(engine, B, rank, world, dist, steps=3, warmup=2, learner_reps=20):
         agent.collect_step()
         agent.train()
 
-    elapsed, kern_ms = _timed(fn, steps, warmup, dist)
+    elapsed, kern_ms = _timed(fn, steps, warmup, dist, ranks_out=RANK_LEGS.setdefault("tqc", []))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(learner_reps):
@@ -377,7 +436,7 @@ def run_ik(args, engine, model, rank, world, dist, steps=None, warmup=None, base
                pos_error=torch.empty(B, device=dev), iterations=torch.empty(B, dtype=torch.int32, device=dev),
                flags=torch.empty(B, dtype=torch.uint8, device=dev))
     elapsed, kern_ms = _timed(lambda i: engine.ik_dls_into(q0, tgt, out, **prm), steps, warmup, dist,
-                              per_call_events=False)
+                              per_call_events=False, ranks_out=RANK_LEGS.setdefault("ik", []))
     iters = out["iterations"].cpu().numpy()
     fl = out["flags"].cpu().numpy()
     achieved = IK_BYTES_PER_SOLVE * B / (kern_ms * 1e-3) / 1e9
@@ -462,15 +521,20 @@ def spawn_ranks(n, argv, poll_s=0.2):
     return rc
 
 
-def _launch_selftest(rank, world):
+def _launch_selftest(rank, world, expected):
     """--launch-selftest: the rank wiring alone (gloo, no GPU): every rank joins the group and
     the job's view of it is printed by rank 0 (tests/test_dist_cpu.py)."""
     torch.distributed.init_process_group("gloo")
     t = torch.tensor([rank, 1], dtype=torch.int64)
     torch.distributed.all_reduce(t)
+    # the N > 1 record's "dist" block, built by the same code as a GPU run's (timings: a stand-in
+    # "wall" of 1 + rank s)
+    ident = gather_ranks(rank_identity(int(os.environ.get("LOCAL_RANK", "0")), "cpu"))
+    legs = {"step": gather_ranks([1.0 + rank, 0.5 + rank])}
+    drec = dist_record(expected, world, True, ident, legs)
     if rank == 0:
         print(json.dumps({"world": torch.distributed.get_world_size(), "rank_sum": int(t[0]), "ranks": int(t[1]),
-                          "local_ranks": os.environ.get("LOCAL_RANK")}), flush=True)
+                          "local_ranks": os.environ.get("LOCAL_RANK"), "dist": drec}), flush=True)
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
 
@@ -506,7 +570,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.launch_selftest:
-        _launch_selftest(rank, world)
+        _launch_selftest(rank, world, args.gpus if args.gpus is not None else world)
         return
     dist = world > 1
     if dist:
@@ -523,6 +587,9 @@ def main():
         rec = run_step(args, engine, model, rank, world, dist)
     else:
         rec = run_ik(args, engine, model, rank, world, dist)
+    me = rank_identity(local, "cuda")
+    ident = gather_ranks(me) if dist else [me]
+    rec["dist"] = dist_record(args.gpus if args.gpus is not None else world, world, dist, ident, RANK_LEGS)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if dist:

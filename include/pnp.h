@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 9
+#define PNP_ABI_VERSION 10
 
 #define PNP_OK 0
 #define PNP_ERR_ARG -1
@@ -384,6 +384,13 @@ int32_t pnp_env_step(pnp_model* model, const pnp_state* state, const pnp_env_par
 int32_t pnp_env_step_f64(pnp_model* model, const pnp_state_f64* state, const pnp_env_params* params,
                          const pnp_env_state* env, const double* action, const pnp_env_out* out, int32_t B,
                          void* stream);
+/* Hand-over queue of the routed fp32 gym step (csrc/env_dev.h PNP_HQ_*), after the last such step
+ * on the current device; synchronises the device.  out5: [0] envs the full-tier passes handed to
+ * the wide tier through the queue, [1] producer workgroups done, [2] consumer claims, [3] consumers
+ * that gave up waiting (PNP_GYM_QUEUE_TIMEOUT_US, default 20 s), [4] envs the fallback wide resume
+ * pass finished after the join (the envs such consumers left).  Diagnostic: an env is never left
+ * mid-step ([3] > 0 costs time, not results). */
+int32_t pnp_env_queue_status(int32_t* out5);
 
 /* ------------------------------------------------------------------ skills */
 /* RotateSkill.reset's trajectory (reference skills/rotate.py:39-46) for B skills: target =

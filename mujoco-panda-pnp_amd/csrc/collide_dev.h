@@ -247,8 +247,8 @@ __device__ void c_box_face(const T* pr, const T* Rr, const T* sr, int ia, const 
 }
 
 template <typename T, class S>
-__device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, const T* R2, const T* s2, T margin, S& out) {
-  const T Tv[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+__device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, const T* R2, const T* s2, const T* Tv,
+                          T margin, S& out) {
   T A[3][3], Bm[3][3], AB[3][3];
   for (int i = 0; i < 3; i++)
     for (int k = 0; k < 3; k++) { A[i][k] = R1[3 * k + i]; Bm[i][k] = R2[3 * k + i]; }
@@ -928,6 +928,67 @@ __device__ __forceinline__ bool c_mpr_contact(const DevPhys<T>& /*image: phys<T>
   for (int k = 0; k < 3; k++) { c[1 + k] = T(pos[k]); c[4 + k] = T(nrm[k]); }
   return true;
 }
+// A geom's world frame for the colliders, in CT.  fp32 builds (PNP_XLO): the position from the
+// body's fp32 pair xpos + xlo (the fp64 kinematic chain's position) plus the body frame times the
+// geom offset, in CT; the rotation (MPR) from xquat + xqlo, the chain's quaternion, where the
+// build keeps it (PNP_XQLO), else gmat -- not the geom's fp32 gpos / gmat, rounded at world scale
+// (~3e-8 m at 1 m) and per body (~6e-8 rad).  fp64: gpos / gmat.  R may be null (position only).
+template <typename T>
+__device__ __forceinline__ void c_geom_frame64(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int g, CT* pos,
+                                               CT* R) {
+#if PNP_XLO
+  if constexpr (sizeof(T) == 4) {
+    const DevPhys<T>& m = phys<T>();
+    const int b = m.geom_bodyid[g];
+    const T* Rb = s.xmat[b];
+    const T* gp = m.geom_pos[g];
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+      pos[k] = (CT(s.xpos[b][k]) + CT(s.xlo[b][k])) +
+               (CT(Rb[3 * k]) * CT(gp[0]) + CT(Rb[3 * k + 1]) * CT(gp[1]) + CT(Rb[3 * k + 2]) * CT(gp[2]));
+    if (R) {
+#if PNP_XQLO
+      CT q[4], gq[4], qg[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) { q[k] = CT(s.xquat[b][k]) + CT(s.xqlo[b][k]); gq[k] = CT(m.geom_quat[g][k]); }
+      d_mulquat(qg, q, gq);
+      d_quat2mat(R, qg);
+#else
+#pragma unroll
+      for (int k = 0; k < 9; k++) R[k] = CT(s.gmat[g][k]);
+#endif
+    }
+    return;
+  }
+#endif
+#pragma unroll
+  for (int k = 0; k < 3; k++) pos[k] = CT(s.gpos[g][k]);
+  if (R)
+#pragma unroll
+    for (int k = 0; k < 9; k++) R[k] = CT(s.gmat[g][k]);
+}
+// geom g2's centre relative to g1's: in fp32 builds the difference of the two fp64 centres
+// (c_geom_frame64) rounded once -- the relative position of two bodies near each other (closed
+// finger pads, a cube in the fingers), not the difference of two world positions each rounded at
+// ~1 m (~6e-8 m: ~300 times the fp32 resolution of a finger's slide joint; the one-ulp
+// conditioning floor of the closed-finger fixture is 5e-5 and pad-pad contacts turned that
+// rounding into 1.6e-4, round 4); fp64: gpos[g2] - gpos[g1]
+template <typename T>
+__device__ __forceinline__ void c_rel_pos(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int g1, int g2, T* d) {
+#if PNP_XLO
+  if constexpr (sizeof(T) == 4) {
+    const DevPhys<T>& m = phys<T>();
+    CT o1[3], o2[3];
+    c_geom_frame64(m, s, g1, o1, (CT*)nullptr);
+    c_geom_frame64(m, s, g2, o2, (CT*)nullptr);
+#pragma unroll
+    for (int k = 0; k < 3; k++) d[k] = T(o2[k] - o1[k]);
+    return;
+  }
+#endif
+#pragma unroll
+  for (int k = 0; k < 3; k++) d[k] = s.gpos[g2][k] - s.gpos[g1][k];
+}
 // the pair's two shapes, origin at geom 1's centre (oracle/convex.c): centimetre-scale support
 // points, so the fp32 Minkowski differences keep ~20x more bits than in world coordinates
 template <typename T>
@@ -935,26 +996,27 @@ __device__ __forceinline__ void c_convex_shapes(const DevPhys<T>& /*image: phys<
                                                 T margin, CShape<T>* sh) {
   const DevPhys<T>& m = phys<T>();
   const int gs[2] = {g1, g2};
+  CT o1[3], o2[3];
+  c_geom_frame64(m, s, g1, o1, sh[0].R);
+  c_geom_frame64(m, s, g2, o2, sh[1].R);
 #pragma unroll
   for (int i = 0; i < 2; i++) {
     const int g = gs[i];
     sh[i].type = m.geom_type[g];
     sh[i].mesh = m.geom_dataid[g];
     sh[i].margin = margin;
-    for (int k = 0; k < 3; k++) { sh[i].pos[k] = CT(s.gpos[g][k]) - CT(s.gpos[g1][k]); sh[i].size[k] = m.geom_size[g][k]; }
-    for (int k = 0; k < 9; k++) sh[i].R[k] = s.gmat[g][k];
+    for (int k = 0; k < 3; k++) { sh[i].pos[k] = i == 0 ? CT(0) : o2[k] - o1[k]; sh[i].size[k] = m.geom_size[g][k]; }
     c_load_shape(m, sh[i]);
   }
 }
 // multiccd trial t (0..3): geom 1 rotated by q, geom 2 by q^-1, both about the first contact's
 // position o (mjc_rotateFrame; an unverified assumption, oracle/convex.c), q the rotation by
 // a = -+1e-3 rad about the first contact's tangent axis t >> 1 (frame f = mju_makeFrame of its
-// normal): q = (cos(a/2), axis sin(a/2)) (oracle: sp_axisangle2quat), R(q^-1) = R(q)^T.  Ra, Rb:
-// the unperturbed frames (the Env's geom frames: nothing extra held in registers across MPR);
-// sh[].pos holds the unperturbed centres on entry.
+// normal): q = (cos(a/2), axis sin(a/2)) (oracle: sp_axisangle2quat), R(q^-1) = R(q)^T.  sh[].pos
+// and sh[].R hold the unperturbed frames on entry (c_convex_shapes).
 // (One function for the serial and the multi-wave convex passes: same bits.)
 template <typename T>
-__device__ __forceinline__ void c_fan_rotate(CShape<T>* sh, const T* Ra, const T* Rb, const CT* f, const CT* o, int t) {
+__device__ __forceinline__ void c_fan_rotate(CShape<T>* sh, const CT* f, const CT* o, int t) {
   const bool second = (t >> 1) != 0;   // (selects, not an index: f stays in registers)
   const CT ax[3] = {second ? f[6] : f[3], second ? f[7] : f[4], second ? f[8] : f[5]};
   const CT sh_ = (t & 1) ? CT(0.0004999999791666669) : CT(-0.0004999999791666669), q0 = CT(0.9999998750000026);
@@ -966,12 +1028,15 @@ __device__ __forceinline__ void c_fan_rotate(CShape<T>* sh, const T* Ra, const T
   Rq[0] = q00 + q11 - q22 - q33; Rq[4] = q00 - q11 + q22 - q33; Rq[8] = q00 - q11 - q22 + q33;
   Rq[1] = 2 * (q12 - q03); Rq[2] = 2 * (q13 + q02); Rq[3] = 2 * (q12 + q03);
   Rq[5] = 2 * (q23 - q01); Rq[6] = 2 * (q13 - q02); Rq[7] = 2 * (q23 + q01);
+  CT Ra[9], Rb[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) { Ra[k] = sh[0].R[k]; Rb[k] = sh[1].R[k]; }
 #pragma unroll
   for (int i = 0; i < 3; i++)
 #pragma unroll
     for (int j = 0; j < 3; j++) {
-      sh[0].R[3 * i + j] = Rq[3 * i] * CT(Ra[j]) + Rq[3 * i + 1] * CT(Ra[3 + j]) + Rq[3 * i + 2] * CT(Ra[6 + j]);
-      sh[1].R[3 * i + j] = Rq[i] * CT(Rb[j]) + Rq[3 + i] * CT(Rb[3 + j]) + Rq[6 + i] * CT(Rb[6 + j]);
+      sh[0].R[3 * i + j] = Rq[3 * i] * Ra[j] + Rq[3 * i + 1] * Ra[3 + j] + Rq[3 * i + 2] * Ra[6 + j];
+      sh[1].R[3 * i + j] = Rq[i] * Rb[j] + Rq[3 + i] * Rb[3 + j] + Rq[6 + i] * Rb[6 + j];
     }
   CT r0[3], r1[3];
 #pragma unroll
@@ -1020,7 +1085,7 @@ __device__ C_RUN_INLINE bool c_convex_run(const Env<T>& s, int g1, int g2, T mar
     CT f[9];
     c_fan_frame(val[0] + 4, f);
     const CT o[3] = {CT(val[0][1]), CT(val[0][2]), CT(val[0][3])};   // first contact (geom-1-centred)
-    c_fan_rotate(sh, s.gmat[g1], s.gmat[g2], f, o, t);
+    c_fan_rotate(sh, f, o, t);
   }
   T c[7];
 #if PNP_MPR_SLOTS
@@ -1056,9 +1121,12 @@ __device__ __forceinline__ int c_convex(const DevPhys<T>& /*image: phys<T>()*/, 
     if (distinct) n++;
   }
   wsync();
-  if (l == 0)
+  if (l == 0) {
+    CT o1[3];
+    c_geom_frame64(m, s, g1, o1, (CT*)nullptr);
     for (int i = 0; i < n; i++)
-      for (int k = 0; k < 3; k++) val[i][1 + k] += s.gpos[g1][k];
+      for (int k = 0; k < 3; k++) val[i][1 + k] = T(CT(val[i][1 + k]) + o1[k]);
+  }
   wsync();
   return n;
 }
@@ -1101,7 +1169,11 @@ __device__ void collide_geoms(const DevPhys<T>& /*image: phys<T>()*/, const Env<
   else if (t1 == 0 && t2 == 7) c_plane_mesh(m, p1, R1, p2, R2, m.geom_dataid[g2], margin, out);
   else if (t1 == 2 && t2 == 2) c_sphere_sphere(p1, s1[0], p2, s2[0], margin, out);
   else if (t1 == 2 && t2 == 6) c_sphere_box(p1, s1[0], p2, R2, s2, margin, out);
-  else if (t1 == 6 && t2 == 6) c_box_box(p1, R1, s1, p2, R2, s2, margin, out);
+  else if (t1 == 6 && t2 == 6) {
+    T Tv[3];   // box 2's centre relative to box 1's
+    c_rel_pos(m, s, g1, g2, Tv);
+    c_box_box(p1, R1, s1, p2, R2, s2, Tv, margin, out);
+  }
   // convex pairs: st_collision's MPR pass
 }
 template <typename T, class S>

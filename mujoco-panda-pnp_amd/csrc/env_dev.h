@@ -532,15 +532,21 @@ __device__ __forceinline__ void env_step_one(const DevPhys<T>& m, Env<T>& s, con
 // queue, each full-tier workgroup that hands its env over publishes it at once, and a persistent
 // wide consumer grid (on a few CUs, launched after the producers in host order) resumes it while
 // the full passes still run.  Layout (ints): count of entries, producer workgroups done, the
-// consumers' claim counter, a timeout flag, then the entries (-1 until published).  Every env's
-// computation is unchanged: only when its wide sub-steps start.
+// consumers' claim counter, the consumers that timed out, the envs the fallback pass finished,
+// then the entries (-1 until published).  Every env's computation is unchanged: only when its
+// wide sub-steps start.
+// A consumer that waits longer than its timeout for a producer gives up (counted in PNP_HQ_ERR)
+// instead of holding the GPU; the env it waited for keeps its resume bits, and after the join the
+// list-based wide resume pass finishes every env still carrying them (their count lands in
+// PNP_HQ_LATE; one selection kernel when there are none).  So no env is ever left mid-step, and
+// pnp_env_queue_status reports both counts.
 #define PNP_HQ_COUNT 0
 #define PNP_HQ_DONE 1
 #define PNP_HQ_NEXT 2
 #define PNP_HQ_ERR 3
+#define PNP_HQ_LATE 4
 #define PNP_HQ_ENTRY 8
-// a consumer that waits longer than this for a producer gives up (flag PNP_HQ_ERR; the env keeps
-// its resume bits) instead of holding the GPU: 20 s of the 100 MHz constant clock
+// default consumer timeout: 20 s of the 100 MHz constant clock (PNP_GYM_QUEUE_TIMEOUT_US)
 #define PNP_HQ_TIMEOUT 2000000000ll
 // producer side: after the workgroup's last state store, publish its env if it handed over, and
 // count the workgroup done (every workgroup of the grid, so the consumers know when to stop)
@@ -557,7 +563,7 @@ __device__ __forceinline__ void hq_publish(int* hq, int b, bool handed) {
 }
 // consumer side: entry i (claimed by this workgroup) once published, or -1 once every producer
 // workgroup is done and fewer than i + 1 entries exist (or on the timeout); wave-uniform
-__device__ __forceinline__ int hq_take(int* hq, int i, int target, int cap) {
+__device__ __forceinline__ int hq_take(int* hq, int i, int target, int cap, long long timeout) {
   if (i >= cap) return -1;   // (at most one entry per env)
   int b = -1;
   if (lane_id() == 0) {
@@ -568,8 +574,8 @@ __device__ __forceinline__ int hq_take(int* hq, int i, int target, int cap) {
       if (__hip_atomic_load(&hq[PNP_HQ_DONE], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= target &&
           __hip_atomic_load(&hq[PNP_HQ_COUNT], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) <= i)
         break;
-      if (wall_clock64() - t0 > PNP_HQ_TIMEOUT) {
-        __hip_atomic_store(&hq[PNP_HQ_ERR], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (wall_clock64() - t0 > timeout) {
+        __hip_atomic_fetch_add(&hq[PNP_HQ_ERR], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       __builtin_amdgcn_s_sleep(8);
@@ -609,7 +615,8 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_s
 // 25 % slower even with the helpers idle; a resident grid over the selected envs does not.
 __global__ void __launch_bounds__(1024) wide_select_kernel(const uint8_t* __restrict__ tier,
                                                            const uint32_t* __restrict__ warn, int B, int resume,
-                                                           int only_tier, int* __restrict__ list) {
+                                                           int only_tier, int* __restrict__ list,
+                                                           int* __restrict__ count_out) {
   __shared__ int wcount[16];
   __shared__ int base;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -634,7 +641,10 @@ __global__ void __launch_bounds__(1024) wide_select_kernel(const uint8_t* __rest
     }
     __syncthreads();
   }
-  if (t == 0) list[0] = base;
+  if (t == 0) {
+    list[0] = base;
+    if (count_out) *count_out = base;
+  }
 }
 // hq (resume passes of the gym step): consume the hand-over queue instead of the list -- claim
 // entries one at a time until hq_take reports the producers done (hq_target workgroups) and
@@ -643,7 +653,7 @@ __global__ void __launch_bounds__(NT * MW_WAVES, PNP_WIDE ? 1 : 4) env_step_wide
                                                                           EnvSoA<float> es, const float* __restrict__ action,
                                                                           EnvOutT<float> out, const int* __restrict__ list,
                                                                           int resume, int hand, int* __restrict__ hq,
-                                                                          int hq_target, int B) {
+                                                                          int hq_target, int B, long long hq_timeout) {
   __shared__ __attribute__((aligned(16))) Env<float> s_env;   // static LDS: see env_lds_note
   Env<float>& s = s_env;
   const DevPhys<float>& m = phys<float>();
@@ -661,7 +671,7 @@ __global__ void __launch_bounds__(NT * MW_WAVES, PNP_WIDE ? 1 : 4) env_step_wide
       int i = 0;
       if (lane_id() == 0) i = __hip_atomic_fetch_add(&hq[PNP_HQ_NEXT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       i = __builtin_amdgcn_readfirstlane(__shfl(i, 0));
-      const int b = hq_take(hq, i, hq_target, B);
+      const int b = hq_take(hq, i, hq_target, B, hq_timeout);
       if (b < 0) break;
       one(b);
     }
@@ -730,7 +740,7 @@ static int32_t wide_list(int kind, int32_t B, int** out, int* ncu) {
 static int32_t launch_env_step_mw(const pnp_state_t<float>* st, const pnp_env_params* p, const pnp_env_state* e,
                                   const float* action, const pnp_env_out* o, int32_t B, void* stream, int resume,
                                   int only_tier, int hand, const char* what, int* hq = nullptr, int hq_target = 0,
-                                  int hq_grid = 0) {
+                                  int hq_grid = 0, long long hq_timeout = PNP_HQ_TIMEOUT, int* count_out = nullptr) {
   if (B <= 0) return PNP_OK;
   int* list = nullptr;
   int ncu = 0;
@@ -739,16 +749,20 @@ static int32_t launch_env_step_mw(const pnp_state_t<float>* st, const pnp_env_pa
   int grid = B < per_cu * ncu ? B : per_cu * ncu;
   if (hq) {
     // the consumer grid leaves the other CUs to the producers it waits for (no deadlock: they
-    // always have room, and they are enqueued before it on any shared hardware queue)
+    // always have room, and they are enqueued before it on any shared hardware queue); the
+    // caller's grid is clamped to that (launch_env_step only takes the queue path when the device
+    // has a CU to spare)
     grid = hq_grid < grid ? hq_grid : grid;
-    if (grid < 1 || grid >= per_cu * ncu) { pnp_set_error("pnp_env_step: hand-over queue grid %d", grid); return PNP_ERR_ARG; }
+    if (grid > per_cu * ncu - 1) grid = per_cu * ncu - 1;
+    if (grid < 1) { pnp_set_error("pnp_env_step: hand-over queue grid %d", grid); return PNP_ERR_ARG; }
   } else {
     hipLaunchKernelGGL(wide_select_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, e->tier, st->warn, B, resume,
-                       only_tier, list);
+                       only_tier, list, count_out);
     if (const int32_t rc = pnp_check_launch("wide_select_kernel")) return rc;
   }
   hipLaunchKernelGGL(env_step_wide_kernel, dim3(grid), dim3(NT * MW_WAVES), 0, (hipStream_t)stream, *st, *p,
-                     env_view<float>(e), action, out_view<float>(o), (const int*)list, resume, hand, hq, hq_target, B);
+                     env_view<float>(e), action, out_view<float>(o), (const int*)list, resume, hand, hq, hq_target, B,
+                     hq_timeout);
   return pnp_check_launch(what);
 }
 #endif
@@ -796,7 +810,8 @@ int32_t env_compact_lds_bytes() { return (int32_t)sizeof(Env<float>); }
 // the full image's lease like the route streams.
 int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
                              const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
-                             void* stream, int resume, int only_tier, int* hq, int hq_target, int hq_grid) {
+                             void* stream, int resume, int only_tier, int* hq, int hq_target, int hq_grid,
+                             long long hq_timeout, int* count_out) {
   const DevPhys<float>* src = phys_image<float>(model);
   if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
   if (B <= 0) return PNP_OK;
@@ -806,7 +821,8 @@ int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* s
     return rc;
   if (const int32_t rc = launch_env_step_mw(st, p, e, action, o, B, stream, resume, only_tier, gym_wide_pct() << 8 | gym_full_pct() << 16,
                                             hq ? "env_step_wide_kernel (hand-over queue)" : "env_step_wide_kernel",
-                                            hq, hq_target, hq_grid))
+                                            hq, hq_target, hq_grid, hq_timeout > 0 ? hq_timeout : PNP_HQ_TIMEOUT,
+                                            count_out))
     return rc;
   return lease.launched();
 }
@@ -935,8 +951,9 @@ static bool gym_full_mw_enabled() {
 // PNP_GYM_QUEUE: unset / 1 = routed fp32 gym steps hand the full tier's hand-overs to the wide
 // tier through the device queue (hq_publish / hq_take), consumed concurrently with the full passes
 // (default); 0 = the wide resume pass starts after the full passes (A/B runs).  PNP_GYM_QUEUE_CU:
-// the consumer grid, one wide workgroup per CU (default 224 of 256: leaves 32 CUs to the producers,
-// whose progress is all the consumers wait for).  Measured (4096 envs, random actions,
+// the consumer grid, one wide workgroup per CU (default: the device's CUs less an eighth -- 224 of
+// 256 on an MI355X -- leaving the rest to the producers, whose progress is all the consumers wait
+// for; clamped to the CU count - 1, and a device with a single CU takes the non-queue path).  Measured (4096 envs, random actions,
 // gym-steps/s; profiles/r04/gym_queue_ab.log), with round 3's routing: queue off 18.5 k; consumers
 // 32: 9.5 k, 64: 15.2 k, 128: 19.5 k, 160-255: 19.9-20.4 k; with the routing shares (50 %): off
 // 18.8 k, 96: 18.8 k, 160: 22.3 k, 192: 22.9 k, 240: 23.2 k -- the full passes hand envs to the
@@ -945,16 +962,39 @@ static bool gym_queue_enabled() {
   const char* e = getenv("PNP_GYM_QUEUE");
   return !(e && e[0] == '0');
 }
-static int gym_queue_grid() {
+static int gym_queue_grid(int ncu) {
+  const int def = ncu - (ncu / 8 > 1 ? ncu / 8 : 1);
   const char* e = getenv("PNP_GYM_QUEUE_CU");
-  const int g = e ? atoi(e) : 224;
-  return g > 0 ? g : 224;
+  const int g = e ? atoi(e) : def;
+  const int v = g > 0 ? g : def;
+  return v < ncu - 1 ? v : ncu - 1;
+}
+// PNP_GYM_QUEUE_TIMEOUT_US: how long a consumer waits for a producer before it gives up (the
+// fallback resume pass then finishes that env); default 20 s.  Tests set it tiny to exercise the
+// fallback.
+static long long gym_queue_timeout() {
+  const char* e = getenv("PNP_GYM_QUEUE_TIMEOUT_US");
+  const long long us = e ? atoll(e) : 0;
+  return us > 0 ? us * 100 : PNP_HQ_TIMEOUT;   // 100 MHz constant clock
+}
+// CUs of the current device (cached per device)
+static int device_cus() {
+  static std::mutex mu;
+  static int ncu[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!ncu[dev] && hipDeviceGetAttribute(&ncu[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    ncu[dev] = 0;
+  return ncu[dev];
 }
 // the hand-over queue buffer per device (PNP_HQ_ENTRY header ints + one entry per env); its users
 // are serialised by the full image's lease like the route streams
+static std::mutex g_hq_mu;
+static int* g_hq_buf[64] = {};
 static int32_t hand_queue(int32_t B, int** out) {
-  static std::mutex mu;
-  static int* buf[64] = {};
+  std::mutex& mu = g_hq_mu;
+  int** buf = g_hq_buf;
   static int cap[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { pnp_set_error("pnp_env_step: bad device"); return PNP_ERR_HIP; }
@@ -1040,7 +1080,8 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   // fp32 full-tier passes: persistent, two waves per env (helper wave for the convex pass)
   const bool full_mw = tiers && gym_full_mw_enabled();
   // the full passes' hand-overs reach the wide tier through the device queue (routed steps)
-  const bool queue = route && !full_mw && gym_full_resume_enabled() && gym_queue_enabled();
+  const int ncu = device_cus();
+  const bool queue = route && !full_mw && gym_full_resume_enabled() && gym_queue_enabled() && ncu >= 2;
   int* hq = nullptr;
   RouteStreams* rs = nullptr;
   // join side stream i back into the caller's stream (its kernels read the full image and write
@@ -1113,13 +1154,19 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
       pnp_set_error("pnp_env_step: consumer wait: %s", hipGetErrorString(he));
       return fail(PNP_ERR_HIP);
     }
-    if ((rc = launch_env_step_wide(model, st32, p, e, a32, o, B, rs->side[2], 1, -1, hq, 2 * B, gym_queue_grid())))
+    if ((rc = launch_env_step_wide(model, st32, p, e, a32, o, B, rs->side[2], 1, -1, hq, 2 * B, gym_queue_grid(ncu),
+                                   gym_queue_timeout())))
       return fail(rc);
     for (int i = 0; i < 3; i++)
       if (const hipError_t he = join_side(i)) {
         pnp_set_error("pnp_env_step: join: %s", hipGetErrorString(he));
         return fail(PNP_ERR_HIP);
       }
+    // fallback: any env a consumer gave up on still carries its resume bits -- the list-based
+    // wide resume pass finishes it (its count -> hq[PNP_HQ_LATE]; nothing to do: one selection
+    // kernel and an empty grid)
+    if ((rc = launch_env_step_wide(model, st32, p, e, a32, o, B, stream, 1, -1, nullptr, 0, 0, 0, hq + PNP_HQ_LATE)))
+      return fail(rc);
   } else {
     if (route) {   // the wide resume pass also takes the routed full pass's hand-overs
       if (const hipError_t he = join_side(0)) {
@@ -1150,6 +1197,27 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
 }
 
 extern "C" int32_t pnp_env_params_size(void) { return (int32_t)sizeof(pnp_env_params); }
+
+// the hand-over queue's header after the last routed fp32 gym step on the current device
+// (synchronises the device): [0] entries published, [1] producer workgroups done, [2] consumer
+// claims, [3] consumers that timed out, [4] envs the fallback resume pass finished.  All zero
+// before any queued step.
+extern "C" int32_t pnp_env_queue_status(int32_t* out5) {
+  if (!out5) { pnp_set_error("pnp_env_queue_status: null out"); return PNP_ERR_ARG; }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { pnp_set_error("pnp_env_queue_status: bad device"); return PNP_ERR_HIP; }
+  int h[PNP_HQ_ENTRY] = {};
+  {
+    std::lock_guard<std::mutex> lk(g_hq_mu);
+    if (g_hq_buf[dev]) {
+      hipError_t e = hipDeviceSynchronize();
+      if (e == hipSuccess) e = hipMemcpy(h, g_hq_buf[dev], sizeof(h), hipMemcpyDeviceToHost);
+      if (e != hipSuccess) { pnp_set_error("pnp_env_queue_status: %s", hipGetErrorString(e)); return PNP_ERR_HIP; }
+    }
+  }
+  for (int i = 0; i < 5; i++) out5[i] = h[i];
+  return PNP_OK;
+}
 
 extern "C" int32_t pnp_env_init(pnp_model* model, const pnp_state* st, const pnp_env_params* p,
                                 const pnp_env_state* e, int32_t B, void* stream) {

@@ -112,10 +112,12 @@ int32_t launch_step_wide(const pnp_model* model, const pnp_state_t<float>* st, i
                          void* stream, unsigned long long* prof, int resume);
 // hq / hq_target: the gym step's hand-over queue (env_dev.h, PNP_HQ_*): the resume pass then
 // consumes the envs the full-tier passes publish, concurrently with them, on hq_grid workgroups
+// (each gives up after hq_timeout ticks of the 100 MHz clock; <= 0: the default).  count_out
+// (list-based passes): receives the number of envs the pass selected (device int).
 int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* st, const pnp_env_params* p,
                              const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
                              void* stream, int resume, int only_tier, int* hq = nullptr, int hq_target = 0,
-                             int hq_grid = 0);
+                             int hq_grid = 0, long long hq_timeout = 0, int* count_out = nullptr);
 int32_t step_wide_lds_bytes();
 // step_wide64.hip: the fp64 wide tier (resume passes of pnp_step_f64 and pnp_env_step_f64)
 int32_t launch_step_wide64(const pnp_model* model, const pnp_state_t<double>* st, int32_t B, int32_t nsub,

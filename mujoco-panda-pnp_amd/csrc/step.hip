@@ -64,6 +64,16 @@
 // MPR's portal support points in per-wave LDS slots (collide_dev.h SVertL): the full and wide
 // builds (the compact builds run no MPR; the fp64 wide build keeps registers)
 #define PNP_MPR_SLOTS (!PNP_COMPACT && !PNP_WIDE64)
+// PNP_XLO: the fp32 builds keep each body's world position and quaternion as fp32 pairs (xpos /
+// xquat + the remainders of the fp64 kinematic chain, Env::xlo / xqlo); MPR's geom frames and the
+// box-box collider's centre offset are formed from them in fp64 (collide_dev.h c_geom_frame64,
+// c_rel_pos): the relative geometry of two bodies then matches the fp64 chain's, not its per-body
+// rounding to fp32 at world scale (~3e-8 m at 1 m, ~6e-8 rad).  The position remainder in every
+// fp32 tier alike (box-box runs in all of them, and the hand-overs are exact only if every tier
+// does the same arithmetic); the quaternion remainder (PNP_XQLO) where MPR runs (it does not fit
+// the compact tier's 20 KB).
+#define PNP_XLO (!PNP_WIDE64)
+#define PNP_XQLO (!PNP_COMPACT && !PNP_WIDE64)
 #define PNP_LEAN (PNP_COMPACT || PNP_WIDE || PNP_WIDE64)
 // PNP_BIG_ISLANDS: the solver's whole-wave paths for islands with more rows than a wave (line
 // search, gradient, MFMA Hessian).  Compiled out of the compact build, which hands such islands
@@ -152,6 +162,11 @@ struct Env {
       union {
         struct {
           T gpos[PH_MAXG][3], gmat[PH_MAXG][9];   // kinematics -> collision
+#if PNP_XQLO
+          // the remainder of the fp64 kinematic chain's body quaternion past xquat (fp32 builds
+          // that run MPR; with xlo below, collide_dev.h c_geom_frame64)
+          float xqlo[PH_MAXB][4];
+#endif
           union {
             struct {                              // kinematics -> CRB
               T xipos[PH_MAXB][3], xanchor[PH_MAXJ][3], xaxis[PH_MAXJ][3];
@@ -226,7 +241,15 @@ struct Env {
   unsigned char con_dim[PH_MAXCON];
   T con_b[PH_MAXCON];          // contact: the reference acceleration's damping b (st_noslip's pair rows)
   int tree_island[PH_MAXT], isl_n[PH_MAXT];
-  unsigned char isl_dof[PH_MAXT][PH_MAXV];
+  union {
+    unsigned char isl_dof[PH_MAXT][PH_MAXV];   // build_islands -> the solver stages (Newton, noslip)
+#if PNP_XLO
+    // fp32 builds, kinematics -> collision: the remainder of the fp64 kinematic chain's body
+    // position past xpos (collide_dev.h c_geom_frame64 / c_rel_pos).  Dead before build_islands
+    // writes isl_dof; shares its bytes (the compact Env has no 288 B to spare for 8 envs per CU)
+    float xlo[PH_MAXB][3];
+#endif
+  };
   int isl_eoff[PH_MAXT + 1], isl_roff[PH_MAXT + 1];
   int isl_joff[PH_MAXT + 1], tree_ipos[PH_MAXT], jt_ok;   // dense island Jacobian blocks (jt)
   unsigned char dof_ipos[PH_MAXV];                         // a dof's position in its island
@@ -641,6 +664,12 @@ __device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
       d_quat2mat(R, q);
       for (int t = 0; t < 3; t++) s.xpos[b][t] = (T)p[t];
       for (int t = 0; t < 4; t++) s.xquat[b][t] = (T)q[t];
+#if PNP_XLO
+      for (int t = 0; t < 3; t++) s.xlo[b][t] = (float)(p[t] - (double)s.xpos[b][t]);
+#endif
+#if PNP_XQLO
+      for (int t = 0; t < 4; t++) s.xqlo[b][t] = (float)(q[t] - (double)s.xquat[b][t]);
+#endif
       for (int t = 0; t < 9; t++) s.xmat[b][t] = (T)R[t];
       if (one && jt == 0) {
         for (int t = 0; t < 3; t++) { s.xanchor[ja][t] = (T)p[t]; s.xaxis[ja][t] = m.jnt_axis[ja][t]; }
@@ -753,6 +782,12 @@ __device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
       T R[9];
       d_quat2mat(R, q);
       for (int t = 0; t < 3; t++) s.xpos[b][t] = p[t];
+#if PNP_XLO
+      for (int t = 0; t < 3; t++) s.xlo[b][t] = 0.0f;   // (the T chain: no remainder)
+#endif
+#if PNP_XQLO
+      for (int t = 0; t < 4; t++) s.xqlo[b][t] = 0.0f;
+#endif
       for (int t = 0; t < 4; t++) s.xquat[b][t] = q[t];
       for (int t = 0; t < 9; t++) s.xmat[b][t] = R[t];
     }
@@ -770,6 +805,12 @@ __device__ void st_kinematics(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s,
         if (m.weld_body[k] == 0)
           for (int t = 0; t < 7; t++) s.wpose[k][t] = t == 3 ? 1.0 : 0.0;
     for (int t = 0; t < 3; t++) s.xpos[0][t] = 0;
+#if PNP_XLO
+    for (int t = 0; t < 3; t++) s.xlo[0][t] = 0.0f;
+#endif
+#if PNP_XQLO
+    for (int t = 0; t < 4; t++) s.xqlo[0][t] = 0.0f;
+#endif
     s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
     for (int t = 0; t < 9; t++) s.xmat[0][t] = (t % 4 == 0) ? T(1) : T(0);
   }
@@ -1456,8 +1497,10 @@ __device__ __attribute__((noinline)) void st_collision_convex_mw(Env<float>& s) 
     const int at = ncon + eo + __popc(ao & ((1u << j) - 1u));
     if (o < n && ((ao >> j) & 1) && at < PH_MAXCON) {
       const int p = s.cst_key[o], g1 = m.pair_g1[p], g2 = m.pair_g2[p];
-      const float* org = s.gpos[g1];
-      const float pos[3] = {s.cst_val[l][1] + org[0], s.cst_val[l][2] + org[1], s.cst_val[l][3] + org[2]};
+      CT org[3];
+      c_geom_frame64(m, s, g1, org, (CT*)nullptr);
+      const float pos[3] = {(float)(CT(s.cst_val[l][1]) + org[0]), (float)(CT(s.cst_val[l][2]) + org[1]),
+                            (float)(CT(s.cst_val[l][3]) + org[2])};
       const float nrm[3] = {s.cst_val[l][4], s.cst_val[l][5], s.cst_val[l][6]};
       LdsSink<float> ls{s.con + at, 1};
       ls.emit(s.cst_val[l][0], pos, nrm);

@@ -10,7 +10,7 @@ from .model import PnpIKParams, PnpModelDesc
 # PNP_LIB: another build of the same sources (tools/asan_cpu_tests.sh: the host-sanitizer build)
 LIB_PATH = os.environ.get("PNP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpnp.so")
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 # every symbol include/pnp.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -20,7 +20,7 @@ EXPORTS = [
     "pnp_forward_debug", "pnp_forward_debug_f64", "pnp_step_lds_bytes", "pnp_step_profile",
     "pnp_env_params_size", "pnp_env_init", "pnp_env_init_f64", "pnp_env_reset", "pnp_env_reset_f64",
     "pnp_env_step", "pnp_env_step_f64", "pnp_env_evaluate", "pnp_env_evaluate_f64",
-    "pnp_slerp_track_f64",
+    "pnp_slerp_track_f64", "pnp_env_queue_status",
 ]
 
 STATE_FIELDS = ("qpos", "qvel", "ctrl", "mocap_pos", "mocap_quat", "qacc_warmstart", "time", "warn")
@@ -140,6 +140,8 @@ def load():
         f.restype = I32
     L.pnp_slerp_track_f64.argtypes = [P, P, I32, P, P, I32, P]
     L.pnp_slerp_track_f64.restype = I32
+    L.pnp_env_queue_status.argtypes = [P]
+    L.pnp_env_queue_status.restype = I32
     if L.pnp_abi_version() != ABI_VERSION:
         raise PnpError(f"libpnp ABI {L.pnp_abi_version()} != binding ABI {ABI_VERSION}")
     if L.pnp_env_params_size() != C.sizeof(PnpEnvParams):
@@ -156,3 +158,12 @@ def check(rc, what):
     if rc != 0:
         msg = load().pnp_last_error().decode(errors="replace")
         raise PnpError(f"{what} failed ({rc}): {msg}")
+
+
+def env_queue_status():
+    """pnp_env_queue_status: the hand-over queue's counts after the last routed fp32 gym step on
+    the current device (synchronises): published, producers_done, claims, timeouts, fallback."""
+    L = load()
+    buf = (C.c_int32 * 5)()
+    check(L.pnp_env_queue_status(buf), "pnp_env_queue_status")
+    return dict(zip(("published", "producers_done", "claims", "timeouts", "fallback"), list(buf)))

@@ -526,7 +526,11 @@ class _ModelBuilder:
                 if mname not in mesh_names:
                     hv = _convex_hull(_load_mesh_vertices(self.c.meshes[mname]))
                     cen = _hull_centroid(hv)
-                    hv = hv - cen
+                    # stored in single precision like MuJoCo's mjModel.mesh_vert (float*): the
+                    # recentred vertices rounded once, so the fp64 oracle and the fp32 kernels'
+                    # images hold the same values (unrounded, the fp32 image's own rounding tilted
+                    # two finger faces in contact by ~1e-7 rad against the oracle's)
+                    hv = (hv - cen).astype(np.float32).astype(np.float64)
                     mesh_vertadr.append(sum(len(v) for v in mesh_vert))
                     mesh_vertnum.append(len(hv))
                     mesh_vert.append(hv)

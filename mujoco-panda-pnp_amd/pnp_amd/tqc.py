@@ -466,7 +466,9 @@ class TQC:
 
     def train(self, gradient_steps=None):
         """gradient_steps (default cfg.gradient_steps) gradient steps; with a captured step each
-        is one graph replay.  Results are the eager steps' bit for bit (tests/test_tqc_gpu.py)."""
+        is one graph replay.  Results are the eager steps' bit for bit (tests/test_tqc_gpu.py).
+        Returns (and keeps in self.logs) the last step's losses as 0-d device tensors, not floats
+        (sb3's logger gets floats; here `float(v)` where a host value is wanted)."""
         c = self.cfg
         lr = self._update_lr()
         n = gradient_steps or c.gradient_steps
@@ -488,6 +490,11 @@ class TQC:
             self._graph.replay()
             self.n_updates += 1
             out = self._graph_out
+        # the logs are device tensors (no host sync per call); on the graph path `out` is the
+        # captured graph's static outputs, which the next replay overwrites in place -- cloned, so
+        # a caller that keeps a returned dict across train() calls keeps this call's values
+        if out is self._graph_out:
+            out = tuple(t.clone() for t in out)
         self.logs = {"lr": lr, "ent_coef": out[0], "critic_loss": out[1], "actor_loss": out[2],
                      "ent_coef_loss": out[3]}
         return self.logs

@@ -110,7 +110,28 @@ def test_bench_spawns_ranks_from_gpus_flag():
                        env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     rec = json.loads(r.stdout.strip().splitlines()[-1])
+    d = rec.pop("dist")
     assert rec == {"world": 2, "rank_sum": 1, "ranks": 2, "local_ranks": "0"}
+    # the record's dist block (bench.dist_record, the same code a GPU run prints): the process
+    # group's own world size and backend, every rank with its own timings
+    assert d["world_size"] == 2 and d["backend"] == "gloo" and d["gpus_flag"] == 2
+    assert [x["rank"] for x in d["ranks"]] == [0, 1] and [x["local_rank"] for x in d["ranks"]] == [0, 1]
+    assert [x["step_wall_s"] for x in d["ranks"]] == [1.0, 2.0]
+    assert [x["step_kernel_ms"] for x in d["ranks"]] == [0.5, 1.5]
     bad = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--launch-selftest"],
                          env=dict(env, WORLD_SIZE="2"), capture_output=True, text=True, timeout=120)
     assert bad.returncode != 0 and "disagrees" in bad.stderr
+
+
+def test_dist_record_rejects_a_job_that_is_not_the_one_asked_for():
+    """bench.dist_record raises (rank 0 prints no record) when the process group is not --gpus
+    ranks, ranks are missing, or RCCL ranks share a GPU."""
+    import bench
+    one = [{"rank": 0, "local_rank": 0, "device": "cpu"}]
+    rec = bench.dist_record(1, 1, False, one, {"step": [[2.0, 1.0]]})
+    assert rec["world_size"] == 1 and rec["backend"] is None
+    assert rec["ranks"][0]["step_wall_s"] == 2.0 and rec["ranks"][0]["step_kernel_ms"] == 1.0
+    with pytest.raises(SystemExit, match="world size"):
+        bench.dist_record(2, 1, False, one, {})
+    with pytest.raises(SystemExit, match="not 0"):
+        bench.dist_record(1, 1, False, [{"rank": 3, "local_rank": 0}], {})

@@ -232,6 +232,74 @@ def test_gym_hand_over_queue_is_exact(grid):
     assert not bool((w >> 16).any()) and int((w & 0xFFFF).max()) == 0
 
 
+def test_gym_queue_timeout_falls_back_exactly():
+    """A consumer of the hand-over queue that gives up waiting (here after 1 us:
+    PNP_GYM_QUEUE_TIMEOUT_US) leaves its env's resume bits, and the list-based wide resume pass
+    after the join finishes it (env_dev.h, PNP_HQ_LATE): the bits of the queue-less step, no env
+    left mid-step, and the give-ups counted by pnp_env_queue_status.  With the default timeout
+    nothing times out and every published hand-over is consumed by the queue."""
+    from pnp_amd import _lib
+    a, oa = _gym_run("1", 96, 3, pressed=True, route="1", PNP_GYM_QUEUE="1", PNP_GYM_QUEUE_TIMEOUT_US="1")
+    st_fast = _lib.env_queue_status()
+    b, ob = _gym_run("1", 96, 3, pressed=True, route="1", PNP_GYM_QUEUE="0")
+    c, oc = _gym_run("1", 96, 3, pressed=True, route="1", PNP_GYM_QUEUE="1")
+    st_def = _lib.env_queue_status()
+    print("queue status, 1 us timeout:", st_fast, " default:", st_def)
+    for x, y, z in zip(oa, ob, oc):
+        for u, v, w in zip(x, y, z):
+            assert torch.equal(u, v) and torch.equal(w, v)
+    for k in a.state:
+        assert torch.equal(a.state[k], b.state[k]) and torch.equal(c.state[k], b.state[k]), k
+    for g in (a, c):
+        w = g.state["warn"].to(torch.int64) & 0xFFFFFFFF
+        assert not bool((w >> 16).any()) and int((w & 0xFFFF).max()) == 0
+    assert st_fast["fallback"] <= st_fast["timeouts"]
+    assert st_def["timeouts"] == 0 and st_def["fallback"] == 0
+    assert st_def["producers_done"] == 2 * 96 and st_def["claims"] >= st_def["published"]
+
+
+def test_two_routed_gym_steps_in_flight_on_two_streams():
+    """Two batches' routed fp32 gym steps issued on two streams with no host sync between them
+    share the device's selection lists and hand-over queue; the second waits (on the GPU) for the
+    first (env_dev.h RouteStreams::last).  Each batch's results equal its steps run alone."""
+    from pnp_amd.envs import BatchedFrankaShelfPNPEnv
+
+    def make(off, B):
+        g = BatchedFrankaShelfPNPEnv(B, autoreset=True, env_offset=off)
+        g.reset()
+        g.state["qpos"][::3, 7:9] = -0.002
+        return g
+    Ba, Bb = 96, 64
+    rng = np.random.default_rng(5)
+    acts = [(torch.as_tensor(rng.uniform(-1, 1, size=(Ba, 7)), dtype=torch.float32, device="cuda"),
+             torch.as_tensor(rng.uniform(-1, 1, size=(Bb, 7)), dtype=torch.float32, device="cuda")) for _ in range(3)]
+    # serial
+    ga, gb = make(0, Ba), make(1000, Bb)
+    ser = []
+    for x, y in acts:
+        oa = ga.step(x)[0]["observation"].clone()
+        torch.cuda.synchronize()
+        ob = gb.step(y)[0]["observation"].clone()
+        torch.cuda.synchronize()
+        ser.append((oa, ob))
+    # in flight on two streams
+    ha, hb = make(0, Ba), make(1000, Bb)
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    par = []
+    for x, y in acts:
+        with torch.cuda.stream(s1):
+            oa = ha.step(x)[0]["observation"].clone()
+        with torch.cuda.stream(s2):
+            ob = hb.step(y)[0]["observation"].clone()
+        par.append((oa, ob))
+    torch.cuda.synchronize()
+    for (u, v), (p, q) in zip(ser, par):
+        assert torch.equal(u, p) and torch.equal(v, q)
+    for k in ga.state:
+        assert torch.equal(ga.state[k], ha.state[k]) and torch.equal(gb.state[k], hb.state[k]), k
+
+
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_full_gym_step_bounded(model, dtype):
     g = _env(dtype)
