@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 10
+#define PNP_ABI_VERSION 11
 
 #define PNP_OK 0
 #define PNP_ERR_ARG -1
@@ -391,6 +391,44 @@ int32_t pnp_env_step_f64(pnp_model* model, const pnp_state_f64* state, const pnp
  * pass finished after the join (the envs such consumers left).  Diagnostic: an env is never left
  * mid-step ([3] > 0 costs time, not results). */
 int32_t pnp_env_queue_status(int32_t* out5);
+
+/* ------------------------------------------------------------------ TQC learner (C5) */
+/* One TQC gradient step (sb3-contrib tqc.py train(): entropy coefficient, critics against the
+ * truncated target quantiles, actor, Polyak; the reference's learner, scripts/train.py:74-93) in
+ * four launches on the matrix cores (csrc/tqc_fused.hip): per 16-row slab of the batch a workgroup
+ * runs the networks' forward and backward passes, the Adam kernels reduce the slabs' gradients.
+ * Parameters in PyTorch's layouts -- actor: latent Linear 25->256->256->256 (weight [out][in],
+ * bias [out]) W0 b0 W1 b1 W2 b2, heads mu / log_std 256->7 Wmu bmu Wls bls; critics (and their
+ * target copies): n_critics stacked MLPs 32->256->256->256->25, weight [n_critics][in][out], bias
+ * [n_critics][1][out], w0 b0 .. w3 b3 -- updated in place, with torch.optim.Adam's fused state
+ * (exp_avg, exp_avg_sq, the per-parameter step scalars).  Supported: obs 25, action 7, hidden 256,
+ * 2 critics x 25 quantiles, 2 dropped per net, batch a multiple of 16 (PNP_ERR_UNSUPPORTED
+ * otherwise).  All pointers are device fp32. */
+typedef struct pnp_tqc_desc {
+  int32_t batch, obs_dim, act_dim, hidden, n_critics, n_quantiles, n_drop_per_net;
+  float gamma, tau, target_entropy, beta1, beta2, adam_eps;
+  float* actor[10]; float* actor_m[10]; float* actor_v[10]; float* actor_step[10];
+  float* critic[8]; float* critic_m[8]; float* critic_v[8]; float* critic_step[8];
+  float* target[8];
+  float* log_ent_coef; float* ent_m; float* ent_v; float* ent_step;
+  const float* lr;             /* learning rate (device scalar: the linear schedule writes it) */
+  float* workspace;            /* pnp_tqc_workspace_floats() floats */
+  int64_t workspace_floats;
+  float* logs;                 /* [4] out: ent_coef (before the step), critic loss, actor loss, ent-coef loss */
+} pnp_tqc_desc;
+/* One sampled, normalised batch: obs / next_obs [batch*25], act [batch*7], done / reward [batch],
+ * and the two N(0, 1) draws of the step's squashed-Gaussian samples (actor on obs, on next_obs)
+ * [batch*7] each -- drawn by the caller in sb3's order so the step is the PyTorch step's. */
+typedef struct pnp_tqc_batch {
+  const float* obs; const float* act; const float* next_obs; const float* done; const float* reward;
+  const float* eps_pi; const float* eps_next;
+} pnp_tqc_batch;
+int64_t pnp_tqc_workspace_floats(const pnp_tqc_desc* d);
+/* flat gradient sizes (actor, critics) of grads_out below */
+int32_t pnp_tqc_param_counts(int32_t* actor_params, int32_t* critic_params);
+/* grads_out (optional, tests): the step's reduced gradients, actor then critics, in the
+ * parameters' own layouts and order.  Stream-ordered, no host sync; capturable in a HIP graph. */
+int32_t pnp_tqc_update(const pnp_tqc_desc* d, const pnp_tqc_batch* b, float* grads_out, void* stream);
 
 /* ------------------------------------------------------------------ skills */
 /* RotateSkill.reset's trajectory (reference skills/rotate.py:39-46) for B skills: target =

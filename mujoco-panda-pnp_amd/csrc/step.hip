@@ -2775,6 +2775,128 @@ __device__ __attribute__((noinline)) void hess_mfma(Env<float>& s, int I) {
   }
 }
 
+// ---- fp32 Newton: mixed-precision iterative refinement
+// Once an island's Newton step kept its active set, x is the minimiser of that quadratic up to the
+// fp32 solve's own error, cond(H) eps: with the closed fingers' pad contacts (200+ rows on the
+// arm, cond(H) ~6e3) ~5e-6 of |x|, and a second fp32 Newton step does not improve it (its gradient
+// carries the same fp32 rounding; round 4: the closed-finger fixture's arm tree 1.4-1.6e-4 against
+// a one-ulp floor of 5e-5).  Instead: the gradient g = M (x - x_smooth) + J^T D (J x - aref) of
+// that quadratic accumulated in fp64 from the fp32 data (products of fp32 values are exact in
+// fp64; D (J x - aref) is kept as an fp32 pair), then p = -H^-1 g with the island's kept factor
+// and x += p, no line search (the quadratic's own minimiser); the rows' jar / active set are
+// re-evaluated at the new x (fp64 accumulation).  An island whose active set still holds is done;
+// one whose set changed goes on with Newton iterations.  (CPU model of the arm island, tools/
+// mpir_model.py: fp32 Newton + fp32 refinement 1.4-1.2e-5 .. 5e-6 of |x|, one fp64-residual
+// refinement 6e-8 .. 1.3e-7 -- the fp32 data's own rounding.)  This replaces the second,
+// line-searched Newton iteration fp32 ran on 63 % of the C3 sub-steps.
+template <typename T>
+__device__ __forceinline__ double row_dot64(const Env<T>& s, int r, const T* x) {
+  const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], off = s.efc_off[r];
+  const int n0 = s.c_tree_dofnum[t0], a0 = s.c_tree_dofadr[t0];
+  const int t1c = t1 >= 0 ? t1 : 0;
+  const int n1 = t1 >= 0 ? s.c_tree_dofnum[t1c] : 0, a1 = s.c_tree_dofadr[t1c];
+  const T* J = s.efc_Jv + off;
+  double v = 0;
+#pragma unroll 3
+  for (int q = 0; q < n0; q++) v += (double)J[q] * (double)x[a0 + q];
+#pragma unroll 3
+  for (int q = 0; q < n1; q++) v += (double)J[n0 + q] * (double)x[a1 + q];
+  return v;
+}
+// fp64 gradient of the island quadratics at x (active set efc_act, dense island blocks): s.grad =
+// g rounded to fp32, s.v2 = g^2 (for the island norms)
+__device__ __attribute__((noinline)) void newton_refine_grad(Env<float>& s) {
+  const DevPhys<float>& m = phys<float>();
+  const int l = lane_id();
+  const int nisl = s.nisland;
+  // rows, island row order: f = D (J x - aref) on the active rows, an fp32 pair (rr_f + rr_d; the
+  // Hessian blocks are kept, so rr_d is free)
+  for (int rr = l; rr < s.nefc; rr += NT) {
+    const int r = s.isl_row[rr];
+    const double jar = row_dot64(s, r, s.x) - (double)s.efc_aref[r];
+    const double f = s.efc_act[r] ? (double)s.efc_D[r] * jar : 0.0;
+    const float hi = (float)f;
+    s.rr_f[rr] = hi;
+    s.rr_d[rr] = (float)(f - (double)hi);
+  }
+  wsync();
+  // islands with more rows than a wave: lane (dof a, slice k) sums rows k, k + S .. in fp64 (as the
+  // fp32 gradient's whole-wave path), partials as fp32 pairs in ntmp, then lane a's sum as a pair
+  // in v2 / p (p is rewritten by the direction below)
+  const uint32_t bigg = PNP_BIG_ISLANDS ? (uint32_t)__ballot(l < nisl && s.isl_roff[l + 1] - s.isl_roff[l] > NT &&
+                                                             s.isl_n[l] <= 32)
+                                        : 0u;
+  for (uint32_t bm = bigg; bm; bm &= bm - 1) {
+    const int I = __builtin_ctz(bm);
+    const int n = s.isl_n[I], r0 = s.isl_roff[I], nr = s.isl_roff[I + 1] - r0, S = NT / n;
+    const int a = l % n, k0 = l / n;
+    if (k0 < S) {
+      const float* col = s.jt + s.isl_joff[I] + a;
+      double part = 0;
+      for (int k = k0; k < nr; k += S) part += (double)col[k * n] * ((double)s.rr_f[r0 + k] + (double)s.rr_d[r0 + k]);
+      const float hi = (float)part;
+      s.ntmp[l] = hi;
+      s.ntmp[NT + l] = (float)(part - (double)hi);
+    }
+    wsync();
+    if (l < n) {
+      double g = 0;
+      for (int k = 0; k < S; k++) g += (double)s.ntmp[l + k * n] + (double)s.ntmp[NT + l + k * n];
+      const int d = s.isl_dof[I][l];
+      const float hi = (float)g;
+      s.v2[d] = hi;
+      s.p[d] = (float)(g - (double)hi);
+    }
+    wsync();
+  }
+  if (l < m.nv) {
+    const int t = s.c_dof_tree[l], I = s.tree_island[t];
+    const int a = s.c_tree_dofadr[t], n = s.c_tree_dofnum[t], o = s.c_tree_moff[t] + (l - a) * n;
+    double g = 0;
+    for (int k = 0; k < n; k++) g += (double)s.M[o + k] * ((double)s.x[a + k] - (double)s.qacc_smooth[a + k]);
+    if (bigg >> I & 1u) {
+      g += (double)s.v2[l] + (double)s.p[l];
+    } else {
+      const int ni = s.isl_n[I], r0 = s.isl_roff[I], nr = s.isl_roff[I + 1] - r0;
+      const float* col = s.jt + s.isl_joff[I] + s.dof_ipos[l];
+#pragma unroll 4
+      for (int k = 0; k < nr; k++) g += (double)col[k * ni] * ((double)s.rr_f[r0 + k] + (double)s.rr_d[r0 + k]);
+    }
+    s.grad[l] = (float)g;
+    s.v2[l] = (float)(g * g);
+  }
+  wsync();
+}
+// x += p on the live islands (isl_flag clear), their rows' jar and active set re-evaluated at the
+// new x (fp64 accumulation, rounded once); per island whether its active set changed -> isl_val
+__device__ __attribute__((noinline)) void newton_refine_update(Env<float>& s) {
+  const DevPhys<float>& m = phys<float>();
+  const int l = lane_id();
+  if (l < m.nv && !s.isl_flag[s.tree_island[s.c_dof_tree[l]]]) s.x[l] += s.p[l];
+  wsync();
+  for (int r = l; r < s.nefc; r += NT) {
+    const unsigned char old = s.efc_act[r];
+    s.efc_Jp[r] = (float)old;
+    if (s.isl_flag[s.tree_island[s.efc_t0[r]]]) continue;
+    const double jar = row_dot64(s, r, s.x) - (double)s.efc_aref[r];
+    s.efc_jar[r] = (float)jar;
+    s.efc_act[r] = r < s.ne || jar < 0;
+  }
+  wsync();
+  {
+    const int q = l & 7, I = l >> 3;
+    bool ch = false;
+    if (I < s.nisland)
+      for (int rr = s.isl_roff[I] + q; rr < s.isl_roff[I + 1]; rr += 8) {
+        const int r = s.isl_row[rr];
+        ch |= (float)s.efc_act[r] != s.efc_Jp[r];
+      }
+    const bool any = ((__ballot(ch) >> (l & 56)) & 0xFFull) != 0;
+    if (I < s.nisland && q == 0) s.isl_val[I] = any ? 1.0f : 0.0f;
+  }
+  wsync();
+}
+
 template <typename T, class CLK>
 __device__ void st_newton_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk) {
   const DevPhys<T>& m = phys<T>();
@@ -2838,8 +2960,54 @@ __device__ void st_newton_islands(const DevPhys<T>& /*image: phys<T>()*/, Env<T>
   // group-parallel island factorisation when every island fits a 9-lane group
   const bool gch = s.nisland <= GCH_GROUPS && !__ballot(l < s.nisland && s.isl_n[l] > GCH_N);
   const int nisl = s.nisland;
+  int nref = 0;   // refinement steps (not Newton iterations: solver_iter does not count them)
   for (; it < m.iterations; it++) {
     clk.sub_start();
+    // every live island kept its active set over its last step and holds its Hessian factor: one
+    // step of mixed-precision iterative refinement (newton_refine_grad) instead of another Newton
+    // iteration
+    if constexpr (sizeof(T) == 4) {
+      if (jt && nref < 4 && !__ballot(l < nisl && !done && (unchanged < 1 || !s.isl_hvalid[l]))) {
+        nref++;
+        newton_refine_grad(s);
+        clk.sub_lap(SC_N_GRAD);
+        island_sums(s, s.v2, (const T*)nullptr, s.isl_val);
+        if (!done && PM<T>::sqrt_(s.isl_val[l]) * gscale < gtol) done = true;
+        if (l < PH_MAXT) s.isl_flag[l] = done;
+        wsync();
+        clk.sub_lap(SC_N_CONV);
+        clk.lap(9);
+        if (!__ballot(!done)) break;
+        if (gch) {
+          newton_dir_groups(s, done);
+        } else {   // (every live island holds its factor: <= 9 dofs, the register path)
+          const int n = !done ? s.isl_n[l] : 0;
+          if (!done) island_newton_dir_reg<T, 9>(s, l, n);
+          wsync();
+        }
+        clk.lap(10);
+        newton_refine_update(s);
+        bool anych = false;
+        if (!done) {
+          if (s.isl_val[l] != T(0)) {
+            unchanged = 0;
+            s.isl_hvalid[l] = 0;
+            anych = true;
+          } else {
+            done = true;
+          }
+        }
+        wsync();
+        if (__ballot(anych)) {   // a changed island goes on with Newton iterations: its cost
+          eval_cost(m, s, s.x, true, s.isl_cost);
+          if (anych) cost = s.isl_cost[l];
+        }
+        clk.lap(11);
+        if (!__ballot(!done)) break;
+        it--;   // (a refinement is not a Newton iteration)
+        continue;
+      }
+    }
     // gradient g = M (x - x_smooth) + J^T (D jar) over the dof's island rows
     if (l < m.nv) s.v1[l] = s.x[l] - s.qacc_smooth[l];
     if (jt)

@@ -10,7 +10,7 @@ from .model import PnpIKParams, PnpModelDesc
 # PNP_LIB: another build of the same sources (tools/asan_cpu_tests.sh: the host-sanitizer build)
 LIB_PATH = os.environ.get("PNP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpnp.so")
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 # every symbol include/pnp.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -20,7 +20,8 @@ EXPORTS = [
     "pnp_forward_debug", "pnp_forward_debug_f64", "pnp_step_lds_bytes", "pnp_step_profile",
     "pnp_env_params_size", "pnp_env_init", "pnp_env_init_f64", "pnp_env_reset", "pnp_env_reset_f64",
     "pnp_env_step", "pnp_env_step_f64", "pnp_env_evaluate", "pnp_env_evaluate_f64",
-    "pnp_slerp_track_f64", "pnp_env_queue_status",
+    "pnp_slerp_track_f64", "pnp_env_queue_status", "pnp_tqc_workspace_floats", "pnp_tqc_param_counts",
+    "pnp_tqc_update",
 ]
 
 STATE_FIELDS = ("qpos", "qvel", "ctrl", "mocap_pos", "mocap_quat", "qacc_warmstart", "time", "warn")
@@ -59,6 +60,27 @@ class PnpEnvState(C.Structure):
 
 class PnpEnvOut(C.Structure):
     _fields_ = [(f, C.c_void_p) for f in ENV_OUT_FIELDS]
+
+
+_F = C.POINTER(C.c_float)
+
+
+class PnpTqcDesc(C.Structure):
+    """include/pnp.h pnp_tqc_desc."""
+    _fields_ = [("batch", C.c_int32), ("obs_dim", C.c_int32), ("act_dim", C.c_int32), ("hidden", C.c_int32),
+                ("n_critics", C.c_int32), ("n_quantiles", C.c_int32), ("n_drop_per_net", C.c_int32),
+                ("gamma", C.c_float), ("tau", C.c_float), ("target_entropy", C.c_float), ("beta1", C.c_float),
+                ("beta2", C.c_float), ("adam_eps", C.c_float),
+                ("actor", C.c_void_p * 10), ("actor_m", C.c_void_p * 10), ("actor_v", C.c_void_p * 10),
+                ("actor_step", C.c_void_p * 10),
+                ("critic", C.c_void_p * 8), ("critic_m", C.c_void_p * 8), ("critic_v", C.c_void_p * 8),
+                ("critic_step", C.c_void_p * 8), ("target", C.c_void_p * 8),
+                ("log_ent_coef", C.c_void_p), ("ent_m", C.c_void_p), ("ent_v", C.c_void_p), ("ent_step", C.c_void_p),
+                ("lr", C.c_void_p), ("workspace", C.c_void_p), ("workspace_floats", C.c_int64), ("logs", C.c_void_p)]
+
+
+class PnpTqcBatch(C.Structure):
+    _fields_ = [(f, C.c_void_p) for f in ("obs", "act", "next_obs", "done", "reward", "eps_pi", "eps_next")]
 
 
 # debug record layout (include/pnp.h PNP_DBG_*)
@@ -142,6 +164,12 @@ def load():
     L.pnp_slerp_track_f64.restype = I32
     L.pnp_env_queue_status.argtypes = [P]
     L.pnp_env_queue_status.restype = I32
+    L.pnp_tqc_workspace_floats.argtypes = [C.POINTER(PnpTqcDesc)]
+    L.pnp_tqc_workspace_floats.restype = C.c_int64
+    L.pnp_tqc_param_counts.argtypes = [P, P]
+    L.pnp_tqc_param_counts.restype = I32
+    L.pnp_tqc_update.argtypes = [C.POINTER(PnpTqcDesc), C.POINTER(PnpTqcBatch), P, P]
+    L.pnp_tqc_update.restype = I32
     if L.pnp_abi_version() != ABI_VERSION:
         raise PnpError(f"libpnp ABI {L.pnp_abi_version()} != binding ABI {ABI_VERSION}")
     if L.pnp_env_params_size() != C.sizeof(PnpEnvParams):

@@ -31,6 +31,7 @@ in lockstep (data-parallel learner).
 """
 from __future__ import annotations
 
+import ctypes as C
 import dataclasses
 import math
 import time
@@ -67,6 +68,11 @@ class TQCConfig:
     # one gradient step captured in a HIP graph and replayed gradient_steps times per train() (single
     # process only; the data-parallel learner all-reduces eagerly)
     graph: bool = True
+    # the hand-written fused gradient step (csrc/tqc_fused.hip, pnp_tqc_update) when the shapes are
+    # train.py's (obs 25, action 7, [256, 256, 256], 2 x 25 quantiles, batch a multiple of 16), on
+    # one GPU; else (and for the first gradient step, which creates the optimisers' state) the
+    # PyTorch step
+    fused: bool = True
 
 
 def _world():
@@ -306,6 +312,7 @@ class TQC:
         self.ent_opt = torch.optim.Adam([self.log_ent_coef], **kw)
         self._graph = None          # the captured gradient step (TQC._capture)
         self._graph_out = None
+        self._fdesc = None          # pnp_tqc_desc of the fused step (TQC._fused_desc)
         self._eager_updates = 0     # steps run eagerly before the capture (allocator / optimiser state)
         self.vecnorm = VecNormalize(dims, self.device, c.clip_obs, c.norm_eps)
         self.buffer = DictReplayBuffer(c.buffer_size, self.n_envs, self.obs_dim, self.act_dim, self.device)
@@ -348,11 +355,13 @@ class TQC:
             p.grad.copy_(flat[o:o + n].view_as(p.grad))
             o += n
 
-    def _step_opt(self, opt, loss, params):
+    def _step_opt(self, opt, loss, params, record=None):
         opt.zero_grad(set_to_none=True)
         loss.backward()
         if _world() > 1:
             self._allreduce_grads(params)
+        if record is not None:   # (tests: the gradients the step applies)
+            record.extend(p.grad.detach().clone() for p in params)
         opt.step()
 
     # ------------------------------------------------------------------ rollout
@@ -410,8 +419,18 @@ class TQC:
     def _update(self):
         """One gradient step (sb3-contrib tqc.py train() order) on device tensors, no host sync:
         entropy coefficient, critics, actor, Polyak target update.  Returns the logged values as
-        device scalars."""
+        device scalars.  The fused HIP step when it applies (_fused_ok), else PyTorch."""
+        if self._fused_ok() and self._fused_state_ready():
+            return self._update_fused()
+        return self._update_torch()
+
+    def _update_torch(self, record=None):
+        """The PyTorch gradient step.  record (tests): a dict that receives the applied gradients,
+        'actor' and 'critic', in _fused_params order."""
         c = self.cfg
+        rc = ra = None
+        if record is not None:
+            rc, ra = record.setdefault("critic", []), record.setdefault("actor", [])
         obs, act, nobs, done, rew = self._sample_norm()
         a_pi, lp = self.actor.action_log_prob(obs, self.gen)
         lp = lp.reshape(-1, 1)
@@ -429,10 +448,10 @@ class TQC:
             tq = tq.unsqueeze(1)
         cq = self.critic(obs, act)
         critic_loss = quantile_huber_loss(cq, tq, sum_over_quantiles=False)
-        self._step_opt(self.critic_opt, critic_loss, self.critic.parameters())
+        self._step_opt(self.critic_opt, critic_loss, list(self.critic.parameters()), rc)
         qpi = self.critic(obs, a_pi).mean(dim=2).mean(dim=1, keepdim=True)
         actor_loss = (ent_coef * lp - qpi).mean()
-        self._step_opt(self.actor_opt, actor_loss, self.actor.parameters())
+        self._step_opt(self.actor_opt, actor_loss, list(self.actor.parameters()), ra)
         if (self.n_updates + 1) % c.target_update_interval == 0:
             with torch.no_grad():
                 tps, ps = list(self.critic_target.parameters()), list(self.critic.parameters())
@@ -440,6 +459,90 @@ class TQC:
                 torch._foreach_add_(tps, ps, alpha=c.tau)
         self.n_updates += 1
         return ent_coef, critic_loss.detach(), actor_loss.detach(), ent_loss.detach()
+
+    # ------------------------------------------------------------------ the fused gradient step
+    def _fused_ok(self):
+        c = self.cfg
+        return (c.fused and self.device.type == "cuda" and _world() == 1 and tuple(c.net_arch) == (256, 256, 256)
+                and c.n_critics == 2 and c.n_quantiles == 25 and c.top_quantiles_to_drop_per_net == 2
+                and c.batch_size % 16 == 0 and self.obs_dim == 25 and self.act_dim == 7
+                and c.target_update_interval == 1)
+
+    def _fused_params(self):
+        a = self.actor
+        pa = [a.latent[0].weight, a.latent[0].bias, a.latent[2].weight, a.latent[2].bias, a.latent[4].weight,
+              a.latent[4].bias, a.mu.weight, a.mu.bias, a.log_std.weight, a.log_std.bias]
+        pc = [t for pair in zip(self.critic.weights, self.critic.biases) for t in pair]
+        pt = [t for pair in zip(self.critic_target.weights, self.critic_target.biases) for t in pair]
+        return pa, pc, pt
+
+    def _fused_state_ready(self):
+        pa, pc, _ = self._fused_params()
+        return (all(p in self.actor_opt.state and "exp_avg" in self.actor_opt.state[p] for p in pa)
+                and all(p in self.critic_opt.state and "exp_avg" in self.critic_opt.state[p] for p in pc)
+                and self.log_ent_coef in self.ent_opt.state)
+
+    def _fused_desc(self):
+        """pnp_tqc_desc over the live parameter, target and Adam-state tensors (built once they all
+        exist; rebuilt after load_state_dict, which replaces the optimiser state)."""
+        if self._fdesc is not None:
+            return self._fdesc
+        from . import _lib
+        L = _lib.load()
+        c = self.cfg
+        pa, pc, pt = self._fused_params()
+        d = _lib.PnpTqcDesc()
+        d.batch, d.obs_dim, d.act_dim, d.hidden = c.batch_size, self.obs_dim, self.act_dim, c.net_arch[0]
+        d.n_critics, d.n_quantiles, d.n_drop_per_net = c.n_critics, c.n_quantiles, c.top_quantiles_to_drop_per_net
+        d.gamma, d.tau, d.target_entropy = c.gamma, c.tau, self.target_entropy
+        b1, b2 = self.actor_opt.defaults["betas"]
+        d.beta1, d.beta2, d.adam_eps = b1, b2, self.actor_opt.defaults["eps"]
+        keep = []
+        for name, opt, ps in (("actor", self.actor_opt, pa), ("critic", self.critic_opt, pc)):
+            for i, p in enumerate(ps):
+                st = opt.state[p]
+                for suffix, t in (("", p), ("_m", st["exp_avg"]), ("_v", st["exp_avg_sq"]), ("_step", st["step"])):
+                    assert t.is_contiguous() and t.dtype == torch.float32 and t.device == self.device, (name, suffix)
+                    getattr(d, name + suffix)[i] = t.data_ptr()
+                    keep.append(t)
+        for i, t in enumerate(pt):
+            d.target[i] = t.data_ptr()
+        es = self.ent_opt.state[self.log_ent_coef]
+        d.log_ent_coef, d.ent_m, d.ent_v, d.ent_step = (self.log_ent_coef.data_ptr(), es["exp_avg"].data_ptr(),
+                                                          es["exp_avg_sq"].data_ptr(), es["step"].data_ptr())
+        d.lr = self._lr.data_ptr()
+        n = L.pnp_tqc_workspace_floats(C.byref(d))
+        if n < 0:
+            _lib.check(int(n), "pnp_tqc_workspace_floats")
+        self._fws = torch.empty(int(n), dtype=torch.float32, device=self.device)
+        self._flogs = torch.zeros(4, dtype=torch.float32, device=self.device)
+        d.workspace, d.workspace_floats, d.logs = self._fws.data_ptr(), int(n), self._flogs.data_ptr()
+        self._fkeep = keep + list(pt) + [es["exp_avg"], es["exp_avg_sq"], es["step"]]
+        self._fdesc = d
+        return d
+
+    def _update_fused(self, grads_out=None):
+        """One gradient step by pnp_tqc_update (csrc/tqc_fused.hip): the same replay sample and the
+        same two N(0, 1) draws as _update (sb3's order), then the whole step -- entropy coefficient,
+        critics, Polyak, actor -- in four launches.  grads_out (tests): the step's reduced
+        gradients, actor then critics."""
+        from . import _lib
+        L = _lib.load()
+        d = self._fused_desc()
+        c = self.cfg
+        obs, act, nobs, done, rew = self._sample_norm()
+        B = c.batch_size
+        eps_pi = torch.randn(B, self.act_dim, device=self.device, generator=self.gen)
+        eps_next = torch.randn(B, self.act_dim, device=self.device, generator=self.gen)
+        ts = [t.contiguous() for t in (obs, act, nobs, done, rew, eps_pi, eps_next)]
+        b = _lib.PnpTqcBatch(*[t.data_ptr() for t in ts])
+        gp = None if grads_out is None else C.c_void_p(grads_out.data_ptr())
+        _lib.check(L.pnp_tqc_update(C.byref(d), C.byref(b), gp, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
+                   "pnp_tqc_update")
+        self._fbatch = ts   # (alive until the launch has read them; in a capture, the graph's pool)
+        self.n_updates += 1
+        lg = self._flogs
+        return lg[0], lg[1], lg[2], lg[3]
 
     def _graph_ok(self):
         return (self.cfg.graph and _world() == 1 and self.device.type == "cuda"
@@ -548,6 +651,7 @@ class TQC:
                 for g in opt.param_groups:
                     g["lr"] = self._lr
         self._graph, self._graph_out, self._eager_updates = None, None, 0
+        self._fdesc = None
 
     def save(self, path):
         torch.save(self.state_dict(), path)

@@ -1,0 +1,80 @@
+"""Box-box contacts and the reset random walk's deep spawns on the GPU (libpnp.so through the C
+ABI) against the fp64 CPU oracle: tests/box_states.py's configurations -- a cube resting flat,
+tilted onto an edge and onto a corner, two cubes crossing edge to edge, the closed fingers' pad
+boxes pressed together, a cube inside a shelf leg (1 and 3.9 cm deep), inside a table leg on the
+floor, two cubes overlapping, a cube half over a board edge.
+
+  * fp64 kernel = oracle: contact list (order, geoms, positions, normals, depths) and every stage
+    within 1e-9, one and ten sub-steps within 1e-9 / 1e-8, warning bits equal.
+  * fp32 product kernel: warning bits equal, finite, and the per-tree bar of test_step_gpu.py
+    (1e-5 or three times the one-ulp conditioning floor) on one sub-step.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+import box_states as BS
+import physics_states as PS
+import test_step_gpu as T
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def boxes(model):
+    return BS.box_states(model)
+
+
+def test_box_contacts_f64_match_oracle(engine, model, boxes):
+    """Contact for contact: the fp64 kernel's list equals the oracle's (same order and geom pairs;
+    position, normal and depth within 1e-9), then every forward stage within 1e-9.  (forward_debug
+    runs the full tier alone, 48 contacts: the pressed pads' 56 are compared by the step tests,
+    which run the wide tier.)"""
+    from pnp_amd import _lib
+    D = _lib.DBG
+    idx, st = boxes
+    idx = {c: b for c, b in idx.items() if c != "pads"}
+    sel = np.array(sorted(idx.values()))
+    st = {k: v[sel] for k, v in st.items()}
+    idx = {c: int(np.nonzero(sel == b)[0][0]) for c, b in idx.items()}
+    dbg = engine.forward_debug(T._dev(st, torch.float64)).cpu().numpy()
+    for case, b in idx.items():
+        f = O.forward_fields({k: st[k][b] for k in O.STATE_KEYS}, ["ncon", "contact"], model=model)
+        n = int(f["ncon"][0])
+        c = f["contact"].reshape(n, 30)
+        kn = int(dbg[b, D["COUNTS"]])
+        assert kn == n, (case, kn, n)
+        kc = dbg[b, D["CON"]:D["CON"] + 16 * kn].reshape(kn, 16)
+        assert np.array_equal(kc[:, 13:15].astype(int), c[:, 27:29].astype(int)), case
+        assert np.abs(kc[:, 0:3] - c[:, 0:3]).max() < 1e-9, case
+        assert np.abs(kc[:, 3:6] - c[:, 3:6]).max() < 1e-9, case
+        assert np.abs(kc[:, 12] - c[:, 12]).max() < 1e-9, case
+    w = T._forward_compare(engine, model, st, torch.float64)
+    assert max(w.values()) < 1e-9, w
+
+
+@pytest.mark.parametrize("nsub", [1, 10])
+def test_box_fixtures_step_f64(engine, model, boxes, nsub):
+    _, st = boxes
+    ref = PS.copy_state(st)
+    O.step(ref, nsub=nsub, nthreads=8, model=model)
+    g = T._host(engine.step(T._dev(st, torch.float64), nsub))
+    tol = 1e-9 if nsub == 1 else 1e-8
+    assert np.abs(g["qpos"] - ref["qpos"]).max() < tol
+    assert np.abs(g["qvel"] - ref["qvel"]).max() < tol * max(1.0, np.abs(ref["qvel"]).max())
+    assert np.array_equal(g["warn"], ref["warn"])
+
+
+def test_box_fixtures_f32(engine, model, boxes):
+    """fp32: warning bits equal the oracle's over 25 sub-steps (one mj_step(nstep=25) call of the
+    gym step) from the deep spawns, state finite; one sub-step within the per-tree bar."""
+    _, st = boxes
+    s32 = T._round32(st)
+    ref = PS.copy_state(s32)
+    O.step(ref, nsub=25, nthreads=8, model=model)
+    g = T._host(engine.step(T._dev(s32, torch.float32), 25))
+    assert np.array_equal(g["warn"], ref["warn"]), (g["warn"], ref["warn"])
+    assert np.isfinite(g["qpos"]).all() and np.isfinite(g["qvel"]).all()
+    T._assert_per_tree(engine, model, st, 1, "box fixtures")

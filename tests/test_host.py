@@ -61,7 +61,7 @@ def test_workload_is_shard_invariant(model):
 
 def _header_symbols():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int32_t|const char\*)\s+(pnp_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int32_t|int64_t|const char\*)\s+(pnp_\w+)\s*\(", src, re.M)))
 
 
 def test_library_loads_and_exports_header_symbols():
@@ -72,7 +72,7 @@ def test_library_loads_and_exports_header_symbols():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_lib.EXPORTS)
-    assert L.pnp_abi_version() == _lib.ABI_VERSION == 10
+    assert L.pnp_abi_version() == _lib.ABI_VERSION == 11
     from pnp_amd.model import PnpModelDesc
     assert L.pnp_model_desc_size() == C.sizeof(PnpModelDesc)
 

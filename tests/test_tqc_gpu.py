@@ -9,6 +9,7 @@ gym env (libpnp.so pnp_env_step through pnp_amd.envs).
 * the full C5 configuration (fp32, 250 sub-steps per gym step): rollout + gradient steps stay
   finite, and the replay buffer holds exactly what the env returned.
 """
+import ctypes as C
 import math
 
 import numpy as np
@@ -100,8 +101,9 @@ def test_c5_config_8192_envs():
 
 
 def test_captured_learner_step_equals_eager():
-    """The HIP-graph gradient step (TQC._capture: one captured update replayed gradient_steps
-    times) gives the eager steps' results bit for bit -- same replay samples, same exploration
+    """The HIP-graph gradient step of the PyTorch learner (TQC._capture: one captured update
+    replayed gradient_steps times; the fused HIP step has its own tests below) gives the eager
+    steps' results bit for bit -- same replay samples, same exploration
     noise (the generator is registered with the graph), fused Adam either way -- over 12 updates
     across two train() calls, and its learner step is faster than the eager one."""
     import time
@@ -111,7 +113,7 @@ def test_captured_learner_step_equals_eager():
     agents = []
     for graph in (False, True):
         env = BatchedFrankaShelfPNPEnv(B, config=EnvConfig(**SHORT))
-        a = TQC(env, TQCConfig(learning_starts=0, graph=graph))
+        a = TQC(env, TQCConfig(learning_starts=0, graph=graph, fused=False))
         a.total_timesteps = 10 ** 6
         a.reset()
         for _ in range(3):
@@ -136,3 +138,94 @@ def test_captured_learner_step_equals_eager():
         ms.append((time.perf_counter() - t0) / 50 * 1e3)
     print(f"learner step: eager {ms[0]:.3f} ms, captured {ms[1]:.3f} ms")
     assert ms[1] < ms[0]
+
+
+def _fused_agent(B=64, **cfg):
+    from pnp_amd.envs import BatchedFrankaShelfPNPEnv, EnvConfig
+    from pnp_amd.tqc import TQC, TQCConfig
+    env = BatchedFrankaShelfPNPEnv(B, config=EnvConfig(**SHORT))
+    a = TQC(env, TQCConfig(**cfg))
+    a.total_timesteps = 10 ** 6
+    a.reset()
+    for _ in range(12):            # 768 transitions: past learning_starts and one batch
+        a.collect_step()
+    return a
+
+
+def test_fused_learner_step_matches_pytorch():
+    """pnp_tqc_update (csrc/tqc_fused.hip: the whole TQC gradient step in four launches) against
+    the PyTorch step (pnp_amd/tqc.py _update_torch, autograd) from the same state, replay sample and
+    Gaussian draws: every gradient tensor it applies within 1e-4 (critics) / 1e-3 (actor, computed
+    against the Adam-updated critics) of the PyTorch gradient in norm, the logged losses within
+    1e-4, and the parameters after Adam (actor, critics, Polyak targets, log entropy coefficient)
+    within a small fraction of the learning rate."""
+    import copy
+    from pnp_amd import _lib
+    a = _fused_agent(graph=False)
+    for _ in range(3):
+        a.train()                  # the first creates the Adam state (PyTorch), then fused steps
+    assert a._fdesc is not None
+    L = _lib.load()
+    na, nc = C.c_int32(), C.c_int32()
+    L.pnp_tqc_param_counts(C.byref(na), C.byref(nc))
+    na, nc = na.value, nc.value
+    pa, pc, pt = a._fused_params()
+    sd = copy.deepcopy(a.state_dict())
+    gs = a.gen.get_state()
+    g = torch.zeros(na + nc, device=a.device)
+    lf = [float(t) for t in a._update_fused(g)]
+    after_f = [p.detach().clone() for p in pa + pc + pt] + [a.log_ent_coef.detach().clone()]
+    a.load_state_dict(sd)
+    a.gen.set_state(gs)
+    rec = {}
+    lt = [float(t) for t in a._update_torch(rec)]
+    after_t = [p.detach().clone() for p in pa + pc + pt] + [a.log_ent_coef.detach().clone()]
+    byid = {id(p): gr for p, gr in zip(list(a.actor.parameters()), rec["actor"])}
+    byid.update({id(p): gr for p, gr in zip(list(a.critic.parameters()), rec["critic"])})
+    o = 0
+    worst = {}
+    for name, ps in (("actor", pa), ("critic", pc)):
+        for i, p in enumerate(ps):
+            n = p.numel()
+            gf, gt = g[o:o + n].view_as(p), byid[id(p)]
+            o += n
+            e = float((gf - gt).norm() / gt.norm().clamp_min(1e-30))
+            worst[f"{name}{i}"] = e
+            assert e < (1e-4 if name == "critic" else 1e-3), (name, i, e)
+    print("fused vs PyTorch gradient (relative norm):", {k: f"{v:.1e}" for k, v in worst.items()})
+    print("logs fused", lf, "PyTorch", lt)
+    for x, y in zip(lf, lt):
+        assert abs(x - y) <= 1e-4 * max(1.0, abs(y)), (lf, lt)
+    lr = float(a._lr)
+    for x, y in zip(after_f, after_t):
+        d = (x - y).abs()
+        assert float(d.max()) <= 2.5 * lr and float(d.median()) <= 1e-3 * lr, (float(d.max()), float(d.median()), lr)
+
+
+def test_fused_learner_step_captured_and_timed():
+    """The fused step inside TQC.train (HIP-graph captured, replayed gradient_steps times) equals
+    the uncaptured fused step bit for bit (fixed-order reductions, no atomics), stays finite, and
+    is timed against the PyTorch captured step (printed; the bench's tqc leg records both)."""
+    import time
+    agents = [_fused_agent(graph=g) for g in (False, True)]
+    for n in (5, 7):
+        le, lg = agents[0].train(n), agents[1].train(n)
+        for k in ("critic_loss", "actor_loss", "ent_coef_loss", "ent_coef"):
+            assert torch.equal(le[k], lg[k]), k
+            assert math.isfinite(float(le[k])), k
+    assert agents[1]._graph is not None and agents[0]._fdesc is not None
+    for name in ("actor", "critic", "critic_target"):
+        for (kp, p), (_, q) in zip(getattr(agents[0], name).state_dict().items(),
+                                   getattr(agents[1], name).state_dict().items()):
+            assert torch.equal(p, q), (name, kp)
+    ref = _fused_agent(graph=True, fused=False)
+    ms = []
+    for a in (agents[1], ref):
+        a.train(5)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        a.train(200)
+        torch.cuda.synchronize()
+        ms.append((time.perf_counter() - t0) / 200 * 1e3)
+    print(f"learner step (captured): fused HIP {ms[0]:.3f} ms, PyTorch {ms[1]:.3f} ms")
+    assert ms[0] < ms[1]

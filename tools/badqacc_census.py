@@ -18,11 +18,16 @@ runs E times), and records per episode and cube:
     and mocap as reset), max |qacc| over each cube's dofs -- the transient a deep spawn causes;
   * every bad-state warning bit (BADQPOS / BADQVEL / BADQACC: the engine resets that env like
     mj_resetData) with its gym step, and the max |qacc_warmstart| (qacc of the last sub-step) over
-    the cube dofs after each gym step.
-Events are saved (spawn state + actions) for replay on the fp64 CPU oracle: tools/badqacc_replay.py.
+    the cube dofs after each gym step;
+  * --far: after each gym step, the contacts of a forward at the new state (forward_debug, the
+    full tier's 48 contacts) that involve a cube, and how far each lies from that cube's centre --
+    a box-box edge-edge contact of nearly parallel edges placed far along the edge lines would put
+    a huge lever arm on the cube's angular dofs (one candidate for the reference's BADQACC on
+    cube3's angular dofs 24 / 25).
+Events are saved (spawn state + actions, --out) for replay on the fp64 CPU oracle.
 
 usage: python tools/badqacc_census.py [--envs B] [--episodes E] [--steps S] [--policy small|uniform]
-                                      [--probe N] [--dtype f32|f64] [--out file.npz]
+                                      [--probe N] [--dtype f32|f64] [--far] [--out file.npz]
 """
 import argparse
 import collections
@@ -110,6 +115,7 @@ def main():
     ap.add_argument("--dtype", default="f32", choices=("f32", "f64"))
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--far", action="store_true", help="contact-distance check after every gym step")
     args = ap.parse_args()
     dt = torch.float32 if args.dtype == "f32" else torch.float64
     B = args.envs
@@ -120,6 +126,9 @@ def main():
     qadr = [int(m.jnt_qposadr[m.joint_id(f"{c}_joint")]) for c in CUBES]
     dadr = [int(m.jnt_dofadr[m.joint_id(f"{c}_joint")]) for c in CUBES]
     rng = np.random.default_rng(args.seed)
+    cube_geoms = [m.geom_id(f"{c}_geom") for c in CUBES]
+    far_max = 0.0
+    far_n = 0
     t0 = time.time()
     rows = []          # per (episode, env, cube)
     events = []        # bad-state warnings
@@ -156,6 +165,10 @@ def main():
             qa = g.state["qacc_warmstart"].double().abs().cpu().numpy()
             for i, d in enumerate(dadr):
                 smax[:, i] = np.maximum(smax[:, i], qa[:, d:d + 6].max(1))
+            if args.far:
+                fd, fn = far_contacts(eng, g, cube_geoms, qadr)
+                far_max = max(far_max, fd)
+                far_n += fn
         for b in np.nonzero(first_bad >= 0)[0]:
             ev = dict(episode=ep, env=int(b), step=int(first_bad[b]), bits=int(bad_bits[b]),
                       time_window=[0.5 + 0.5 * first_bad[b], 0.5 + 0.5 * (first_bad[b] + 1)],
@@ -180,6 +193,7 @@ def main():
         print(f"episode {ep}: spawn in a static box {int((cl['static_depth'] > 1e-4).sum())}, in a cube "
               f"{int((cl['cube_depth'] > 1e-4).sum())}, unsupported {int((~cl['supported']).sum())} (of {3 * B} cubes); "
               f"probe max|qacc| {pmax.max():.3g}; step max|qacc| {smax.max():.3g}; bad-state envs {nbad}; "
+              + (f"cube contacts farthest from the cube centre {far_max:.4f} m, beyond 0.05 m: {far_n}; " if args.far else "") +
               f"{time.time() - t0:.0f} s", flush=True)
     R = np.concatenate(rows)
     cols = ["episode", "env", "cube", "x", "y", "z", "static_depth", "cube_depth", "floor_depth", "supported",
@@ -188,6 +202,33 @@ def main():
     if args.out:
         np.savez_compressed(args.out, census=R, columns=np.array(cols), events=json.dumps(events),
                             **{f"replay_{k}": np.array(v) for k, v in replay.items()})
+
+
+def far_contacts(eng, g, cube_geoms, qadr):
+    """After a gym step: (the largest distance from a cube contact to that cube's centre, the number
+    of such contacts beyond 0.05 m) over the envs' current contacts (forward_debug, full tier)."""
+    from pnp_amd import _lib
+    D = _lib.DBG
+    dbg = eng.forward_debug(g.state).double().cpu().numpy()
+    n = dbg[:, D["COUNTS"]].astype(int)
+    q = g.state["qpos"].double().cpu().numpy()
+    far, cnt = 0.0, 0
+    K = int(n.max()) if n.size else 0
+    if K == 0:
+        return far, cnt
+    con = dbg[:, D["CON"]:D["CON"] + 16 * K].reshape(-1, K, 16)
+    valid = np.arange(K)[None] < n[:, None]
+    for cg, a in zip(cube_geoms, qadr):
+        hit = valid & ((con[..., 13] == cg) | (con[..., 14] == cg))
+        d = np.linalg.norm(con[..., 0:3] - q[:, None, a:a + 3], axis=-1)
+        d = np.where(hit, d, 0.0)
+        far = max(far, float(d.max()))
+        cnt += int((d > 0.05).sum())
+        for e, k in zip(*np.nonzero(d > 0.05)):
+            r = con[e, k]
+            print(f"  far contact: env {e}, geoms {int(r[13])}-{int(r[14])}, {d[e, k]:.4f} m from the cube centre, "
+                  f"dist {r[12]:.3g}, pos {np.round(r[0:3], 4)}, normal {np.round(r[3:6], 4)}", flush=True)
+    return far, cnt
 
 
 def summarize(R, cols, names, events):
