@@ -28,9 +28,12 @@
 namespace {
 
 constexpr int R = 16;              // rows per slab (one MFMA tile of rows)
-constexpr int NTH = 256;           // threads per workgroup: 4 waves
+constexpr int NW = 8;              // waves per workgroup (two per SIMD)
+constexpr int NTH = 64 * NW;
+constexpr int KC = 32;             // reduction rows per staged weight chunk
 constexpr int OBS = 25, ACT = 7, HID = 256, NC = 2, NQ = 25, NIN = OBS + ACT, NALL = NC * NQ;
 constexpr int LD = HID + 4;        // LDS row stride (floats)
+constexpr int LDW = HID + 4;       // staged weight chunk row stride
 constexpr float LOG_STD_MIN = -20.0f, LOG_STD_MAX = 2.0f, SQUASH_EPS = 1e-6f;
 constexpr float HALF_LOG_2PI = 0.91893853320467274178f;
 
@@ -47,96 +50,119 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// ---- slab matrix products (X, Y, dY, dX: LDS [16][LD]; W: global)
-// Wk(k, n): the layer's weight as in x Wk, from nn.Linear's [out][in] (TR) or the stacked critics'
-// [in][out] layout.  Every MFMA runs with the whole wave (per-lane predicates only select operands).
-template <bool TR>
-__device__ __forceinline__ float wk(const float* __restrict__ W, int k, int n, int K, int N) {
-  return TR ? W[(size_t)n * K + k] : W[(size_t)k * N + n];
+// ---- slab matrix products (X, Y, dY, dX: LDS [16][LD]; W: global, staged through LDS)
+// acc = X[16][K] B[K][N]: B(r, c) (r the reduction index, c the output column) is the weight
+// element W[c * ld + r] (CR: contiguous in r) or W[r * ld + c] (RC).  The weight streams through
+// two LDS chunk buffers of KC reduction rows (Ws: 2 x KC x LDW floats): every thread fetches its
+// share of chunk ch + 1 into registers (coalesced global loads) while the waves run chunk ch's
+// MFMAs from LDS, then stores it and the workgroup syncs -- the MFMA chains never wait on a global
+// load.  Wave w owns the output tiles w and w + NW (16 columns each; every MFMA runs with the whole
+// wave, per-lane predicates only select operands).  Every thread of the workgroup must call it.
+template <bool CR>
+__device__ __forceinline__ float bget(const float* __restrict__ W, int ld, int r, int c) {
+  return CR ? W[(size_t)c * ld + r] : W[(size_t)r * ld + c];
 }
-// Y = act(X Wk + b): output tiles of 16 columns, wave w takes tiles w, w + 4, w + 8, w + 12 (their
-// MFMA chains interleaved)
-template <bool TR>
-__device__ void lin_fwd(const float* X, int K, const float* __restrict__ W, const float* __restrict__ bias, int N,
-                        float* Y, bool relu) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 15, kq = lane >> 4;
-  const int ntile = (N + 15) >> 4;
-  if (wv >= ntile) return;
-  const int nt = (ntile - wv + 3) >> 2;   // tiles of this wave (<= 4)
-  f32x4 acc[4];
+template <bool CR, int N>
+__device__ void slab_gemm(const float* X, int K, const float* __restrict__ W, int ld, float* Ws, f32x4 acc[2]) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, i = lane & 15, kq = lane >> 4;
+  constexpr int NTILE = (N + 15) / 16, NELEM = KC * N, PER = (NELEM + NTH - 1) / NTH;
+  acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nch = (K + KC - 1) / KC;
+  float pre[PER];
+  auto fetch = [&](int ch) {
 #pragma unroll
-  for (int q = 0; q < 4; q++) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-  for (int k0 = 0; k0 < K; k0 += 4) {
-    const int k = k0 + kq;
-    const float a = k < K ? X[i * LD + k] : 0.f;
+    for (int j = 0; j < PER; j++) {
+      const int f = t + j * NTH;
+      const int rr = CR ? f % KC : f / N, c = CR ? f / KC : f % N, r = ch * KC + rr;
+      pre[j] = (f < NELEM && r < K) ? bget<CR>(W, ld, r, c) : 0.f;
+    }
+  };
+  auto put = [&](int buf) {
+    float* D = Ws + buf * KC * LDW;
 #pragma unroll
-    for (int q = 0; q < 4; q++)
-      if (q < nt) {
-        const int n = (wv + 4 * q) * 16 + i;
-        const float b = (k < K && n < N) ? wk<TR>(W, k, n, K, N) : 0.f;
-        acc[q] = mfma4(a, b, acc[q]);
-      }
-  }
+    for (int j = 0; j < PER; j++) {
+      const int f = t + j * NTH;
+      const int rr = CR ? f % KC : f / N, c = CR ? f / KC : f % N;
+      if (f < NELEM) D[rr * LDW + c] = pre[j];
+    }
+  };
+  fetch(0);
+  put(0);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ch++) {
+    if (ch + 1 < nch) fetch(ch + 1);
+    const float* D = Ws + (ch & 1) * KC * LDW;
 #pragma unroll
-  for (int q = 0; q < 4; q++)
-    if (q < nt) {
-      const int n = (wv + 4 * q) * 16 + i;
-      if (n < N) {
-        const float bn = bias[n];
+    for (int k4 = 0; k4 < KC; k4 += 4) {
+      const int rr = k4 + kq, r = ch * KC + rr;
+      const float a = r < K ? X[i * LD + r] : 0.f;
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const float v = bn + acc[q][r];
-          Y[(4 * kq + r) * LD + n] = relu ? fmaxf(v, 0.f) : v;
+      for (int q = 0; q < 2; q++) {
+        const int tile = wv + q * NW;
+        if (tile < NTILE) {
+          const int c = tile * 16 + i;
+          const float b = c < N ? D[rr * LDW + c] : 0.f;
+          acc[q] = mfma4(a, b, acc[q]);
         }
       }
     }
+    if (ch + 1 < nch) put((ch + 1) & 1);
+    __syncthreads();
+  }
 }
-// dX (+)= (dY Wk^T) masked by relu'(H) (H: the layer input's post-ReLU activation, or null)
-template <bool TR>
-__device__ void lin_dgrad(const float* dY, int N, const float* __restrict__ W, int K, float* dX, const float* H,
-                          bool accumulate) {
+// Y = act(X Wk + b) with Wk(k, n) from nn.Linear's [out][in] (TR: CR view, ld = K) or the stacked
+// critics' [in][out] (RC view, ld = N)
+template <bool TR, int N>
+__device__ __attribute__((noinline)) void lin_fwd(const float* X, int K, const float* __restrict__ W, const float* __restrict__ bias, float* Y,
+                        bool relu, float* Ws) {
+  f32x4 acc[2];
+  slab_gemm<TR, N>(X, K, W, TR ? K : N, Ws, acc);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 15, kq = lane >> 4;
-  const int ntile = (K + 15) >> 4;
-  if (wv >= ntile) return;
-  const int nt = (ntile - wv + 3) >> 2;
-  f32x4 acc[4];
 #pragma unroll
-  for (int q = 0; q < 4; q++) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-  for (int n0 = 0; n0 < N; n0 += 4) {
-    const int n = n0 + kq;
-    const float a = n < N ? dY[i * LD + n] : 0.f;
+  for (int q = 0; q < 2; q++) {
+    const int n = (wv + q * NW) * 16 + i;
+    if (n < N) {
+      const float bn = bias[n];
 #pragma unroll
-    for (int q = 0; q < 4; q++)
-      if (q < nt) {
-        const int k = (wv + 4 * q) * 16 + i;
-        const float b = (n < N && k < K) ? wk<TR>(W, k, n, K, N) : 0.f;
-        acc[q] = mfma4(a, b, acc[q]);
+      for (int r = 0; r < 4; r++) {
+        const float v = bn + acc[q][r];
+        Y[(4 * kq + r) * LD + n] = relu ? fmaxf(v, 0.f) : v;
+      }
+    }
+  }
+}
+// dX[16][K] (+)= dY[16][N] Wk^T, masked by relu'(H) (H: the layer input's post-ReLU activation,
+// or null).  Wk as in lin_fwd: the reduction runs over the layer's outputs n, B(n, k) = Wk(k, n)
+// -- nn.Linear [out][in]: W[n * K + k] (RC view, ld = K); critics [in][out]: W[k * N + n] (CR
+// view, ld = N)
+template <bool TR, int K>
+__device__ __attribute__((noinline)) void lin_dgrad(const float* dY, int N, const float* __restrict__ W, float* dX, const float* H, bool accumulate,
+                          float* Ws) {
+  f32x4 acc[2];
+  slab_gemm<!TR, K>(dY, N, W, TR ? K : N, Ws, acc);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const int k = (wv + q * NW) * 16 + i;
+    if (k < K)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = 4 * kq + r;
+        float v = acc[q][r];
+        if (accumulate) v += dX[row * LD + k];
+        if (H && !(H[row * LD + k] > 0.f)) v = 0.f;
+        dX[row * LD + k] = v;
       }
   }
-#pragma unroll
-  for (int q = 0; q < 4; q++)
-    if (q < nt) {
-      const int k = (wv + 4 * q) * 16 + i;
-      if (k < K)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int row = 4 * kq + r;
-          float v = acc[q][r];
-          if (accumulate) v += dX[row * LD + k];
-          if (H && !(H[row * LD + k] > 0.f)) v = 0.f;
-          dX[row * LD + k] = v;
-        }
-    }
 }
 // per-slab weight gradient P(k, n) = sum over the 16 rows of X[r][k] dY[r][n] (P in Wk's storage
 // layout) and the bias gradient Pb[n] = sum_r dY[r][n]
 template <bool TR>
-__device__ void lin_wgrad(const float* X, int K, const float* dY, int N, float* __restrict__ P, float* __restrict__ Pb) {
+__device__ __attribute__((noinline)) void lin_wgrad(const float* X, int K, const float* dY, int N, float* __restrict__ P, float* __restrict__ Pb) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 15, kq = lane >> 4;
   const int tk = (K + 15) >> 4, tn = (N + 15) >> 4, nt = tk * tn;
-  for (int t0 = wv * 4; t0 < nt; t0 += 16) {
+  for (int t0 = wv * 4; t0 < nt; t0 += 4 * NW) {
     f32x4 acc[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -223,8 +249,9 @@ __host__ __device__ constexpr int act_size(int t) {
 __host__ __device__ constexpr int act_off(int t) { return t == 0 ? 0 : act_off(t - 1) + act_size(t - 1); }
 constexpr int ACT_P = act_off(10);
 
-struct Lds {   // 62 KB
+struct Lds {   // 128 KB (a workgroup may hold all 160 KB of a CU's LDS)
   float A[R * LD], Bf[R * LD], C[R * LD];
+  float W[2 * KC * LDW];
   float row[R][NALL + 14], q[R][NALL], tq[R][NALL];
   float red[NTH];
 };
@@ -234,18 +261,18 @@ struct Lds {   // 62 KB
 __device__ void actor_fwd(Lds& L, const TqcArgs& g, const float* __restrict__ eps, int row0, float* hs, float (*aout)[8],
                           float* lpo, float* row_ws) {
   const float* const* P = g.actor;
-  lin_fwd<true>(L.A, OBS, P[0], P[1], HID, L.Bf, true);
+  lin_fwd<true, HID>(L.A, OBS, P[0], P[1], L.Bf, true, L.W);
   __syncthreads();
   if (hs) save_slab(hs, L.Bf, HID);
-  lin_fwd<true>(L.Bf, HID, P[2], P[3], HID, L.C, true);
+  lin_fwd<true, HID>(L.Bf, HID, P[2], P[3], L.C, true, L.W);
   __syncthreads();
   if (hs) save_slab(hs + WS_H, L.C, HID);
-  lin_fwd<true>(L.C, HID, P[4], P[5], HID, L.Bf, true);
+  lin_fwd<true, HID>(L.C, HID, P[4], P[5], L.Bf, true, L.W);
   __syncthreads();
   if (hs) save_slab(hs + 2 * WS_H, L.Bf, HID);
   // heads: mu and log_std into C's first 16 columns (N = 7 each)
-  lin_fwd<true>(L.Bf, HID, P[6], P[7], ACT, L.C, false);
-  lin_fwd<true>(L.Bf, HID, P[8], P[9], ACT, L.C + 8, false);
+  lin_fwd<true, ACT>(L.Bf, HID, P[6], P[7], L.C, false, L.W);
+  lin_fwd<true, ACT>(L.Bf, HID, P[8], P[9], L.C + 8, false, L.W);
   __syncthreads();
   const int t = threadIdx.x;
   if (t < R * ACT) {
@@ -282,16 +309,16 @@ __device__ void critic_fwd(Lds& L, const float* const* P, int c, float* hs, floa
   const float* w1 = P[2] + (size_t)c * HID * HID;
   const float* w2 = P[4] + (size_t)c * HID * HID;
   const float* w3 = P[6] + (size_t)c * HID * NQ;
-  lin_fwd<false>(L.A, NIN, w0, P[1] + c * HID, HID, L.Bf, true);
+  lin_fwd<false, HID>(L.A, NIN, w0, P[1] + c * HID, L.Bf, true, L.W);
   __syncthreads();
   if (hs) save_slab(hs, L.Bf, HID);
-  lin_fwd<false>(L.Bf, HID, w1, P[3] + c * HID, HID, L.C, true);
+  lin_fwd<false, HID>(L.Bf, HID, w1, P[3] + c * HID, L.C, true, L.W);
   __syncthreads();
   if (hs) save_slab(hs + WS_H, L.C, HID);
-  lin_fwd<false>(L.C, HID, w2, P[5] + c * HID, HID, L.Bf, true);
+  lin_fwd<false, HID>(L.C, HID, w2, P[5] + c * HID, L.Bf, true, L.W);
   __syncthreads();
   if (hs) save_slab(hs + 2 * WS_H, L.Bf, HID);
-  lin_fwd<false>(L.Bf, HID, w3, P[7] + c * NQ, NQ, L.C, false);
+  lin_fwd<false, NQ>(L.Bf, HID, w3, P[7] + c * NQ, L.C, false, L.W);
   __syncthreads();
   for (int e = threadIdx.x; e < R * NQ; e += NTH) {
     const int r = e / NQ, j = e - r * NQ;
@@ -311,19 +338,19 @@ __device__ void critic_bwd(Lds& L, const float* const* P, int c, const float* hs
   load_slab(L.A, hs + 2 * WS_H, HID);
   __syncthreads();
   if (pw) lin_wgrad<false>(L.A, HID, L.C, NQ, pw + crit_off(6) + c * HID * NQ, pw + crit_off(7) + c * NQ);
-  lin_dgrad<false>(L.C, NQ, w3, HID, L.Bf, L.A, false);   // dH3 = dq w3^T, relu'(H3)
+  lin_dgrad<false, HID>(L.C, NQ, w3, L.Bf, L.A, false, L.W);   // dH3 = dq w3^T, relu'(H3)
   __syncthreads();
   // layer 2: dY = dH3 (Bf), X = H2 -> A
   load_slab(L.A, hs + WS_H, HID);
   __syncthreads();
   if (pw) lin_wgrad<false>(L.A, HID, L.Bf, HID, pw + crit_off(4) + c * HID * HID, pw + crit_off(5) + c * HID);
-  lin_dgrad<false>(L.Bf, HID, w2, HID, L.C, L.A, false);   // dH2
+  lin_dgrad<false, HID>(L.Bf, HID, w2, L.C, L.A, false, L.W);   // dH2
   __syncthreads();
   // layer 1: dY = dH2 (C), X = H1 -> A
   load_slab(L.A, hs, HID);
   __syncthreads();
   if (pw) lin_wgrad<false>(L.A, HID, L.C, HID, pw + crit_off(2) + c * HID * HID, pw + crit_off(3) + c * HID);
-  lin_dgrad<false>(L.C, HID, w1, HID, L.Bf, L.A, false);   // dH1
+  lin_dgrad<false, HID>(L.C, HID, w1, L.Bf, L.A, false, L.W);   // dH1
   __syncthreads();
   // layer 0: dY = dH1 (Bf), X = [obs, action] -> A
   load_rows(L.A, g.obs, row0, OBS, OBS);
@@ -336,7 +363,7 @@ __device__ void critic_bwd(Lds& L, const float* const* P, int c, const float* hs
   if (pw) lin_wgrad<false>(L.A, NIN, L.Bf, HID, pw + crit_off(0) + c * NIN * HID, pw + crit_off(1) + c * HID);
   __syncthreads();
   if (want_dx) {
-    lin_dgrad<false>(L.Bf, HID, P[0] + (size_t)c * NIN * HID, NIN, L.A, nullptr, false);
+    lin_dgrad<false, NIN>(L.Bf, HID, P[0] + (size_t)c * NIN * HID, L.A, nullptr, false, L.W);
     __syncthreads();
   }
 }
@@ -489,21 +516,21 @@ __global__ void __launch_bounds__(NTH) tqc_actor_kernel(TqcArgs g) {
   // stage d mu in Bf's high columns first)
   for (int e = t; e < R * 8; e += NTH) L.Bf[(e / 8) * LD + 16 + e % 8] = L.C[(e / 8) * LD + e % 8];
   __syncthreads();
-  lin_dgrad<true>(L.Bf + 16, ACT, P[6], HID, L.C, nullptr, false);
+  lin_dgrad<true, HID>(L.Bf + 16, ACT, P[6], L.C, nullptr, false, L.W);
   __syncthreads();
-  lin_dgrad<true>(L.Bf, ACT, P[8], HID, L.C, L.A, true);
+  lin_dgrad<true, HID>(L.Bf, ACT, P[8], L.C, L.A, true, L.W);
   __syncthreads();
   // layer 2: X = H2, dY = dH3 (C)
   load_slab(L.A, ws + WS_ACTOR + WS_H, HID);
   __syncthreads();
   lin_wgrad<true>(L.A, HID, L.C, HID, pw + act_off(4), pw + act_off(5));
-  lin_dgrad<true>(L.C, HID, P[4], HID, L.Bf, L.A, false);
+  lin_dgrad<true, HID>(L.C, HID, P[4], L.Bf, L.A, false, L.W);
   __syncthreads();
   // layer 1: X = H1, dY = dH2 (Bf)
   load_slab(L.A, ws + WS_ACTOR, HID);
   __syncthreads();
   lin_wgrad<true>(L.A, HID, L.Bf, HID, pw + act_off(2), pw + act_off(3));
-  lin_dgrad<true>(L.Bf, HID, P[2], HID, L.C, L.A, false);
+  lin_dgrad<true, HID>(L.Bf, HID, P[2], L.C, L.A, false, L.W);
   __syncthreads();
   // layer 0: X = obs, dY = dH1 (C)
   load_rows(L.A, g.obs, row0, OBS, OBS);
