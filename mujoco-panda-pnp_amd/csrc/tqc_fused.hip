@@ -25,6 +25,8 @@
 // [256, 256, 256] ReLU MLPs, 2 critics x 25 quantiles, batch a multiple of 16.
 #include "pnp_internal.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int R = 16;              // rows per slab (one MFMA tile of rows)
@@ -32,8 +34,12 @@ constexpr int NW = 8;              // waves per workgroup (two per SIMD)
 constexpr int NTH = 64 * NW;
 constexpr int KC = 32;             // reduction rows per staged weight chunk
 constexpr int OBS = 25, ACT = 7, HID = 256, NC = 2, NQ = 25, NIN = OBS + ACT, NALL = NC * NQ;
-constexpr int LD = HID + 4;        // LDS row stride (floats)
-constexpr int LDW = HID + 4;       // staged weight chunk row stride
+constexpr int LD = HID + 4;        // LDS row stride of the slab buffers (floats; = 4 mod 64: the A
+                                   // operand's b128 reads and the row-permuted wgrad reads are
+                                   // conflict-free)
+constexpr int LDT = KC + 4;        // staged weight chunk, [column][reduction row] layout (CR)
+constexpr int LDW = HID + 4;       // staged weight chunk, [reduction row][column] layout (RC)
+constexpr int WCH = HID * LDT > KC * LDW ? HID * LDT : KC * LDW;   // one chunk buffer (floats)
 constexpr float LOG_STD_MIN = -20.0f, LOG_STD_MAX = 2.0f, SQUASH_EPS = 1e-6f;
 constexpr float HALF_LOG_2PI = 0.91893853320467274178f;
 
@@ -51,73 +57,112 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 }
 
 // ---- slab matrix products (X, Y, dY, dX: LDS [16][LD]; W: global, staged through LDS)
-// acc = X[16][K] B[K][N]: B(r, c) (r the reduction index, c the output column) is the weight
-// element W[c * ld + r] (CR: contiguous in r) or W[r * ld + c] (RC).  The weight streams through
-// two LDS chunk buffers of KC reduction rows (Ws: 2 x KC x LDW floats): every thread fetches its
-// share of chunk ch + 1 into registers (coalesced global loads) while the waves run chunk ch's
-// MFMAs from LDS, then stores it and the workgroup syncs -- the MFMA chains never wait on a global
-// load.  Wave w owns the output tiles w and w + NW (16 columns each; every MFMA runs with the whole
-// wave, per-lane predicates only select operands).  Every thread of the workgroup must call it.
-template <bool CR>
-__device__ __forceinline__ float bget(const float* __restrict__ W, int ld, int r, int c) {
-  return CR ? W[(size_t)c * ld + r] : W[(size_t)r * ld + c];
-}
-template <bool CR, int N>
-__device__ void slab_gemm(const float* X, int K, const float* __restrict__ W, int ld, float* Ws, f32x4 acc[2]) {
+// acc = X[16][GK] B[GK][GN]: B(r, c) (r the reduction index, c the output column) is the weight
+// element W[c * GK + r] (CR: contiguous in r) or W[r * GN + c] (RC).  The weight streams through
+// two LDS chunk buffers of KC reduction rows, stored [c][r] (stride LDT) for CR and [r][c] (stride
+// LDW) for RC so that the global fetches are float4 and coalesced: every thread fetches its share
+// of chunk ch + 1 into registers while the waves run chunk ch's MFMAs from LDS, then stores it and
+// the workgroup syncs -- the MFMA chains never wait on a global load.  Wave w owns the output
+// tiles w and w + NW (16 columns each; every MFMA runs with the whole wave).
+// The reduction index is permuted within each block of 16: at step s lane (kq = lane / 16, i)
+// supplies A[i][16 kb + 4 kq + s] and B[16 kb + 4 kq + s][c] -- one b128 LDS read of A per four
+// MFMAs (and of B in the CR layout); the sum is the same, the fp32 accumulation order differs.
+// Reduction rows past GK read zeros from the staged chunk and are masked in A; columns past GN
+// compute garbage in output columns nobody keeps.  Every thread of the workgroup must call it.
+template <bool CR, int GK, int GN>
+__device__ void slab_gemm(const float* X, const float* __restrict__ W, float* Ws, f32x4 acc[2]) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, i = lane & 15, kq = lane >> 4;
-  constexpr int NTILE = (N + 15) / 16, NELEM = KC * N, PER = (NELEM + NTH - 1) / NTH;
+  constexpr int NTILE = (GN + 15) / 16, NCH = (GK + KC - 1) / KC;
+  constexpr int LDG = CR ? GK : GN;                          // global row stride
+  constexpr bool VEC = LDG % 4 == 0;
+  constexpr int NUNIT = VEC ? KC * GN / 4 : KC * GN;          // float4 (or float) units per chunk
+  constexpr int PER = (NUNIT + NTH - 1) / NTH;
+  static_assert(NTILE <= 2 * NW && (CR ? GN * LDT : KC * LDW) <= WCH, "slab_gemm shape");
   acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
   acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nch = (K + KC - 1) / KC;
-  float pre[PER];
+  using U = typename std::conditional<VEC, f32x4, float>::type;
+  U pre[PER];
+  // unit u of chunk ch: its global address, its LDS slot, whether it lies inside the matrix
+  auto unit = [&](int u, int ch, const float*& src, int& dst, bool& in) {
+    if (VEC) {
+      if (CR) {
+        const int c = u / (KC / 4), j = u % (KC / 4), r = ch * KC + 4 * j;
+        src = W + (size_t)c * LDG + r; dst = c * LDT + 4 * j; in = r < GK;
+      } else {
+        const int rr = u / (GN / 4), j = u % (GN / 4), r = ch * KC + rr;
+        src = W + (size_t)r * LDG + 4 * j; dst = rr * LDW + 4 * j; in = r < GK;
+      }
+    } else {
+      if (CR) {
+        const int c = u / KC, rr = u % KC, r = ch * KC + rr;
+        src = W + (size_t)c * LDG + r; dst = c * LDT + rr; in = r < GK;
+      } else {
+        const int rr = u / GN, c = u % GN, r = ch * KC + rr;
+        src = W + (size_t)r * LDG + c; dst = rr * LDW + c; in = r < GK;
+      }
+    }
+  };
   auto fetch = [&](int ch) {
 #pragma unroll
     for (int j = 0; j < PER; j++) {
-      const int f = t + j * NTH;
-      const int rr = CR ? f % KC : f / N, c = CR ? f / KC : f % N, r = ch * KC + rr;
-      pre[j] = (f < NELEM && r < K) ? bget<CR>(W, ld, r, c) : 0.f;
+      const int u = t + j * NTH;
+      const float* src; int dst; bool in;
+      unit(u, ch, src, dst, in);
+      pre[j] = U{};
+      if (u < NUNIT && in) pre[j] = *reinterpret_cast<const U*>(src);
     }
   };
-  auto put = [&](int buf) {
-    float* D = Ws + buf * KC * LDW;
+  auto put = [&](int buf, int ch) {
+    float* D = Ws + buf * WCH;
 #pragma unroll
     for (int j = 0; j < PER; j++) {
-      const int f = t + j * NTH;
-      const int rr = CR ? f % KC : f / N, c = CR ? f / KC : f % N;
-      if (f < NELEM) D[rr * LDW + c] = pre[j];
+      const int u = t + j * NTH;
+      const float* src; int dst; bool in;
+      unit(u, ch, src, dst, in);
+      if (u < NUNIT) *reinterpret_cast<U*>(D + dst) = pre[j];
     }
   };
   fetch(0);
-  put(0);
+  put(0, 0);
   __syncthreads();
-  for (int ch = 0; ch < nch; ch++) {
-    if (ch + 1 < nch) fetch(ch + 1);
-    const float* D = Ws + (ch & 1) * KC * LDW;
+  for (int ch = 0; ch < NCH; ch++) {
+    if (ch + 1 < NCH) fetch(ch + 1);
+    const float* D = Ws + (ch & 1) * WCH;
 #pragma unroll
-    for (int k4 = 0; k4 < KC; k4 += 4) {
-      const int rr = k4 + kq, r = ch * KC + rr;
-      const float a = r < K ? X[i * LD + r] : 0.f;
+    for (int kb = 0; kb < KC; kb += 16) {
+      const int k0 = kb + 4 * kq, k = ch * KC + k0;
+      f32x4 a = *reinterpret_cast<const f32x4*>(X + i * LD + k);
+      if (GK % KC != 0)
+#pragma unroll
+        for (int s = 0; s < 4; s++) a[s] = k + s < GK ? a[s] : 0.f;
 #pragma unroll
       for (int q = 0; q < 2; q++) {
         const int tile = wv + q * NW;
         if (tile < NTILE) {
           const int c = tile * 16 + i;
-          const float b = c < N ? D[rr * LDW + c] : 0.f;
-          acc[q] = mfma4(a, b, acc[q]);
+          f32x4 b;
+          if (CR) {
+            b = *reinterpret_cast<const f32x4*>(D + c * LDT + k0);
+          } else {
+#pragma unroll
+            for (int s = 0; s < 4; s++) b[s] = D[(k0 + s) * LDW + c];
+          }
+#pragma unroll
+          for (int s = 0; s < 4; s++) acc[q] = mfma4(a[s], b[s], acc[q]);
         }
       }
     }
-    if (ch + 1 < nch) put((ch + 1) & 1);
+    if (ch + 1 < NCH) put((ch + 1) & 1, ch + 1);
     __syncthreads();
   }
 }
-// Y = act(X Wk + b) with Wk(k, n) from nn.Linear's [out][in] (TR: CR view, ld = K) or the stacked
-// critics' [in][out] (RC view, ld = N)
-template <bool TR, int N>
-__device__ __attribute__((noinline)) void lin_fwd(const float* X, int K, const float* __restrict__ W, const float* __restrict__ bias, float* Y,
-                        bool relu, float* Ws) {
+// Y = act(X Wk + b) with Wk(k, n) from nn.Linear's [out][in] (TR: CR view) or the stacked critics'
+// [in][out] (RC view)
+template <bool TR, int K, int N>
+__device__ __attribute__((noinline)) void lin_fwd(const float* X, const float* __restrict__ W, const float* __restrict__ bias,
+                                                  float* Y, bool relu, float* Ws) {
   f32x4 acc[2];
-  slab_gemm<TR, N>(X, K, W, TR ? K : N, Ws, acc);
+  slab_gemm<TR, K, N>(X, W, Ws, acc);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 15, kq = lane >> 4;
 #pragma unroll
   for (int q = 0; q < 2; q++) {
@@ -134,13 +179,12 @@ __device__ __attribute__((noinline)) void lin_fwd(const float* X, int K, const f
 }
 // dX[16][K] (+)= dY[16][N] Wk^T, masked by relu'(H) (H: the layer input's post-ReLU activation,
 // or null).  Wk as in lin_fwd: the reduction runs over the layer's outputs n, B(n, k) = Wk(k, n)
-// -- nn.Linear [out][in]: W[n * K + k] (RC view, ld = K); critics [in][out]: W[k * N + n] (CR
-// view, ld = N)
-template <bool TR, int K>
-__device__ __attribute__((noinline)) void lin_dgrad(const float* dY, int N, const float* __restrict__ W, float* dX, const float* H, bool accumulate,
-                          float* Ws) {
+// -- nn.Linear [out][in]: W[n * K + k] (RC view); critics [in][out]: W[k * N + n] (CR view)
+template <bool TR, int N, int K>
+__device__ __attribute__((noinline)) void lin_dgrad(const float* dY, const float* __restrict__ W, float* dX, const float* H,
+                                                    bool accumulate, float* Ws) {
   f32x4 acc[2];
-  slab_gemm<!TR, K>(dY, N, W, TR ? K : N, Ws, acc);
+  slab_gemm<!TR, N, K>(dY, W, Ws, acc);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 15, kq = lane >> 4;
 #pragma unroll
   for (int q = 0; q < 2; q++) {
@@ -157,18 +201,19 @@ __device__ __attribute__((noinline)) void lin_dgrad(const float* dY, int N, cons
   }
 }
 // per-slab weight gradient P(k, n) = sum over the 16 rows of X[r][k] dY[r][n] (P in Wk's storage
-// layout) and the bias gradient Pb[n] = sum_r dY[r][n]
-template <bool TR>
-__device__ __attribute__((noinline)) void lin_wgrad(const float* X, int K, const float* dY, int N, float* __restrict__ P, float* __restrict__ Pb) {
+// layout) and the bias gradient Pb[n] = sum_r dY[r][n].  Rows permuted as in slab_gemm (step s,
+// lane kq: row 4 kq + s): the b32 reads of X and dY are then conflict-free with LD = 4 mod 64.
+template <bool TR, int K, int N>
+__device__ __attribute__((noinline)) void lin_wgrad(const float* X, const float* dY, float* __restrict__ P, float* __restrict__ Pb) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 15, kq = lane >> 4;
-  const int tk = (K + 15) >> 4, tn = (N + 15) >> 4, nt = tk * tn;
+  constexpr int tk = (K + 15) >> 4, tn = (N + 15) >> 4, nt = tk * tn;
   for (int t0 = wv * 4; t0 < nt; t0 += 4 * NW) {
     f32x4 acc[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int r0 = 0; r0 < R; r0 += 4) {
-      const int r = r0 + kq;
+    for (int s = 0; s < 4; s++) {
+      const int r = 4 * kq + s;
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int t = t0 + q;
@@ -201,23 +246,28 @@ __device__ __attribute__((noinline)) void lin_wgrad(const float* X, int K, const
   }
 }
 
-// global <-> LDS slab copies
-__device__ void load_rows(float* D, const float* __restrict__ src, int row0, int cols, int ld_src, int col0 = 0) {
-  for (int e = threadIdx.x; e < R * cols; e += NTH) {
-    const int r = e / cols, c = e - r * cols;
+// global <-> LDS slab copies (save/load: float4 both sides)
+template <int COLS>
+__device__ void load_rows(float* D, const float* __restrict__ src, int row0, int ld_src, int col0 = 0) {
+  for (int e = threadIdx.x; e < R * COLS; e += NTH) {
+    const int r = e / COLS, c = e - r * COLS;
     D[r * LD + col0 + c] = src[(size_t)(row0 + r) * ld_src + c];
   }
 }
-__device__ void save_slab(float* __restrict__ dst, const float* S, int cols) {
-  for (int e = threadIdx.x; e < R * cols; e += NTH) {
-    const int r = e / cols, c = e - r * cols;
-    dst[e] = S[r * LD + c];
+template <int COLS>
+__device__ void save_slab(float* __restrict__ dst, const float* S) {
+  static_assert(COLS % 4 == 0, "save_slab");
+  for (int e = threadIdx.x; e < R * COLS / 4; e += NTH) {
+    const int r = e / (COLS / 4), c = 4 * (e - r * (COLS / 4));
+    *reinterpret_cast<f32x4*>(dst + 4 * e) = *reinterpret_cast<const f32x4*>(S + r * LD + c);
   }
 }
-__device__ void load_slab(float* D, const float* __restrict__ src, int cols) {
-  for (int e = threadIdx.x; e < R * cols; e += NTH) {
-    const int r = e / cols, c = e - r * cols;
-    D[r * LD + c] = src[e];
+template <int COLS>
+__device__ void load_slab(float* D, const float* __restrict__ src) {
+  static_assert(COLS % 4 == 0, "load_slab");
+  for (int e = threadIdx.x; e < R * COLS / 4; e += NTH) {
+    const int r = e / (COLS / 4), c = 4 * (e - r * (COLS / 4));
+    *reinterpret_cast<f32x4*>(D + r * LD + c) = *reinterpret_cast<const f32x4*>(src + 4 * e);
   }
 }
 
@@ -249,9 +299,9 @@ __host__ __device__ constexpr int act_size(int t) {
 __host__ __device__ constexpr int act_off(int t) { return t == 0 ? 0 : act_off(t - 1) + act_size(t - 1); }
 constexpr int ACT_P = act_off(10);
 
-struct Lds {   // 128 KB (a workgroup may hold all 160 KB of a CU's LDS)
+struct alignas(16) Lds {   // 136 KB (a workgroup may hold all 160 KB of a CU's LDS)
   float A[R * LD], Bf[R * LD], C[R * LD];
-  float W[2 * KC * LDW];
+  float W[2 * WCH];
   float row[R][NALL + 14], q[R][NALL], tq[R][NALL];
   float red[NTH];
 };
@@ -261,18 +311,18 @@ struct Lds {   // 128 KB (a workgroup may hold all 160 KB of a CU's LDS)
 __device__ void actor_fwd(Lds& L, const TqcArgs& g, const float* __restrict__ eps, int row0, float* hs, float (*aout)[8],
                           float* lpo, float* row_ws) {
   const float* const* P = g.actor;
-  lin_fwd<true, HID>(L.A, OBS, P[0], P[1], L.Bf, true, L.W);
+  lin_fwd<true, OBS, HID>(L.A, P[0], P[1], L.Bf, true, L.W);
   __syncthreads();
-  if (hs) save_slab(hs, L.Bf, HID);
-  lin_fwd<true, HID>(L.Bf, HID, P[2], P[3], L.C, true, L.W);
+  if (hs) save_slab<HID>(hs, L.Bf);
+  lin_fwd<true, HID, HID>(L.Bf, P[2], P[3], L.C, true, L.W);
   __syncthreads();
-  if (hs) save_slab(hs + WS_H, L.C, HID);
-  lin_fwd<true, HID>(L.C, HID, P[4], P[5], L.Bf, true, L.W);
+  if (hs) save_slab<HID>(hs + WS_H, L.C);
+  lin_fwd<true, HID, HID>(L.C, P[4], P[5], L.Bf, true, L.W);
   __syncthreads();
-  if (hs) save_slab(hs + 2 * WS_H, L.Bf, HID);
+  if (hs) save_slab<HID>(hs + 2 * WS_H, L.Bf);
   // heads: mu and log_std into C's first 16 columns (N = 7 each)
-  lin_fwd<true, ACT>(L.Bf, HID, P[6], P[7], L.C, false, L.W);
-  lin_fwd<true, ACT>(L.Bf, HID, P[8], P[9], L.C + 8, false, L.W);
+  lin_fwd<true, HID, ACT>(L.Bf, P[6], P[7], L.C, false, L.W);
+  lin_fwd<true, HID, ACT>(L.Bf, P[8], P[9], L.C + 8, false, L.W);
   __syncthreads();
   const int t = threadIdx.x;
   if (t < R * ACT) {
@@ -309,16 +359,16 @@ __device__ void critic_fwd(Lds& L, const float* const* P, int c, float* hs, floa
   const float* w1 = P[2] + (size_t)c * HID * HID;
   const float* w2 = P[4] + (size_t)c * HID * HID;
   const float* w3 = P[6] + (size_t)c * HID * NQ;
-  lin_fwd<false, HID>(L.A, NIN, w0, P[1] + c * HID, L.Bf, true, L.W);
+  lin_fwd<false, NIN, HID>(L.A, w0, P[1] + c * HID, L.Bf, true, L.W);
   __syncthreads();
-  if (hs) save_slab(hs, L.Bf, HID);
-  lin_fwd<false, HID>(L.Bf, HID, w1, P[3] + c * HID, L.C, true, L.W);
+  if (hs) save_slab<HID>(hs, L.Bf);
+  lin_fwd<false, HID, HID>(L.Bf, w1, P[3] + c * HID, L.C, true, L.W);
   __syncthreads();
-  if (hs) save_slab(hs + WS_H, L.C, HID);
-  lin_fwd<false, HID>(L.C, HID, w2, P[5] + c * HID, L.Bf, true, L.W);
+  if (hs) save_slab<HID>(hs + WS_H, L.C);
+  lin_fwd<false, HID, HID>(L.C, w2, P[5] + c * HID, L.Bf, true, L.W);
   __syncthreads();
-  if (hs) save_slab(hs + 2 * WS_H, L.Bf, HID);
-  lin_fwd<false, NQ>(L.Bf, HID, w3, P[7] + c * NQ, L.C, false, L.W);
+  if (hs) save_slab<HID>(hs + 2 * WS_H, L.Bf);
+  lin_fwd<false, HID, NQ>(L.Bf, w3, P[7] + c * NQ, L.C, false, L.W);
   __syncthreads();
   for (int e = threadIdx.x; e < R * NQ; e += NTH) {
     const int r = e / NQ, j = e - r * NQ;
@@ -335,35 +385,35 @@ __device__ void critic_bwd(Lds& L, const float* const* P, int c, const float* hs
   const float* w2 = P[4] + (size_t)c * HID * HID;
   const float* w3 = P[6] + (size_t)c * HID * NQ;
   // layer 3 (linear): dq in C; H3 -> A
-  load_slab(L.A, hs + 2 * WS_H, HID);
+  load_slab<HID>(L.A, hs + 2 * WS_H);
   __syncthreads();
-  if (pw) lin_wgrad<false>(L.A, HID, L.C, NQ, pw + crit_off(6) + c * HID * NQ, pw + crit_off(7) + c * NQ);
-  lin_dgrad<false, HID>(L.C, NQ, w3, L.Bf, L.A, false, L.W);   // dH3 = dq w3^T, relu'(H3)
+  if (pw) lin_wgrad<false, HID, NQ>(L.A, L.C, pw + crit_off(6) + c * HID * NQ, pw + crit_off(7) + c * NQ);
+  lin_dgrad<false, NQ, HID>(L.C, w3, L.Bf, L.A, false, L.W);   // dH3 = dq w3^T, relu'(H3)
   __syncthreads();
   // layer 2: dY = dH3 (Bf), X = H2 -> A
-  load_slab(L.A, hs + WS_H, HID);
+  load_slab<HID>(L.A, hs + WS_H);
   __syncthreads();
-  if (pw) lin_wgrad<false>(L.A, HID, L.Bf, HID, pw + crit_off(4) + c * HID * HID, pw + crit_off(5) + c * HID);
-  lin_dgrad<false, HID>(L.Bf, HID, w2, L.C, L.A, false, L.W);   // dH2
+  if (pw) lin_wgrad<false, HID, HID>(L.A, L.Bf, pw + crit_off(4) + c * HID * HID, pw + crit_off(5) + c * HID);
+  lin_dgrad<false, HID, HID>(L.Bf, w2, L.C, L.A, false, L.W);   // dH2
   __syncthreads();
   // layer 1: dY = dH2 (C), X = H1 -> A
-  load_slab(L.A, hs, HID);
+  load_slab<HID>(L.A, hs);
   __syncthreads();
-  if (pw) lin_wgrad<false>(L.A, HID, L.C, HID, pw + crit_off(2) + c * HID * HID, pw + crit_off(3) + c * HID);
-  lin_dgrad<false, HID>(L.C, HID, w1, L.Bf, L.A, false, L.W);   // dH1
+  if (pw) lin_wgrad<false, HID, HID>(L.A, L.C, pw + crit_off(2) + c * HID * HID, pw + crit_off(3) + c * HID);
+  lin_dgrad<false, HID, HID>(L.C, w1, L.Bf, L.A, false, L.W);   // dH1
   __syncthreads();
   // layer 0: dY = dH1 (Bf), X = [obs, action] -> A
-  load_rows(L.A, g.obs, row0, OBS, OBS);
+  load_rows<OBS>(L.A, g.obs, row0, OBS);
   if (x_is_pi) {
     for (int e = threadIdx.x; e < R * ACT; e += NTH) L.A[(e / ACT) * LD + OBS + e % ACT] = api[e / ACT][e % ACT];
   } else {
-    load_rows(L.A, g.act, row0, ACT, ACT, OBS);
+    load_rows<ACT>(L.A, g.act, row0, ACT, OBS);
   }
   __syncthreads();
-  if (pw) lin_wgrad<false>(L.A, NIN, L.Bf, HID, pw + crit_off(0) + c * NIN * HID, pw + crit_off(1) + c * HID);
+  if (pw) lin_wgrad<false, NIN, HID>(L.A, L.Bf, pw + crit_off(0) + c * NIN * HID, pw + crit_off(1) + c * HID);
   __syncthreads();
   if (want_dx) {
-    lin_dgrad<false, NIN>(L.Bf, HID, P[0] + (size_t)c * NIN * HID, L.A, nullptr, false, L.W);
+    lin_dgrad<false, HID, NIN>(L.Bf, P[0] + (size_t)c * NIN * HID, L.A, nullptr, false, L.W);
     __syncthreads();
   }
 }
@@ -389,16 +439,16 @@ __global__ void __launch_bounds__(NTH) tqc_critic_kernel(TqcArgs g) {
   const float ent_coef = expf(g.log_ent_coef[0]);
   // actor(obs): a_pi, log_prob (kept for the actor step)
   __shared__ float api[R][8], lp[R], na[R][8], nlp[R];
-  load_rows(L.A, g.obs, row0, OBS, OBS);
+  load_rows<OBS>(L.A, g.obs, row0, OBS);
   __syncthreads();
   actor_fwd(L, g, g.eps_pi, row0, ws + WS_ACTOR, api, lp, ws + WS_ROW);
   // actor(next_obs): next action and its log_prob
-  load_rows(L.A, g.nobs, row0, OBS, OBS);
+  load_rows<OBS>(L.A, g.nobs, row0, OBS);
   __syncthreads();
   actor_fwd(L, g, g.eps_next, row0, nullptr, na, nlp, nullptr);
   // target critics on (next_obs, next_action)
   for (int c = 0; c < NC; c++) {
-    load_rows(L.A, g.nobs, row0, OBS, OBS);
+    load_rows<OBS>(L.A, g.nobs, row0, OBS);
     for (int e = t; e < R * ACT; e += NTH) L.A[(e / ACT) * LD + OBS + e % ACT] = na[e / ACT][e % ACT];
     __syncthreads();
     critic_fwd(L, g.target, c, nullptr, &L.q[0][0]);
@@ -426,8 +476,8 @@ __global__ void __launch_bounds__(NTH) tqc_critic_kernel(TqcArgs g) {
   __syncthreads();
   // critics on (obs, action), activations saved
   for (int c = 0; c < NC; c++) {
-    load_rows(L.A, g.obs, row0, OBS, OBS);
-    load_rows(L.A, g.act, row0, ACT, ACT, OBS);
+    load_rows<OBS>(L.A, g.obs, row0, OBS);
+    load_rows<ACT>(L.A, g.act, row0, ACT, OBS);
     __syncthreads();
     critic_fwd(L, g.critic, c, ws + WS_CRIT + c * 3 * WS_H, &L.q[0][0]);
   }
@@ -474,7 +524,7 @@ __global__ void __launch_bounds__(NTH) tqc_actor_kernel(TqcArgs g) {
   // critics (updated) on (obs, a_pi): q_pi, then d loss / d a_pi through both critics
   float qsum = 0.f;
   for (int c = 0; c < NC; c++) {
-    load_rows(L.A, g.obs, row0, OBS, OBS);
+    load_rows<OBS>(L.A, g.obs, row0, OBS);
     for (int e = t; e < R * ACT; e += NTH) L.A[(e / ACT) * LD + OBS + e % ACT] = api[e / ACT][e % ACT];
     __syncthreads();
     float* hs = g.ws + (size_t)slab * WS_SLAB + WS_CRIT + c * 3 * WS_H;
@@ -506,36 +556,36 @@ __global__ void __launch_bounds__(NTH) tqc_actor_kernel(TqcArgs g) {
   __syncthreads();
   const float* const* P = g.actor;
   // heads: X = H3 (A), dY = d mu / d log_std (C columns 0.. / 8..)
-  load_slab(L.A, ws + WS_ACTOR + 2 * WS_H, HID);
+  load_slab<HID>(L.A, ws + WS_ACTOR + 2 * WS_H);
   for (int e = t; e < R * 8; e += NTH) { L.Bf[(e / 8) * LD + e % 8] = L.C[(e / 8) * LD + 8 + e % 8]; }
   __syncthreads();
-  lin_wgrad<true>(L.A, HID, L.C, ACT, pw + act_off(6), pw + act_off(7));
-  lin_wgrad<true>(L.A, HID, L.Bf, ACT, pw + act_off(8), pw + act_off(9));
+  lin_wgrad<true, HID, ACT>(L.A, L.C, pw + act_off(6), pw + act_off(7));
+  lin_wgrad<true, HID, ACT>(L.A, L.Bf, pw + act_off(8), pw + act_off(9));
   __syncthreads();
   // d H3 = dmu Wmu + dls Wls, relu'(H3): into the free buffer (C's columns > 15 are unused:
   // stage d mu in Bf's high columns first)
   for (int e = t; e < R * 8; e += NTH) L.Bf[(e / 8) * LD + 16 + e % 8] = L.C[(e / 8) * LD + e % 8];
   __syncthreads();
-  lin_dgrad<true, HID>(L.Bf + 16, ACT, P[6], L.C, nullptr, false, L.W);
+  lin_dgrad<true, ACT, HID>(L.Bf + 16, P[6], L.C, nullptr, false, L.W);
   __syncthreads();
-  lin_dgrad<true, HID>(L.Bf, ACT, P[8], L.C, L.A, true, L.W);
+  lin_dgrad<true, ACT, HID>(L.Bf, P[8], L.C, L.A, true, L.W);
   __syncthreads();
   // layer 2: X = H2, dY = dH3 (C)
-  load_slab(L.A, ws + WS_ACTOR + WS_H, HID);
+  load_slab<HID>(L.A, ws + WS_ACTOR + WS_H);
   __syncthreads();
-  lin_wgrad<true>(L.A, HID, L.C, HID, pw + act_off(4), pw + act_off(5));
-  lin_dgrad<true, HID>(L.C, HID, P[4], L.Bf, L.A, false, L.W);
+  lin_wgrad<true, HID, HID>(L.A, L.C, pw + act_off(4), pw + act_off(5));
+  lin_dgrad<true, HID, HID>(L.C, P[4], L.Bf, L.A, false, L.W);
   __syncthreads();
   // layer 1: X = H1, dY = dH2 (Bf)
-  load_slab(L.A, ws + WS_ACTOR, HID);
+  load_slab<HID>(L.A, ws + WS_ACTOR);
   __syncthreads();
-  lin_wgrad<true>(L.A, HID, L.Bf, HID, pw + act_off(2), pw + act_off(3));
-  lin_dgrad<true, HID>(L.Bf, HID, P[2], L.C, L.A, false, L.W);
+  lin_wgrad<true, HID, HID>(L.A, L.Bf, pw + act_off(2), pw + act_off(3));
+  lin_dgrad<true, HID, HID>(L.Bf, P[2], L.C, L.A, false, L.W);
   __syncthreads();
   // layer 0: X = obs, dY = dH1 (C)
-  load_rows(L.A, g.obs, row0, OBS, OBS);
+  load_rows<OBS>(L.A, g.obs, row0, OBS);
   __syncthreads();
-  lin_wgrad<true>(L.A, OBS, L.C, HID, pw + act_off(0), pw + act_off(1));
+  lin_wgrad<true, OBS, HID>(L.A, L.C, pw + act_off(0), pw + act_off(1));
 }
 
 // ---- reduction of the per-slab gradients + Adam (torch.optim.Adam fused / capturable semantics)
