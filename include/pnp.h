@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 11
+#define PNP_ABI_VERSION 12
 
 #define PNP_OK 0
 #define PNP_ERR_ARG -1
@@ -394,9 +394,10 @@ int32_t pnp_env_queue_status(int32_t* out5);
 
 /* ------------------------------------------------------------------ TQC learner (C5) */
 /* One TQC gradient step (sb3-contrib tqc.py train(): entropy coefficient, critics against the
- * truncated target quantiles, actor, Polyak; the reference's learner, scripts/train.py:74-93) in
- * four launches on the matrix cores (csrc/tqc_fused.hip): per 16-row slab of the batch a workgroup
- * runs the networks' forward and backward passes, the Adam kernels reduce the slabs' gradients.
+ * truncated target quantiles, actor, Polyak; the reference's learner, scripts/train.py:74-93) on
+ * the matrix cores (csrc/tqc_fused.hip): per 16-row slab of the batch and per network a workgroup
+ * runs the forward and backward chains; the weight gradients are whole-batch tile GEMMs with Adam
+ * applied in place (no per-slab partial gradients).
  * Parameters in PyTorch's layouts -- actor: latent Linear 25->256->256->256 (weight [out][in],
  * bias [out]) W0 b0 W1 b1 W2 b2, heads mu / log_std 256->7 Wmu bmu Wls bls; critics (and their
  * target copies): n_critics stacked MLPs 32->256->256->256->25, weight [n_critics][in][out], bias
@@ -423,6 +424,27 @@ typedef struct pnp_tqc_batch {
   const float* obs; const float* act; const float* next_obs; const float* done; const float* reward;
   const float* eps_pi; const float* eps_next;
 } pnp_tqc_batch;
+/* The replay buffer and the observation normaliser a batch is drawn from: sb3 DictReplayBuffer
+ * (optimize_memory_usage=False) rows [rows][n_envs][dim] of obs / next_obs (the dict keys
+ * flattened in sorted key order), actions, rewards, dones; `upper` the device scalar count of
+ * filled rows; VecNormalize's per-key running mean / var (fp64, key_dim[k] each, same key order),
+ * its clip_obs and epsilon. */
+typedef struct pnp_tqc_replay {
+  const float* obs; const float* next_obs; const float* actions; const float* rewards; const float* dones;
+  const float* upper;
+  int32_t rows, n_envs, obs_dim, act_dim, n_keys;
+  int32_t key_dim[4];
+  const double* mean[4]; const double* var[4];
+  double clip_obs, norm_eps;
+} pnp_tqc_replay;
+/* DictReplayBuffer.sample + VecNormalize.normalize (pnp_amd/tqc.py TQC._sample_norm) for one
+ * gradient step in one launch: u [2*batch] U[0, 1) draws (the caller's generator, sb3's order) ->
+ * row = min(trunc(u[b] * upper), rows - 1), env = min(trunc(u[batch + b] * n_envs), n_envs - 1);
+ * obs / next_obs normalised in fp64, clipped and rounded to fp32 ([batch*obs_dim]), act
+ * [batch*act_dim], done / reward [batch] -- bit-identical to the PyTorch expressions.  Device
+ * pointers, stream-ordered, capturable. */
+int32_t pnp_tqc_sample(const pnp_tqc_replay* rb, const float* u, int32_t batch, float* obs, float* act, float* next_obs,
+                       float* done, float* reward, void* stream);
 int64_t pnp_tqc_workspace_floats(const pnp_tqc_desc* d);
 /* flat gradient sizes (actor, critics) of grads_out below */
 int32_t pnp_tqc_param_counts(int32_t* actor_params, int32_t* critic_params);

@@ -1,22 +1,31 @@
 // tqc_fused.hip — one TQC gradient step (sb3-contrib tqc.py train(), the reference's learner in
-// scripts/train.py:74-93) as four launches on the matrix cores, for C5 at train.py's update ratio.
+// scripts/train.py:74-93) on the matrix cores, for C5 at train.py's update ratio.
 //
 // The PyTorch restatement (pnp_amd/tqc.py TQC._update) replays ~400 kernels per gradient step from
 // a HIP graph: 512-row GEMMs of 256-wide layers, each a few microseconds, plus the elementwise and
-// reduction kernels between them -- launch and latency bound (1.9 ms per step).  Here the batch is
-// cut into slabs of 16 rows, one workgroup (4 waves) per slab, and each workgroup runs a whole
-// network chain for its rows with v_mfma_f32_16x16x4_f32 tiles (fp32 in, fp32 accumulate: the
-// precision of the PyTorch step); the per-slab weight gradients are reduced in a fixed order by
-// the Adam kernels (deterministic):
-//   K1 tqc_critic_kernel   per slab: actor(obs) -> a_pi, log_prob (kept for K2); actor(next_obs);
-//                          target critics(next_obs, next_action) -> the 50 quantiles sorted, the top
-//                          4 dropped, the TD target; critics(obs, action) and the quantile Huber
-//                          loss; its backward pass through both critics -> per-slab gradients
-//   K2 tqc_adam_kernel     critic Adam (+ Polyak update of the target critics), entropy Adam
-//   K3 tqc_actor_kernel    per slab: critics(obs, a_pi) with the updated critics -> actor loss;
-//                          backward through the critics (input gradient), the squashed Gaussian and
-//                          the actor -> per-slab actor gradients
-//   K4 tqc_adam_kernel     actor Adam
+// reduction kernels between them -- launch and latency bound (1.9 ms per step).  Here the step is
+// two kinds of kernel, all fp32 in / fp32 accumulate on v_mfma_f32_16x16x4_f32 (the precision of
+// the PyTorch step):
+//   * chain kernels: the batch cut into slabs of 16 rows; one workgroup (8 waves) runs one network
+//     chain (forward, or backward to the layer inputs) for one slab and one network, the weights
+//     streamed through LDS, the activations and the backward pass's layer-output gradients stored
+//     [B][256] in the workspace;
+//   * weight-gradient kernels: dW = X^T dY over the whole batch, one workgroup per 32 x 32 tile of
+//     a parameter tensor (the bias as the ones-row of X), the four waves' partial sums added in a
+//     fixed order (deterministic) and Adam applied to the tile in place -- no per-slab partial
+//     gradients go through HBM.
+//   K1 tqc_fwd_kernel        (slab, 5 jobs) job 0: actor(obs) -> a_pi, log_prob, activations;
+//                            job 1 + c: critic c on (obs, action) -> 25 quantiles, activations;
+//                            job 3 + c: actor(next_obs) -> next action; target critic c on it ->
+//                            25 quantiles
+//   K2 tqc_critic_bwd_kernel (slab, critic c) the 50 target quantiles sorted, the top 4 dropped, the
+//                            TD target; critic c's quantile Huber loss and its gradient; backward
+//                            through critic c's layers
+//   K3 tqc_wgrad_adam_kernel critic weight gradients + Adam + Polyak update of the target critics;
+//                            entropy-coefficient Adam
+//   K4 tqc_pi_critic_kernel  (slab, critic c) critic c (updated) on (obs, a_pi); backward to a_pi
+//   K5 tqc_actor_bwd_kernel  (slab) the squashed Gaussian's gradient; backward through the actor
+//   K6 tqc_wgrad_adam_kernel actor weight gradients + Adam
 // The order is sb3-contrib's: entropy coefficient (its pre-update value in both losses), critic
 // step, actor loss against the updated critics, Polyak.  Adam is torch.optim.Adam's fused /
 // capturable update (per-parameter step tensors, incremented first; bias corrections from them),
@@ -30,26 +39,32 @@
 namespace {
 
 constexpr int R = 16;              // rows per slab (one MFMA tile of rows)
-constexpr int NW = 8;              // waves per workgroup (two per SIMD)
+constexpr int NW = 8;              // waves per workgroup of the chain kernels (two per SIMD)
 constexpr int NTH = 64 * NW;
 constexpr int KC = 32;             // reduction rows per staged weight chunk
 constexpr int OBS = 25, ACT = 7, HID = 256, NC = 2, NQ = 25, NIN = OBS + ACT, NALL = NC * NQ;
+constexpr int KEEP = NALL - 2 * NC;   // target quantiles kept (top_quantiles_to_drop_per_net = 2)
 constexpr int LD = HID + 4;        // LDS row stride of the slab buffers (floats; = 4 mod 64: the A
-                                   // operand's b128 reads and the row-permuted wgrad reads are
-                                   // conflict-free)
+                                   // operand's b128 reads are conflict-free)
 constexpr int LDT = KC + 4;        // staged weight chunk, [column][reduction row] layout (CR)
 constexpr int LDW = HID + 4;       // staged weight chunk, [reduction row][column] layout (RC)
 constexpr int WCH = HID * LDT > KC * LDW ? HID * LDT : KC * LDW;   // one chunk buffer (floats)
 constexpr float LOG_STD_MIN = -20.0f, LOG_STD_MAX = 2.0f, SQUASH_EPS = 1e-6f;
 constexpr float HALF_LOG_2PI = 0.91893853320467274178f;
 
-// per-slab workspace (floats): the actor's hidden activations and per-row values K3 needs, and
-// the critics' hidden activations (K1 and K3 scratch)
-constexpr int WS_H = R * HID;
-constexpr int WS_ACTOR = 0;                       // 3 x [16][256]
-constexpr int WS_CRIT = WS_ACTOR + 3 * WS_H;      // [2 critics][3][16][256]
-constexpr int WS_ROW = WS_CRIT + NC * 3 * WS_H;   // a_pi, std, eps, log_std raw [16][7] each; log_prob [16]
-constexpr int WS_SLAB = WS_ROW + 4 * R * ACT + R;
+// workspace: NMAT matrices [B][256] (row b of the batch at b * 256), then the per-slab sums
+constexpr int M_AH = 0;            // actor(obs) H1..H3
+constexpr int M_CH = 3;            // critic c on (obs, action): H1..H3 at 3 + 3c + l
+constexpr int M_CD = 9;            // critic c: dH1..dH3 (the layer-output gradients) at 9 + 3c + l
+constexpr int M_PH = 15;           // critic c on (obs, a_pi): H1..H3 at 15 + 3c + l
+constexpr int M_AD = 21;           // actor: dH1..dH3
+constexpr int M_SM = 24;           // per-row values, columns:
+constexpr int S_API = 0, S_STD = 8, S_EPS = 16, S_LSR = 24, S_LP = 32, S_NLP = 33, S_Q = 40, S_TQ = 96,
+              S_DQ = 152, S_DA = 208, S_DMU = 224, S_DLS = 232;
+constexpr int NMAT = 25;
+constexpr int NSUM = 8;            // per slab: critic loss (c = 0, 1), sum(log_prob + target entropy),
+                                   // sum q_pi (c = 0, 1), actor loss
+static_assert(S_TQ + NALL <= S_DQ && S_DQ + NALL <= S_DA && S_DLS + 8 <= HID, "per-row layout");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
@@ -200,52 +215,6 @@ __device__ __attribute__((noinline)) void lin_dgrad(const float* dY, const float
       }
   }
 }
-// per-slab weight gradient P(k, n) = sum over the 16 rows of X[r][k] dY[r][n] (P in Wk's storage
-// layout) and the bias gradient Pb[n] = sum_r dY[r][n].  Rows permuted as in slab_gemm (step s,
-// lane kq: row 4 kq + s): the b32 reads of X and dY are then conflict-free with LD = 4 mod 64.
-template <bool TR, int K, int N>
-__device__ __attribute__((noinline)) void lin_wgrad(const float* X, const float* dY, float* __restrict__ P, float* __restrict__ Pb) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 15, kq = lane >> 4;
-  constexpr int tk = (K + 15) >> 4, tn = (N + 15) >> 4, nt = tk * tn;
-  for (int t0 = wv * 4; t0 < nt; t0 += 4 * NW) {
-    f32x4 acc[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 4; s++) {
-      const int r = 4 * kq + s;
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int t = t0 + q;
-        if (t < nt) {
-          const int k = (t / tn) * 16 + i, n = (t % tn) * 16 + i;
-          const float a = k < K ? X[r * LD + k] : 0.f;
-          const float b = n < N ? dY[r * LD + n] : 0.f;
-          acc[q] = mfma4(a, b, acc[q]);
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int t = t0 + q;
-      if (t < nt) {
-        const int n = (t % tn) * 16 + i;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int k = (t / tn) * 16 + 4 * kq + r;
-          if (k < K && n < N) P[TR ? (size_t)n * K + k : (size_t)k * N + n] = acc[q][r];
-        }
-      }
-    }
-  }
-  for (int n = threadIdx.x; n < N; n += NTH) {
-    float s = 0.f;
-#pragma unroll
-    for (int r = 0; r < R; r++) s += dY[r * LD + n];
-    Pb[n] = s;
-  }
-}
-
 // global <-> LDS slab copies (save/load: float4 both sides)
 template <int COLS>
 __device__ void load_rows(float* D, const float* __restrict__ src, int row0, int ld_src, int col0 = 0) {
@@ -278,14 +247,21 @@ struct TqcArgs {
   const float* obs; const float* act; const float* nobs; const float* done; const float* rew;
   const float* eps_pi; const float* eps_next;
   const float* log_ent_coef;
-  float* ws;                 // [slabs][WS_SLAB]
-  float* part_c;             // [slabs][critic params]
-  float* part_a;             // [slabs][actor params]
-  float* part_s;             // [slabs][4]: critic loss sum, sum(log_prob + target entropy), actor loss sum
-  float* logs;               // [4]: ent_coef (pre-update), critic loss, actor loss, entropy-coefficient loss
+  float* ws;                 // NMAT x [B][256]
+  float* sums;               // [slabs][NSUM]
+  const float* logs;         // [4]: ent_coef (pre-update), critic loss, actor loss, entropy-coefficient loss
+  // the optimisers' step tensors (torch increments every parameter's own): the actor's before
+  // its Adam (K1, which runs before K6 reads them), the critics' and the entropy coefficient's
+  // after theirs (K4, after K3 read them)
+  float* astep[10];
+  float* cstep[9];          // critic w0 b0 .. w3 b3, entropy coefficient
   float gamma, target_entropy;
   int B;
 };
+// rows row0.. of workspace matrix id
+__device__ __forceinline__ float* wmat(const TqcArgs& g, int id, int row0) {
+  return g.ws + ((size_t)id * g.B + row0) * HID;
+}
 // critic parameter offsets (per tensor, both critics) in the flat critic gradient vector; actor
 // likewise
 __host__ __device__ constexpr int crit_size(int t) {
@@ -306,20 +282,35 @@ struct alignas(16) Lds {   // 136 KB (a workgroup may hold all 160 KB of a CU's 
   float red[NTH];
 };
 
+// block sum of v (all threads), result on every thread
+__device__ float block_sum(Lds& L, float v) {
+  L.red[threadIdx.x] = v;
+  __syncthreads();
+  for (int s = NTH / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) L.red[threadIdx.x] += L.red[threadIdx.x + s];
+    __syncthreads();
+  }
+  const float r = L.red[0];
+  __syncthreads();
+  return r;
+}
+
 // the actor's forward pass on the slab's rows of x (LDS A): a = tanh(mu + std eps), log_prob;
-// hidden activations saved to hs (or not, null); leaves a in aout[16][7] (LDS), log_prob in lpo[16]
+// hidden activations saved to hs (workspace matrices M_AH.., or not: null) and the per-row values
+// to sm (or not); leaves a in aout[16][8] (LDS), log_prob in lpo[16]
 __device__ void actor_fwd(Lds& L, const TqcArgs& g, const float* __restrict__ eps, int row0, float* hs, float (*aout)[8],
-                          float* lpo, float* row_ws) {
+                          float* lpo, float* sm) {
   const float* const* P = g.actor;
+  const size_t MS = (size_t)g.B * HID;
   lin_fwd<true, OBS, HID>(L.A, P[0], P[1], L.Bf, true, L.W);
   __syncthreads();
   if (hs) save_slab<HID>(hs, L.Bf);
   lin_fwd<true, HID, HID>(L.Bf, P[2], P[3], L.C, true, L.W);
   __syncthreads();
-  if (hs) save_slab<HID>(hs + WS_H, L.C);
+  if (hs) save_slab<HID>(hs + MS, L.C);
   lin_fwd<true, HID, HID>(L.C, P[4], P[5], L.Bf, true, L.W);
   __syncthreads();
-  if (hs) save_slab<HID>(hs + 2 * WS_H, L.Bf);
+  if (hs) save_slab<HID>(hs + 2 * MS, L.Bf);
   // heads: mu and log_std into C's first 16 columns (N = 7 each)
   lin_fwd<true, HID, ACT>(L.Bf, P[6], P[7], L.C, false, L.W);
   lin_fwd<true, HID, ACT>(L.Bf, P[8], P[9], L.C + 8, false, L.W);
@@ -334,11 +325,12 @@ __device__ void actor_fwd(Lds& L, const TqcArgs& g, const float* __restrict__ ep
     aout[r][j] = a;
     L.row[r][j] = -0.5f * e * e - ls - HALF_LOG_2PI;
     L.row[r][7 + j] = logf(1.f - a * a + SQUASH_EPS);
-    if (row_ws) {
-      row_ws[t] = a;                     // a_pi
-      row_ws[R * ACT + t] = sd;          // std
-      row_ws[2 * R * ACT + t] = e;       // eps
-      row_ws[3 * R * ACT + t] = lsr;     // raw log_std (the clamp's gradient mask)
+    if (sm) {
+      float* s = sm + r * HID;
+      s[S_API + j] = a;
+      s[S_STD + j] = sd;
+      s[S_EPS + j] = e;
+      s[S_LSR + j] = lsr;        // raw log_std (the clamp's gradient mask)
     }
   }
   __syncthreads();
@@ -347,14 +339,14 @@ __device__ void actor_fwd(Lds& L, const TqcArgs& g, const float* __restrict__ ep
 #pragma unroll
     for (int j = 0; j < ACT; j++) { s1 += L.row[t][j]; s2 += L.row[t][7 + j]; }
     lpo[t] = s1 - s2;
-    if (row_ws) row_ws[4 * R * ACT + t] = s1 - s2;
+    if (sm) sm[t * HID + S_LP] = s1 - s2;
   }
   __syncthreads();
 }
 
-// one critic network c on x (LDS A, 32 columns) -> q[16][25] into out (LDS, row stride NALL,
-// column offset c * 25); hidden activations saved to hs (or not)
-__device__ void critic_fwd(Lds& L, const float* const* P, int c, float* hs, float* out) {
+// one critic network c on x (LDS A, 32 columns) -> q[16][25] into out (row stride os); hidden
+// activations saved to hs (workspace matrices, or not)
+__device__ void critic_fwd(Lds& L, const float* const* P, int c, float* hs, float* out, int os, size_t MS) {
   const float* w0 = P[0] + (size_t)c * NIN * HID;
   const float* w1 = P[2] + (size_t)c * HID * HID;
   const float* w2 = P[4] + (size_t)c * HID * HID;
@@ -364,97 +356,91 @@ __device__ void critic_fwd(Lds& L, const float* const* P, int c, float* hs, floa
   if (hs) save_slab<HID>(hs, L.Bf);
   lin_fwd<false, HID, HID>(L.Bf, w1, P[3] + c * HID, L.C, true, L.W);
   __syncthreads();
-  if (hs) save_slab<HID>(hs + WS_H, L.C);
+  if (hs) save_slab<HID>(hs + MS, L.C);
   lin_fwd<false, HID, HID>(L.C, w2, P[5] + c * HID, L.Bf, true, L.W);
   __syncthreads();
-  if (hs) save_slab<HID>(hs + 2 * WS_H, L.Bf);
+  if (hs) save_slab<HID>(hs + 2 * MS, L.Bf);
   lin_fwd<false, HID, NQ>(L.Bf, w3, P[7] + c * NQ, L.C, false, L.W);
   __syncthreads();
   for (int e = threadIdx.x; e < R * NQ; e += NTH) {
     const int r = e / NQ, j = e - r * NQ;
-    out[r * NALL + c * NQ + j] = L.C[r * LD + j];
+    out[r * os + j] = L.C[r * LD + j];
   }
   __syncthreads();
 }
-// backward through critic c from dq (LDS C, [16][25]) with its saved activations hs and input x
-// (global rows, re-staged): weight gradients into pw (the slab's critic gradient vector) when
-// non-null; the input gradient d x (32 columns) left in L.A when want_dx
-__device__ void critic_bwd(Lds& L, const float* const* P, int c, const float* hs, float* pw, bool want_dx,
-                           const TqcArgs& g, int row0, bool x_is_pi, float (*api)[8]) {
+// backward through critic c's layers from dq (LDS C, [16][25]) with its saved activations hs: the
+// layer-output gradients dH3, dH2, dH1 saved to ds (or not); the input gradient d x (32 columns)
+// left in L.A when want_dx
+__device__ void critic_dgrad(Lds& L, const float* const* P, int c, const float* hs, float* ds, bool want_dx, size_t MS) {
   const float* w1 = P[2] + (size_t)c * HID * HID;
   const float* w2 = P[4] + (size_t)c * HID * HID;
   const float* w3 = P[6] + (size_t)c * HID * NQ;
-  // layer 3 (linear): dq in C; H3 -> A
-  load_slab<HID>(L.A, hs + 2 * WS_H);
+  load_slab<HID>(L.A, hs + 2 * MS);
   __syncthreads();
-  if (pw) lin_wgrad<false, HID, NQ>(L.A, L.C, pw + crit_off(6) + c * HID * NQ, pw + crit_off(7) + c * NQ);
   lin_dgrad<false, NQ, HID>(L.C, w3, L.Bf, L.A, false, L.W);   // dH3 = dq w3^T, relu'(H3)
   __syncthreads();
-  // layer 2: dY = dH3 (Bf), X = H2 -> A
-  load_slab<HID>(L.A, hs + WS_H);
+  if (ds) save_slab<HID>(ds + 2 * MS, L.Bf);
+  load_slab<HID>(L.A, hs + MS);
   __syncthreads();
-  if (pw) lin_wgrad<false, HID, HID>(L.A, L.Bf, pw + crit_off(4) + c * HID * HID, pw + crit_off(5) + c * HID);
-  lin_dgrad<false, HID, HID>(L.Bf, w2, L.C, L.A, false, L.W);   // dH2
+  lin_dgrad<false, HID, HID>(L.Bf, w2, L.C, L.A, false, L.W);  // dH2
   __syncthreads();
-  // layer 1: dY = dH2 (C), X = H1 -> A
+  if (ds) save_slab<HID>(ds + MS, L.C);
   load_slab<HID>(L.A, hs);
   __syncthreads();
-  if (pw) lin_wgrad<false, HID, HID>(L.A, L.C, pw + crit_off(2) + c * HID * HID, pw + crit_off(3) + c * HID);
-  lin_dgrad<false, HID, HID>(L.C, w1, L.Bf, L.A, false, L.W);   // dH1
+  lin_dgrad<false, HID, HID>(L.C, w1, L.Bf, L.A, false, L.W);  // dH1
   __syncthreads();
-  // layer 0: dY = dH1 (Bf), X = [obs, action] -> A
-  load_rows<OBS>(L.A, g.obs, row0, OBS);
-  if (x_is_pi) {
-    for (int e = threadIdx.x; e < R * ACT; e += NTH) L.A[(e / ACT) * LD + OBS + e % ACT] = api[e / ACT][e % ACT];
-  } else {
-    load_rows<ACT>(L.A, g.act, row0, ACT, OBS);
-  }
-  __syncthreads();
-  if (pw) lin_wgrad<false, NIN, HID>(L.A, L.Bf, pw + crit_off(0) + c * NIN * HID, pw + crit_off(1) + c * HID);
-  __syncthreads();
+  if (ds) save_slab<HID>(ds, L.Bf);
   if (want_dx) {
     lin_dgrad<false, HID, NIN>(L.Bf, P[0] + (size_t)c * NIN * HID, L.A, nullptr, false, L.W);
     __syncthreads();
   }
 }
 
-// block sum of v (all threads), result on every thread
-__device__ float block_sum(Lds& L, float v) {
-  L.red[threadIdx.x] = v;
-  __syncthreads();
-  for (int s = NTH / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) L.red[threadIdx.x] += L.red[threadIdx.x + s];
-    __syncthreads();
-  }
-  const float r = L.red[0];
-  __syncthreads();
-  return r;
-}
-
-__global__ void __launch_bounds__(NTH) tqc_critic_kernel(TqcArgs g) {
+__global__ void __launch_bounds__(NTH) tqc_fwd_kernel(TqcArgs g) {
   __shared__ Lds L;
-  const int slab = blockIdx.x, row0 = slab * R, t = threadIdx.x;
-  float* ws = g.ws + (size_t)slab * WS_SLAB;
-  float* pw = g.part_c + (size_t)slab * CRIT_P;
-  const float ent_coef = expf(g.log_ent_coef[0]);
-  // actor(obs): a_pi, log_prob (kept for the actor step)
-  __shared__ float api[R][8], lp[R], na[R][8], nlp[R];
-  load_rows<OBS>(L.A, g.obs, row0, OBS);
-  __syncthreads();
-  actor_fwd(L, g, g.eps_pi, row0, ws + WS_ACTOR, api, lp, ws + WS_ROW);
-  // actor(next_obs): next action and its log_prob
+  __shared__ float ap[R][8], lp[R];
+  const int slab = blockIdx.x, job = blockIdx.y, row0 = slab * R, t = threadIdx.x;
+  const size_t MS = (size_t)g.B * HID;
+  float* sm = wmat(g, M_SM, row0);
+  if (slab == 0 && job == 0 && t < 10) g.astep[t][0] += 1.f;
+  if (job == 0) {   // actor(obs): a_pi, log_prob, activations (the actor step's)
+    load_rows<OBS>(L.A, g.obs, row0, OBS);
+    __syncthreads();
+    actor_fwd(L, g, g.eps_pi, row0, wmat(g, M_AH, row0), ap, lp, sm);
+    const float es = block_sum(L, t < R ? lp[t] + g.target_entropy : 0.f);
+    if (t == 0) g.sums[slab * NSUM + 2] = es;
+    return;
+  }
+  if (job <= NC) {   // critic c = job - 1 on (obs, action), activations saved
+    const int c = job - 1;
+    load_rows<OBS>(L.A, g.obs, row0, OBS);
+    load_rows<ACT>(L.A, g.act, row0, ACT, OBS);
+    __syncthreads();
+    critic_fwd(L, g.critic, c, wmat(g, M_CH + 3 * c, row0), sm + S_Q + c * NQ, HID, MS);
+    return;
+  }
+  // actor(next_obs) -> next action and its log_prob; target critic c = job - 3 on them
+  const int c = job - 1 - NC;
   load_rows<OBS>(L.A, g.nobs, row0, OBS);
   __syncthreads();
-  actor_fwd(L, g, g.eps_next, row0, nullptr, na, nlp, nullptr);
-  // target critics on (next_obs, next_action)
-  for (int c = 0; c < NC; c++) {
-    load_rows<OBS>(L.A, g.nobs, row0, OBS);
-    for (int e = t; e < R * ACT; e += NTH) L.A[(e / ACT) * LD + OBS + e % ACT] = na[e / ACT][e % ACT];
-    __syncthreads();
-    critic_fwd(L, g.target, c, nullptr, &L.q[0][0]);
-  }
+  actor_fwd(L, g, g.eps_next, row0, nullptr, ap, lp, nullptr);
+  if (c == 0 && t < R) sm[t * HID + S_NLP] = lp[t];
+  load_rows<OBS>(L.A, g.nobs, row0, OBS);
+  for (int e = t; e < R * ACT; e += NTH) L.A[(e / ACT) * LD + OBS + e % ACT] = ap[e / ACT][e % ACT];
+  __syncthreads();
+  critic_fwd(L, g.target, c, nullptr, sm + S_TQ + c * NQ, HID, MS);
+}
+
+__global__ void __launch_bounds__(NTH) tqc_critic_bwd_kernel(TqcArgs g) {
+  __shared__ Lds L;
+  const int slab = blockIdx.x, c = blockIdx.y, row0 = slab * R, t = threadIdx.x;
+  const size_t MS = (size_t)g.B * HID;
+  float* sm = wmat(g, M_SM, row0);
+  const float ent_coef = expf(g.log_ent_coef[0]);
   // sort the 50 target quantiles per row (rank by counting; ties broken by index), keep the
   // lowest 46, TD target
+  for (int e = t; e < R * NALL; e += NTH) L.q[e / NALL][e % NALL] = sm[(e / NALL) * HID + S_TQ + e % NALL];
+  __syncthreads();
   for (int e = t; e < R * NALL; e += NTH) {
     const int r = e / NALL, j = e - r * NALL;
     const float v = L.q[r][j];
@@ -466,27 +452,20 @@ __global__ void __launch_bounds__(NTH) tqc_critic_kernel(TqcArgs g) {
     L.row[r][rank] = v;
   }
   __syncthreads();
-  constexpr int KEEP = NALL - 2 * NC;
   for (int e = t; e < R * KEEP; e += NTH) {
     const int r = e / KEEP, j = e - r * KEEP;
     const float d = g.done[row0 + r], rw = g.rew[row0 + r];
-    const float tq = L.row[r][j] - ent_coef * nlp[r];
+    const float tq = L.row[r][j] - ent_coef * sm[r * HID + S_NLP];
     L.tq[r][j] = rw + (1.f - d) * g.gamma * tq;
   }
   __syncthreads();
-  // critics on (obs, action), activations saved
-  for (int c = 0; c < NC; c++) {
-    load_rows<OBS>(L.A, g.obs, row0, OBS);
-    load_rows<ACT>(L.A, g.act, row0, ACT, OBS);
-    __syncthreads();
-    critic_fwd(L, g.critic, c, ws + WS_CRIT + c * 3 * WS_H, &L.q[0][0]);
-  }
-  // quantile Huber loss (mean over rows x critics x quantiles x targets) and its gradient dq
+  // critic c's share of the quantile Huber loss (mean over rows x critics x quantiles x targets)
+  // and its gradient dq
   const float scale = 1.f / ((float)g.B * NC * NQ * KEEP);
   float lsum = 0.f;
-  for (int e = t; e < R * NALL; e += NTH) {
-    const int r = e / NALL, ci = e - r * NALL, i = ci % NQ;
-    const float cq = L.q[r][ci], tau = ((float)i + 0.5f) / NQ;
+  for (int e = t; e < R * NQ; e += NTH) {
+    const int r = e / NQ, i = e - r * NQ;
+    const float cq = sm[r * HID + S_Q + c * NQ + i], tau = ((float)i + 0.5f) / NQ;
     float gsum = 0.f;
     for (int j = 0; j < KEEP; j++) {
       const float d = L.tq[r][j] - cq, ad = fabsf(d);
@@ -494,113 +473,110 @@ __global__ void __launch_bounds__(NTH) tqc_critic_kernel(TqcArgs g) {
       lsum += w * (ad > 1.f ? ad - 0.5f : 0.5f * d * d);
       gsum += w * (ad > 1.f ? (d > 0.f ? 1.f : -1.f) : d);
     }
-    L.row[r][ci] = -gsum * scale;   // dL / dq
+    const float dq = -gsum * scale;
+    L.C[r * LD + i] = dq;
+    sm[r * HID + S_DQ + c * NQ + i] = dq;
   }
   lsum = block_sum(L, lsum);
-  // per-row log_prob + target entropy (entropy-coefficient gradient)
-  const float esum = block_sum(L, t < R ? lp[t] + g.target_entropy : 0.f);
-  if (t == 0) {
-    g.part_s[slab * 4 + 0] = lsum;
-    g.part_s[slab * 4 + 1] = esum;
-  }
-  // backward through each critic: weight gradients
-  for (int c = 0; c < NC; c++) {
-    for (int e = t; e < R * NQ; e += NTH) L.C[(e / NQ) * LD + e % NQ] = L.row[e / NQ][c * NQ + e % NQ];
-    __syncthreads();
-    critic_bwd(L, g.critic, c, ws + WS_CRIT + c * 3 * WS_H, pw, false, g, row0, false, nullptr);
-  }
+  if (t == 0) g.sums[slab * NSUM + c] = lsum;
+  critic_dgrad(L, g.critic, c, wmat(g, M_CH + 3 * c, row0), wmat(g, M_CD + 3 * c, row0), false, MS);
 }
 
-__global__ void __launch_bounds__(NTH) tqc_actor_kernel(TqcArgs g) {
+__global__ void __launch_bounds__(NTH) tqc_pi_critic_kernel(TqcArgs g) {
+  __shared__ Lds L;
+  const int slab = blockIdx.x, c = blockIdx.y, row0 = slab * R, t = threadIdx.x;
+  const size_t MS = (size_t)g.B * HID;
+  float* sm = wmat(g, M_SM, row0);
+  if (slab == 0 && c == 0 && t < 9) g.cstep[t][0] += 1.f;
+  // critic c (updated) on (obs, a_pi): q_pi, then d loss / d a_pi
+  load_rows<OBS>(L.A, g.obs, row0, OBS);
+  for (int e = t; e < R * ACT; e += NTH) L.A[(e / ACT) * LD + OBS + e % ACT] = sm[(e / ACT) * HID + S_API + e % ACT];
+  __syncthreads();
+  float* hs = wmat(g, M_PH + 3 * c, row0);
+  critic_fwd(L, g.critic, c, hs, &L.q[0][0], NALL, MS);
+  float qs = 0.f;
+  for (int e = t; e < R * NQ; e += NTH) qs += L.q[e / NQ][e % NQ];
+  qs = block_sum(L, qs);
+  if (t == 0) g.sums[slab * NSUM + 3 + c] = qs;
+  // actor loss = mean_rows(ent_coef log_prob - mean_{c,q} q): d / dq = -1 / (B NC NQ)
+  const float dq = -1.f / ((float)g.B * NC * NQ);
+  for (int e = t; e < R * NQ; e += NTH) L.C[(e / NQ) * LD + e % NQ] = dq;
+  __syncthreads();
+  critic_dgrad(L, g.critic, c, hs, nullptr, true, MS);
+  for (int e = t; e < R * ACT; e += NTH) sm[(e / ACT) * HID + S_DA + c * 8 + e % ACT] = L.A[(e / ACT) * LD + OBS + e % ACT];
+}
+
+__global__ void __launch_bounds__(NTH) tqc_actor_bwd_kernel(TqcArgs g) {
   __shared__ Lds L;
   const int slab = blockIdx.x, row0 = slab * R, t = threadIdx.x;
-  const float* ws = g.ws + (size_t)slab * WS_SLAB;
-  float* pw = g.part_a + (size_t)slab * ACT_P;
+  float* sm = wmat(g, M_SM, row0);
   const float ent_coef = g.logs[0];   // sb3: the coefficient before this step's entropy update
-  __shared__ float api[R][8], dap[R][8];
-  const float* rw = ws + WS_ROW;
-  for (int e = t; e < R * ACT; e += NTH) { api[e / ACT][e % ACT] = rw[e]; dap[e / ACT][e % ACT] = 0.f; }
-  __syncthreads();
-  // critics (updated) on (obs, a_pi): q_pi, then d loss / d a_pi through both critics
-  float qsum = 0.f;
-  for (int c = 0; c < NC; c++) {
-    load_rows<OBS>(L.A, g.obs, row0, OBS);
-    for (int e = t; e < R * ACT; e += NTH) L.A[(e / ACT) * LD + OBS + e % ACT] = api[e / ACT][e % ACT];
-    __syncthreads();
-    float* hs = g.ws + (size_t)slab * WS_SLAB + WS_CRIT + c * 3 * WS_H;
-    critic_fwd(L, g.critic, c, hs, &L.q[0][0]);
-    for (int e = t; e < R * NQ; e += NTH) qsum += L.q[e / NQ][c * NQ + e % NQ];
-    // actor loss = mean_rows(ent_coef log_prob - mean_{c,q} q): d / dq = -1 / (B NC NQ)
-    const float dq = -1.f / ((float)g.B * NC * NQ);
-    for (int e = t; e < R * NQ; e += NTH) L.C[(e / NQ) * LD + e % NQ] = dq;
-    __syncthreads();
-    critic_bwd(L, g.critic, c, hs, nullptr, true, g, row0, true, api);
-    for (int e = t; e < R * ACT; e += NTH) dap[e / ACT][e % ACT] += L.A[(e / ACT) * LD + OBS + e % ACT];
-    __syncthreads();
+  const float lpsum = block_sum(L, t < R ? sm[t * HID + S_LP] : 0.f);
+  if (t == 0) {
+    const float* s = g.sums + slab * NSUM;
+    g.sums[slab * NSUM + 5] = ent_coef * lpsum - (s[3] + s[4]) / (NC * NQ);
   }
-  const float lpsum = block_sum(L, t < R ? rw[4 * R * ACT + t] : 0.f);
-  qsum = block_sum(L, qsum);
-  if (t == 0) g.part_s[slab * 4 + 2] = ent_coef * lpsum - qsum / (NC * NQ);
   // the squashed Gaussian: a = tanh(mu + std eps), std = exp(clamp(log_std)),
   // log_prob = sum(-eps^2 / 2 - log_std - log(2 pi) / 2) - sum(log(1 - a^2 + 1e-6))
   const float dlp = ent_coef / (float)g.B;
   if (t < R * ACT) {
     const int r = t / ACT, j = t - r * ACT;
-    const float a = rw[t], sd = rw[R * ACT + t], e = rw[2 * R * ACT + t], lsr = rw[3 * R * ACT + t];
-    const float da = dap[r][j] + dlp * (2.f * a / (1.f - a * a + SQUASH_EPS));
+    float* s = sm + r * HID;
+    const float a = s[S_API + j], sd = s[S_STD + j], e = s[S_EPS + j], lsr = s[S_LSR + j];
+    const float da = s[S_DA + j] + s[S_DA + 8 + j] + dlp * (2.f * a / (1.f - a * a + SQUASH_EPS));
     const float dgg = da * (1.f - a * a);
     const bool inside = lsr >= LOG_STD_MIN && lsr <= LOG_STD_MAX;
-    L.C[r * LD + j] = dgg;                                       // d mu
-    L.C[r * LD + 8 + j] = inside ? dgg * sd * e - dlp : 0.f;     // d log_std (raw)
+    const float dmu = dgg, dls = inside ? dgg * sd * e - dlp : 0.f;   // d mu, d log_std (raw)
+    s[S_DMU + j] = dmu;
+    s[S_DLS + j] = dls;
+    L.Bf[r * LD + 16 + j] = dmu;
+    L.Bf[r * LD + j] = dls;
   }
-  __syncthreads();
   const float* const* P = g.actor;
-  // heads: X = H3 (A), dY = d mu / d log_std (C columns 0.. / 8..)
-  load_slab<HID>(L.A, ws + WS_ACTOR + 2 * WS_H);
-  for (int e = t; e < R * 8; e += NTH) { L.Bf[(e / 8) * LD + e % 8] = L.C[(e / 8) * LD + 8 + e % 8]; }
+  load_slab<HID>(L.A, wmat(g, M_AH + 2, row0));
   __syncthreads();
-  lin_wgrad<true, HID, ACT>(L.A, L.C, pw + act_off(6), pw + act_off(7));
-  lin_wgrad<true, HID, ACT>(L.A, L.Bf, pw + act_off(8), pw + act_off(9));
-  __syncthreads();
-  // d H3 = dmu Wmu + dls Wls, relu'(H3): into the free buffer (C's columns > 15 are unused:
-  // stage d mu in Bf's high columns first)
-  for (int e = t; e < R * 8; e += NTH) L.Bf[(e / 8) * LD + 16 + e % 8] = L.C[(e / 8) * LD + e % 8];
-  __syncthreads();
+  // d H3 = dmu Wmu + dls Wls, relu'(H3)
   lin_dgrad<true, ACT, HID>(L.Bf + 16, P[6], L.C, nullptr, false, L.W);
   __syncthreads();
   lin_dgrad<true, ACT, HID>(L.Bf, P[8], L.C, L.A, true, L.W);
   __syncthreads();
-  // layer 2: X = H2, dY = dH3 (C)
-  load_slab<HID>(L.A, ws + WS_ACTOR + WS_H);
+  save_slab<HID>(wmat(g, M_AD + 2, row0), L.C);
+  load_slab<HID>(L.A, wmat(g, M_AH + 1, row0));
   __syncthreads();
-  lin_wgrad<true, HID, HID>(L.A, L.C, pw + act_off(4), pw + act_off(5));
-  lin_dgrad<true, HID, HID>(L.C, P[4], L.Bf, L.A, false, L.W);
+  lin_dgrad<true, HID, HID>(L.C, P[4], L.Bf, L.A, false, L.W);   // dH2
   __syncthreads();
-  // layer 1: X = H1, dY = dH2 (Bf)
-  load_slab<HID>(L.A, ws + WS_ACTOR);
+  save_slab<HID>(wmat(g, M_AD + 1, row0), L.Bf);
+  load_slab<HID>(L.A, wmat(g, M_AH, row0));
   __syncthreads();
-  lin_wgrad<true, HID, HID>(L.A, L.Bf, pw + act_off(2), pw + act_off(3));
-  lin_dgrad<true, HID, HID>(L.Bf, P[2], L.C, L.A, false, L.W);
+  lin_dgrad<true, HID, HID>(L.Bf, P[2], L.C, L.A, false, L.W);   // dH1
   __syncthreads();
-  // layer 0: X = obs, dY = dH1 (C)
-  load_rows<OBS>(L.A, g.obs, row0, OBS);
-  __syncthreads();
-  lin_wgrad<true, OBS, HID>(L.A, L.C, pw + act_off(0), pw + act_off(1));
+  save_slab<HID>(wmat(g, M_AD, row0), L.C);
 }
 
-// ---- reduction of the per-slab gradients + Adam (torch.optim.Adam fused / capturable semantics)
-struct AdamArgs {
-  float* p[10]; float* m[10]; float* v[10]; float* tgt[10]; float* step[10];
-  int off[11];               // flat offsets (off[nt] = total)
-  int nt;
-  const float* part; int nparts; int stride;   // per-slab gradient vectors
+// ---- weight gradients over the whole batch + Adam (torch.optim.Adam fused / capturable semantics)
+// One job per parameter tensor: dW(k, n) = sum_b X[b][k] dY[b][n] with X's columns k < kx from x0,
+// kx <= k < K from x1, and the ones-column k = K for the bias (db = sum_b dY).  One workgroup per
+// 32 x 32 tile of (K + 1) x N; wave w reduces rows [w B / 4, (w + 1) B / 4) on the matrix cores
+// (A lane (kq, i) = X[b + kq][k0 + i], B lane = dY[b + kq][n0 + i]), the four partial tiles are
+// added in wave order through LDS and the tile's Adam runs in place.
+constexpr int WT = 32, WNW = 4, WTH = 64 * WNW, MAXJ = 10;
+struct WJob {
+  const float* x0; const float* x1; const float* dy;
+  float* p; float* m; float* v; float* tgt; const float* step;       // weight ([out][in] if tr, else [in][out])
+  float* pb; float* mb; float* vb; float* tgtb; const float* stepb;  // bias
+  int ldx0, kx, ldx1, ldy, K, N, tr, tiles_n, tile0, goff, goffb;
+};
+struct WArgs {
+  WJob j[MAXJ];
+  int nj, B;
   const float* lr;
   float beta1, beta2, eps, tau;
-  float* grad_out;           // optional: the reduced gradients (tests)
-  // entropy coefficient (the critic pass): log_ent_coef, its Adam state, the gradient's source
+  float* grad_out;           // optional: the gradients (tests), flat
+  // the critic pass: the entropy coefficient's Adam and the losses; the actor pass: its loss
   float* ent; float* ent_m; float* ent_v; float* ent_step;
-  const float* part_s; int nslab; float target_entropy; int B;
-  float* logs; float critic_scale;
+  const float* sums; int nslab;
+  float* logs; float critic_scale; int actor;
+  float step_add;            // 1: the step tensors are incremented after this kernel, 0: before
 };
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float gr, float lr, float b1, float b2, float eps,
                                           float step) {
@@ -610,49 +586,135 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float gr
   const float denom = sqrtf(v) / sqrtf(bc2) + eps;
   p -= (lr / bc1) * m / denom;
 }
-__global__ void tqc_adam_kernel(AdamArgs a) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(WTH) tqc_wgrad_adam_kernel(WArgs a) {
+  __shared__ float red[WNW][WT][WT + 1];
+  int ji = 0;
+  while (ji + 1 < a.nj && (int)blockIdx.x >= a.j[ji + 1].tile0) ji++;
+  const WJob& J = a.j[ji];
+  const int tile = blockIdx.x - J.tile0, k0 = (tile / J.tiles_n) * WT, n0 = (tile % J.tiles_n) * WT;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, i = lane & 15, kq = lane >> 4;
+  const float* xp[2]; int xld[2]; float xc[2]; bool xl[2];
+  const float* yp[2]; bool yl[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int k = k0 + 16 * h + i, n = n0 + 16 * h + i;
+    xl[h] = k < J.K;
+    xp[h] = k < J.kx ? J.x0 + k : J.x1 + (xl[h] ? k - J.kx : 0);
+    xld[h] = k < J.kx ? J.ldx0 : J.ldx1;
+    xc[h] = k == J.K ? 1.f : 0.f;
+    yl[h] = n < J.N;
+    yp[h] = J.dy + (yl[h] ? n : 0);
+  }
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+#pragma unroll
+    for (int h2 = 0; h2 < 2; h2++) acc[h][h2] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int rows = a.B / WNW, b0 = w * rows, b1 = b0 + rows;
+  for (int b = b0; b < b1; b += 16) {   // four row groups per trip: 16 loads in flight
+    float xa[4][2], yb[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int bb = b + 4 * u;
+      const size_t r = bb + kq;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {   // rows past b1: zeros (the sum is unchanged)
+        xa[u][h] = bb < b1 ? (xl[h] ? xp[h][r * xld[h]] : xc[h]) : 0.f;
+        yb[u][h] = bb < b1 && yl[h] ? yp[h][r * J.ldy] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; h2++) acc[h][h2] = mfma4(xa[u][h], yb[u][h2], acc[h][h2]);
+  }
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+#pragma unroll
+    for (int h2 = 0; h2 < 2; h2++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) red[w][16 * h + 4 * kq + q][16 * h2 + i] = acc[h][h2][q];
+  __syncthreads();
   const float lr = a.lr[0];
-  if (e < a.off[a.nt]) {
-    int ti = 0;
-    while (ti + 1 < a.nt && e >= a.off[ti + 1]) ti++;
-    const int k = e - a.off[ti];
-    float gr = 0.f;
-    for (int s = 0; s < a.nparts; s++) gr += a.part[(size_t)s * a.stride + e];
-    if (a.grad_out) a.grad_out[e] = gr;
-    const float step = a.step[ti][0] + 1.f;
-    float p = a.p[ti][k], m = a.m[ti][k], v = a.v[ti][k];
+  for (int e = t; e < WT * WT; e += WTH) {
+    // consecutive threads along the parameter's contiguous index
+    const int kk = J.tr ? e % WT : e / WT, nn = J.tr ? e / WT : e % WT, k = k0 + kk, n = n0 + nn;
+    if (k > J.K || n >= J.N) continue;
+    const float gr = ((red[0][kk][nn] + red[1][kk][nn]) + red[2][kk][nn]) + red[3][kk][nn];
+    float *pp, *mp, *vp, *tp;
+    float step;
+    int gi;
+    if (k < J.K) {
+      const int idx = J.tr ? n * J.K + k : k * J.N + n;
+      pp = J.p + idx; mp = J.m + idx; vp = J.v + idx; tp = J.tgt ? J.tgt + idx : nullptr;
+      step = J.step[0] + a.step_add;
+      gi = J.goff + idx;
+    } else {
+      pp = J.pb + n; mp = J.mb + n; vp = J.vb + n; tp = J.tgtb ? J.tgtb + n : nullptr;
+      step = J.stepb[0] + a.step_add;
+      gi = J.goffb + n;
+    }
+    if (a.grad_out) a.grad_out[gi] = gr;
+    float p = *pp, m = *mp, v = *vp;
     adam_elem(p, m, v, gr, lr, a.beta1, a.beta2, a.eps, step);
-    a.p[ti][k] = p; a.m[ti][k] = m; a.v[ti][k] = v;
-    if (a.tgt[ti]) {   // Polyak (torch._foreach_mul_ then _foreach_add_ with alpha = tau)
-      const float t1 = a.tgt[ti][k] * (1.f - a.tau);
-      a.tgt[ti][k] = t1 + a.tau * p;
+    *pp = p; *mp = m; *vp = v;
+    if (tp) *tp = *tp * (1.f - a.tau) + a.tau * p;   // Polyak (torch._foreach_mul_, then _foreach_add_ alpha = tau)
+  }
+  if (blockIdx.x == 0 && t == 0) {
+    if (a.ent) {   // entropy coefficient: loss = -(log_ent_coef * mean(log_prob + target)).mean()
+      float s = 0.f, l = 0.f;
+      for (int q = 0; q < a.nslab; q++) {
+        s += a.sums[q * NSUM + 2];
+        l += a.sums[q * NSUM + 0] + a.sums[q * NSUM + 1];
+      }
+      const float mean = s / (float)a.B;
+      const float le = a.ent[0];
+      a.logs[0] = expf(le);
+      a.logs[1] = l * a.critic_scale;
+      a.logs[3] = -(le * mean);
+      float p = le, m = a.ent_m[0], v = a.ent_v[0];
+      adam_elem(p, m, v, -mean, lr, a.beta1, a.beta2, a.eps, a.ent_step[0] + a.step_add);
+      a.ent[0] = p; a.ent_m[0] = m; a.ent_v[0] = v;
+    }
+    if (a.actor) {
+      float s = 0.f;
+      for (int q = 0; q < a.nslab; q++) s += a.sums[q * NSUM + 5];
+      a.logs[2] = s / (float)a.B;
     }
   }
-  if (a.ent && e == 0) {   // entropy coefficient: loss = -(log_ent_coef * mean(log_prob + target)).mean()
-    float s = 0.f, l = 0.f;
-    for (int i = 0; i < a.nslab; i++) { s += a.part_s[i * 4 + 1]; l += a.part_s[i * 4 + 0]; }
-    const float mean = s / (float)a.B;
-    const float le = a.ent[0];
-    a.logs[0] = expf(le);
-    a.logs[1] = l * a.critic_scale;
-    a.logs[3] = -(le * mean);
-    float p = le, m = a.ent_m[0], v = a.ent_v[0];
-    const float step = a.ent_step[0] + 1.f;
-    adam_elem(p, m, v, -mean, lr, a.beta1, a.beta2, a.eps, step);
-    a.ent[0] = p; a.ent_m[0] = m; a.ent_v[0] = v;
-  }
-  if (!a.ent && a.logs && e == 0) {
-    float s = 0.f;
-    for (int i = 0; i < a.nslab; i++) s += a.part_s[i * 4 + 2];
-    a.logs[2] = s / (float)a.B;
-  }
 }
-// the optimisers' step tensors, after their update (torch increments every parameter's own)
-__global__ void tqc_step_inc(AdamArgs a) {
-  const int t = threadIdx.x;
-  if (t < a.nt) a.step[t][0] += 1.f;
-  if (t == 0 && a.ent_step) a.ent_step[0] += 1.f;
+// ---- replay sample + observation normalisation (pnp_amd/tqc.py DictReplayBuffer.sample,
+// VecNormalize.normalize, flat_obs): one workgroup of 64 per batch row; lanes: obs columns,
+// next_obs columns, action, done, reward.  fp32 index products truncated like Tensor.long(); the
+// normalisation in fp64 ((x - mean) / sqrt(var + eps), clamp, round to fp32) like the torch ops.
+struct SampleArgs {
+  pnp_tqc_replay rb;
+  const float* u;
+  int B;
+  float* obs; float* act; float* nobs; float* done; float* rew;
+};
+__device__ __forceinline__ float norm_col(const SampleArgs& a, float x, int j) {
+  int k = 0, o = j;
+  while (k + 1 < a.rb.n_keys && o >= a.rb.key_dim[k]) { o -= a.rb.key_dim[k]; k++; }
+  const double y = ((double)x - a.rb.mean[k][o]) / sqrt(a.rb.var[k][o] + a.rb.norm_eps);
+  const double c = y < -a.rb.clip_obs ? -a.rb.clip_obs : (y > a.rb.clip_obs ? a.rb.clip_obs : y);   // NaN passes, as torch.clamp
+  return (float)c;
+}
+__global__ void __launch_bounds__(64) tqc_sample_kernel(SampleArgs a) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int OD = a.rb.obs_dim, AD = a.rb.act_dim;
+  const float fu = a.u[b] * a.rb.upper[0], fe = a.u[a.B + b] * (float)a.rb.n_envs;
+  const long long bi = min((long long)fu, (long long)a.rb.rows - 1), ei = min((long long)fe, (long long)a.rb.n_envs - 1);
+  const size_t cell = (size_t)bi * a.rb.n_envs + ei;
+  for (int j = t; j < 2 * OD + AD + 2; j += 64) {
+    if (j < OD) a.obs[(size_t)b * OD + j] = norm_col(a, a.rb.obs[cell * OD + j], j);
+    else if (j < 2 * OD) a.nobs[(size_t)b * OD + j - OD] = norm_col(a, a.rb.next_obs[cell * OD + j - OD], j - OD);
+    else if (j < 2 * OD + AD) a.act[(size_t)b * AD + j - 2 * OD] = a.rb.actions[cell * AD + j - 2 * OD];
+    else if (j == 2 * OD + AD) a.done[b] = a.rb.dones[cell];
+    else a.rew[b] = a.rb.rewards[cell];
+  }
 }
 
 }  // namespace
@@ -670,11 +732,11 @@ static bool tqc_desc_ok(const pnp_tqc_desc* d) {
     if (!d->critic[i] || !d->critic_m[i] || !d->critic_v[i] || !d->critic_step[i] || !d->target[i]) return false;
   return d->ent_m && d->ent_v && d->ent_step && d->workspace && d->logs;
 }
+static int64_t tqc_ws_floats(int64_t B) { return (int64_t)NMAT * B * HID + (B / R) * NSUM; }
 
 extern "C" int64_t pnp_tqc_workspace_floats(const pnp_tqc_desc* d) {
   if (!tqc_shape_ok(d)) { pnp_set_error("pnp_tqc_workspace_floats: unsupported TQC shape"); return PNP_ERR_UNSUPPORTED; }
-  const int64_t S = d->batch / R;
-  return S * ((int64_t)WS_SLAB + CRIT_P + ACT_P + 4);
+  return tqc_ws_floats(d->batch);
 }
 extern "C" int32_t pnp_tqc_param_counts(int32_t* actor_params, int32_t* critic_params) {
   if (!actor_params || !critic_params) { pnp_set_error("pnp_tqc_param_counts: null"); return PNP_ERR_ARG; }
@@ -683,14 +745,48 @@ extern "C" int32_t pnp_tqc_param_counts(int32_t* actor_params, int32_t* critic_p
   return PNP_OK;
 }
 
+extern "C" int32_t pnp_tqc_sample(const pnp_tqc_replay* rb, const float* u, int32_t batch, float* obs, float* act,
+                                  float* next_obs, float* done, float* reward, void* stream) {
+  if (!rb || !u || batch <= 0 || !obs || !act || !next_obs || !done || !reward || !rb->obs || !rb->next_obs ||
+      !rb->actions || !rb->rewards || !rb->dones || !rb->upper || rb->rows <= 0 || rb->n_envs <= 0 || rb->obs_dim <= 0 ||
+      rb->act_dim <= 0 || rb->n_keys <= 0 || rb->n_keys > 4) {
+    pnp_set_error("pnp_tqc_sample: null pointer or bad replay shape");
+    return PNP_ERR_ARG;
+  }
+  int sum = 0;
+  for (int k = 0; k < rb->n_keys; k++) {
+    if (!rb->mean[k] || !rb->var[k] || rb->key_dim[k] <= 0) { pnp_set_error("pnp_tqc_sample: bad normaliser key"); return PNP_ERR_ARG; }
+    sum += rb->key_dim[k];
+  }
+  if (sum != rb->obs_dim) { pnp_set_error("pnp_tqc_sample: key dims do not add up to obs_dim"); return PNP_ERR_ARG; }
+  SampleArgs a{*rb, u, batch, obs, act, next_obs, done, reward};
+  hipLaunchKernelGGL(tqc_sample_kernel, dim3(batch), dim3(64), 0, (hipStream_t)stream, a);
+  return pnp_check_launch("tqc_sample_kernel");
+}
+
+// one weight-gradient job: a layer's weight (and bias) tensors with their Adam state
+static int add_wjob(WArgs& a, int tile, const float* x0, int ldx0, int kx, const float* x1, int ldx1, const float* dy,
+                    int K, int N, int tr, float* p, float* m, float* v, float* tgt, const float* step, float* pb, float* mb,
+                    float* vb, float* tgtb, const float* stepb, int goff, int goffb) {
+  WJob& J = a.j[a.nj++];
+  J.x0 = x0; J.ldx0 = ldx0; J.kx = kx; J.x1 = x1; J.ldx1 = ldx1; J.dy = dy; J.ldy = HID;
+  J.K = K; J.N = N; J.tr = tr;
+  J.p = p; J.m = m; J.v = v; J.tgt = tgt; J.step = step;
+  J.pb = pb; J.mb = mb; J.vb = vb; J.tgtb = tgtb; J.stepb = stepb;
+  J.goff = goff; J.goffb = goffb;
+  J.tiles_n = (N + WT - 1) / WT;
+  J.tile0 = tile;
+  return tile + (K + 1 + WT - 1) / WT * J.tiles_n;
+}
+
 extern "C" int32_t pnp_tqc_update(const pnp_tqc_desc* d, const pnp_tqc_batch* b, float* grads_out, void* stream) {
   if (!tqc_desc_ok(d)) { pnp_set_error("pnp_tqc_update: unsupported TQC shape or null pointer"); return PNP_ERR_UNSUPPORTED; }
   if (!b || !b->obs || !b->act || !b->next_obs || !b->done || !b->reward || !b->eps_pi || !b->eps_next) {
     pnp_set_error("pnp_tqc_update: null batch buffer");
     return PNP_ERR_ARG;
   }
-  const int S = d->batch / R;
-  if (d->workspace_floats < (int64_t)S * (WS_SLAB + CRIT_P + ACT_P + 4)) {
+  const int B = d->batch, S = B / R;
+  if (d->workspace_floats < tqc_ws_floats(B)) {
     pnp_set_error("pnp_tqc_update: workspace too small");
     return PNP_ERR_ARG;
   }
@@ -702,45 +798,64 @@ extern "C" int32_t pnp_tqc_update(const pnp_tqc_desc* d, const pnp_tqc_batch* b,
   g.eps_pi = b->eps_pi; g.eps_next = b->eps_next;
   g.log_ent_coef = d->log_ent_coef;
   g.ws = d->workspace;
-  g.part_c = g.ws + (size_t)S * WS_SLAB;
-  g.part_a = g.part_c + (size_t)S * CRIT_P;
-  g.part_s = g.part_a + (size_t)S * ACT_P;
+  g.sums = g.ws + (size_t)NMAT * B * HID;
   g.logs = d->logs;
   g.gamma = d->gamma;
   g.target_entropy = d->target_entropy;
-  g.B = d->batch;
-  hipLaunchKernelGGL(tqc_critic_kernel, dim3(S), dim3(NTH), 0, st, g);
-  if (const int32_t rc = pnp_check_launch("tqc_critic_kernel")) return rc;
-  AdamArgs ac{};
-  for (int i = 0; i < 8; i++) {
-    ac.p[i] = d->critic[i]; ac.m[i] = d->critic_m[i]; ac.v[i] = d->critic_v[i]; ac.tgt[i] = d->target[i];
-    ac.step[i] = d->critic_step[i]; ac.off[i] = crit_off(i);
-  }
-  ac.off[8] = CRIT_P; ac.nt = 8;
-  ac.part = g.part_c; ac.nparts = S; ac.stride = CRIT_P;
-  ac.lr = d->lr; ac.beta1 = d->beta1; ac.beta2 = d->beta2; ac.eps = d->adam_eps; ac.tau = d->tau;
-  ac.grad_out = grads_out ? grads_out + ACT_P : nullptr;
+  g.B = B;
+  for (int i = 0; i < 10; i++) g.astep[i] = d->actor_step[i];
+  for (int i = 0; i < 8; i++) g.cstep[i] = d->critic_step[i];
+  g.cstep[8] = d->ent_step;
+  float* ws = d->workspace;
+  auto M = [&](int id) { return ws + (size_t)id * B * HID; };
+  float* SM = M(M_SM);
+
+  hipLaunchKernelGGL(tqc_fwd_kernel, dim3(S, 1 + 2 * NC), dim3(NTH), 0, st, g);
+  if (const int32_t rc = pnp_check_launch("tqc_fwd_kernel")) return rc;
+  hipLaunchKernelGGL(tqc_critic_bwd_kernel, dim3(S, NC), dim3(NTH), 0, st, g);
+  if (const int32_t rc = pnp_check_launch("tqc_critic_bwd_kernel")) return rc;
+
+  WArgs ac{};
+  ac.B = B; ac.lr = d->lr; ac.beta1 = d->beta1; ac.beta2 = d->beta2; ac.eps = d->adam_eps; ac.tau = d->tau;
+  WArgs aa = ac;
+  ac.step_add = 1.f;   // the critics' steps: incremented by K4
+  aa.step_add = 0.f;   // the actor's: by K1
+  int tiles = 0;
+  for (int c = 0; c < NC; c++)
+    for (int l = 0; l < 4; l++) {
+      const int K = l == 0 ? NIN : HID, N = l == 3 ? NQ : HID, tw = 2 * l, tb = 2 * l + 1;
+      const size_t ow = (size_t)c * K * N, ob = (size_t)c * N;
+      const float* x0 = l == 0 ? b->obs : M(M_CH + 3 * c + l - 1);
+      const float* dy = l == 3 ? SM + S_DQ + c * NQ : M(M_CD + 3 * c + l);
+      tiles = add_wjob(ac, tiles, x0, l == 0 ? OBS : HID, l == 0 ? OBS : K, l == 0 ? b->act : x0, l == 0 ? ACT : HID, dy, K, N,
+                       0, d->critic[tw] + ow, d->critic_m[tw] + ow, d->critic_v[tw] + ow, d->target[tw] + ow,
+                       d->critic_step[tw], d->critic[tb] + ob, d->critic_m[tb] + ob, d->critic_v[tb] + ob,
+                       d->target[tb] + ob, d->critic_step[tb], ACT_P + crit_off(tw) + (int)ow, ACT_P + crit_off(tb) + (int)ob);
+    }
+  ac.grad_out = grads_out;
   ac.ent = d->log_ent_coef; ac.ent_m = d->ent_m; ac.ent_v = d->ent_v; ac.ent_step = d->ent_step;
-  ac.part_s = g.part_s; ac.nslab = S; ac.target_entropy = d->target_entropy; ac.B = d->batch; ac.logs = d->logs;
-  ac.critic_scale = 1.f / ((float)d->batch * NC * NQ * (NALL - 2 * NC));
-  hipLaunchKernelGGL(tqc_adam_kernel, dim3((CRIT_P + 255) / 256), dim3(256), 0, st, ac);
-  if (const int32_t rc = pnp_check_launch("tqc_adam_kernel (critics)")) return rc;
-  hipLaunchKernelGGL(tqc_step_inc, dim3(1), dim3(64), 0, st, ac);
-  if (const int32_t rc = pnp_check_launch("tqc_step_inc (critics)")) return rc;
-  hipLaunchKernelGGL(tqc_actor_kernel, dim3(S), dim3(NTH), 0, st, g);
-  if (const int32_t rc = pnp_check_launch("tqc_actor_kernel")) return rc;
-  AdamArgs aa{};
-  for (int i = 0; i < 10; i++) {
-    aa.p[i] = d->actor[i]; aa.m[i] = d->actor_m[i]; aa.v[i] = d->actor_v[i]; aa.tgt[i] = nullptr;
-    aa.step[i] = d->actor_step[i]; aa.off[i] = act_off(i);
+  ac.sums = g.sums; ac.nslab = S; ac.logs = d->logs;
+  ac.critic_scale = 1.f / ((float)B * NC * NQ * KEEP);
+  hipLaunchKernelGGL(tqc_wgrad_adam_kernel, dim3(tiles), dim3(WTH), 0, st, ac);
+  if (const int32_t rc = pnp_check_launch("tqc_wgrad_adam_kernel (critics)")) return rc;
+
+  hipLaunchKernelGGL(tqc_pi_critic_kernel, dim3(S, NC), dim3(NTH), 0, st, g);
+  if (const int32_t rc = pnp_check_launch("tqc_pi_critic_kernel")) return rc;
+  hipLaunchKernelGGL(tqc_actor_bwd_kernel, dim3(S), dim3(NTH), 0, st, g);
+  if (const int32_t rc = pnp_check_launch("tqc_actor_bwd_kernel")) return rc;
+
+  tiles = 0;
+  for (int l = 0; l < 5; l++) {
+    const int K = l == 0 ? OBS : HID, N = l >= 3 ? ACT : HID, tw = 2 * l, tb = 2 * l + 1;
+    const float* x0 = l == 0 ? b->obs : M(M_AH + (l < 3 ? l - 1 : 2));
+    const float* dy = l == 3 ? SM + S_DMU : l == 4 ? SM + S_DLS : M(M_AD + l);
+    tiles = add_wjob(aa, tiles, x0, l == 0 ? OBS : HID, K, x0, HID, dy, K, N, 1, d->actor[tw], d->actor_m[tw],
+                     d->actor_v[tw], nullptr, d->actor_step[tw], d->actor[tb], d->actor_m[tb], d->actor_v[tb], nullptr,
+                     d->actor_step[tb], act_off(tw), act_off(tb));
   }
-  aa.off[10] = ACT_P; aa.nt = 10;
-  aa.part = g.part_a; aa.nparts = S; aa.stride = ACT_P;
-  aa.lr = d->lr; aa.beta1 = d->beta1; aa.beta2 = d->beta2; aa.eps = d->adam_eps; aa.tau = d->tau;
   aa.grad_out = grads_out;
-  aa.part_s = g.part_s; aa.nslab = S; aa.B = d->batch; aa.logs = d->logs;
-  hipLaunchKernelGGL(tqc_adam_kernel, dim3((ACT_P + 255) / 256), dim3(256), 0, st, aa);
-  if (const int32_t rc = pnp_check_launch("tqc_adam_kernel (actor)")) return rc;
-  hipLaunchKernelGGL(tqc_step_inc, dim3(1), dim3(64), 0, st, aa);
-  return pnp_check_launch("tqc_step_inc (actor)");
+  aa.sums = g.sums; aa.nslab = S; aa.logs = d->logs; aa.actor = 1;
+  hipLaunchKernelGGL(tqc_wgrad_adam_kernel, dim3(tiles), dim3(WTH), 0, st, aa);
+  if (const int32_t rc = pnp_check_launch("tqc_wgrad_adam_kernel (actor)")) return rc;
+  return PNP_OK;
 }

@@ -10,7 +10,7 @@ from .model import PnpIKParams, PnpModelDesc
 # PNP_LIB: another build of the same sources (tools/asan_cpu_tests.sh: the host-sanitizer build)
 LIB_PATH = os.environ.get("PNP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpnp.so")
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 # every symbol include/pnp.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -21,7 +21,7 @@ EXPORTS = [
     "pnp_env_params_size", "pnp_env_init", "pnp_env_init_f64", "pnp_env_reset", "pnp_env_reset_f64",
     "pnp_env_step", "pnp_env_step_f64", "pnp_env_evaluate", "pnp_env_evaluate_f64",
     "pnp_slerp_track_f64", "pnp_env_queue_status", "pnp_tqc_workspace_floats", "pnp_tqc_param_counts",
-    "pnp_tqc_update",
+    "pnp_tqc_update", "pnp_tqc_sample",
 ]
 
 STATE_FIELDS = ("qpos", "qvel", "ctrl", "mocap_pos", "mocap_quat", "qacc_warmstart", "time", "warn")
@@ -81,6 +81,14 @@ class PnpTqcDesc(C.Structure):
 
 class PnpTqcBatch(C.Structure):
     _fields_ = [(f, C.c_void_p) for f in ("obs", "act", "next_obs", "done", "reward", "eps_pi", "eps_next")]
+
+
+class PnpTqcReplay(C.Structure):
+    """include/pnp.h pnp_tqc_replay."""
+    _fields_ = [(f, C.c_void_p) for f in ("obs", "next_obs", "actions", "rewards", "dones", "upper")] + \
+               [("rows", C.c_int32), ("n_envs", C.c_int32), ("obs_dim", C.c_int32), ("act_dim", C.c_int32),
+                ("n_keys", C.c_int32), ("key_dim", C.c_int32 * 4), ("mean", C.c_void_p * 4), ("var", C.c_void_p * 4),
+                ("clip_obs", C.c_double), ("norm_eps", C.c_double)]
 
 
 # debug record layout (include/pnp.h PNP_DBG_*)
@@ -170,6 +178,8 @@ def load():
     L.pnp_tqc_param_counts.restype = I32
     L.pnp_tqc_update.argtypes = [C.POINTER(PnpTqcDesc), C.POINTER(PnpTqcBatch), P, P]
     L.pnp_tqc_update.restype = I32
+    L.pnp_tqc_sample.argtypes = [C.POINTER(PnpTqcReplay), P, I32, P, P, P, P, P, P]
+    L.pnp_tqc_sample.restype = I32
     if L.pnp_abi_version() != ABI_VERSION:
         raise PnpError(f"libpnp ABI {L.pnp_abi_version()} != binding ABI {ABI_VERSION}")
     if L.pnp_env_params_size() != C.sizeof(PnpEnvParams):

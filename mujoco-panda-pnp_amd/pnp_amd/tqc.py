@@ -313,6 +313,7 @@ class TQC:
         self._graph = None          # the captured gradient step (TQC._capture)
         self._graph_out = None
         self._fdesc = None          # pnp_tqc_desc of the fused step (TQC._fused_desc)
+        self._frb = None            # pnp_tqc_replay of the fused sample (TQC._fused_replay)
         self._eager_updates = 0     # steps run eagerly before the capture (allocator / optimiser state)
         self.vecnorm = VecNormalize(dims, self.device, c.clip_obs, c.norm_eps)
         self.buffer = DictReplayBuffer(c.buffer_size, self.n_envs, self.obs_dim, self.act_dim, self.device)
@@ -521,16 +522,51 @@ class TQC:
         self._fdesc = d
         return d
 
+    def _fused_replay(self):
+        """pnp_tqc_replay over the replay buffer's and the normaliser's device tensors (fixed
+        addresses: the buffer is written in place, VecNormalize updates its statistics in place),
+        and the sampled batch's buffers."""
+        if self._frb is not None:
+            return self._frb
+        from . import _lib
+        rb, vn, B = self.buffer, self.vecnorm, self.cfg.batch_size
+        r = _lib.PnpTqcReplay()
+        r.obs, r.next_obs, r.actions, r.rewards, r.dones, r.upper = (
+            t.data_ptr() for t in (rb.obs, rb.next_obs, rb.actions, rb.rewards, rb.dones, rb.upper))
+        r.rows, r.n_envs, r.obs_dim, r.act_dim, r.n_keys = rb.size, rb.n_envs, self.obs_dim, self.act_dim, len(OBS_KEYS)
+        for k, key in enumerate(OBS_KEYS):
+            rms = vn.obs_rms[key]
+            r.key_dim[k], r.mean[k], r.var[k] = rms.mean.numel(), rms.mean.data_ptr(), rms.var.data_ptr()
+        r.clip_obs, r.norm_eps = vn.clip_obs, vn.epsilon
+        z = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)
+        self._fsb = (z(B, self.obs_dim), z(B, self.act_dim), z(B, self.obs_dim), z(B, 1), z(B, 1))
+        self._frb = r
+        return r
+
+    def _sample_fused(self):
+        """_sample_norm in one launch (pnp_tqc_sample): the same U[0, 1) draw, the same batch bit
+        for bit (tests/test_tqc_gpu.py)."""
+        from . import _lib
+        L = _lib.load()
+        r = self._fused_replay()
+        B = self.cfg.batch_size
+        u = torch.rand(2, B, device=self.device, generator=self.gen)
+        out = self._fsb
+        _lib.check(L.pnp_tqc_sample(C.byref(r), u.data_ptr(), B, *[t.data_ptr() for t in out],
+                                    C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)), "pnp_tqc_sample")
+        self._fu = u   # alive until the launch has read it
+        return out
+
     def _update_fused(self, grads_out=None):
-        """One gradient step by pnp_tqc_update (csrc/tqc_fused.hip): the same replay sample and the
-        same two N(0, 1) draws as _update (sb3's order), then the whole step -- entropy coefficient,
-        critics, Polyak, actor -- in four launches.  grads_out (tests): the step's reduced
-        gradients, actor then critics."""
+        """One gradient step by pnp_tqc_sample + pnp_tqc_update (csrc/tqc_fused.hip): the same
+        replay sample and the same two N(0, 1) draws as _update (sb3's order), then the whole step
+        -- entropy coefficient, critics, Polyak, actor.  grads_out (tests): the step's gradients,
+        actor then critics."""
         from . import _lib
         L = _lib.load()
         d = self._fused_desc()
         c = self.cfg
-        obs, act, nobs, done, rew = self._sample_norm()
+        obs, act, nobs, done, rew = self._sample_fused()
         B = c.batch_size
         eps_pi = torch.randn(B, self.act_dim, device=self.device, generator=self.gen)
         eps_next = torch.randn(B, self.act_dim, device=self.device, generator=self.gen)

@@ -152,8 +152,27 @@ def _fused_agent(B=64, **cfg):
     return a
 
 
+def test_fused_sample_matches_pytorch():
+    """pnp_tqc_sample (one launch) against DictReplayBuffer.sample + VecNormalize.normalize +
+    flat_obs (pnp_amd/tqc.py TQC._sample_norm) from the same generator state: the same rows, the
+    normalised observations bit for bit, on a partly filled buffer (indices below `upper`) and with
+    statistics that clip (achieved_goal's variance shrunk so |x| > clip_obs)."""
+    a = _fused_agent(graph=False)
+    for trial in range(3):
+        a.vecnorm.obs_rms["achieved_goal"].var.fill_(1e-12)   # these three columns clip at +-10
+        gs = a.gen.get_state()
+        ref = [t.clone() for t in a._sample_norm()]
+        a.gen.set_state(gs)
+        got = a._sample_fused()
+        torch.cuda.synchronize()
+        for name, x, y in zip(("obs", "act", "next_obs", "done", "reward"), got, ref):
+            assert x.shape == y.shape and torch.equal(x, y), (trial, name, float((x - y).abs().max()))
+        assert float(got[0][:, :3].abs().max()) == a.vecnorm.clip_obs > float(got[0][:, 3:].abs().max())
+        a.collect_step()
+
+
 def test_fused_learner_step_matches_pytorch():
-    """pnp_tqc_update (csrc/tqc_fused.hip: the whole TQC gradient step in four launches) against
+    """pnp_tqc_update (csrc/tqc_fused.hip: the whole TQC gradient step on the matrix cores) against
     the PyTorch step (pnp_amd/tqc.py _update_torch, autograd) from the same state, replay sample and
     Gaussian draws: every gradient tensor it applies within 1e-4 (critics) / 1e-3 (actor, computed
     against the Adam-updated critics) of the PyTorch gradient in norm, the logged losses within
