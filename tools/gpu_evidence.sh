@@ -1,10 +1,11 @@
 #!/bin/bash
 # Round evidence on the current tree, one GPU-box pass (each GPU step under its own time limit; a
 # fault, abort or timeout ends the script):
-#   1. every GPU test (step tests first), 2. smoke(), 3. the default bench (CPU baseline included),
+#   1. every GPU test, 2. smoke(), 3. the default bench (CPU baseline included),
 #   4. rocprofv3 kernel trace + stats of the bench's step and gym legs,
 #   5. PMC HBM traffic of the step leg (FETCH_SIZE and WRITE_SIZE in separate passes),
-#   6. SQ counters of the step leg (two passes of 8), 7. the stage-cycle profile on bench inputs.
+#   6. SQ counters of the step leg (two passes of 8), 7. the stage-cycle profile on bench inputs,
+#   8. rocprofv3 kernel trace of the fused TQC learner step.
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out"; mkdir -p "$OUT"; cd "$ROOT"
@@ -18,9 +19,7 @@ step() {  # name, timeout, cmd...  (pytest's exit 1 = test failures: reported, t
   if [ $rc -ne 0 ] && ! { [ "$name" = pytest ] && [ $rc -eq 1 ]; }; then exit $rc; fi
 }
 if [ -z "${SKIP_TESTS:-}" ]; then
-  step pytest 1100 python -u -m pytest tests/test_step_gpu.py tests/test_ik_gpu.py tests/test_env_gpu.py \
-    tests/test_tqc_gpu.py tests/test_skills_gpu.py tests/test_reference_behaviour_gpu.py tests/test_bt_gpu.py \
-    -m gpu -v --timeout 240 --timeout-method thread
+  step pytest 1100 python -u -m pytest tests -m gpu -v -s --timeout 240 --timeout-method thread
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 step bench 600 python -u bench.py
@@ -45,4 +44,9 @@ python3 tools/pmc_traffic.py "$OUT/${TAG}_pmc_FETCH_SIZE" "$OUT/${TAG}_pmc_WRITE
 python3 tools/sq_summary.py "$OUT/${TAG}_sq_p1" "$OUT/${TAG}_sq_p2" "pnp_compact::step_kernel<float, false>" \
   --json "$OUT/${TAG}_sq.json" --waves-per-simd 2 > "$OUT/${TAG}_sq_summary.txt" 2>&1; tail -12 "$OUT/${TAG}_sq_summary.txt"
 step stageprof 300 python3 -u tools/step_parity.py 4096 prof bench
+cd /tmp
+# the fused TQC learner step (C5 at train.py's update ratio is ~all learner): kernel trace
+step tqc_prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_tqc_prof" -o run -- \
+  python3 "$ROOT/tools/tqc_learner_bench.py" fused 200
+cd "$ROOT"
 echo "all done"
