@@ -254,6 +254,33 @@ static int box_face_contacts(const double* pr, const double* Rr, const double* s
   return cnt;
 }
 
+/* Box-box (MuJoCo 2.3.3 engine_collision_box.c mjc_BoxBox -- absent here; what follows is a
+ * separating-axis restatement, and each point where it may differ from MuJoCo's routine is an
+ * assumption, unverified, listed so a reader with the source can check them one by one):
+ *   A1. Axes: the 15 SAT axes -- box 1's face normals, box 2's, then the 9 edge cross products
+ *       A_i x B_j (skipped when |A_i x B_j| < 1e-6: parallel edges add nothing a face axis lacks).
+ *   A2. Separation on any axis beyond the margin: no contact (the pair's early exit).
+ *   A3. The contact axis is the one of least penetration, with ties and near-ties resolved toward
+ *       faces: box 2's face replaces box 1's only when deeper by more than BB_TOL, and an edge axis
+ *       wins only when 1.05 x its separation still beats the best face's (ODE's dBoxBox uses the
+ *       same 1.05 edge fudge factor; MuJoCo's exact bias is assumed, not known).
+ *   A4. Face axis: the incident face of the other box (the face most anti-parallel to the contact
+ *       normal) is clipped against the reference face's rectangle (grown by BB_TOL); the contacts
+ *       are the clipped polygon's vertices -- incident edge entry / exit points in edge order, then
+ *       the reference corners inside the incident face -- at most 8, each with its own depth along
+ *       the normal, kept when that depth is within the margin.  MuJoCo may reduce the polygon to
+ *       fewer points (a known difference of contact COUNT on tilted faces, not on a box resting
+ *       flat, where every routine yields the four corners of the contact face).
+ *   A5. Contact position: halfway between the two surfaces along the normal (MuJoCo's convention
+ *       for every primitive pair), normal from box 1 to box 2, dist = -penetration.
+ *   A6. Edge axis: one contact at the midpoint of the two edges' closest points, depth = the axis
+ *       separation.
+ * Pinned without MuJoCo by geometric known answers (tests/test_boxbox_cpu.py: a cube resting flat,
+ * tilted onto an edge and onto a corner, two cubes crossing edge to edge, deep spawns inside a shelf
+ * or table leg and inside another cube -- the contact points and depths any correct box-box routine
+ * must produce there) and by the reference's behavioural tests (grasp, lift, placement).  The
+ * device colliders (collide_dev.h c_box_box / c_box_face) are this routine in box-relative
+ * coordinates, equal to it at 1e-9 in fp64 (tests/test_boxbox_gpu.py). */
 static int box_box(const double* p1, const double* R1, const double* s1, const double* p2, const double* R2,
                    const double* s2, double margin, orc_contact* c) {
   double T[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
