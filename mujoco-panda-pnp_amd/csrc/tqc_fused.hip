@@ -150,22 +150,26 @@ __device__ void slab_gemm(const float* X, const float* __restrict__ W, float* Ws
       if (GK % KC != 0)
 #pragma unroll
         for (int s = 0; s < 4; s++) a[s] = k + s < GK ? a[s] : 0.f;
+      f32x4 b[2];
 #pragma unroll
       for (int q = 0; q < 2; q++) {
-        const int tile = wv + q * NW;
-        if (tile < NTILE) {
-          const int c = tile * 16 + i;
-          f32x4 b;
+        const int c = (wv + q * NW) * 16 + i;
+        if (wv + q * NW < NTILE) {
           if (CR) {
-            b = *reinterpret_cast<const f32x4*>(D + c * LDT + k0);
+            b[q] = *reinterpret_cast<const f32x4*>(D + c * LDT + k0);
           } else {
 #pragma unroll
-            for (int s = 0; s < 4; s++) b[s] = D[(k0 + s) * LDW + c];
+            for (int s = 0; s < 4; s++) b[q][s] = D[(k0 + s) * LDW + c];
           }
-#pragma unroll
-          for (int s = 0; s < 4; s++) acc[q] = mfma4(a[s], b[s], acc[q]);
         }
       }
+      // the two tiles' accumulations alternate: a dependent MFMA is issued two slots after its
+      // source (past the 40-cycle dependent latency), not back to back
+#pragma unroll
+      for (int s = 0; s < 4; s++)
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+          if (wv + q * NW < NTILE) acc[q] = mfma4(a[s], b[q][s], acc[q]);
     }
     if (ch + 1 < NCH) put((ch + 1) & 1, ch + 1);
     __syncthreads();
@@ -176,14 +180,20 @@ __device__ void slab_gemm(const float* X, const float* __restrict__ W, float* Ws
 template <bool TR, int K, int N>
 __device__ __attribute__((noinline)) void lin_fwd(const float* X, const float* __restrict__ W, const float* __restrict__ bias,
                                                   float* Y, bool relu, float* Ws) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 15, kq = lane >> 4;
+  float bq[2];   // the bias loads issued before the product (their latency hidden under it)
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const int n = (wv + q * NW) * 16 + i;
+    bq[q] = n < N ? bias[n] : 0.f;
+  }
   f32x4 acc[2];
   slab_gemm<TR, K, N>(X, W, Ws, acc);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 15, kq = lane >> 4;
 #pragma unroll
   for (int q = 0; q < 2; q++) {
     const int n = (wv + q * NW) * 16 + i;
     if (n < N) {
-      const float bn = bias[n];
+      const float bn = bq[q];
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const float v = bn + acc[q][r];
