@@ -44,10 +44,14 @@ constexpr int NTH = 64 * NW;
 constexpr int KC = 32;             // reduction rows per staged weight chunk
 constexpr int OBS = 25, ACT = 7, HID = 256, NC = 2, NQ = 25, NIN = OBS + ACT, NALL = NC * NQ;
 constexpr int KEEP = NALL - 2 * NC;   // target quantiles kept (top_quantiles_to_drop_per_net = 2)
-constexpr int LD = HID + 4;        // LDS row stride of the slab buffers (floats; = 4 mod 64: the A
-                                   // operand's b128 reads are conflict-free)
-constexpr int LDT = KC + 4;        // staged weight chunk, [column][reduction row] layout (CR)
-constexpr int LDW = HID + 4;       // staged weight chunk, [reduction row][column] layout (RC)
+// LDS strides, from gfx950's ds_read_b128 lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...,
+// bank = dword address mod 64; MI355X_MICROARCH.md LDS table): lane (kq, i) of an MFMA operand read
+// fetches 4 dwords at i * S + 4 kq, and a stride S = 8 mod 16 (S / 4 = 2 mod 4) puts the 16 lanes
+// of every group on 64 distinct banks (S = 4 mod 64 collided 2-way)
+constexpr int LD = HID + 8;        // slab buffers (A operands, activations)
+constexpr int LDT = KC + 8;        // staged weight chunk, [column][reduction row] layout (CR)
+constexpr int LDW = HID + 4;       // staged weight chunk, [reduction row][column] layout (RC): its b32
+                                   // reads (32-lane groups, bank mod 32) need 4 LDW = 16 mod 32
 constexpr int WCH = HID * LDT > KC * LDW ? HID * LDT : KC * LDW;   // one chunk buffer (floats)
 constexpr float LOG_STD_MIN = -20.0f, LOG_STD_MAX = 2.0f, SQUASH_EPS = 1e-6f;
 constexpr float HALF_LOG_2PI = 0.91893853320467274178f;
@@ -87,37 +91,43 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 template <bool CR, int GK, int GN>
 __device__ void slab_gemm(const float* X, const float* __restrict__ W, float* Ws, f32x4 acc[2]) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, i = lane & 15, kq = lane >> 4;
-  constexpr int NTILE = (GN + 15) / 16, NCH = (GK + KC - 1) / KC;
+  // narrow products (N <= 32: the heads, the critics' quantile layer, the input gradient) stage
+  // the whole reduction at once -- one chunk, one barrier -- instead of 8 chunks whose MFMA work
+  // (one or two tiles) could not cover a chunk's load latency
+  constexpr int KCE = GN <= 32 ? (GK + 15) / 16 * 16 : KC;
+  constexpr int LDTE = KCE + 8;                              // = 8 mod 16: conflict-free b128 reads
+  constexpr int LDWE = GN <= 32 ? 28 : LDW;                  // 4 LDWE = 16 or 48 mod 64: conflict-free
+  constexpr int NTILE = (GN + 15) / 16, NCH = (GK + KCE - 1) / KCE;
   constexpr int LDG = CR ? GK : GN;                          // global row stride
   constexpr bool VEC = LDG % 4 == 0;
-  constexpr int NUNIT = VEC ? KC * GN / 4 : KC * GN;          // float4 (or float) units per chunk
+  constexpr int NUNIT = VEC ? KCE * GN / 4 : KCE * GN;        // float4 (or float) units per chunk
   constexpr int PER = (NUNIT + NTH - 1) / NTH;
-  static_assert(NTILE <= 2 * NW && (CR ? GN * LDT : KC * LDW) <= WCH, "slab_gemm shape");
+  static_assert(NTILE <= 2 * NW && (CR ? NTILE * 16 * LDTE : KCE * LDWE) <= WCH && (CR || GN <= LDWE),
+                "slab_gemm shape");
   acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
   acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
   using U = typename std::conditional<VEC, f32x4, float>::type;
-  U pre[PER];
   // unit u of chunk ch: its global address, its LDS slot, whether it lies inside the matrix
   auto unit = [&](int u, int ch, const float*& src, int& dst, bool& in) {
     if (VEC) {
       if (CR) {
-        const int c = u / (KC / 4), j = u % (KC / 4), r = ch * KC + 4 * j;
-        src = W + (size_t)c * LDG + r; dst = c * LDT + 4 * j; in = r < GK;
+        const int c = u / (KCE / 4), j = u % (KCE / 4), r = ch * KCE + 4 * j;
+        src = W + (size_t)c * LDG + r; dst = c * LDTE + 4 * j; in = r < GK;
       } else {
-        const int rr = u / (GN / 4), j = u % (GN / 4), r = ch * KC + rr;
-        src = W + (size_t)r * LDG + 4 * j; dst = rr * LDW + 4 * j; in = r < GK;
+        const int rr = u / (GN / 4), j = u % (GN / 4), r = ch * KCE + rr;
+        src = W + (size_t)r * LDG + 4 * j; dst = rr * LDWE + 4 * j; in = r < GK;
       }
     } else {
       if (CR) {
-        const int c = u / KC, rr = u % KC, r = ch * KC + rr;
-        src = W + (size_t)c * LDG + r; dst = c * LDT + rr; in = r < GK;
+        const int c = u / KCE, rr = u % KCE, r = ch * KCE + rr;
+        src = W + (size_t)c * LDG + r; dst = c * LDTE + rr; in = r < GK;
       } else {
-        const int rr = u / GN, c = u % GN, r = ch * KC + rr;
-        src = W + (size_t)r * LDG + c; dst = rr * LDW + c; in = r < GK;
+        const int rr = u / GN, c = u % GN, r = ch * KCE + rr;
+        src = W + (size_t)r * LDG + c; dst = rr * LDWE + c; in = r < GK;
       }
     }
   };
-  auto fetch = [&](int ch) {
+  auto fetch = [&](U (&pre)[PER], int ch) {
 #pragma unroll
     for (int j = 0; j < PER; j++) {
       const int u = t + j * NTH;
@@ -127,7 +137,7 @@ __device__ void slab_gemm(const float* X, const float* __restrict__ W, float* Ws
       if (u < NUNIT && in) pre[j] = *reinterpret_cast<const U*>(src);
     }
   };
-  auto put = [&](int buf, int ch) {
+  auto put = [&](const U (&pre)[PER], int buf, int ch) {
     float* D = Ws + buf * WCH;
 #pragma unroll
     for (int j = 0; j < PER; j++) {
@@ -137,17 +147,13 @@ __device__ void slab_gemm(const float* X, const float* __restrict__ W, float* Ws
       if (u < NUNIT) *reinterpret_cast<U*>(D + dst) = pre[j];
     }
   };
-  fetch(0);
-  put(0, 0);
-  __syncthreads();
-  for (int ch = 0; ch < NCH; ch++) {
-    if (ch + 1 < NCH) fetch(ch + 1);
-    const float* D = Ws + (ch & 1) * WCH;
+  auto compute = [&](int buf, int ch) {
+    const float* D = Ws + buf * WCH;
 #pragma unroll
-    for (int kb = 0; kb < KC; kb += 16) {
-      const int k0 = kb + 4 * kq, k = ch * KC + k0;
+    for (int kb = 0; kb < KCE; kb += 16) {
+      const int k0 = kb + 4 * kq, k = ch * KCE + k0;
       f32x4 a = *reinterpret_cast<const f32x4*>(X + i * LD + k);
-      if (GK % KC != 0)
+      if (GK % KCE != 0)
 #pragma unroll
         for (int s = 0; s < 4; s++) a[s] = k + s < GK ? a[s] : 0.f;
       f32x4 b[2];
@@ -156,10 +162,10 @@ __device__ void slab_gemm(const float* X, const float* __restrict__ W, float* Ws
         const int c = (wv + q * NW) * 16 + i;
         if (wv + q * NW < NTILE) {
           if (CR) {
-            b[q] = *reinterpret_cast<const f32x4*>(D + c * LDT + k0);
+            b[q] = *reinterpret_cast<const f32x4*>(D + c * LDTE + k0);
           } else {
 #pragma unroll
-            for (int s = 0; s < 4; s++) b[q][s] = D[(k0 + s) * LDW + c];
+            for (int s = 0; s < 4; s++) b[q][s] = D[(k0 + s) * LDWE + c];
           }
         }
       }
@@ -171,7 +177,24 @@ __device__ void slab_gemm(const float* X, const float* __restrict__ W, float* Ws
         for (int q = 0; q < 2; q++)
           if (wv + q * NW < NTILE) acc[q] = mfma4(a[s], b[q][s], acc[q]);
     }
-    if (ch + 1 < NCH) put((ch + 1) & 1, ch + 1);
+  };
+  // two register stages: chunk ch + 2's global loads are issued before chunk ch's MFMAs, and chunk
+  // ch + 1 (loaded a whole chunk earlier) is stored to the other LDS buffer after them -- the
+  // loads have two chunks of MFMA work to land in, one was not enough to cover L2 latency
+  U p0[PER], p1[PER];
+  fetch(p0, 0);
+  if (NCH > 1) fetch(p1, 1);
+  put(p0, 0, 0);
+  __syncthreads();
+  for (int ch = 0; ch < NCH; ch += 2) {
+    if (ch + 2 < NCH) fetch(p0, ch + 2);
+    compute(0, ch);
+    if (ch + 1 < NCH) put(p1, 1, ch + 1);
+    __syncthreads();
+    if (ch + 1 >= NCH) break;
+    if (ch + 3 < NCH) fetch(p1, ch + 3);
+    compute(1, ch + 1);
+    if (ch + 2 < NCH) put(p0, 0, ch + 2);
     __syncthreads();
   }
 }
@@ -285,7 +308,7 @@ __host__ __device__ constexpr int act_size(int t) {
 __host__ __device__ constexpr int act_off(int t) { return t == 0 ? 0 : act_off(t - 1) + act_size(t - 1); }
 constexpr int ACT_P = act_off(10);
 
-struct alignas(16) Lds {   // 136 KB (a workgroup may hold all 160 KB of a CU's LDS)
+struct alignas(16) Lds {   // 146 KB (a workgroup may hold all 160 KB of a CU's LDS)
   float A[R * LD], Bf[R * LD], C[R * LD];
   float W[2 * WCH];
   float row[R][NALL + 14], q[R][NALL], tq[R][NALL];
@@ -621,10 +644,10 @@ __global__ void __launch_bounds__(WTH) tqc_wgrad_adam_kernel(WArgs a) {
 #pragma unroll
     for (int h2 = 0; h2 < 2; h2++) acc[h][h2] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int rows = a.B / WNW, b0 = w * rows, b1 = b0 + rows;
-  for (int b = b0; b < b1; b += 16) {   // four row groups per trip: 16 loads in flight
-    float xa[4][2], yb[4][2];
+  for (int b = b0; b < b1; b += 32) {   // eight row groups per trip: 32 loads in flight
+    float xa[8][2], yb[8][2];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < 8; u++) {
       const int bb = b + 4 * u;
       const size_t r = bb + kq;
 #pragma unroll
@@ -634,7 +657,7 @@ __global__ void __launch_bounds__(WTH) tqc_wgrad_adam_kernel(WArgs a) {
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++)
+    for (int u = 0; u < 8; u++)
 #pragma unroll
       for (int h = 0; h < 2; h++)
 #pragma unroll
