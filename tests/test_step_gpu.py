@@ -22,9 +22,11 @@ Tolerances:
     under it: an fp32 computation cannot be held closer than its inputs' rounding moves the
     answer).  On `scene` / `fresh` every tree is within 1e-5 except scene's cube2 (2.1e-5, under
     its own 3.0e-5 floor).  Convex-mesh contacts (`mesh_scene`; the closed-finger `pressed`
-    states) run libccd's MPR, whose termination tolerance makes the contact normal / depth
-    path-dependent (contact Jacobian 1.7e-4 apart): arm 4.2e-5 / 1.1e-4 against floors of
-    5.8e-5 / 5.1e-5.
+    states) run libccd's MPR in fp64 on frames built from the fp64 chain (round 5): measured
+    (profiles/r05/gpu_tests.log) mesh arm 9.3e-6 (0.43 of its bar), pressed arm 1.39e-4 = 0.90 of
+    its one-ulp bar (floor ~5e-5: the pads' 16-56 stiff contacts inside one tree).  The
+    world-scale floor (half an fp32 ulp of 1.0 per coordinate) is printed beside it, not
+    asserted.
   * Full BASELINE size (B = 4096): size-independent properties — bit-identical results across
     launches and across batch splits (shard invariance), finite state, no warnings.
 """
@@ -286,11 +288,10 @@ def test_step_f32_matches_oracle_per_tree(engine, model, fixture, request):
     state makes in the exact result (`_conditioning_floor`: an fp32 computation cannot be held
     closer than its inputs' own rounding moves the answer; the pipeline rounds many times).
     Every env's tree against its own floor (a batch-wide floor would let one env's knife edge
-    decide another env's bar).  Measured (tools/f32_precision.py, profiles/r03/f32_precision.log):
-    box-contact fixtures 1e-7 .. 2.1e-5 per tree, every tree within 1e-5 or below its own floor
-    (scene cube2: 2.1e-5 against a floor of 3.0e-5); the MPR fixtures: mesh arm 4.2e-5 (floor
-    5.8e-5), pressed arm 1.1e-4 (floor 5.1e-5); with multiccd's contact fans (round 3) a cube held
-    by 8 mesh contacts 2.4e-5 against a floor of 1.4e-4 (tools/mccd_diag.py)."""
+    decide another env's bar).  Measured (round 5, profiles/r05/gpu_tests.log, worst error / bar
+    per tree): scene and fresh within 1e-5 but scene's cube2 (under its own floor); mesh_scene arm
+    0.43; pressed arm 0.90 (1.39e-4 against a one-ulp floor of ~5e-5; round 4: 1.64e-4, 1.07x,
+    before the colliders took positions from the fp64 chain)."""
     _assert_per_tree(engine, model, request.getfixturevalue(fixture), 1, fixture)
 
 
