@@ -592,7 +592,10 @@ __global__ void __launch_bounds__(NTH) tqc_actor_bwd_kernel(TqcArgs g) {
 // 32 x 32 tile of (K + 1) x N; wave w reduces rows [w B / 4, (w + 1) B / 4) on the matrix cores
 // (A lane (kq, i) = X[b + kq][k0 + i], B lane = dY[b + kq][n0 + i]), the four partial tiles are
 // added in wave order through LDS and the tile's Adam runs in place.
-constexpr int WT = 32, WNW = 4, WTH = 64 * WNW, MAXJ = 10;
+// WRG: row groups of 4 a wave loads before its MFMAs -- 32 (128 rows: train.py's batch of 512
+// split over the 4 waves in one trip, 128 loads in flight per lane; the tiles' operands come from
+// L2 / the Infinity Cache, each trip waits one round trip)
+constexpr int WT = 32, WNW = 4, WTH = 64 * WNW, MAXJ = 10, WRG = 32;
 struct WJob {
   const float* x0; const float* x1; const float* dy;
   float* p; float* m; float* v; float* tgt; const float* step;       // weight ([out][in] if tr, else [in][out])
@@ -644,10 +647,10 @@ __global__ void __launch_bounds__(WTH) tqc_wgrad_adam_kernel(WArgs a) {
 #pragma unroll
     for (int h2 = 0; h2 < 2; h2++) acc[h][h2] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int rows = a.B / WNW, b0 = w * rows, b1 = b0 + rows;
-  for (int b = b0; b < b1; b += 32) {   // eight row groups per trip: 32 loads in flight
-    float xa[8][2], yb[8][2];
+  for (int b = b0; b < b1; b += 4 * WRG) {   // WRG row groups per trip, all their loads in flight
+    float xa[WRG][2], yb[WRG][2];
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
+    for (int u = 0; u < WRG; u++) {
       const int bb = b + 4 * u;
       const size_t r = bb + kq;
 #pragma unroll
@@ -657,7 +660,7 @@ __global__ void __launch_bounds__(WTH) tqc_wgrad_adam_kernel(WArgs a) {
       }
     }
 #pragma unroll
-    for (int u = 0; u < 8; u++)
+    for (int u = 0; u < WRG; u++)
 #pragma unroll
       for (int h = 0; h < 2; h++)
 #pragma unroll
