@@ -88,6 +88,32 @@ def test_library_rejects_bad_arguments_without_gpu():
     assert rc == -1 and b"bad argument" in L.pnp_last_error()
 
 
+def test_tqc_entry_points_validate_without_gpu():
+    """The fused learner's C entry points check shapes and pointers before any HIP call: the
+    workspace size for train.py's shape (25 matrices [B][256] + 8 sums per 16-row slab), the
+    parameter counts of the actor / critics, and refusals of unsupported shapes and null buffers."""
+    from pnp_amd import _lib
+    L = _lib.load()
+    d = _lib.PnpTqcDesc()
+    d.batch, d.obs_dim, d.act_dim, d.hidden, d.n_critics, d.n_quantiles, d.n_drop_per_net = 512, 25, 7, 256, 2, 25, 2
+    assert L.pnp_tqc_workspace_floats(C.byref(d)) == 25 * 512 * 256 + (512 // 16) * 8
+    na, nc = C.c_int32(), C.c_int32()
+    assert L.pnp_tqc_param_counts(C.byref(na), C.byref(nc)) == 0
+    # actor 25-256-256-256 + two 7-wide heads; critics 2 x (32-256-256-256-25)
+    assert na.value == 25 * 256 + 256 + 2 * (256 * 256 + 256) + 2 * (256 * 7 + 7)
+    assert nc.value == 2 * (32 * 256 + 256 + 2 * (256 * 256 + 256) + 256 * 25 + 25)
+    d.hidden = 128                                   # not train.py's network
+    assert L.pnp_tqc_workspace_floats(C.byref(d)) < 0 and b"unsupported" in L.pnp_last_error()
+    d.hidden, d.batch = 256, 500                     # not a multiple of 16 rows
+    assert L.pnp_tqc_workspace_floats(C.byref(d)) < 0
+    d.batch = 512
+    b = _lib.PnpTqcBatch()
+    assert L.pnp_tqc_update(C.byref(d), C.byref(b), None, None) < 0   # no parameter pointers
+    r = _lib.PnpTqcReplay()
+    assert L.pnp_tqc_sample(C.byref(r), None, 512, None, None, None, None, None, None) < 0
+    assert b"pnp_tqc_sample" in L.pnp_last_error()
+
+
 def test_product_package_never_imports_oracle():
     pkg = os.path.join(ROOT, "mujoco-panda-pnp_amd")
     for dp, _, fs in os.walk(pkg):
