@@ -381,10 +381,10 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_e
 #define PNP_GC_MAXJSLOT 800
 #define PNP_GC_JTCAP 768
 #define PNP_GC_HCAP 288
-#define PNP_GF_MAXCON 48
-#define PNP_GF_MAXEFC 208
-#define PNP_GF_MAXJSLOT 2048
-#define PNP_GF_JTCAP 1792
+#define PNP_GF_MAXCON 64
+#define PNP_GF_MAXEFC 272
+#define PNP_GF_MAXJSLOT 2688
+#define PNP_GF_JTCAP 2560
 template <typename T>
 __device__ __forceinline__ int tier_need(const DevPhys<T>& m, const Env<T>& s) {
   const int ne = s.nefc, nc = s.ncon_raw;
@@ -467,7 +467,7 @@ __device__ __forceinline__ void env_step_one(const DevPhys<T>& m, Env<T>& s, con
     }
   }
   // an env that needed the wide tier on fewer than wide_pct % of the sub-steps it ran here starts
-  // its next step in the full tier (4 envs per CU instead of 1) and is handed over -- through the
+  // its next step in the full tier (3 envs per CU instead of 1) and is handed over -- through the
   // hand-over queue, at once -- when a sub-step needs it (closed fingers: pad contacts flicker in
   // and out, most sub-steps light)
   if (need_tier == 2 && 100 * nwide < wide_pct * nrun) need_tier = 1;
@@ -545,6 +545,7 @@ __device__ __forceinline__ void env_step_one(const DevPhys<T>& m, Env<T>& s, con
 #define PNP_HQ_NEXT 2
 #define PNP_HQ_ERR 3
 #define PNP_HQ_LATE 4
+#define PNP_HQ_PREV 7   // the last queued step's published count (kept across steps: the consumer grid's size)
 #define PNP_HQ_ENTRY 8
 // default consumer timeout: 20 s of the 100 MHz constant clock (PNP_GYM_QUEUE_TIMEOUT_US)
 #define PNP_HQ_TIMEOUT 2000000000ll
@@ -588,15 +589,18 @@ template <typename T>
 __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) env_step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st,
                                                       pnp_env_params prm, EnvSoA<T> es, const T* __restrict__ action,
                                                       EnvOutT<T> out, int B, int resume, int hand, int only_tier,
-                                                      int* __restrict__ hq) {
+                                                      int* __restrict__ hq, const int* __restrict__ order) {
   __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
   Env<T>& s = s_env;
   const DevPhys<T>& m = phys<T>();
   (void)mp;
-  const int b = blockIdx.x;
+  int b = blockIdx.x;
   if (b >= B) return;   // (grid = B)
-  const int cur = es.tier ? (es.tier[b] & 3) : 0;
-  bool run = !(only_tier >= 0 && es.tier && cur != only_tier);   // else routed to another tier's pass
+  // order (resume passes): workgroup i runs the env at list position i (resume_order_kernel: the
+  // longest remaining chains first), the workgroups past the list none
+  if (order) b = b < order[0] ? order[1 + b] : -1;
+  const int cur = b >= 0 && es.tier ? (es.tier[b] & 3) : 0;
+  bool run = b >= 0 && !(only_tier >= 0 && es.tier && cur != only_tier);   // else routed to another tier's pass
   int k0 = 0;
   if (run && resume) {
     const uint32_t w = st.warn[b];
@@ -653,7 +657,8 @@ __global__ void __launch_bounds__(NT * MW_WAVES, PNP_WIDE ? 1 : 4) env_step_wide
                                                                           EnvSoA<float> es, const float* __restrict__ action,
                                                                           EnvOutT<float> out, const int* __restrict__ list,
                                                                           int resume, int hand, int* __restrict__ hq,
-                                                                          int hq_target, int B, long long hq_timeout) {
+                                                                          int hq_target, int B, long long hq_timeout,
+                                                                          int hq_min, int hq_pct) {
   __shared__ __attribute__((aligned(16))) Env<float> s_env;   // static LDS: see env_lds_note
   Env<float>& s = s_env;
   const DevPhys<float>& m = phys<float>();
@@ -666,7 +671,15 @@ __global__ void __launch_bounds__(NT * MW_WAVES, PNP_WIDE ? 1 : 4) env_step_wide
     const int k0 = resume ? (int)((st.warn[b] >> PNP_RESUME_SHIFT) & PNP_RESUME_MAXSUB) : 0;
     env_step_one(m, s, st, prm, es, action, out, b, cur, k0, resume, hand, MW_WAVES);
   };
+  // the consumers this step keeps: about as many as the last step published (hand-overs arrive over
+  // the whole step, and a consumer holds its CU's LDS while it waits, away from the producers);
+  // the others end at once
+  bool active = true;
   if (hq) {
+    const int prev = __hip_atomic_load(&hq[PNP_HQ_PREV], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    active = (int)blockIdx.x < max(hq_min, (int)((long long)prev * hq_pct / 100));
+  }
+  if (hq && active) {
     for (;;) {
       int i = 0;
       if (lane_id() == 0) i = __hip_atomic_fetch_add(&hq[PNP_HQ_NEXT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -675,7 +688,7 @@ __global__ void __launch_bounds__(NT * MW_WAVES, PNP_WIDE ? 1 : 4) env_step_wide
       if (b < 0) break;
       one(b);
     }
-  } else {
+  } else if (!hq) {
     const int count = list[0];
     for (int i = blockIdx.x; i < count; i += gridDim.x) one(list[1 + i]);
   }
@@ -685,8 +698,49 @@ __global__ void __launch_bounds__(NT * MW_WAVES, PNP_WIDE ? 1 : 4) env_step_wide
 #endif
 
 #if !PNP_COMPACT && !PNP_WIDE && !PNP_WIDE64
-__global__ void route_commit_kernel(uint8_t* __restrict__ tier, int B) {
+// The full tier's resume pass in order of remaining sub-steps, most first (a counting sort of the
+// selected envs by resume sub-step; ties in any order -- only which workgroup runs an env changes,
+// never what it computes).  The dispatcher starts workgroups in index order, so the envs with the
+// longest chains left start first and the pass does not end on one started late.
+__global__ void __launch_bounds__(1024) resume_order_kernel(const uint8_t* __restrict__ tier,
+                                                            const uint32_t* __restrict__ warn, int B, int only_tier,
+                                                            int* __restrict__ list) {
+  constexpr int NB = PNP_RESUME_MAXSUB + 1;
+  __shared__ int cnt[NB];
+  __shared__ int wtot[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  for (int i = t; i < NB; i += 1024) cnt[i] = 0;
+  __syncthreads();
+  auto sel = [&](int b) {
+    return (only_tier < 0 || !tier || (tier[b] & 3) == only_tier) && (warn[b] & PNP_RESUME_FLAG);
+  };
+  auto key = [&](int b) { return (int)((warn[b] >> PNP_RESUME_SHIFT) & PNP_RESUME_MAXSUB); };
+  for (int b = t; b < B; b += 1024)
+    if (sel(b)) atomicAdd(&cnt[key(b)], 1);
+  __syncthreads();
+  // exclusive scan of the NB bins: thread t owns NB / 1024 consecutive bins
+  constexpr int PER = NB / 1024;
+  static_assert(NB % 1024 == 0, "bins per thread");
+  int v[PER], tot = 0;
+  for (int j = 0; j < PER; j++) { v[j] = cnt[t * PER + j]; tot += v[j]; }
+  int inc = tot;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int u = __shfl_up(inc, d);
+    if (lane >= d) inc += u;
+  }
+  if (lane == 63) wtot[w] = inc;
+  __syncthreads();
+  int base = inc - tot;
+  for (int i = 0; i < w; i++) base += wtot[i];
+  for (int j = 0; j < PER; j++) { cnt[t * PER + j] = base; base += v[j]; }
+  __syncthreads();
+  for (int b = t; b < B; b += 1024)
+    if (sel(b)) list[1 + atomicAdd(&cnt[key(b)], 1)] = b;
+  if (t == 1023) list[0] = base;   // the last thread's running offset = the total
+}
+__global__ void route_commit_kernel(uint8_t* __restrict__ tier, int B, int* __restrict__ hq) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (hq && i == 0) hq[PNP_HQ_PREV] = hq[PNP_HQ_COUNT];   // the next queued step's consumer count
   if (i < B) {
     const uint8_t t = tier[i];
     if (t & 0x10) tier[i] = (uint8_t)((t >> 2) & 3);
@@ -709,10 +763,23 @@ static EnvOutT<T> out_view(const pnp_env_out* o) {
                     o->terminated, o->truncated};
 }
 
+// PNP_GYM_QUEUE_MIN / PNP_GYM_QUEUE_PCT: the hand-over queue's consumers this step = max(MIN,
+// PCT % of the envs the last queued step published), at most the launched grid
+// (PNP_GYM_QUEUE_CU); the rest of the grid ends at once.  Defaults 8 and 100.
+static int gym_queue_min() {
+  const char* e = getenv("PNP_GYM_QUEUE_MIN");
+  const int v = e ? atoi(e) : 8;
+  return v < 0 ? 0 : v;   // (0 with PCT 0: no consumer -- the fallback pass takes every hand-over; tests)
+}
+static int gym_queue_pct() {
+  const char* e = getenv("PNP_GYM_QUEUE_PCT");
+  const int v = e ? atoi(e) : 100;
+  return v < 0 ? 0 : (v > 10000 ? 10000 : v);
+}
 #if PNP_MW
-struct WideLists {
-  int* list[2] = {nullptr, nullptr};
-  int cap[2] = {0, 0};
+struct WideLists {   // kinds: 0 / 1 the persistent passes' lists, 2 the full resume pass's order
+  int* list[3] = {nullptr, nullptr, nullptr};
+  int cap[3] = {0, 0, 0};
   int ncu = 0;
 };
 static int32_t wide_list(int kind, int32_t B, int** out, int* ncu) {
@@ -762,7 +829,7 @@ static int32_t launch_env_step_mw(const pnp_state_t<float>* st, const pnp_env_pa
   }
   hipLaunchKernelGGL(env_step_wide_kernel, dim3(grid), dim3(NT * MW_WAVES), 0, (hipStream_t)stream, *st, *p,
                      env_view<float>(e), action, out_view<float>(o), (const int*)list, resume, hand, hq, hq_target, B,
-                     hq_timeout);
+                     hq_timeout, gym_queue_min(), gym_queue_pct());
   return pnp_check_launch(what);
 }
 #endif
@@ -796,7 +863,7 @@ int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>
                                        sizeof(DevPhys<float>), stream))
     return rc;
   hipLaunchKernelGGL(env_step_kernel<float>, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, *p,
-                     env_view<float>(e), action, out_view<float>(o), B, 0, 1, only_tier, (int*)nullptr);
+                     env_view<float>(e), action, out_view<float>(o), B, 0, 1, only_tier, (int*)nullptr, (const int*)nullptr);
   if (const int32_t rc = pnp_check_launch("env_step_kernel (compact)")) return rc;
   return lease.launched();
 }
@@ -840,7 +907,7 @@ int32_t launch_env_step_wide64(const pnp_model* model, const pnp_state_t<double>
                                        sizeof(DevPhys<double>), stream))
     return rc;
   hipLaunchKernelGGL(env_step_kernel<double>, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, *p,
-                     env_view<double>(e), action, out_view<double>(o), B, 1, 0, -1, (int*)nullptr);
+                     env_view<double>(e), action, out_view<double>(o), B, 1, 0, -1, (int*)nullptr, (const int*)nullptr);
   if (const int32_t rc = pnp_check_launch("env_step_kernel (wide64)")) return rc;
   return lease.launched();
 }
@@ -958,6 +1025,12 @@ static bool gym_full_mw_enabled() {
 // 32: 9.5 k, 64: 15.2 k, 128: 19.5 k, 160-255: 19.9-20.4 k; with the routing shares (50 %): off
 // 18.8 k, 96: 18.8 k, 160: 22.3 k, 192: 22.9 k, 240: 23.2 k -- the full passes hand envs to the
 // wide tier at every point of the step, and each needs a free consumer then
+// PNP_GYM_FULL_ORDER: unset / 1 = the full tier's resume pass starts its envs in order of
+// remaining sub-steps, most first (resume_order_kernel); 0 = in env order
+static bool gym_full_order_enabled() {
+  const char* e = getenv("PNP_GYM_FULL_ORDER");
+  return !(e && e[0] == '0');
+}
 static bool gym_queue_enabled() {
   const char* e = getenv("PNP_GYM_QUEUE");
   return !(e && e[0] == '0');
@@ -1005,6 +1078,7 @@ static int32_t hand_queue(int32_t B, int** out) {
     buf[dev] = nullptr;
     cap[dev] = 0;
     if (e == hipSuccess) e = hipMalloc((void**)&buf[dev], sizeof(int) * (size_t)(B + PNP_HQ_ENTRY));
+    if (e == hipSuccess) e = hipMemset(buf[dev], 0, sizeof(int) * PNP_HQ_ENTRY);   // (PNP_HQ_PREV: none yet)
     if (e == hipSuccess) cap[dev] = B + PNP_HQ_ENTRY;
   }
   if (e != hipSuccess) { pnp_set_error("pnp_env_step: hand-over queue: %s", hipGetErrorString(e)); return PNP_ERR_HIP; }
@@ -1060,7 +1134,7 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
     // sub-steps outgrow it to the fp64 wide tier's resume pass
     const int w64 = p->n_substeps * p->n_calls <= PNP_RESUME_MAXSUB && wide_enabled();
     hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, *p, env_view<T>(e), action,
-                       out_view<T>(o), B, 0, w64, -1, (int*)nullptr);
+                       out_view<T>(o), B, 0, w64, -1, (int*)nullptr, (const int*)nullptr);
     if ((rc = pnp_check_launch("env_step_kernel (fp64)"))) return rc;
     if (w64 && (rc = launch_env_step_wide64(model, st, p, e, action, o, B, stream))) return rc;
     return lease.launched();
@@ -1107,7 +1181,7 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
     hipError_t he = rs->last_valid ? hipStreamWaitEvent(s0, rs->last, 0) : hipSuccess;
     if (queue && he == hipSuccess) {   // a fresh queue, ordered before every pass of this step
       if ((rc = hand_queue(B, &hq))) return rc;
-      he = hipMemsetAsync(hq, 0, sizeof(int) * PNP_HQ_ENTRY, s0);
+      he = hipMemsetAsync(hq, 0, sizeof(int) * PNP_HQ_PREV, s0);   // the header but PNP_HQ_PREV
       if (he == hipSuccess) he = hipMemsetAsync(hq + PNP_HQ_ENTRY, 0xFF, sizeof(int) * (size_t)B, s0);
     }
     if (he == hipSuccess) he = hipEventRecord(rs->fork, s0);   // after the full image's copy and the last step
@@ -1119,7 +1193,7 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
       rc = launch_env_step_mw(st32, p, e, a32, o, B, rs->side[0], 0, 1, hand_pct, "env_step_wide_kernel (full, routed)");
     } else {
       hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, rs->side[0], dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
-                         0, hand_pct, 1, hq);
+                         0, hand_pct, 1, hq, (const int*)nullptr);
       rc = pnp_check_launch("env_step_kernel (full, routed)");
     }
     if (rc) return fail(rc);
@@ -1141,8 +1215,16 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
       rc = launch_env_step_mw(st32, p, e, a32, o, B, stream, compact ? 1 : 0, route ? 0 : -1, hand_pct,
                               "env_step_wide_kernel (full)");
     } else {
+      // the resume pass in order of remaining sub-steps (PNP_GYM_FULL_ORDER, default on)
+      int* order = nullptr;
+      if (compact && sizeof(T) == 4 && gym_full_order_enabled()) {
+        int ncu_unused = 0;
+        if ((rc = wide_list(2, B, &order, &ncu_unused))) return fail(rc);
+        hipLaunchKernelGGL(resume_order_kernel, dim3(1), dim3(1024), 0, s0, e->tier, st->warn, B, route ? 0 : -1, order);
+        if ((rc = pnp_check_launch("resume_order_kernel"))) return fail(rc);
+      }
       hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, s0, dm, *st, *p, env_view<T>(e), action, out_view<T>(o), B,
-                         compact ? 1 : 0, hand_pct, route ? 0 : -1, hq);
+                         compact ? 1 : 0, hand_pct, route ? 0 : -1, hq, (const int*)order);
       rc = pnp_check_launch("env_step_kernel");
     }
     if (rc) return fail(rc);
@@ -1183,7 +1265,7 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
     }
   }
   if (e->tier) {   // every pass has run: the next step's tiers become current
-    hipLaunchKernelGGL(route_commit_kernel, dim3((B + 255) / 256), dim3(256), 0, s0, e->tier, B);
+    hipLaunchKernelGGL(route_commit_kernel, dim3((B + 255) / 256), dim3(256), 0, s0, e->tier, B, hq);
     if ((rc = pnp_check_launch("route_commit_kernel"))) return fail(rc);
   }
   if (route) {

@@ -34,16 +34,20 @@
 #define PH_MAXMESHV 1400
 #define PH_MAXMESH 16
 #ifndef PH_MAXCON
-#define PH_MAXCON 48      // contacts per env (lane per contact: <= 64)
+// The full build's capacities.  64 contacts (round 5; 48 before): the random-action gym workload's
+// closed grippers peak at 57-64 contacts (tools/gym_queue_census.py: ~97 % of the envs the 48-contact
+// full tier handed to the wide tier, 465-574 per 4096-env step), and the wide tier holds one env per
+// CU against the full tier's 3 (Env 51.9 KB; 40.4 KB and 4 per CU at 48).
+#define PH_MAXCON 64      // contacts per env (lane per contact: <= 64)
 #endif
 #ifndef PH_MAXEFC
-#define PH_MAXEFC 208     // 6 weld + 9 limit + 4 x 48 contact rows
+#define PH_MAXEFC 272     // 6 weld + 9 limit + 4 x 64 contact rows
 #endif
 #ifndef PH_MAXJSLOT
-#define PH_MAXJSLOT 2048  // packed constraint-Jacobian slots (sum of row widths)
+#define PH_MAXJSLOT 2688  // packed constraint-Jacobian slots (sum of row widths)
 #endif
 #ifndef PH_JTCAP
-#define PH_JTCAP 1792    // dense island Jacobian entries (sum over islands of rows x dofs; larger: slot path)
+#define PH_JTCAP 2560    // dense island Jacobian entries (sum over islands of rows x dofs; larger: slot path)
 #endif
 #define PH_ROWW 16        // sparse row width: dofs of <= 2 trees (arm 9 + cube 6)
 #define PH_MAXMENTRY 160  // (i, j in ancestors(i)) entries of M

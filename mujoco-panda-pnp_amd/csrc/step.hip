@@ -25,7 +25,7 @@
 
 // Three builds of this file, three capacity tiers of the same device code (fp32):
 //   step_compact.hip  pnp_compact  20 contacts / 96 rows: 20 KB of LDS per env, 8 envs per CU
-//   step.hip          pnp_full     48 contacts / 208 rows: 38 KB, 4 envs per CU; also the fp64
+//   step.hip          pnp_full     64 contacts / 272 rows: 51 KB, 3 envs per CU; also the fp64
 //                                  debugging instantiation, the debug kernels and the C ABI
 //   step_wide.hip     pnp_wide     192 contacts / 784 rows: 1 env per CU
 // A sub-step that would overflow a tier's capacity is abandoned before it changes the state and
@@ -59,7 +59,7 @@
 // when its kernel is launched with hand = 1); PNP_LEAN: no debug-only fields outside the unions
 #define PNP_HANDS (!PNP_WIDE)
 // PNP_MW: the fp32 gym kernels of this build run several waves per env (helper waves for the convex
-// pass): the wide build (4 waves, 1 env per CU) and the full build (2 waves, 4 envs per CU)
+// pass): the wide build (4 waves, 1 env per CU) and the full build (2 waves, 3 envs per CU)
 #define PNP_MW ((PNP_WIDE || (!PNP_COMPACT && !PNP_GYM)) && !PNP_WIDE64)
 // MPR's portal support points in per-wave LDS slots (collide_dev.h SVertL): the full and wide
 // builds (the compact builds run no MPR; the fp64 wide build keeps registers)
@@ -1378,7 +1378,7 @@ enum { MW_EXIT = 0, MW_MPR = 1, MW_FAN = 2 };
 // Four waves, one per SIMD: the wide tier's Env (192 contacts) holds one env per CU, so the helpers
 // cost no residency, and multiccd makes up to five MPR runs per convex pair to spread.  (Round 2 /
 // early round 3, at two envs per CU: two waves, four were slower -- profiles/r03/ab_mpr_helper_waves.log.)
-constexpr int MW_WAVES = PNP_WIDE ? 4 : 2;   // full build: 2 x 4 envs per CU = 2 waves per SIMD
+constexpr int MW_WAVES = PNP_WIDE ? 4 : 2;   // full build: 2 x 3 envs per CU
 // A round's convex pairs (up to RN, listed by wave 0 in cst_key in live-list order), each with
 // `per` staging slots (cst_val, mw_hit): slot per o holds pair o's first MPR contact, slots
 // per o + 1 + t its multiccd trial t (positions relative to geom 1's centre).  Items are taken one
@@ -4514,7 +4514,7 @@ int32_t step_wide_lds_bytes() { return (int32_t)sizeof(Env<float>); }
 #elif PNP_WIDE64
 // fp64 wide tier: the resume pass of pnp_step_f64 after the full fp64 kernel handed an env over
 // (the single-env facade and the batched behaviour trees run in fp64; closed fingers on a cube make
-// more than the full tier's 48 contacts); truncates past its own capacities with a warning
+// more than the full tier's 64 contacts); truncates past its own capacities with a warning
 int32_t launch_step_wide64(const pnp_model* model, const pnp_state_t<double>* st, int32_t B, int32_t nsub,
                            void* stream) {
   const DevPhys<double>* src = phys_image<double>(model);

@@ -5,7 +5,7 @@
 // survivors, 96 constraint rows, 800 packed Jacobian slots, 768 dense island-Jacobian entries and
 // 288 packed island-Hessian entries.  The per-env LDS working set (Env, laid out by lifetime) is
 // then 20.1 KB: 8 envs per CU, two waves on every SIMD, so 4096 envs run in 2 rounds of 2048
-// resident waves (the full build: 4 envs per CU).  Registers are budgeted for two waves per SIMD
+// resident waves (the full build: 3 envs per CU).  Registers are budgeted for two waves per SIMD
 // (<= 256 VGPR + AGPR).  An env whose sub-step would overflow one of these capacities stops before
 // that sub-step changes its state and is finished by the full kernel's resume pass (step.hip:
 // launch_step, PNP_RESUME_*), so results are the full kernel's.

@@ -50,5 +50,32 @@ def random_ctrl(st, seed=1, model=None):
     return st
 
 
+# the full tier's contact capacity (mujoco-panda-pnp_amd/csrc/phys_model.h PH_MAXCON): the fixtures
+# that exercise the wide tier must pass it
+FULL_MAXCON = 64
+
+PILE_XY = (1.371, 0.48)   # on board2 (shelf_pnp.xml:51, top at z 0.71)
+
+
+def cube_pile(qpos, model, rows=slice(None)):
+    """Pile the three cubes on board2 for the given rows of a qpos batch: cube2 0.6 mm into cube1's
+    top, cube3 0.4 mm into cube1's side, cube1 0.2 mm into the board (box-box contacts, 4-8 each).
+    With the closed-finger pads pressed 1-4 mm together (52-63 contacts) that makes 76-87: past the
+    full tier's capacity, so the wide tier finishes those sub-steps."""
+    m = model
+    top, h = 0.71, 0.02
+    x, y = PILE_XY
+    poses = {"cube1": [x, y, top + h - 2e-4], "cube2": [x + 0.005, y, top + 3 * h - 6e-4],
+             "cube3": [x + 2 * h - 4e-4, y + 0.01, top + h - 2e-4]}
+    for name, p in poses.items():
+        a = int(m.jnt_qposadr[m.joint_id(f"{name}_joint")])
+        v = np.array(p + [1.0, 0.0, 0.0, 0.0])
+        if not isinstance(qpos, np.ndarray):   # a device tensor (the gym tests)
+            import torch
+            v = torch.as_tensor(v, dtype=qpos.dtype, device=qpos.device)
+        qpos[rows, a:a + 7] = v
+    return qpos
+
+
 def copy_state(st):
     return {k: v.copy() for k, v in st.items()}

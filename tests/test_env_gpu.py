@@ -17,6 +17,7 @@ import numpy as np
 import pytest
 import torch
 
+import physics_states as PS
 from oracle.env_oracle import EnvConfig as OCfg, EnvOracle
 
 pytestmark = pytest.mark.gpu
@@ -115,14 +116,16 @@ def test_env_logic_short_physics_f32(model):
 
 
 def test_gym_step_wide_tier_pressed_fingers(model):
-    """Gym steps from closed fingers pressed into each other (52-61 contacts: the wide tier
-    finishes those sub-steps, env_dev.h), fp32 short physics against the oracle env: observations
-    and rewards within 1e-3, flags identical, no truncation warning."""
+    """Gym steps from closed fingers pressed into each other (52-63 contacts: the full tier) and,
+    in every other env, the cubes piled on board2 too (76-87: the wide tier finishes those
+    sub-steps, env_dev.h), fp32 short physics against the oracle env: observations and rewards
+    within 1e-3, flags identical, no truncation warning."""
     g = _env(torch.float32, **SHORT)
     o = EnvOracle(B, cfg=OCfg(**SHORT), model=model)
     g.reset()
     o.reset()
     g.state["qpos"][:, 7:9] = -torch.linspace(0.001, 0.004, B, dtype=torch.float32, device="cuda")[:, None]
+    PS.cube_pile(g.state["qpos"], model, slice(None, None, 2))
     _sync_oracle(g, o)
     o.st["warn"][:] = 0
     for k in range(3):
@@ -149,6 +152,7 @@ def _gym_run(mode, B, nsteps, pressed=False, route="1", tiers=None, **extra_env)
         g.reset()
         if pressed:
             g.state["qpos"][::3, 7:9] = -0.002          # a third of the envs: pads pressed together
+            PS.cube_pile(g.state["qpos"], g.engine.model, slice(None, None, 6))   # half of those: cubes piled too (> 64)
         rng = np.random.default_rng(21)
         outs = []
         for k in range(nsteps):
@@ -170,7 +174,8 @@ def _gym_run(mode, B, nsteps, pressed=False, route="1", tiers=None, **extra_env)
 def test_gym_compact_tier_is_exact():
     """The fp32 gym step starts in the compact tier (8 envs per CU) and hands envs over to the full
     and wide tiers (env_compact.hip, env_dev.h): bit-identical to starting in the full tier, on a
-    batch whose envs stay under 20 contacts, pass 20 (random grippers) and pass 48 (pads pressed)."""
+    batch whose envs stay under 20 contacts, pass 20 (random grippers), pass 48 (pads pressed)
+    and pass 64 (pads pressed, cubes piled)."""
     a, oa = _gym_run("1", 96, 3, pressed=True)
     b, ob = _gym_run("0", 96, 3, pressed=True)
     for x, y in zip(oa, ob):
@@ -236,24 +241,32 @@ def test_gym_queue_timeout_falls_back_exactly():
     """A consumer of the hand-over queue that gives up waiting (here after 1 us:
     PNP_GYM_QUEUE_TIMEOUT_US) leaves its env's resume bits, and the list-based wide resume pass
     after the join finishes it (env_dev.h, PNP_HQ_LATE): the bits of the queue-less step, no env
-    left mid-step, and the give-ups counted by pnp_env_queue_status.  With the default timeout
-    nothing times out and every published hand-over is consumed by the queue."""
+    left mid-step, and the give-ups counted by pnp_env_queue_status.  With no consumer at all the
+    fallback pass finishes every published hand-over, and with the default timeout nothing times
+    out and every published hand-over is consumed by the queue."""
     from pnp_amd import _lib
     a, oa = _gym_run("1", 96, 3, pressed=True, route="1", PNP_GYM_QUEUE="1", PNP_GYM_QUEUE_TIMEOUT_US="1")
     st_fast = _lib.env_queue_status()
+    # no consumer at all (PNP_GYM_QUEUE_MIN=0, PNP_GYM_QUEUE_PCT=0): the fallback pass finishes every
+    # published hand-over
+    d, od = _gym_run("1", 96, 3, pressed=True, route="1", PNP_GYM_QUEUE="1", PNP_GYM_QUEUE_MIN="0",
+                     PNP_GYM_QUEUE_PCT="0")
+    st_none = _lib.env_queue_status()
     b, ob = _gym_run("1", 96, 3, pressed=True, route="1", PNP_GYM_QUEUE="0")
     c, oc = _gym_run("1", 96, 3, pressed=True, route="1", PNP_GYM_QUEUE="1")
     st_def = _lib.env_queue_status()
-    print("queue status, 1 us timeout:", st_fast, " default:", st_def)
-    for x, y, z in zip(oa, ob, oc):
-        for u, v, w in zip(x, y, z):
-            assert torch.equal(u, v) and torch.equal(w, v)
+    print("queue status, 1 us timeout:", st_fast, " no consumer:", st_none, " default:", st_def)
+    for x, y, z, q in zip(oa, ob, oc, od):
+        for u, v, w, r in zip(x, y, z, q):
+            assert torch.equal(u, v) and torch.equal(w, v) and torch.equal(r, v)
     for k in a.state:
         assert torch.equal(a.state[k], b.state[k]) and torch.equal(c.state[k], b.state[k]), k
-    for g in (a, c):
+        assert torch.equal(d.state[k], b.state[k]), k
+    for g in (a, c, d):
         w = g.state["warn"].to(torch.int64) & 0xFFFFFFFF
         assert not bool((w >> 16).any()) and int((w & 0xFFFF).max()) == 0
-    assert st_fast["fallback"] <= st_fast["timeouts"]
+    assert st_fast["fallback"] <= st_fast["timeouts"] and st_fast["timeouts"] >= 1
+    assert st_none["published"] > 0 and st_none["fallback"] == st_none["published"] and st_none["claims"] == 0
     assert st_def["timeouts"] == 0 and st_def["fallback"] == 0
     assert st_def["producers_done"] == 2 * 96 and st_def["claims"] >= st_def["published"]
 

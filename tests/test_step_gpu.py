@@ -241,14 +241,14 @@ def _f32_tree_errors(engine, model, st, nsub=1, per_env=False):
         dbg = engine.forward_debug(_dev(st, torch.float32)).cpu().numpy()
         ncon = [O.forward_fields({k: st[k][b] for k in O.STATE_KEYS}, ["ncon"], model=model)["ncon"][0]
                 for b in range(st["qpos"].shape[0])]
-        # forward_debug runs the full tier alone (48 contacts, truncating like MuJoCo at a full
+        # forward_debug runs the full tier alone (64 contacts, truncating like MuJoCo at a full
         # buffer): envs beyond that capacity are left out of M dqacc (their dqvel is checked), and
         # so are envs at a contact knife edge (the oracle's own contact count changes under a one-ulp
         # perturbation of the state: pads touching at distance ~0); any other count difference fails
         qa_got, knife = [], None
         for b in range(st["qpos"].shape[0]):
             same = int(dbg[b, D["COUNTS"]]) == int(ncon[b])
-            if not same and int(ncon[b]) <= 48:
+            if not same and int(ncon[b]) <= PS.FULL_MAXCON:
                 knife = _knife_edge_envs(model, st) if knife is None else knife
                 assert knife[b], f"env {b}: contact count {int(dbg[b, D['COUNTS']])} != oracle {int(ncon[b])}"
                 print(f"env {b}: contact knife edge (kernel {int(dbg[b, D['COUNTS']])}, oracle {int(ncon[b])}): "
@@ -448,7 +448,7 @@ def mesh_states(model):
     """States with convex-mesh contacts (MPR): the hand pushed into cube1 (4 envs), and envs whose
     mocap target was driven into the table / onto cube1's shelf / towards the shelf for 300 oracle
     sub-steps (hand, finger and link hulls against the boards with physical penetrations).  Envs
-    past the kernel's 48-contact capacity (CONTACTFULL) are left out; arbitrary arm poses are
+    past 40 contacts are left out (the full tier's capacity was 48 when this was written); arbitrary arm poses are
     avoided too (links placed 0.1 m inside the table put MPR's sign tests on rounding edges)."""
     st = PS.reset_states(16, seed=11, model=model)
     st["qpos"][:, 7:9] = 0.004          # off the closed-finger pad knife edge (see `fresh`)
@@ -603,14 +603,24 @@ def _step_f32_mode(engine, st, nsub, mode):
 @pytest.fixture(scope="module")
 def pressed(model):
     """Closed fingers pressed into each other (pad boxes interpenetrating 1-4 mm, finger servos
-    closing; past -2.5 mm per finger the two finger hulls touch face to face too): 47-63 contacts,
-    mostly more than the full tier's 48 -- the closed-gripper states of the random-action gym
-    workload (tools/contact_census.py, tools/gym_profile.py)."""
+    closing; past -2.5 mm per finger the two finger hulls touch face to face too): 47-63 contacts
+    -- the closed-gripper states of the random-action gym workload (tools/contact_census.py,
+    tools/gym_profile.py), within the full tier's 64 since round 5 (tools/gym_queue_census.py: 57-64
+    contacts was where nearly every full -> wide hand-over of the gym workload peaked)."""
     n = 12
     st = PS.reset_states(n, seed=11, model=model)
     st["qpos"][:, 7:9] = -np.linspace(0.001, 0.004, n)[:, None]
     st["ctrl"][:, -2:] = 0.0
     st["qvel"] += np.random.default_rng(5).normal(size=st["qvel"].shape) * 0.02
+    return st
+
+
+@pytest.fixture(scope="module")
+def pile(pressed, model):
+    """`pressed` with the three cubes piled on board2 (physics_states.cube_pile): 76-87 contacts,
+    past the full tier's 64 -- the wide tier's fixture."""
+    st = PS.copy_state(pressed)
+    PS.cube_pile(st["qpos"], model)
     return st
 
 
@@ -630,31 +640,31 @@ def _run_env(engine, g, nsub, **env):
     return g
 
 
-def test_wide_tier_matches_oracle(engine, model, pressed):
+def test_wide_tier_matches_oracle(engine, model, pile):
     """Sub-steps with more contacts than the full kernel holds are finished by the wide tier (192
     contacts): one fp32 step matches the fp64 oracle (which holds 192 too) with no truncation
-    warning; the full kernel alone (PNP_STEP_WIDE=0) truncates at 48 and says so."""
-    n = pressed["qpos"].shape[0]
-    nc = [int(_oracle_fields(pressed, b, model)["ncon"][0]) for b in range(n)]
-    assert min(nc) > 48 and max(nc) <= 192, nc
-    ref = PS.copy_state(pressed)
+    warning; the full kernel alone (PNP_STEP_WIDE=0) truncates at its 64 and says so."""
+    n = pile["qpos"].shape[0]
+    nc = [int(_oracle_fields(pile, b, model)["ncon"][0]) for b in range(n)]
+    assert min(nc) > PS.FULL_MAXCON and max(nc) <= 192, nc
+    ref = PS.copy_state(pile)
     O.step(ref, nsub=1, nthreads=8, model=model)
-    g = _host(_run_env(engine, _dev(pressed, torch.float32), 1, PNP_STEP_COMPACT="1", PNP_STEP_WIDE="1"))
+    g = _host(_run_env(engine, _dev(pile, torch.float32), 1, PNP_STEP_COMPACT="1", PNP_STEP_WIDE="1"))
     assert not (g["warn"] & 0xFFFF).any() and not (ref["warn"]).any()
-    _assert_per_tree(engine, model, pressed, 1, "pressed (wide tier)")
-    trunc = _host(_run_env(engine, _dev(pressed, torch.float32), 1, PNP_STEP_COMPACT="1", PNP_STEP_WIDE="0"))
-    # which envs overflow 48 is decided on the state the kernel gets (fp32-rounded): rounding moves
-    # the most-pressed env's pad pairs across the contact margin (61 -> 45 contacts in the oracle)
-    nc32 = np.array([int(_oracle_fields(_round32(pressed), b, model)["ncon"][0]) for b in range(n)])
+    _assert_per_tree(engine, model, pile, 1, "pressed + cube pile (wide tier)")
+    trunc = _host(_run_env(engine, _dev(pile, torch.float32), 1, PNP_STEP_COMPACT="1", PNP_STEP_WIDE="0"))
+    # which envs overflow is decided on the state the kernel gets (fp32-rounded): rounding can move
+    # pad pairs across the contact margin
+    nc32 = np.array([int(_oracle_fields(_round32(pile), b, model)["ncon"][0]) for b in range(n)])
     flagged = (trunc["warn"] & 8) != 0
-    assert (flagged == (nc32 > 48)).all(), (nc32, trunc["warn"])
+    assert (flagged == (nc32 > PS.FULL_MAXCON)).all(), (nc32, trunc["warn"])
 
 
-def test_wide_tier_hand_over_is_exact(engine, model, scene, mesh_scene, pressed):
+def test_wide_tier_hand_over_is_exact(engine, model, scene, mesh_scene, pressed, pile):
     """compact -> full -> wide (default), full -> wide (PNP_STEP_COMPACT=0) and the wide kernel
     alone (3) give the same bits on a batch that mixes envs within the compact capacities, envs
-    between 20 and 48 contacts and envs beyond 48; no resume bit leaks into warn."""
-    st = {k: np.concatenate([scene[k], mesh_scene[k], pressed[k]]) for k in scene}
+    between 20 and 64 contacts and envs beyond 64; no resume bit leaks into warn."""
+    st = {k: np.concatenate([scene[k], mesh_scene[k], pressed[k], pile[k]]) for k in scene}
     for nsub in (1, 6):
         a = _run_env(engine, _dev(st, torch.float32), nsub, PNP_STEP_COMPACT="1")
         b = _run_env(engine, _dev(st, torch.float32), nsub, PNP_STEP_COMPACT="0")
