@@ -697,6 +697,30 @@ __global__ void __launch_bounds__(NT * MW_WAVES, PNP_WIDE ? 1 : 4) env_step_wide
 }
 #endif
 
+#if PNP_COMPACT && PNP_GYM
+// Routing probe (routed fp32 gym steps, before the passes): the compact tier's collision stage at
+// each compact-routed env's current state -- the contacts of its step's first sub-step, which the
+// action does not change.  An env that would overflow there is routed to the full tier for this
+// step, so it starts on the routed full pass at once instead of waiting out the whole compact pass
+// before its hand-over is resumed.  A hint: only where an env runs changes, never what it computes.
+__global__ void __launch_bounds__(NT, PNP_STEP_WAVES) route_probe_kernel(pnp_state_t<float> st,
+                                                                         uint8_t* __restrict__ tier, int B) {
+  __shared__ __attribute__((aligned(16))) Env<float> s_env;   // static LDS: see env_lds_note
+  Env<float>& s = s_env;
+  const DevPhys<float>& m = phys<float>();
+  const int b = blockIdx.x;
+  if (b >= B || (tier[b] & 3) != 0) return;   // (grid = B) routed past the compact tier already
+  NoClock clk;
+  load_env(m, s, st, b, 1);
+  st_kinematics(m, s);
+  st_compos_crb(m, s);
+  st_factor_M(m, s);
+  st_collision(m, s, clk);
+  if (s.nconvex && !s.ovf) st_collision_convex(m, s);
+  if (lane_id() == 0 && s.ovf) tier[b] = 1;
+}
+#endif
+
 #if !PNP_COMPACT && !PNP_WIDE && !PNP_WIDE64
 // The full tier's resume pass in order of remaining sub-steps, most first (a counting sort of the
 // selected envs by resume sub-step; ties in any order -- only which workgroup runs an env changes,
@@ -868,6 +892,18 @@ int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>
   return lease.launched();
 }
 int32_t env_compact_lds_bytes() { return (int32_t)sizeof(Env<float>); }
+int32_t launch_env_route_probe(const pnp_model* model, const pnp_state_t<float>* st, uint8_t* tier, int32_t B,
+                               void* stream) {
+  const DevPhys<float>* src = phys_image<float>(model);
+  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  ResidentLease lease;
+  if (const int32_t rc = lease.acquire(RES_COMPACT_GYM_F32, model, (const void*)&g_phys_f32, src,
+                                       sizeof(DevPhys<float>), stream))
+    return rc;
+  hipLaunchKernelGGL(route_probe_kernel, dim3(B), dim3(NT), 0, (hipStream_t)stream, *st, tier, B);
+  if (const int32_t rc = pnp_check_launch("route_probe_kernel")) return rc;
+  return lease.launched();
+}
 #elif PNP_WIDE
 // wide tier: resume pass of the gym step over the envs the full kernel handed over (resume = 1),
 // or the routed pass over the envs whose step starts in the wide tier (resume = 0, only_tier = 2);
@@ -1027,6 +1063,13 @@ static bool gym_full_mw_enabled() {
 // wide tier at every point of the step, and each needs a free consumer then
 // PNP_GYM_FULL_ORDER: unset / 1 = the full tier's resume pass starts its envs in order of
 // remaining sub-steps, most first (resume_order_kernel); 0 = in env order
+// PNP_GYM_PROBE: unset / 1 = routed fp32 gym steps probe every compact-routed env's first
+// sub-step's contacts and route the ones the compact tier cannot hold to the full tier for this
+// step (route_probe_kernel); 0 = the last step's routing alone
+static bool gym_probe_enabled() {
+  const char* e = getenv("PNP_GYM_PROBE");
+  return !(e && e[0] == '0');
+}
 static bool gym_full_order_enabled() {
   const char* e = getenv("PNP_GYM_FULL_ORDER");
   return !(e && e[0] == '0');
@@ -1179,6 +1222,11 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
   if (route) {
     if ((rc = route_streams(&rs))) return rc;
     hipError_t he = rs->last_valid ? hipStreamWaitEvent(s0, rs->last, 0) : hipSuccess;
+    // the routing probe: envs whose first sub-step overflows the compact tier start on the routed
+    // full pass (PNP_GYM_PROBE, default on); ordered after the last routed step, before the fork
+    if (he == hipSuccess && gym_probe_enabled() &&
+        (rc = launch_env_route_probe(model, st32, e->tier, B, stream)))
+      return rc;
     if (queue && he == hipSuccess) {   // a fresh queue, ordered before every pass of this step
       if ((rc = hand_queue(B, &hq))) return rc;
       he = hipMemsetAsync(hq, 0, sizeof(int) * PNP_HQ_PREV, s0);   // the header but PNP_HQ_PREV

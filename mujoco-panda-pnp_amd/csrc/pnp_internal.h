@@ -131,6 +131,9 @@ int32_t launch_env_step_compact(const pnp_model* model, const pnp_state_t<float>
                                 const pnp_env_state* e, const float* action, const pnp_env_out* o, int32_t B,
                                 void* stream, int only_tier);
 int32_t env_compact_lds_bytes();
+// env_compact.hip: the routing probe of a routed fp32 gym step (env_dev.h route_probe_kernel)
+int32_t launch_env_route_probe(const pnp_model* model, const pnp_state_t<float>* st, uint8_t* tier, int32_t B,
+                               void* stream);
 
 // ---------------------------------------------------------------------------- error plumbing
 void pnp_set_error(const char* fmt, ...);
