@@ -31,11 +31,15 @@ def test_execute_pnp_three_cubes():
     obj, tgt = r["objects"]["cube1"], r["targets"]["cube1"]
     # cube1 is placed: within the env's own success distance of its target (distance_threshold
     # 0.05, shelf_pnp.py:22 / panda_env.py:303-306); measured 0.022 m.  Cubes 2 and 3 are knocked
-    # off their boards on the way (as in the reference's own runs: its VecNormalize pickle's last
-    # observations have the cubes at z = 0.02) -- printed, not pinned
+    # off their boards on the way and end resting on the floor (z = their half-size 0.02), as in
+    # the reference's own runs: its VecNormalize pickle's last observations have the cubes at
+    # z = 0.02.  Pinned to that: on the floor, at rest height, inside the
+    # scene (parity of the positions themselves unpinned: no reference trajectory to compare)
     assert np.linalg.norm(obj - tgt) < 0.05, (obj, tgt)
     for n in ("cube2", "cube3"):
-        print(f"{n}: at {np.round(r['objects'][n], 3)}, target {r['targets'][n]}")
+        p = np.asarray(r["objects"][n])
+        print(f"{n}: at {np.round(p, 3)}, target {r['targets'][n]}")
+        assert abs(p[2] - 0.02) < 2e-3 and np.abs(p[:2]).max() < 3.0, (n, p)
     # no contact / constraint buffer ever filled (CONTACTFULL 8, CNSTRFULL 16) and no bad-state
     # reset: the fp64 facade's physics kept every contact MuJoCo would
     assert r["warn"] == 0, r["warn"]
@@ -56,7 +60,9 @@ def test_batched_bt_equals_sequential_facade_runs():
     for b in range(0, B, 8):
         r = run(task_sequence=["cube1"], max_tick=1500, verbose=False, env_index=b)
         assert (r["success"], r["ticks"]) == (bool(res["success"][b]), int(res["ticks"][b])), (b, r["ticks"], res["ticks"][b])
-    assert res["success"].mean() >= 0.5
+    # every env's tree finishes (measured 64 / 64, profiles/r05/gpu_tests.log); a tree that stops
+    # finishing on some envs is a regression
+    assert res["success"].mean() >= 0.95, res["success"].mean()
     assert not res["warn"].any(), np.nonzero(res["warn"])   # no full contact / row buffer, no bad state
     # batching really happened: the 128 RotateSkill resets (2 per env) took fewer than B slerp
     # launches, and the planners' IK solves one launch per round at most
