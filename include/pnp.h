@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 12
+#define PNP_ABI_VERSION 13
 
 #define PNP_OK 0
 #define PNP_ERR_ARG -1
@@ -445,6 +445,17 @@ typedef struct pnp_tqc_replay {
  * pointers, stream-ordered, capturable. */
 int32_t pnp_tqc_sample(const pnp_tqc_replay* rb, const float* u, int32_t batch, float* obs, float* act, float* next_obs,
                        float* done, float* reward, void* stream);
+/* pnp_tqc_sample with the step's random numbers drawn on the device (TQC.train's default): the two
+ * U[0, 1) replay draws per row and the actor's two N(0, 1) draws (eps_pi, eps_next [batch*act_dim],
+ * the inputs pnp_tqc_update takes) from Philox4x32-10 keyed by `seed`, counter = (counter[0], row,
+ * lane).  counter: device int64[2], zero-initialised -- [0] the draw index, advanced by one per call
+ * on the device (so a captured graph draws a fresh batch per replay), [1] scratch.  u_out
+ * [2*batch] (optional) receives the uniform draws: pnp_tqc_sample with them gives the same batch
+ * bit for bit.  Same distributions as the caller's torch generator, not its numbers.  act_dim
+ * <= 63.  Stream-ordered, capturable. */
+int32_t pnp_tqc_sample_draw(const pnp_tqc_replay* rb, uint64_t seed, int64_t* counter, int32_t batch, float* u_out,
+                            float* eps_pi, float* eps_next, float* obs, float* act, float* next_obs, float* done,
+                            float* reward, void* stream);
 int64_t pnp_tqc_workspace_floats(const pnp_tqc_desc* d);
 /* flat gradient sizes (actor, critics) of grads_out below */
 int32_t pnp_tqc_param_counts(int32_t* actor_params, int32_t* critic_params);

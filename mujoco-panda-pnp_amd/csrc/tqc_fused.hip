@@ -753,6 +753,66 @@ __global__ void __launch_bounds__(64) tqc_sample_kernel(SampleArgs a) {
   }
 }
 
+// The batch's random numbers drawn on the device (pnp_tqc_sample_draw): Philox4x32-10 keyed by the
+// learner's seed, counter = (draw index, row, lane); lanes 0..act_dim-1 give the row's two
+// N(0, 1) draws (eps_pi, eps_next: Box-Muller in fp32), lane 63 its two U[0, 1) replay-index draws.
+// Replaces three PyTorch generator kernels per gradient step and the captured graph's generator
+// bookkeeping (philox offset fills and copies) -- the same distributions, not the same numbers as
+// torch.rand / torch.randn from the agent's generator (the explicit-draw entry points keep those).
+// The draw index is device state: every block reads it first and the last block to finish (a
+// done count) advances it, so eager and graph-replayed steps draw the same sequence.
+__device__ __forceinline__ void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[0] = n0; c[1] = (uint32_t)p1; c[2] = n2; c[3] = (uint32_t)p0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }   // [0, 1)
+__device__ __forceinline__ float gauss(uint32_t x, uint32_t y) {                            // Box-Muller
+  const float a = (float)((x >> 8) + 1u) * 0x1p-24f, b = (float)(y >> 8) * 0x1p-24f;        // a in (0, 1]
+  return sqrtf(-2.0f * logf(a)) * cosf(6.28318530717958647692f * b);
+}
+struct DrawArgs {
+  uint64_t seed;
+  unsigned long long* counter;   // [0] draw index, [1] blocks done in the current launch
+  float* u_out; float* eps_pi; float* eps_next;
+};
+__global__ void __launch_bounds__(64) tqc_sample_draw_kernel(SampleArgs a, DrawArgs d) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int OD = a.rb.obs_dim, AD = a.rb.act_dim;
+  const unsigned long long c = d.counter[0];
+  uint32_t r[4] = {(uint32_t)c, (uint32_t)(c >> 32), (uint32_t)b, (uint32_t)t};
+  philox4x32(r, (uint32_t)d.seed, (uint32_t)(d.seed >> 32));
+  if (t < AD) {
+    d.eps_pi[(size_t)b * AD + t] = gauss(r[0], r[1]);
+    d.eps_next[(size_t)b * AD + t] = gauss(r[2], r[3]);
+  }
+  const float u0 = __shfl(u01(r[0]), 63), u1 = __shfl(u01(r[1]), 63);
+  if (t == 63 && d.u_out) { d.u_out[b] = u0; d.u_out[a.B + b] = u1; }
+  const float fu = u0 * a.rb.upper[0], fe = u1 * (float)a.rb.n_envs;
+  const long long bi = min((long long)fu, (long long)a.rb.rows - 1), ei = min((long long)fe, (long long)a.rb.n_envs - 1);
+  const size_t cell = (size_t)bi * a.rb.n_envs + ei;
+  for (int j = t; j < 2 * OD + AD + 2; j += 64) {
+    if (j < OD) a.obs[(size_t)b * OD + j] = norm_col(a, a.rb.obs[cell * OD + j], j);
+    else if (j < 2 * OD) a.nobs[(size_t)b * OD + j - OD] = norm_col(a, a.rb.next_obs[cell * OD + j - OD], j - OD);
+    else if (j < 2 * OD + AD) a.act[(size_t)b * AD + j - 2 * OD] = a.rb.actions[cell * AD + j - 2 * OD];
+    else if (j == 2 * OD + AD) a.done[b] = a.rb.dones[cell];
+    else a.rew[b] = a.rb.rewards[cell];
+  }
+  if (t == 0) {   // every block has read the draw index before it counts itself done
+    __threadfence();
+    const unsigned long long done = atomicAdd(&d.counter[1], 1ull);
+    if (done == (unsigned long long)gridDim.x - 1) {
+      d.counter[1] = 0ull;
+      d.counter[0] = c + 1ull;
+      __threadfence();
+    }
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------- C ABI
@@ -798,6 +858,33 @@ extern "C" int32_t pnp_tqc_sample(const pnp_tqc_replay* rb, const float* u, int3
   SampleArgs a{*rb, u, batch, obs, act, next_obs, done, reward};
   hipLaunchKernelGGL(tqc_sample_kernel, dim3(batch), dim3(64), 0, (hipStream_t)stream, a);
   return pnp_check_launch("tqc_sample_kernel");
+}
+
+extern "C" int32_t pnp_tqc_sample_draw(const pnp_tqc_replay* rb, uint64_t seed, int64_t* counter, int32_t batch,
+                                       float* u_out, float* eps_pi, float* eps_next, float* obs, float* act,
+                                       float* next_obs, float* done, float* reward, void* stream) {
+  if (!counter || !eps_pi || !eps_next || (rb && (rb->act_dim <= 0 || rb->act_dim > 63))) {
+    pnp_set_error("pnp_tqc_sample_draw: null counter / eps buffer or act_dim outside 1..63");
+    return PNP_ERR_ARG;
+  }
+  // the replay / normaliser checks of pnp_tqc_sample (u: a dummy non-null pointer, never read here)
+  static const float dummy = 0.0f;
+  if (!rb || batch <= 0 || !obs || !act || !next_obs || !done || !reward || !rb->obs || !rb->next_obs ||
+      !rb->actions || !rb->rewards || !rb->dones || !rb->upper || rb->rows <= 0 || rb->n_envs <= 0 || rb->obs_dim <= 0 ||
+      rb->n_keys <= 0 || rb->n_keys > 4) {
+    pnp_set_error("pnp_tqc_sample_draw: null pointer or bad replay shape");
+    return PNP_ERR_ARG;
+  }
+  int sum = 0;
+  for (int k = 0; k < rb->n_keys; k++) {
+    if (!rb->mean[k] || !rb->var[k] || rb->key_dim[k] <= 0) { pnp_set_error("pnp_tqc_sample_draw: bad normaliser key"); return PNP_ERR_ARG; }
+    sum += rb->key_dim[k];
+  }
+  if (sum != rb->obs_dim) { pnp_set_error("pnp_tqc_sample_draw: key dims do not add up to obs_dim"); return PNP_ERR_ARG; }
+  SampleArgs a{*rb, &dummy, batch, obs, act, next_obs, done, reward};
+  DrawArgs dr{seed, reinterpret_cast<unsigned long long*>(counter), u_out, eps_pi, eps_next};
+  hipLaunchKernelGGL(tqc_sample_draw_kernel, dim3(batch), dim3(64), 0, (hipStream_t)stream, a, dr);
+  return pnp_check_launch("tqc_sample_draw_kernel");
 }
 
 // one weight-gradient job: a layer's weight (and bias) tensors with their Adam state

@@ -10,7 +10,7 @@ from .model import PnpIKParams, PnpModelDesc
 # PNP_LIB: another build of the same sources (tools/asan_cpu_tests.sh: the host-sanitizer build)
 LIB_PATH = os.environ.get("PNP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpnp.so")
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 # every symbol include/pnp.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -21,7 +21,7 @@ EXPORTS = [
     "pnp_env_params_size", "pnp_env_init", "pnp_env_init_f64", "pnp_env_reset", "pnp_env_reset_f64",
     "pnp_env_step", "pnp_env_step_f64", "pnp_env_evaluate", "pnp_env_evaluate_f64",
     "pnp_slerp_track_f64", "pnp_env_queue_status", "pnp_tqc_workspace_floats", "pnp_tqc_param_counts",
-    "pnp_tqc_update", "pnp_tqc_sample",
+    "pnp_tqc_update", "pnp_tqc_sample", "pnp_tqc_sample_draw",
 ]
 
 STATE_FIELDS = ("qpos", "qvel", "ctrl", "mocap_pos", "mocap_quat", "qacc_warmstart", "time", "warn")
@@ -180,6 +180,8 @@ def load():
     L.pnp_tqc_update.restype = I32
     L.pnp_tqc_sample.argtypes = [C.POINTER(PnpTqcReplay), P, I32, P, P, P, P, P, P]
     L.pnp_tqc_sample.restype = I32
+    L.pnp_tqc_sample_draw.argtypes = [C.POINTER(PnpTqcReplay), C.c_uint64, P, I32, P, P, P, P, P, P, P, P, P]
+    L.pnp_tqc_sample_draw.restype = I32
     if L.pnp_abi_version() != ABI_VERSION:
         raise PnpError(f"libpnp ABI {L.pnp_abi_version()} != binding ABI {ABI_VERSION}")
     if L.pnp_env_params_size() != C.sizeof(PnpEnvParams):

@@ -73,6 +73,12 @@ class TQCConfig:
     # one GPU; else (and for the first gradient step, which creates the optimisers' state) the
     # PyTorch step
     fused: bool = True
+    # the fused step's random numbers (replay indices, the actor's two Gaussian draws) drawn on the
+    # device with the replay sample (pnp_tqc_sample_draw: Philox keyed by `seed`, a device draw
+    # counter) instead of by the agent's torch generator: three generator kernels and the captured
+    # graph's generator bookkeeping less per gradient step.  Same distributions, other numbers
+    # than the generator's; False draws from the generator (the tests' bit-exact comparisons)
+    device_rng: bool = True
 
 
 def _world():
@@ -314,6 +320,7 @@ class TQC:
         self._graph_out = None
         self._fdesc = None          # pnp_tqc_desc of the fused step (TQC._fused_desc)
         self._frb = None            # pnp_tqc_replay of the fused sample (TQC._fused_replay)
+        self._fctr = None           # device draw counter of pnp_tqc_sample_draw (cfg.device_rng)
         self._eager_updates = 0     # steps run eagerly before the capture (allocator / optimiser state)
         self.vecnorm = VecNormalize(dims, self.device, c.clip_obs, c.norm_eps)
         self.buffer = DictReplayBuffer(c.buffer_size, self.n_envs, self.obs_dim, self.act_dim, self.device)
@@ -540,6 +547,12 @@ class TQC:
         r.clip_obs, r.norm_eps = vn.clip_obs, vn.epsilon
         z = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)
         self._fsb = (z(B, self.obs_dim), z(B, self.act_dim), z(B, self.obs_dim), z(B, 1), z(B, 1))
+        # device draws (cfg.device_rng): the uniform and Gaussian draws' buffers, the draw counter
+        # (kept across load_state_dict: `fused_rng_draws` restores it) and the Philox key
+        self._fu_dev, self._feps = z(2, B), (z(B, self.act_dim), z(B, self.act_dim))
+        if getattr(self, "_fctr", None) is None:
+            self._fctr = torch.zeros(2, dtype=torch.int64, device=self.device)
+        self._fseed = (int(self.cfg.seed) * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019) & 0xFFFFFFFFFFFFFFFF
         self._frb = r
         return r
 
@@ -550,10 +563,15 @@ class TQC:
         L = _lib.load()
         r = self._fused_replay()
         B = self.cfg.batch_size
-        u = torch.rand(2, B, device=self.device, generator=self.gen)
         out = self._fsb
-        _lib.check(L.pnp_tqc_sample(C.byref(r), u.data_ptr(), B, *[t.data_ptr() for t in out],
-                                    C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)), "pnp_tqc_sample")
+        stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        if self.cfg.device_rng:
+            _lib.check(L.pnp_tqc_sample_draw(C.byref(r), self._fseed, self._fctr.data_ptr(), B, self._fu_dev.data_ptr(),
+                                             self._feps[0].data_ptr(), self._feps[1].data_ptr(),
+                                             *[t.data_ptr() for t in out], stream), "pnp_tqc_sample_draw")
+            return out
+        u = torch.rand(2, B, device=self.device, generator=self.gen)
+        _lib.check(L.pnp_tqc_sample(C.byref(r), u.data_ptr(), B, *[t.data_ptr() for t in out], stream), "pnp_tqc_sample")
         self._fu = u   # alive until the launch has read it
         return out
 
@@ -568,8 +586,11 @@ class TQC:
         c = self.cfg
         obs, act, nobs, done, rew = self._sample_fused()
         B = c.batch_size
-        eps_pi = torch.randn(B, self.act_dim, device=self.device, generator=self.gen)
-        eps_next = torch.randn(B, self.act_dim, device=self.device, generator=self.gen)
+        if self.cfg.device_rng:   # drawn by pnp_tqc_sample_draw with the batch
+            eps_pi, eps_next = self._feps
+        else:
+            eps_pi = torch.randn(B, self.act_dim, device=self.device, generator=self.gen)
+            eps_next = torch.randn(B, self.act_dim, device=self.device, generator=self.gen)
         ts = [t.contiguous() for t in (obs, act, nobs, done, rew, eps_pi, eps_next)]
         b = _lib.PnpTqcBatch(*[t.data_ptr() for t in ts])
         gp = None if grads_out is None else C.c_void_p(grads_out.data_ptr())
@@ -667,7 +688,8 @@ class TQC:
                 "critic_target": self.critic_target.state_dict(), "log_ent_coef": self.log_ent_coef.detach(),
                 "actor_opt": self.actor_opt.state_dict(), "critic_opt": self.critic_opt.state_dict(),
                 "ent_opt": self.ent_opt.state_dict(), "vecnormalize": self.vecnorm.state_dict(),
-                "num_timesteps": self.num_timesteps, "n_updates": self.n_updates}
+                "num_timesteps": self.num_timesteps, "n_updates": self.n_updates,
+                "fused_rng_draws": int(self._fctr[0]) if getattr(self, "_fctr", None) is not None else 0}
 
     def load_state_dict(self, d):
         self.actor.load_state_dict(d["actor"])
@@ -680,6 +702,9 @@ class TQC:
         self.ent_opt.load_state_dict(d["ent_opt"])
         self.vecnorm.load_state_dict(d["vecnormalize"])
         self.num_timesteps, self.n_updates = int(d["num_timesteps"]), int(d["n_updates"])
+        if getattr(self, "_fctr", None) is not None:
+            self._fctr.zero_()
+            self._fctr[0] = int(d.get("fused_rng_draws", 0))
         # the optimisers now hold new state tensors: the schedule's shared lr tensor back in their
         # groups, and a captured step (which read the old ones) is re-captured
         if isinstance(self._lr, torch.Tensor):

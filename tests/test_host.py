@@ -72,7 +72,7 @@ def test_library_loads_and_exports_header_symbols():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_lib.EXPORTS)
-    assert L.pnp_abi_version() == _lib.ABI_VERSION == 12
+    assert L.pnp_abi_version() == _lib.ABI_VERSION == 13
     from pnp_amd.model import PnpModelDesc
     assert L.pnp_model_desc_size() == C.sizeof(PnpModelDesc)
 
@@ -112,6 +112,8 @@ def test_tqc_entry_points_validate_without_gpu():
     r = _lib.PnpTqcReplay()
     assert L.pnp_tqc_sample(C.byref(r), None, 512, None, None, None, None, None, None) < 0
     assert b"pnp_tqc_sample" in L.pnp_last_error()
+    assert L.pnp_tqc_sample_draw(C.byref(r), 1, None, 512, None, None, None, None, None, None, None, None, None) < 0
+    assert b"pnp_tqc_sample_draw" in L.pnp_last_error()
 
 
 def test_product_package_never_imports_oracle():

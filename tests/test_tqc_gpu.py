@@ -157,7 +157,7 @@ def test_fused_sample_matches_pytorch():
     flat_obs (pnp_amd/tqc.py TQC._sample_norm) from the same generator state: the same rows, the
     normalised observations bit for bit, on a partly filled buffer (indices below `upper`) and with
     statistics that clip (achieved_goal's variance shrunk so |x| > clip_obs)."""
-    a = _fused_agent(graph=False)
+    a = _fused_agent(graph=False, device_rng=False)   # u from the agent's generator, as _sample_norm's
     for trial in range(3):
         a.vecnorm.obs_rms["achieved_goal"].var.fill_(1e-12)   # these three columns clip at +-10
         gs = a.gen.get_state()
@@ -189,6 +189,7 @@ def test_fused_learner_step_matches_pytorch():
     L.pnp_tqc_param_counts(C.byref(na), C.byref(nc))
     na, nc = na.value, nc.value
     pa, pc, pt = a._fused_params()
+    a.cfg.device_rng = False       # this step's draws from the generator, like the PyTorch step's
     sd = copy.deepcopy(a.state_dict())
     gs = a.gen.get_state()
     g = torch.zeros(na + nc, device=a.device)
@@ -219,6 +220,43 @@ def test_fused_learner_step_matches_pytorch():
     for x, y in zip(after_f, after_t):
         d = (x - y).abs()
         assert float(d.max()) <= 2.5 * lr and float(d.median()) <= 1e-3 * lr, (float(d.max()), float(d.median()), lr)
+
+
+def test_fused_device_draws():
+    """pnp_tqc_sample_draw (TQC.train's default, cfg.device_rng): the batch's two U[0, 1) replay
+    draws and the actor's two N(0, 1) draws per row from Philox on the device, the draw counter
+    advanced by one per call on the device.  The uniform draws it reports give, through
+    pnp_tqc_sample, the same batch bit for bit; the draws have the moments of U[0, 1) and N(0, 1)
+    (64 calls: 65,536 uniforms, 458,752 Gaussians); consecutive calls draw different numbers."""
+    from pnp_amd import _lib
+    L = _lib.load()
+    a = _fused_agent(graph=False)
+    assert a.cfg.device_rng
+    a.train()                      # the first (PyTorch) step builds the fused descriptors' state
+    r = a._fused_replay()
+    B = a.cfg.batch_size
+    n0 = int(a._fctr[0])
+    us, es = [], []
+    for k in range(64):
+        got = [t.clone() for t in a._sample_fused()]
+        u = a._fu_dev.clone()
+        us.append(u)
+        es.append(torch.cat([e.clone().flatten() for e in a._feps]))
+        if k < 3:
+            ref = [torch.empty_like(t) for t in got]
+            _lib.check(L.pnp_tqc_sample(C.byref(r), u.data_ptr(), B, *[t.data_ptr() for t in ref], None), "pnp_tqc_sample")
+            torch.cuda.synchronize()
+            for name, x, y in zip(("obs", "act", "next_obs", "done", "reward"), got, ref):
+                assert torch.equal(x, y), (k, name)
+    torch.cuda.synchronize()
+    assert int(a._fctr[0]) == n0 + 64 and int(a._fctr[1]) == 0
+    U, E = torch.stack(us).double(), torch.stack(es).double()
+    assert float(U.min()) >= 0.0 and float(U.max()) < 1.0
+    assert abs(float(U.mean()) - 0.5) < 0.005 and abs(float(U.var()) - 1 / 12) < 0.002
+    # (bounds ~5 standard errors of each moment at these sample sizes)
+    assert abs(float(E.mean())) < 0.008 and abs(float(E.var()) - 1.0) < 0.01
+    assert abs(float((E ** 3).mean())) < 0.03 and abs(float((E ** 4).mean()) - 3.0) < 0.08
+    assert not torch.equal(us[0], us[1]) and not torch.equal(es[0], es[1])
 
 
 def test_fused_learner_step_captured_and_timed():
