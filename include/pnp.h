@@ -416,6 +416,7 @@ typedef struct pnp_tqc_desc {
   float* workspace;            /* pnp_tqc_workspace_floats() floats */
   int64_t workspace_floats;
   float* logs;                 /* [4] out: ent_coef (before the step), critic loss, actor loss, ent-coef loss */
+  int64_t* draw_counter;       /* optional: pnp_tqc_sample_draw's counter, advanced by one per step (NULL: none) */
 } pnp_tqc_desc;
 /* One sampled, normalised batch: obs / next_obs [batch*25], act [batch*7], done / reward [batch],
  * and the two N(0, 1) draws of the step's squashed-Gaussian samples (actor on obs, on next_obs)
@@ -448,8 +449,9 @@ int32_t pnp_tqc_sample(const pnp_tqc_replay* rb, const float* u, int32_t batch, 
 /* pnp_tqc_sample with the step's random numbers drawn on the device (TQC.train's default): the two
  * U[0, 1) replay draws per row and the actor's two N(0, 1) draws (eps_pi, eps_next [batch*act_dim],
  * the inputs pnp_tqc_update takes) from Philox4x32-10 keyed by `seed`, counter = (counter[0], row,
- * lane).  counter: device int64[2], zero-initialised -- [0] the draw index, advanced by one per call
- * on the device (so a captured graph draws a fresh batch per replay), [1] scratch.  u_out
+ * lane).  counter: device int64[2], zero-initialised -- [0] the draw index, read here and advanced
+ * by one on the device by the gradient step whose pnp_tqc_desc.draw_counter is this counter (so a
+ * captured graph draws a fresh batch per replay), [1] reserved.  u_out
  * [2*batch] (optional) receives the uniform draws: pnp_tqc_sample with them gives the same batch
  * bit for bit.  Same distributions as the caller's torch generator, not its numbers.  act_dim
  * <= 63.  Stream-ordered, capturable. */

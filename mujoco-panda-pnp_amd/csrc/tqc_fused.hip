@@ -282,6 +282,7 @@ struct TqcArgs {
   const float* log_ent_coef;
   float* ws;                 // NMAT x [B][256]
   float* sums;               // [slabs][NSUM]
+  unsigned long long* draw_counter;   // pnp_tqc_sample_draw's draw index (optional), advanced once per step
   const float* logs;         // [4]: ent_coef (pre-update), critic loss, actor loss, entropy-coefficient loss
   // the optimisers' step tensors (torch increments every parameter's own): the actor's before
   // its Adam (K1, which runs before K6 reads them), the critics' and the entropy coefficient's
@@ -436,6 +437,7 @@ __global__ void __launch_bounds__(NTH) tqc_fwd_kernel(TqcArgs g) {
   const size_t MS = (size_t)g.B * HID;
   float* sm = wmat(g, M_SM, row0);
   if (slab == 0 && job == 0 && t < 10) g.astep[t][0] += 1.f;
+  if (slab == 0 && job == 0 && t == 10 && g.draw_counter) g.draw_counter[0] += 1ull;   // (the sample has read it)
   if (job == 0) {   // actor(obs): a_pi, log_prob, activations (the actor step's)
     load_rows<OBS>(L.A, g.obs, row0, OBS);
     __syncthreads();
@@ -759,8 +761,10 @@ __global__ void __launch_bounds__(64) tqc_sample_kernel(SampleArgs a) {
 // Replaces three PyTorch generator kernels per gradient step and the captured graph's generator
 // bookkeeping (philox offset fills and copies) -- the same distributions, not the same numbers as
 // torch.rand / torch.randn from the agent's generator (the explicit-draw entry points keep those).
-// The draw index is device state: every block reads it first and the last block to finish (a
-// done count) advances it, so eager and graph-replayed steps draw the same sequence.
+// The draw index is device state: read here, advanced by the gradient step's first kernel
+// (tqc_fwd_kernel, pnp_tqc_desc.draw_counter), so eager and graph-replayed steps draw the same
+// sequence.  (A done count advancing it here, from the launch's last workgroup, cost ~10 µs: 512
+// atomics on one address.)
 __device__ __forceinline__ void philox4x32(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; r++) {
@@ -777,7 +781,7 @@ __device__ __forceinline__ float gauss(uint32_t x, uint32_t y) {                
 }
 struct DrawArgs {
   uint64_t seed;
-  unsigned long long* counter;   // [0] draw index, [1] blocks done in the current launch
+  const unsigned long long* counter;   // [0] the draw index
   float* u_out; float* eps_pi; float* eps_next;
 };
 __global__ void __launch_bounds__(64) tqc_sample_draw_kernel(SampleArgs a, DrawArgs d) {
@@ -801,15 +805,6 @@ __global__ void __launch_bounds__(64) tqc_sample_draw_kernel(SampleArgs a, DrawA
     else if (j < 2 * OD + AD) a.act[(size_t)b * AD + j - 2 * OD] = a.rb.actions[cell * AD + j - 2 * OD];
     else if (j == 2 * OD + AD) a.done[b] = a.rb.dones[cell];
     else a.rew[b] = a.rb.rewards[cell];
-  }
-  if (t == 0) {   // every block has read the draw index before it counts itself done
-    __threadfence();
-    const unsigned long long done = atomicAdd(&d.counter[1], 1ull);
-    if (done == (unsigned long long)gridDim.x - 1) {
-      d.counter[1] = 0ull;
-      d.counter[0] = c + 1ull;
-      __threadfence();
-    }
   }
 }
 
@@ -882,7 +877,7 @@ extern "C" int32_t pnp_tqc_sample_draw(const pnp_tqc_replay* rb, uint64_t seed, 
   }
   if (sum != rb->obs_dim) { pnp_set_error("pnp_tqc_sample_draw: key dims do not add up to obs_dim"); return PNP_ERR_ARG; }
   SampleArgs a{*rb, &dummy, batch, obs, act, next_obs, done, reward};
-  DrawArgs dr{seed, reinterpret_cast<unsigned long long*>(counter), u_out, eps_pi, eps_next};
+  DrawArgs dr{seed, reinterpret_cast<const unsigned long long*>(counter), u_out, eps_pi, eps_next};
   hipLaunchKernelGGL(tqc_sample_draw_kernel, dim3(batch), dim3(64), 0, (hipStream_t)stream, a, dr);
   return pnp_check_launch("tqc_sample_draw_kernel");
 }
@@ -923,6 +918,7 @@ extern "C" int32_t pnp_tqc_update(const pnp_tqc_desc* d, const pnp_tqc_batch* b,
   g.ws = d->workspace;
   g.sums = g.ws + (size_t)NMAT * B * HID;
   g.logs = d->logs;
+  g.draw_counter = reinterpret_cast<unsigned long long*>(d->draw_counter);
   g.gamma = d->gamma;
   g.target_entropy = d->target_entropy;
   g.B = B;

@@ -76,7 +76,8 @@ class PnpTqcDesc(C.Structure):
                 ("critic", C.c_void_p * 8), ("critic_m", C.c_void_p * 8), ("critic_v", C.c_void_p * 8),
                 ("critic_step", C.c_void_p * 8), ("target", C.c_void_p * 8),
                 ("log_ent_coef", C.c_void_p), ("ent_m", C.c_void_p), ("ent_v", C.c_void_p), ("ent_step", C.c_void_p),
-                ("lr", C.c_void_p), ("workspace", C.c_void_p), ("workspace_floats", C.c_int64), ("logs", C.c_void_p)]
+                ("lr", C.c_void_p), ("workspace", C.c_void_p), ("workspace_floats", C.c_int64), ("logs", C.c_void_p),
+                ("draw_counter", C.c_void_p)]
 
 
 class PnpTqcBatch(C.Structure):

@@ -525,6 +525,9 @@ class TQC:
         self._fws = torch.empty(int(n), dtype=torch.float32, device=self.device)
         self._flogs = torch.zeros(4, dtype=torch.float32, device=self.device)
         d.workspace, d.workspace_floats, d.logs = self._fws.data_ptr(), int(n), self._flogs.data_ptr()
+        if self._fctr is None:
+            self._fctr = torch.zeros(2, dtype=torch.int64, device=self.device)
+        d.draw_counter = self._fctr.data_ptr()   # pnp_tqc_sample_draw's draw index, advanced per step
         self._fkeep = keep + list(pt) + [es["exp_avg"], es["exp_avg_sq"], es["step"]]
         self._fdesc = d
         return d
@@ -550,7 +553,7 @@ class TQC:
         # device draws (cfg.device_rng): the uniform and Gaussian draws' buffers, the draw counter
         # (kept across load_state_dict: `fused_rng_draws` restores it) and the Philox key
         self._fu_dev, self._feps = z(2, B), (z(B, self.act_dim), z(B, self.act_dim))
-        if getattr(self, "_fctr", None) is None:
+        if self._fctr is None:
             self._fctr = torch.zeros(2, dtype=torch.int64, device=self.device)
         self._fseed = (int(self.cfg.seed) * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019) & 0xFFFFFFFFFFFFFFFF
         self._frb = r

@@ -224,10 +224,11 @@ def test_fused_learner_step_matches_pytorch():
 
 def test_fused_device_draws():
     """pnp_tqc_sample_draw (TQC.train's default, cfg.device_rng): the batch's two U[0, 1) replay
-    draws and the actor's two N(0, 1) draws per row from Philox on the device, the draw counter
-    advanced by one per call on the device.  The uniform draws it reports give, through
-    pnp_tqc_sample, the same batch bit for bit; the draws have the moments of U[0, 1) and N(0, 1)
-    (64 calls: 65,536 uniforms, 458,752 Gaussians); consecutive calls draw different numbers."""
+    draws and the actor's two N(0, 1) draws per row from Philox on the device, at the draw index
+    the gradient step advances on the device (pnp_tqc_desc.draw_counter: one per step).  The uniform
+    draws it reports give, through pnp_tqc_sample, the same batch bit for bit; the draws have the
+    moments of U[0, 1) and N(0, 1) (64 indices: 65,536 uniforms, 458,752 Gaussians); consecutive
+    indices draw different numbers, the same index the same ones."""
     from pnp_amd import _lib
     L = _lib.load()
     a = _fused_agent(graph=False)
@@ -235,9 +236,13 @@ def test_fused_device_draws():
     a.train()                      # the first (PyTorch) step builds the fused descriptors' state
     r = a._fused_replay()
     B = a.cfg.batch_size
-    n0 = int(a._fctr[0])
+    a.train(3)                     # fused steps: the draw index advances once per step
+    torch.cuda.synchronize()
+    assert int(a._fctr[0]) == 3, int(a._fctr[0])
     us, es = [], []
     for k in range(64):
+        if k:
+            a._fctr[0] += 1            # what the next gradient step would do
         got = [t.clone() for t in a._sample_fused()]
         u = a._fu_dev.clone()
         us.append(u)
@@ -248,8 +253,9 @@ def test_fused_device_draws():
             torch.cuda.synchronize()
             for name, x, y in zip(("obs", "act", "next_obs", "done", "reward"), got, ref):
                 assert torch.equal(x, y), (k, name)
+    again = [t.clone() for t in a._sample_fused()]   # the same index: the same draws
     torch.cuda.synchronize()
-    assert int(a._fctr[0]) == n0 + 64 and int(a._fctr[1]) == 0
+    assert torch.equal(a._fu_dev, us[-1]) and torch.equal(again[0], got[0])
     U, E = torch.stack(us).double(), torch.stack(es).double()
     assert float(U.min()) >= 0.0 and float(U.max()) < 1.0
     assert abs(float(U.mean()) - 0.5) < 0.005 and abs(float(U.var()) - 1 / 12) < 0.002
