@@ -237,6 +237,22 @@ def test_gym_hand_over_queue_is_exact(grid):
     assert not bool((w >> 16).any()) and int((w & 0xFFFF).max()) == 0
 
 
+def test_gym_full_order_is_exact():
+    """The full tier's resume pass in order of remaining sub-steps (resume_order_kernel, env_dev.h;
+    PNP_GYM_FULL_ORDER, default on) against env order: the same bits -- only which workgroup runs
+    an env changes, never its arithmetic -- with envs handed over at many sub-steps (pressed pads,
+    piled cubes, random actions)."""
+    a, oa = _gym_run("1", 96, 3, pressed=True, route="1", PNP_GYM_FULL_ORDER="1")
+    b, ob = _gym_run("1", 96, 3, pressed=True, route="1", PNP_GYM_FULL_ORDER="0")
+    for x, y in zip(oa, ob):
+        for u, v in zip(x, y):
+            assert torch.equal(u, v)
+    for k in a.state:
+        assert torch.equal(a.state[k], b.state[k]), k
+    for k in a.env:
+        assert torch.equal(a.env[k], b.env[k]), k
+
+
 def test_gym_queue_timeout_falls_back_exactly():
     """A consumer of the hand-over queue that gives up waiting (here after 1 us:
     PNP_GYM_QUEUE_TIMEOUT_US) leaves its env's resume bits, and the list-based wide resume pass
