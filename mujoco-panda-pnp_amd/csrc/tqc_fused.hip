@@ -591,13 +591,14 @@ __global__ void __launch_bounds__(NTH) tqc_actor_bwd_kernel(TqcArgs g) {
 // ---- weight gradients over the whole batch + Adam (torch.optim.Adam fused / capturable semantics)
 // One job per parameter tensor: dW(k, n) = sum_b X[b][k] dY[b][n] with X's columns k < kx from x0,
 // kx <= k < K from x1, and the ones-column k = K for the bias (db = sum_b dY).  One workgroup per
-// 32 x 32 tile of (K + 1) x N; wave w reduces rows [w B / 4, (w + 1) B / 4) on the matrix cores
-// (A lane (kq, i) = X[b + kq][k0 + i], B lane = dY[b + kq][n0 + i]), the four partial tiles are
-// added in wave order through LDS and the tile's Adam runs in place.
-// WRG: row groups of 4 a wave loads before its MFMAs -- 32 (128 rows: train.py's batch of 512
-// split over the 4 waves in one trip, 128 loads in flight per lane; the tiles' operands come from
-// L2 / the Infinity Cache, each trip waits one round trip)
-constexpr int WT = 32, WNW = 4, WTH = 64 * WNW, MAXJ = 10, WRG = 32;
+// 32 x 32 tile of (K + 1) x N; wave w of WNW reduces rows [w B / WNW, (w + 1) B / WNW) on the
+// matrix cores (A lane (kq, i) = X[b + kq][k0 + i], B lane = dY[b + kq][n0 + i]), the partial
+// tiles are added in wave order through LDS and the tile's Adam runs in place.
+// WNW = 16 waves (train.py's batch of 512: 32 rows per wave, WRG = 8 row groups of 4 loaded before
+// the wave's MFMAs, 32 loads in flight per lane; the tiles' operands come from L2 / the Infinity
+// Cache, each trip waits one round trip): four waves per SIMD hide that wait where one wave per
+// SIMD (WNW = 4, 128 rows each) left it exposed -- 22.2 -> 16.7 (8 waves) -> 15.9 µs per launch.
+constexpr int WT = 32, WNW = 16, WTH = 64 * WNW, MAXJ = 10, WRG = 8;
 struct WJob {
   const float* x0; const float* x1; const float* dy;
   float* p; float* m; float* v; float* tgt; const float* step;       // weight ([out][in] if tr, else [in][out])
@@ -680,7 +681,9 @@ __global__ void __launch_bounds__(WTH) tqc_wgrad_adam_kernel(WArgs a) {
     // consecutive threads along the parameter's contiguous index
     const int kk = J.tr ? e % WT : e / WT, nn = J.tr ? e / WT : e % WT, k = k0 + kk, n = n0 + nn;
     if (k > J.K || n >= J.N) continue;
-    const float gr = ((red[0][kk][nn] + red[1][kk][nn]) + red[2][kk][nn]) + red[3][kk][nn];
+    float gr = red[0][kk][nn];
+#pragma unroll
+    for (int q = 1; q < WNW; q++) gr += red[q][kk][nn];   // the waves' row blocks in order
     float *pp, *mp, *vp, *tp;
     float step;
     int gi;
