@@ -6,12 +6,12 @@
 // reduction kernels between them -- launch and latency bound (1.9 ms per step).  Here the step is
 // two kinds of kernel, all fp32 in / fp32 accumulate on v_mfma_f32_16x16x4_f32 (the precision of
 // the PyTorch step):
-//   * chain kernels: the batch cut into slabs of 16 rows; one workgroup (8 waves) runs one network
+//   * chain kernels: the batch cut into slabs of 16 rows; one workgroup (16 waves) runs one network
 //     chain (forward, or backward to the layer inputs) for one slab and one network, the weights
 //     streamed through LDS, the activations and the backward pass's layer-output gradients stored
 //     [B][256] in the workspace;
 //   * weight-gradient kernels: dW = X^T dY over the whole batch, one workgroup per 32 x 32 tile of
-//     a parameter tensor (the bias as the ones-row of X), the four waves' partial sums added in a
+//     a parameter tensor (the bias as the ones-row of X), the 16 waves' partial sums added in a
 //     fixed order (deterministic) and Adam applied to the tile in place -- no per-slab partial
 //     gradients go through HBM.
 //   K1 tqc_fwd_kernel        (slab, 5 jobs) job 0: actor(obs) -> a_pi, log_prob, activations;
@@ -39,7 +39,12 @@
 namespace {
 
 constexpr int R = 16;              // rows per slab (one MFMA tile of rows)
-constexpr int NW = 8;              // waves per workgroup of the chain kernels (two per SIMD)
+// waves per workgroup of the chain kernels: 16, four per SIMD, one 16-column MFMA tile each of a
+// 256-wide layer (<= 128 VGPRs: 71-87 used).  With 8 (two per SIMD, two tiles each interleaved
+// past the 40-cycle dependent MFMA latency, 246 VGPRs) the waves sat waiting on the staged weight
+// chunks' barriers: 0.200 -> 0.178 ms per gradient step at 16 (fwd 48.9 -> 44.5, pi-critic 52.0
+// -> 42.9, critic bwd 30.4 -> 25.1, actor bwd 25.8 -> 22.8 µs)
+constexpr int NW = 16;
 constexpr int NTH = 64 * NW;
 constexpr int KC = 32;             // reduction rows per staged weight chunk
 constexpr int OBS = 25, ACT = 7, HID = 256, NC = 2, NQ = 25, NIN = OBS + ACT, NALL = NC * NQ;
