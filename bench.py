@@ -384,7 +384,9 @@ def run_tqc(engine, B, rank, world, dist, steps=3, warmup=2, learner_reps=20):
     utd_elapsed, _ = _timed(fn_utd, 1, 0, dist)
     return {"gym_steps_per_s": B * world * steps / elapsed, "env_steps_per_s": B * world * steps * sub / elapsed,
             "ms_per_step": step_ms, "learner_ms_per_update": learner_ms,
-            "learner": (("hand-written fused HIP gradient step (csrc/tqc_fused.hip: pnp_tqc_sample + pnp_tqc_update, 7 launches)"
+            "learner": ((("hand-written fused HIP gradient step (csrc/tqc_fused.hip: "
+                          + ("pnp_tqc_sample_draw, the random numbers drawn on the device"
+                             if agent.cfg.device_rng else "pnp_tqc_sample") + " + pnp_tqc_update, 7 launches)")
                          if agent._fdesc is not None else "PyTorch gradient step (fused Adam)")
                         + (", captured in a HIP graph and replayed" if agent._graph is not None else ", eager")),
             "transitions_per_s_at_reference_utd": B * world / utd_elapsed,
