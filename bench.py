@@ -313,8 +313,11 @@ def run_step(args, engine, model, rank, world, dist):
     if not args.no_gym:
         rec["gym"] = run_gym(engine, B, rank, world, dist)
         _progress(rank, f"gym leg done: {rec['gym']['gym_steps_per_s']:.0f} gym-steps/s")
+        if args.steady_burn > 0:
+            rec["gym"]["steady"] = run_gym_steady(engine, B, rank, world, dist, burn=args.steady_burn)
+            _progress(rank, f"gym steady leg done: {rec['gym']['steady']['gym_steps_per_s']:.0f} gym-steps/s")
     if not args.no_tqc:
-        rec["tqc"] = run_tqc(engine, args.tqc_envs, rank, world, dist)
+        rec["tqc"] = run_tqc(engine, args.tqc_envs, rank, world, dist, steady_burn=args.steady_burn)
         _progress(rank, f"tqc leg done: {rec['tqc']['gym_steps_per_s']:.0f} transitions/s")
     if not args.no_ik:
         ik = run_ik(args, engine, model, rank, world, dist, steps=500, warmup=20,
@@ -331,9 +334,31 @@ def run_step(args, engine, model, rank, world, dist):
 
 
 # ----------------------------------------------------------------------------- fused gym step
+class QueueHealth:
+    """pnp_env_queue_status summed over the routed gym steps it is sampled after: envs handed to
+    the wide tier through the device queue, consumers that gave up waiting, envs the fallback pass
+    finished -- a run whose consumers time out prints a normal-looking rate, so the record carries
+    these next to it.  (Each sample synchronises: taken outside timed regions only.)"""
+
+    def __init__(self):
+        self.n, self.tot = 0, {"published": 0, "timeouts": 0, "fallback": 0}
+
+    def sample(self):
+        from pnp_amd import _lib
+        q = _lib.env_queue_status()
+        self.n += 1
+        for k in self.tot:
+            self.tot[k] += int(q[k])
+        return q
+
+    def record(self, what):
+        return dict(self.tot, steps_sampled=self.n, sampled=what)
+
+
 def run_gym(engine, B, rank, world, dist, steps=3, warmup=1):
     """C5's env side: FrankaShelfPNPDense env.step over B envs per GPU as ONE fused launch
-    (set_action + 250 sub-steps + obs / reward / success / sequencing), random actions."""
+    (set_action + 250 sub-steps + obs / reward / success / sequencing), random actions; gym steps
+    1-3 after a reset (see run_gym_steady for a long run)."""
     from pnp_amd.envs import BatchedFrankaShelfPNPEnv
     env = BatchedFrankaShelfPNPEnv(B, engine=engine, env_offset=rank * B, autoreset=False)
     env.reset()
@@ -341,18 +366,53 @@ def run_gym(engine, B, rank, world, dist, steps=3, warmup=1):
                            device=engine.device)
     elapsed, kern_ms = _timed(lambda i: env.step(acts[i % 4]), steps, warmup, dist,
                               ranks_out=RANK_LEGS.setdefault("gym", []))
+    qh = QueueHealth()
+    qh.sample()
     sub = env.cfg.n_substeps * env.cfg.n_calls
     return {"gym_steps_per_s": B * world * steps / elapsed, "env_steps_per_s": B * world * steps * sub / elapsed,
             "ms_per_gym_step": elapsed / steps * 1e3, "kernel_avg_ms": kern_ms, "sub_steps_per_gym_step": sub,
-            "kernel": "env_step_kernel<float>", "workload": f"{B} FrankaShelfPNPDense envs per GPU, random actions"}
+            "kernel": "env_step_kernel<float>", "workload": f"{B} FrankaShelfPNPDense envs per GPU, random actions, "
+                                                            f"gym steps {warmup + 1}-{warmup + steps} after reset",
+            "queue": qh.record("the last timed step")}
+
+
+def run_gym_steady(engine, B, rank, world, dist, burn=50, steps=5):
+    """The gym step in steady state: train.py runs 300-step episodes
+    under auto-reset (panda_mujoco_gym/__init__.py:15), so later gym steps of a long run -- grippers
+    that stay closed and pressed, cubes grasped or knocked over -- dominate, not the first steps
+    after a reset.  B envs, random actions, auto-reset, `burn` untimed steps (each env's episode at
+    step `burn`), then `steps` timed ones.  The hand-over queue's counters are summed over the
+    burn-in (sampled after every step) and the timed steps' last."""
+    from pnp_amd.envs import BatchedFrankaShelfPNPEnv
+    env = BatchedFrankaShelfPNPEnv(B, engine=engine, env_offset=rank * B, autoreset=True)
+    env.reset()
+    rng = np.random.default_rng(11 + rank)
+    acts = torch.as_tensor(rng.uniform(-1, 1, size=(16, B, 7)), dtype=torch.float32, device=engine.device)
+    qh = QueueHealth()
+    t0 = time.perf_counter()
+    for i in range(burn):
+        env.step(acts[i % 16])
+        qh.sample()
+    burn_s = time.perf_counter() - t0
+    elapsed, kern_ms = _timed(lambda i: env.step(acts[i % 16]), steps, 0, dist,
+                              ranks_out=RANK_LEGS.setdefault("gym_steady", []))
+    qh.sample()
+    sub = env.cfg.n_substeps * env.cfg.n_calls
+    return {"gym_steps_per_s": B * world * steps / elapsed, "env_steps_per_s": B * world * steps * sub / elapsed,
+            "ms_per_gym_step": elapsed / steps * 1e3, "kernel_avg_ms": kern_ms,
+            "burn_in_steps": burn, "burn_in_ms_per_gym_step": burn_s / max(burn, 1) * 1e3,
+            "workload": f"{B} FrankaShelfPNPDense envs per GPU, random actions, auto-reset, gym steps "
+                        f"{burn + 1}-{burn + steps} of a run",
+            "queue": qh.record(f"after each of the {burn} burn-in steps and the last timed step")}
 
 
 # ----------------------------------------------------------------------------- C5 TQC training loop
-def run_tqc(engine, B, rank, world, dist, steps=3, warmup=2, learner_reps=20):
+def run_tqc(engine, B, rank, world, dist, steps=3, warmup=2, learner_reps=20, steady_burn=0):
     """C5: scripts/train.py's TQC loop over B batched envs per GPU (pnp_amd.tqc, train.py
     hyper-parameters): one step = one fused gym step of every env (policy actions, auto-reset,
     replay insert, obs statistics) + one gradient step (batch 512; gradients all-reduced over
-    ranks when N > 1).  Also times the gradient step alone."""
+    ranks when N > 1).  Also times the gradient step alone, train.py's update ratio, and (with
+    steady_burn) the loop after `steady_burn` further steps of the same run."""
     from pnp_amd.envs import BatchedFrankaShelfPNPEnv
     from pnp_amd.tqc import TQC, TQCConfig
     env = BatchedFrankaShelfPNPEnv(B, engine=engine, env_offset=rank * B)
@@ -365,6 +425,8 @@ def run_tqc(engine, B, rank, world, dist, steps=3, warmup=2, learner_reps=20):
         agent.train()
 
     elapsed, kern_ms = _timed(fn, steps, warmup, dist, ranks_out=RANK_LEGS.setdefault("tqc", []))
+    qh = QueueHealth()
+    qh.sample()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(learner_reps):
@@ -382,6 +444,22 @@ def run_tqc(engine, B, rank, world, dist, steps=3, warmup=2, learner_reps=20):
         agent.train(utd)
 
     utd_elapsed, _ = _timed(fn_utd, 1, 0, dist)
+    steady = None
+    if steady_burn > 0:
+        # the same run further on: steady_burn more vector steps (one gradient step each; the
+        # episodes are then at step ~steady_burn + 8 of 300), then timed steps
+        qs = QueueHealth()
+        t0 = time.perf_counter()
+        for _ in range(steady_burn):
+            fn(0)
+            qs.sample()
+        burn_s = time.perf_counter() - t0
+        s_el, _ = _timed(fn, steps, 0, dist, ranks_out=RANK_LEGS.setdefault("tqc_steady", []))
+        qs.sample()
+        steady = {"gym_steps_per_s": B * world * steps / s_el, "ms_per_step": s_el / steps * 1e3,
+                  "burn_in_steps": steady_burn, "burn_in_ms_per_step": burn_s / steady_burn * 1e3,
+                  "vector_steps_before_timing": warmup + steps + 1 + steady_burn,
+                  "queue": qs.record(f"after each of the {steady_burn} burn-in steps and the last timed step")}
     return {"gym_steps_per_s": B * world * steps / elapsed, "env_steps_per_s": B * world * steps * sub / elapsed,
             "ms_per_step": step_ms, "learner_ms_per_update": learner_ms,
             "learner": ((("hand-written fused HIP gradient step (csrc/tqc_fused.hip: "
@@ -393,7 +471,8 @@ def run_tqc(engine, B, rank, world, dist, steps=3, warmup=2, learner_reps=20):
             "reference_utd": {"gradient_steps_per_vector_step": utd, "ms_per_vector_step": utd_elapsed * 1e3,
                               "measured": True},
             "workload": f"C5: TQC (train.py hyper-parameters) on {B} FrankaShelfPNPDense envs per GPU, "
-                        f"one gym step + one gradient step per step"}
+                        f"one gym step + one gradient step per step",
+            "queue": qh.record("the last timed step"), "steady": steady}
 
 
 # ----------------------------------------------------------------------------- C2 IK
@@ -558,6 +637,8 @@ def main():
     ap.add_argument("--tqc-envs", type=int, default=8192, help="C5 envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (C3 leg)")
+    ap.add_argument("--steady-burn", type=int, default=50,
+                    help="gym / tqc legs: untimed steps of a long run before the steady-state timing (0: skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="N > 1: nccl (= RCCL over xGMI, one GPU per rank); gloo only to rehearse several "
                          "ranks on one GPU")

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 13
+#define PNP_ABI_VERSION 14
 
 #define PNP_OK 0
 #define PNP_ERR_ARG -1
@@ -234,7 +234,7 @@ typedef struct pnp_state_f64 {
  * nsub = 25, ten times; skills/base.py:43 and scripts/execute_pnp.py:103 with nsub = 1).
  * ctrl and mocap are held constant over the nsub sub-steps, as in the reference.
  * fp32: three capacity tiers of one kernel source -- compact (20 contacts, 8 envs per CU), full
- * (48 contacts, 4 per CU), wide (192 contacts, 1 per CU).  Each runs the envs the previous tier
+ * (64 contacts, 3 per CU), wide (192 contacts, 1 per CU).  Each runs the envs the previous tier
  * handed over, from the sub-step that would have overflowed its capacities, so results equal the
  * wide kernel's bit for bit; only the wide tier truncates (PNP_WARN_CONTACTFULL / CNSTRFULL).
  * fp64 (the single-env facade, the batched behaviour trees, debugging): the full kernel, whose
@@ -250,24 +250,31 @@ int32_t pnp_step(pnp_model* model, const pnp_state* state, int32_t B, int32_t ns
 int32_t pnp_step_f64(pnp_model* model, const pnp_state_f64* state, int32_t B, int32_t nsub, void* stream);
 
 /* Debug/parity: one mj_forward per env (state not advanced), dumping intermediates into
- * dbg[B * PNP_DBG_SIZE] (float64, device) at the offsets below. */
+ * dbg[B * PNP_DBG_SIZE] (float64, device, zero-initialised by the caller) at the offsets below.
+ * The forward runs through the step's tiers: the full kernel, and for the envs whose forward
+ * outgrows it the wide kernel (fp32: 192 contacts / 784 rows; fp64: 96 / 400), truncating past
+ * that like pnp_step (PNP_STEP_WIDE=0: the full kernel alone, truncating at 64 / 272).  ABI 14:
+ * the record holds the wide tier's capacities (ABI 13's held 48 contacts / 208 rows, less than the
+ * full tier's 64 / 272 since round 5: larger forwards wrote past their record). */
 #define PNP_DBG_QM 0            /* nv*nv dense joint-space inertia (incl. armature) */
 #define PNP_DBG_BIAS 1296       /* qfrc_bias[nv] */
 #define PNP_DBG_ACT 1332        /* qfrc_actuator[nv] */
 #define PNP_DBG_QACC_SMOOTH 1368
 #define PNP_DBG_QACC 1404
 #define PNP_DBG_COUNTS 1440     /* ncon, nefc, solver iterations, warn */
-#define PNP_DBG_CON 1444        /* ncon (<= 48) x 16: pos3 frame9 dist geom1 geom2 dim */
+#define PNP_DBG_CON 1444        /* ncon (<= 192) x 16: pos3 frame9 dist geom1 geom2 dim */
 #define PNP_DBG_CON_STRIDE 16
-#define PNP_DBG_EFC_FORCE 2212  /* nefc (<= 208) */
-#define PNP_DBG_EFC_POS 2420
-#define PNP_DBG_EFC_D 2628
-#define PNP_DBG_EFC_AREF 2836
-#define PNP_DBG_EFC_TYPE 3044
-#define PNP_DBG_EFC_J 3252      /* nefc x nv dense */
-#define PNP_DBG_QACC_NEWTON 10740 /* Newton result before no-slip */
-#define PNP_DBG_NOSLIP_ITER 10776 /* no-slip sweeps run (mj_solNoSlip's early exit) */
-#define PNP_DBG_SIZE 10780
+#define PNP_DBG_EFC_FORCE 4516  /* nefc (<= 784) */
+#define PNP_DBG_EFC_POS 5300
+#define PNP_DBG_EFC_D 6084
+#define PNP_DBG_EFC_AREF 6868
+#define PNP_DBG_EFC_TYPE 7652
+#define PNP_DBG_EFC_J 8436      /* nefc x nv dense */
+#define PNP_DBG_QACC_NEWTON 36660 /* Newton result before no-slip */
+#define PNP_DBG_NOSLIP_ITER 36696 /* no-slip sweeps run (mj_solNoSlip's early exit) */
+#define PNP_DBG_SIZE 36700
+#define PNP_DBG_MAXCON 192
+#define PNP_DBG_MAXEFC 784
 int32_t pnp_forward_debug(pnp_model* model, const pnp_state* state, int32_t B, double* dbg, void* stream);
 int32_t pnp_forward_debug_f64(pnp_model* model, const pnp_state_f64* state, int32_t B, double* dbg,
                               void* stream);
@@ -464,6 +471,20 @@ int32_t pnp_tqc_param_counts(int32_t* actor_params, int32_t* critic_params);
 /* grads_out (optional, tests): the step's reduced gradients, actor then critics, in the
  * parameters' own layouts and order.  Stream-ordered, no host sync; capturable in a HIP graph. */
 int32_t pnp_tqc_update(const pnp_tqc_desc* d, const pnp_tqc_batch* b, float* grads_out, void* stream);
+/* pnp_tqc_update split for a data-parallel learner (one process per GPU; the reference's learner is
+ * single-process, scripts/train.py:67-93 -- this is its multi-GPU form): the caller averages the
+ * gradients over ranks between the phases, as sb3 would with a DDP optimiser.  grads: device fp32
+ * [actor_params + critic_params + 1] (pnp_tqc_param_counts; the last float is the entropy
+ * coefficient's gradient).  The same batch (b) for all three calls of one step.
+ *   phase 0: forward chains, critic backward, critic weight gradients -> grads[actor_params ..]
+ *            (+ the entropy coefficient's), logs[0, 1, 3]; no parameter changes;
+ *   phase 1: Adam on the critics and the entropy coefficient and the Polyak update from
+ *            grads[actor_params ..] (all-reduced by the caller), then the actor's chains against
+ *            the updated critics, actor weight gradients -> grads[0 .. actor_params), logs[2];
+ *   phase 2: Adam on the actor from grads[0 .. actor_params).
+ * With no collective in between the three phases equal pnp_tqc_update bit for bit.  Stream-
+ * ordered, no host sync. */
+int32_t pnp_tqc_update_phase(const pnp_tqc_desc* d, const pnp_tqc_batch* b, float* grads, int32_t phase, void* stream);
 
 /* ------------------------------------------------------------------ skills */
 /* RotateSkill.reset's trajectory (reference skills/rotate.py:39-46) for B skills: target =

@@ -292,7 +292,7 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
       const T rb = (s2[j1] * fabs(AB[i][j2]) + s2[j2] * fabs(AB[i][j1])) * inv;
       const T sep = fabs(tl) - ra - rb;
       if (sep > margin) return;
-      if (T(1.05) * sep > best + T(1e-12)) {
+      if (T(1.05) * sep > best + T(C_BB_TOL)) {   // (oracle/collision.c A3: faces win near-ties)
         best = sep; btype = 2; bi = i; bj = j; btl = tl;
       }
     }

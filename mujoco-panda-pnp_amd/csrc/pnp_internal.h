@@ -119,6 +119,11 @@ int32_t launch_env_step_wide(const pnp_model* model, const pnp_state_t<float>* s
                              void* stream, int resume, int only_tier, int* hq = nullptr, int hq_target = 0,
                              int hq_grid = 0, long long hq_timeout = 0, int* count_out = nullptr);
 int32_t step_wide_lds_bytes();
+// forward_debug's wide tier: the envs whose full-tier forward outgrew it (record COUNTS + 3 = -1)
+int32_t launch_forward_debug_wide(const pnp_model* model, const pnp_state_t<float>* st, int32_t B, double* dbg,
+                                  void* stream);
+int32_t launch_forward_debug_wide64(const pnp_model* model, const pnp_state_t<double>* st, int32_t B, double* dbg,
+                                    void* stream);
 // step_wide64.hip: the fp64 wide tier (resume passes of pnp_step_f64 and pnp_env_step_f64)
 int32_t launch_step_wide64(const pnp_model* model, const pnp_state_t<double>* st, int32_t B, int32_t nsub,
                            void* stream);

@@ -424,6 +424,15 @@ __device__ __forceinline__ T rowsum16(T v) {
   v += dpp_s<0x140>(v);   // row_mirror
   return v;
 }
+// max over each row of 16 lanes, result in every lane of the row
+template <typename T>
+__device__ __forceinline__ T rowmax16(T v) {
+  v = fmax(v, dpp_f<0xB1>(v));
+  v = fmax(v, dpp_f<0x4E>(v));
+  v = fmax(v, dpp_f<0x141>(v));
+  v = fmax(v, dpp_f<0x140>(v));
+  return v;
+}
 // sum over the wave, result (wave-uniform) in every lane
 template <typename T>
 __device__ __forceinline__ T wsum(T v) {
@@ -1831,29 +1840,54 @@ __device__ void st_constraints(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s
       m1 = __shfl(km1, src);
       m2 = __shfl(km2, src);
     }
-    if (c >= nc || s.con_rbase[c] < 0) continue;
-    const int t0 = s.con_t[c][0], t1 = s.con_t[c][1], w = row_width(m, t0, t1);
-    if (k >= w) continue;
-    const Con<T>& con = s.con[c];
-    const int d = slot_dof(m, t0, t1, k);
-    if (!fastc) {
-      const int b1 = m.geom_bodyid[con.g1], b2 = m.geom_bodyid[con.g2];
-      r1 = m.body_rootid[b1];
-      r2 = m.body_rootid[b2];
-      m1 = m.body_dofmask[b1];
-      m2 = m.body_dofmask[b2];
+    // (a contact's slots are one 16-lane DPP row: PH_ROWW = 16; inactive slots take part in the
+    // fp32 row reductions below with zeros)
+    bool act = c < nc && s.con_rbase[c] >= 0;
+    int t0 = 0, t1 = 0, w = 0;
+    if (act) {
+      t0 = s.con_t[c][0]; t1 = s.con_t[c][1]; w = row_width(m, t0, t1);
+      act = k < w;
     }
-    T jp1[3], jr1[3], jp2[3], jr2[3];
-    jac_col_rm(s, r1, m1, d, con.pos, jp1, jr1);
-    jac_col_rm(s, r2, m2, d, con.pos, jp2, jr2);
-    const T jd[3] = {jp2[0] - jp1[0], jp2[1] - jp1[1], jp2[2] - jp1[2]};
-    T cj[3];
-    for (int a = 0; a < 3; a++) cj[a] = con.frame[3 * a] * jd[0] + con.frame[3 * a + 1] * jd[1] + con.frame[3 * a + 2] * jd[2];
-    const int sb = s.con_sbase[c];
-    for (int a = 1; a < con.dim && a < 3; a++) {
-      const T fri = con.friction[a - 1];
-      s.efc_Jv[sb + (2 * (a - 1)) * w + k] = cj[0] + fri * cj[a];
-      s.efc_Jv[sb + (2 * (a - 1) + 1) * w + k] = cj[0] - fri * cj[a];
+    T cj[3] = {0, 0, 0};
+    if (act) {
+      const Con<T>& con = s.con[c];
+      const int d = slot_dof(m, t0, t1, k);
+      if (!fastc) {
+        const int b1 = m.geom_bodyid[con.g1], b2 = m.geom_bodyid[con.g2];
+        r1 = m.body_rootid[b1];
+        r2 = m.body_rootid[b2];
+        m1 = m.body_dofmask[b1];
+        m2 = m.body_dofmask[b2];
+      }
+      T jp1[3], jr1[3], jp2[3], jr2[3];
+      jac_col_rm(s, r1, m1, d, con.pos, jp1, jr1);
+      jac_col_rm(s, r2, m2, d, con.pos, jp2, jr2);
+      const T jd[3] = {jp2[0] - jp1[0], jp2[1] - jp1[1], jp2[2] - jp1[2]};
+      for (int a = 0; a < 3; a++) cj[a] = con.frame[3 * a] * jd[0] + con.frame[3 * a + 1] * jd[1] + con.frame[3 * a + 2] * jd[2];
+    }
+    if constexpr (sizeof(T) == 4) {
+      // A tangent row at the rounding level of its normal row is rounding: two bodies of one tree
+      // whose relative motion has no tangential component (the closed gripper's finger pads, face
+      // to face: only the finger slides move them apart, along the normal) have J_t = 0 exactly in
+      // fp64 (MuJoCo's pyramid edges J_n +- mu J_t are then equal, K1 = 0 and mj_solNoSlip leaves
+      // the pair at its mean), but fp32 frames and joint axes rounded apart at ~6e-8 rad give J_t
+      // ~1e-7: no-slip then projects the pair on noise and saturates it (the pads' finger
+      // accelerations 1.4e-4 off in the tree's M-norm, tools/pads_stage_diag.py).  Such a row (its
+      // largest entry within 16 fp32 ulps of the normal row's largest) is snapped to zero, so the
+      // edges are equal as in fp64; a resolved tangent (J_t / J_n >~ 2e-6) is unchanged.
+      const T nmax = rowmax16(fabs(cj[0])) * T(16 * 1.1920929e-7);
+      const T t1m = rowmax16(fabs(cj[1])), t2m = rowmax16(fabs(cj[2]));
+      if (t1m <= nmax) cj[1] = T(0);
+      if (t2m <= nmax) cj[2] = T(0);
+    }
+    if (act) {
+      const Con<T>& con = s.con[c];
+      const int sb = s.con_sbase[c];
+      for (int a = 1; a < con.dim && a < 3; a++) {
+        const T fri = con.friction[a - 1];
+        s.efc_Jv[sb + (2 * (a - 1)) * w + k] = cj[0] + fri * cj[a];
+        s.efc_Jv[sb + (2 * (a - 1) + 1) * w + k] = cj[0] - fri * cj[a];
+      }
     }
   }
   // row scalars and impedance (lanes over rows)
@@ -4255,6 +4289,19 @@ __device__ void dump_contacts(const DevPhys<T>& /*image: phys<T>()*/, const Env<
   }
 }
 
+// debug record of the smooth forces: written before the solver, because the lean builds keep
+// qfrc_bias / qfrc_actuator in storage the solver stages reuse
+template <typename T>
+__device__ void dump_smooth(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, double* o) {
+  const DevPhys<T>& m = phys<T>();
+  const int l = lane_id();
+  if (l < m.nv) {
+    o[PNP_DBG_BIAS + l] = s.qfrc_bias[l];
+    o[PNP_DBG_ACT + l] = s.qfrc_act[l];
+    o[PNP_DBG_QACC_SMOOTH + l] = s.qacc_smooth[l];
+  }
+}
+
 template <typename T, class CLK>
 __device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& clk, double* dbg = nullptr) {
   const DevPhys<T>& m = phys<T>();
@@ -4286,6 +4333,7 @@ __device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& 
   if (PNP_HANDS && s.ovf) return;
   st_velocity(m, s);        clk.lap(6);
   st_actuation_smooth(m, s); clk.lap(7);
+  if (dbg) dump_smooth(m, s, dbg);
   st_newton(m, s, clk);     // laps 8..12 inside
   if (PNP_HANDS && s.ovf) return;
   clk.count(SN_EFC, s.nefc);
@@ -4414,30 +4462,38 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) step_
   store_env(m, s, st, b);
 }
 
-// debug: one forward, dump intermediates (layout PNP_DBG_* in include/pnp.h)
+// debug: one forward, dump intermediates (layout PNP_DBG_* in include/pnp.h).  mode 0: this tier
+// alone (truncating past its capacities like MuJoCo's full buffers); 1: a forward that outgrows
+// this tier is handed to the next one (its record's COUNTS + 3, the warn slot, set to -1: a warn
+// word is never negative); 2: resume -- only the envs whose record says handed over, rewritten
+// whole by this tier.  So pnp_forward_debug sees the same capacities as pnp_step.
+static_assert(PH_MAXCON <= PNP_DBG_MAXCON && PH_MAXEFC <= PNP_DBG_MAXEFC,
+              "the debug record (include/pnp.h PNP_DBG_*) must hold every tier's contacts and rows");
 template <typename T>
 __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) forward_debug_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st, int B,
-                                                          double* __restrict__ dbg) {
+                                                          double* __restrict__ dbg, int mode) {
   __shared__ __attribute__((aligned(16))) Env<T> s_env;   // static LDS: see env_lds_note
   Env<T>& s = s_env;
   const DevPhys<T>& m = phys<T>();
   (void)mp;
   const int b = blockIdx.x;
   if (b >= B) return;
-  load_env(m, s, st, b);
   double* o = dbg + (size_t)b * PNP_DBG_SIZE;
+  if (mode == 2 && !(o[PNP_DBG_COUNTS + 3] < 0.0)) return;
+  load_env(m, s, st, b, mode == 1);
   NoClock clk;
   forward(m, s, clk, o);
   const int l = lane_id();
+  if (PNP_HANDS && s.ovf) {
+    if (l == 0) o[PNP_DBG_COUNTS + 3] = -1.0;
+    return;
+  }
   const int nv = m.nv;
   for (int e = l; e < nv * nv; e += NT) {
     const int i = e / nv, j = e % nv;
     o[PNP_DBG_QM + e] = m.dof_tree[i] == m.dof_tree[j] ? (double)s.M[mblk(m, i, j)] : 0.0;
   }
-  if (l < nv) {
-    o[PNP_DBG_BIAS + l] = s.qfrc_bias[l];
-    o[PNP_DBG_ACT + l] = s.qfrc_act[l];
-    o[PNP_DBG_QACC_SMOOTH + l] = s.qacc_smooth[l];
+  if (l < nv) {   // (bias, actuation, qacc_smooth: dump_smooth)
     o[PNP_DBG_QACC + l] = s.qacc[l];
     o[PNP_DBG_QACC_NEWTON + l] = s.x[l];
   }
@@ -4450,7 +4506,11 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) forwa
   }
   for (int r = l; r < s.nefc; r += NT) {
     o[PNP_DBG_EFC_FORCE + r] = s.efc_force[r];
+#if PNP_LEAN
+    o[PNP_DBG_EFC_POS + r] = __builtin_nan("");   // (not kept by the lean builds: NaN, never compared)
+#else
     o[PNP_DBG_EFC_POS + r] = s.efc_pos[r];
+#endif
     o[PNP_DBG_EFC_D + r] = s.efc_D[r];
     o[PNP_DBG_EFC_AREF + r] = s.efc_aref[r];
     o[PNP_DBG_EFC_TYPE + r] = s.efc_type[r];
@@ -4509,6 +4569,19 @@ int32_t launch_step_wide(const pnp_model* model, const pnp_state_t<float>* st, i
 
 int32_t step_wide_lds_bytes() { return (int32_t)sizeof(Env<float>); }
 
+int32_t launch_forward_debug_wide(const pnp_model* model, const pnp_state_t<float>* st, int32_t B, double* dbg,
+                                  void* stream) {
+  const DevPhys<float>* src = phys_image<float>(model);
+  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  ResidentLease lease;
+  if (const int32_t rc = lease.acquire(RES_WIDE_F32, model, (const void*)&g_phys_f32, src, sizeof(DevPhys<float>),
+                                       stream))
+    return rc;
+  hipLaunchKernelGGL(forward_debug_kernel<float>, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, B, dbg, 2);
+  if (const int32_t rc = pnp_check_launch("forward_debug_kernel (wide)")) return rc;
+  return lease.launched();
+}
+
 #include "env_dev.h"   // the gym step's wide resume pass
 
 #elif PNP_WIDE64
@@ -4530,6 +4603,19 @@ int32_t launch_step_wide64(const pnp_model* model, const pnp_state_t<double>* st
 }
 
 int32_t step_wide64_lds_bytes() { return (int32_t)sizeof(Env<double>); }
+
+int32_t launch_forward_debug_wide64(const pnp_model* model, const pnp_state_t<double>* st, int32_t B, double* dbg,
+                                    void* stream) {
+  const DevPhys<double>* src = phys_image<double>(model);
+  if (!src) { pnp_set_error("model has no physics image (%s)", model->phys_err); return PNP_ERR_MODEL; }
+  ResidentLease lease;
+  if (const int32_t rc = lease.acquire(RES_WIDE64_F64, model, (const void*)&g_phys_f64, src,
+                                       sizeof(DevPhys<double>), stream))
+    return rc;
+  hipLaunchKernelGGL(forward_debug_kernel<double>, dim3(B), dim3(NT), 0, (hipStream_t)stream, src, *st, B, dbg, 2);
+  if (const int32_t rc = pnp_check_launch("forward_debug_kernel (wide64)")) return rc;
+  return lease.launched();
+}
 
 #include "env_dev.h"   // the fp64 gym step's wide resume pass
 
@@ -4584,9 +4670,23 @@ static int32_t launch_step(pnp_model* model, const pnp_state_t<T>* st, int32_t B
   ResidentLease lease;
   if (const int32_t rc = phys_resident<T>(model, stream, lease)) return rc;
   if (dbg) {
+    // the full tier, handing what outgrows it to the wide tier (fp32: 192 contacts / 784 rows;
+    // fp64: 96 / 400), which truncates like MuJoCo; PNP_STEP_WIDE=0: the full tier truncates
+    const int hand = wide_enabled();
     auto k = forward_debug_kernel<T>;
-    hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, dbg);
+    hipLaunchKernelGGL(k, dim3(B), dim3(NT), 0, (hipStream_t)stream, dm, *st, B, dbg, hand);
     if (const int32_t rc = pnp_check_launch("forward_debug_kernel")) return rc;
+    if (hand) {
+      if constexpr (sizeof(T) == 8) {
+        if (const int32_t rc = launch_forward_debug_wide64(model, reinterpret_cast<const pnp_state_t<double>*>(st), B,
+                                                           dbg, stream))
+          return rc;
+      } else {
+        if (const int32_t rc = launch_forward_debug_wide(model, reinterpret_cast<const pnp_state_t<float>*>(st), B,
+                                                         dbg, stream))
+          return rc;
+      }
+    }
     return lease.launched();
   }
   auto k = prof ? step_kernel<T, true> : step_kernel<T, false>;

@@ -621,7 +621,14 @@ struct WArgs {
   const float* sums; int nslab;
   float* logs; float critic_scale; int actor;
   float step_add;            // 1: the step tensors are incremented after this kernel, 0: before
+  // data-parallel split (pnp_tqc_update_phase): WG_FUSED = gradient + Adam in place; WG_GRAD = the
+  // gradient only, into grad_out (the entropy coefficient's at ent_gi); WG_APPLY = Adam / Polyak
+  // from grad_in (the caller's all-reduced gradients), no product
+  int mode;
+  const float* grad_in;
+  int ent_gi;
 };
+enum { WG_FUSED = 0, WG_GRAD = 1, WG_APPLY = 2 };
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float gr, float lr, float b1, float b2, float eps,
                                           float step) {
   const float bc1 = 1.f - powf(b1, step), bc2 = 1.f - powf(b2, step);
@@ -654,17 +661,19 @@ __global__ void __launch_bounds__(WTH) tqc_wgrad_adam_kernel(WArgs a) {
   for (int h = 0; h < 2; h++)
 #pragma unroll
     for (int h2 = 0; h2 < 2; h2++) acc[h][h2] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int rows = a.B / WNW, b0 = w * rows, b1 = b0 + rows;
+  const int rows = a.mode == WG_APPLY ? 0 : a.B / WNW, b0 = w * rows, b1 = b0 + rows;
   for (int b = b0; b < b1; b += 4 * WRG) {   // WRG row groups per trip, all their loads in flight
     float xa[WRG][2], yb[WRG][2];
 #pragma unroll
     for (int u = 0; u < WRG; u++) {
-      const int bb = b + 4 * u;
-      const size_t r = bb + kq;
+      // each lane guards its own row: with B / WNW not a multiple of 4 a row group straddles the
+      // wave's range end (rows of the next wave, or past B for the last wave)
+      const int r = b + 4 * u + kq;
+      const bool live = r < b1;
 #pragma unroll
       for (int h = 0; h < 2; h++) {   // rows past b1: zeros (the sum is unchanged)
-        xa[u][h] = bb < b1 ? (xl[h] ? xp[h][r * xld[h]] : xc[h]) : 0.f;
-        yb[u][h] = bb < b1 && yl[h] ? yp[h][r * J.ldy] : 0.f;
+        xa[u][h] = live ? (xl[h] ? xp[h][(size_t)r * xld[h]] : xc[h]) : 0.f;
+        yb[u][h] = live && yl[h] ? yp[h][(size_t)r * J.ldy] : 0.f;
       }
     }
 #pragma unroll
@@ -702,7 +711,9 @@ __global__ void __launch_bounds__(WTH) tqc_wgrad_adam_kernel(WArgs a) {
       step = J.stepb[0] + a.step_add;
       gi = J.goffb + n;
     }
+    if (a.mode == WG_APPLY) gr = a.grad_in[gi];
     if (a.grad_out) a.grad_out[gi] = gr;
+    if (a.mode == WG_GRAD) continue;
     float p = *pp, m = *mp, v = *vp;
     adam_elem(p, m, v, gr, lr, a.beta1, a.beta2, a.eps, step);
     *pp = p; *mp = m; *vp = v;
@@ -717,14 +728,22 @@ __global__ void __launch_bounds__(WTH) tqc_wgrad_adam_kernel(WArgs a) {
       }
       const float mean = s / (float)a.B;
       const float le = a.ent[0];
-      a.logs[0] = expf(le);
-      a.logs[1] = l * a.critic_scale;
-      a.logs[3] = -(le * mean);
-      float p = le, m = a.ent_m[0], v = a.ent_v[0];
-      adam_elem(p, m, v, -mean, lr, a.beta1, a.beta2, a.eps, a.ent_step[0] + a.step_add);
-      a.ent[0] = p; a.ent_m[0] = m; a.ent_v[0] = v;
+      float ge = -mean;
+      if (a.mode != WG_APPLY) {
+        a.logs[0] = expf(le);
+        a.logs[1] = l * a.critic_scale;
+        a.logs[3] = -(le * mean);
+        if (a.mode == WG_GRAD) a.grad_out[a.ent_gi] = ge;
+      } else {
+        ge = a.grad_in[a.ent_gi];
+      }
+      if (a.mode != WG_GRAD) {
+        float p = le, m = a.ent_m[0], v = a.ent_v[0];
+        adam_elem(p, m, v, ge, lr, a.beta1, a.beta2, a.eps, a.ent_step[0] + a.step_add);
+        a.ent[0] = p; a.ent_m[0] = m; a.ent_v[0] = v;
+      }
     }
-    if (a.actor) {
+    if (a.actor && a.mode != WG_APPLY) {
       float s = 0.f;
       for (int q = 0; q < a.nslab; q++) s += a.sums[q * NSUM + 5];
       a.logs[2] = s / (float)a.B;
@@ -905,15 +924,21 @@ static int add_wjob(WArgs& a, int tile, const float* x0, int ldx0, int kx, const
   return tile + (K + 1 + WT - 1) / WT * J.tiles_n;
 }
 
-extern "C" int32_t pnp_tqc_update(const pnp_tqc_desc* d, const pnp_tqc_batch* b, float* grads_out, void* stream) {
-  if (!tqc_desc_ok(d)) { pnp_set_error("pnp_tqc_update: unsupported TQC shape or null pointer"); return PNP_ERR_UNSUPPORTED; }
+// phase -1: the whole step (pnp_tqc_update); 0 / 1 / 2: pnp_tqc_update_phase's data-parallel split
+static int32_t tqc_run(const pnp_tqc_desc* d, const pnp_tqc_batch* b, float* grads, int phase, void* stream,
+                       const char* fn) {
+  if (!tqc_desc_ok(d)) { pnp_set_error("%s: unsupported TQC shape or null pointer", fn); return PNP_ERR_UNSUPPORTED; }
   if (!b || !b->obs || !b->act || !b->next_obs || !b->done || !b->reward || !b->eps_pi || !b->eps_next) {
-    pnp_set_error("pnp_tqc_update: null batch buffer");
+    pnp_set_error("%s: null batch buffer", fn);
+    return PNP_ERR_ARG;
+  }
+  if (phase < -1 || phase > 2 || (phase >= 0 && !grads)) {
+    pnp_set_error("%s: phase must be 0, 1 or 2 with a gradient buffer", fn);
     return PNP_ERR_ARG;
   }
   const int B = d->batch, S = B / R;
   if (d->workspace_floats < tqc_ws_floats(B)) {
-    pnp_set_error("pnp_tqc_update: workspace too small");
+    pnp_set_error("%s: workspace too small", fn);
     return PNP_ERR_ARG;
   }
   const hipStream_t st = (hipStream_t)stream;
@@ -937,52 +962,74 @@ extern "C" int32_t pnp_tqc_update(const pnp_tqc_desc* d, const pnp_tqc_batch* b,
   auto M = [&](int id) { return ws + (size_t)id * B * HID; };
   float* SM = M(M_SM);
 
-  hipLaunchKernelGGL(tqc_fwd_kernel, dim3(S, 1 + 2 * NC), dim3(NTH), 0, st, g);
-  if (const int32_t rc = pnp_check_launch("tqc_fwd_kernel")) return rc;
-  hipLaunchKernelGGL(tqc_critic_bwd_kernel, dim3(S, NC), dim3(NTH), 0, st, g);
-  if (const int32_t rc = pnp_check_launch("tqc_critic_bwd_kernel")) return rc;
-
+  // the two weight-gradient launches' jobs (critics, actor)
   WArgs ac{};
   ac.B = B; ac.lr = d->lr; ac.beta1 = d->beta1; ac.beta2 = d->beta2; ac.eps = d->adam_eps; ac.tau = d->tau;
+  ac.ent_gi = ACT_P + CRIT_P;
   WArgs aa = ac;
   ac.step_add = 1.f;   // the critics' steps: incremented by K4
   aa.step_add = 0.f;   // the actor's: by K1
-  int tiles = 0;
+  int ctiles = 0;
   for (int c = 0; c < NC; c++)
     for (int l = 0; l < 4; l++) {
       const int K = l == 0 ? NIN : HID, N = l == 3 ? NQ : HID, tw = 2 * l, tb = 2 * l + 1;
       const size_t ow = (size_t)c * K * N, ob = (size_t)c * N;
       const float* x0 = l == 0 ? b->obs : M(M_CH + 3 * c + l - 1);
       const float* dy = l == 3 ? SM + S_DQ + c * NQ : M(M_CD + 3 * c + l);
-      tiles = add_wjob(ac, tiles, x0, l == 0 ? OBS : HID, l == 0 ? OBS : K, l == 0 ? b->act : x0, l == 0 ? ACT : HID, dy, K, N,
-                       0, d->critic[tw] + ow, d->critic_m[tw] + ow, d->critic_v[tw] + ow, d->target[tw] + ow,
-                       d->critic_step[tw], d->critic[tb] + ob, d->critic_m[tb] + ob, d->critic_v[tb] + ob,
-                       d->target[tb] + ob, d->critic_step[tb], ACT_P + crit_off(tw) + (int)ow, ACT_P + crit_off(tb) + (int)ob);
+      ctiles = add_wjob(ac, ctiles, x0, l == 0 ? OBS : HID, l == 0 ? OBS : K, l == 0 ? b->act : x0, l == 0 ? ACT : HID, dy, K, N,
+                        0, d->critic[tw] + ow, d->critic_m[tw] + ow, d->critic_v[tw] + ow, d->target[tw] + ow,
+                        d->critic_step[tw], d->critic[tb] + ob, d->critic_m[tb] + ob, d->critic_v[tb] + ob,
+                        d->target[tb] + ob, d->critic_step[tb], ACT_P + crit_off(tw) + (int)ow, ACT_P + crit_off(tb) + (int)ob);
     }
-  ac.grad_out = grads_out;
   ac.ent = d->log_ent_coef; ac.ent_m = d->ent_m; ac.ent_v = d->ent_v; ac.ent_step = d->ent_step;
   ac.sums = g.sums; ac.nslab = S; ac.logs = d->logs;
   ac.critic_scale = 1.f / ((float)B * NC * NQ * KEEP);
-  hipLaunchKernelGGL(tqc_wgrad_adam_kernel, dim3(tiles), dim3(WTH), 0, st, ac);
-  if (const int32_t rc = pnp_check_launch("tqc_wgrad_adam_kernel (critics)")) return rc;
-
-  hipLaunchKernelGGL(tqc_pi_critic_kernel, dim3(S, NC), dim3(NTH), 0, st, g);
-  if (const int32_t rc = pnp_check_launch("tqc_pi_critic_kernel")) return rc;
-  hipLaunchKernelGGL(tqc_actor_bwd_kernel, dim3(S), dim3(NTH), 0, st, g);
-  if (const int32_t rc = pnp_check_launch("tqc_actor_bwd_kernel")) return rc;
-
-  tiles = 0;
+  int atiles = 0;
   for (int l = 0; l < 5; l++) {
     const int K = l == 0 ? OBS : HID, N = l >= 3 ? ACT : HID, tw = 2 * l, tb = 2 * l + 1;
     const float* x0 = l == 0 ? b->obs : M(M_AH + (l < 3 ? l - 1 : 2));
     const float* dy = l == 3 ? SM + S_DMU : l == 4 ? SM + S_DLS : M(M_AD + l);
-    tiles = add_wjob(aa, tiles, x0, l == 0 ? OBS : HID, K, x0, HID, dy, K, N, 1, d->actor[tw], d->actor_m[tw],
-                     d->actor_v[tw], nullptr, d->actor_step[tw], d->actor[tb], d->actor_m[tb], d->actor_v[tb], nullptr,
-                     d->actor_step[tb], act_off(tw), act_off(tb));
+    atiles = add_wjob(aa, atiles, x0, l == 0 ? OBS : HID, K, x0, HID, dy, K, N, 1, d->actor[tw], d->actor_m[tw],
+                      d->actor_v[tw], nullptr, d->actor_step[tw], d->actor[tb], d->actor_m[tb], d->actor_v[tb], nullptr,
+                      d->actor_step[tb], act_off(tw), act_off(tb));
   }
-  aa.grad_out = grads_out;
   aa.sums = g.sums; aa.nslab = S; aa.logs = d->logs; aa.actor = 1;
-  hipLaunchKernelGGL(tqc_wgrad_adam_kernel, dim3(tiles), dim3(WTH), 0, st, aa);
-  if (const int32_t rc = pnp_check_launch("tqc_wgrad_adam_kernel (actor)")) return rc;
+  auto wlaunch = [&](WArgs a, int tiles, int mode, const char* what) -> int32_t {
+    a.mode = mode;
+    if (mode == WG_APPLY) { a.grad_in = grads; a.grad_out = nullptr; }
+    else a.grad_out = grads;
+    hipLaunchKernelGGL(tqc_wgrad_adam_kernel, dim3(tiles), dim3(WTH), 0, st, a);
+    return pnp_check_launch(what);
+  };
+
+  if (phase <= 0) {
+    hipLaunchKernelGGL(tqc_fwd_kernel, dim3(S, 1 + 2 * NC), dim3(NTH), 0, st, g);
+    if (const int32_t rc = pnp_check_launch("tqc_fwd_kernel")) return rc;
+    hipLaunchKernelGGL(tqc_critic_bwd_kernel, dim3(S, NC), dim3(NTH), 0, st, g);
+    if (const int32_t rc = pnp_check_launch("tqc_critic_bwd_kernel")) return rc;
+    if (const int32_t rc = wlaunch(ac, ctiles, phase < 0 ? WG_FUSED : WG_GRAD, "tqc_wgrad_adam_kernel (critics)")) return rc;
+    if (phase == 0) return PNP_OK;
+  }
+  if (phase <= 1) {
+    if (phase == 1)
+      if (const int32_t rc = wlaunch(ac, ctiles, WG_APPLY, "tqc_wgrad_adam_kernel (critics, apply)")) return rc;
+    hipLaunchKernelGGL(tqc_pi_critic_kernel, dim3(S, NC), dim3(NTH), 0, st, g);
+    if (const int32_t rc = pnp_check_launch("tqc_pi_critic_kernel")) return rc;
+    hipLaunchKernelGGL(tqc_actor_bwd_kernel, dim3(S), dim3(NTH), 0, st, g);
+    if (const int32_t rc = pnp_check_launch("tqc_actor_bwd_kernel")) return rc;
+    if (const int32_t rc = wlaunch(aa, atiles, phase < 0 ? WG_FUSED : WG_GRAD, "tqc_wgrad_adam_kernel (actor)")) return rc;
+    if (phase == 1) return PNP_OK;
+  }
+  if (phase == 2)
+    if (const int32_t rc = wlaunch(aa, atiles, WG_APPLY, "tqc_wgrad_adam_kernel (actor, apply)")) return rc;
   return PNP_OK;
+}
+
+extern "C" int32_t pnp_tqc_update(const pnp_tqc_desc* d, const pnp_tqc_batch* b, float* grads_out, void* stream) {
+  return tqc_run(d, b, grads_out, -1, stream, "pnp_tqc_update");
+}
+
+extern "C" int32_t pnp_tqc_update_phase(const pnp_tqc_desc* d, const pnp_tqc_batch* b, float* grads, int32_t phase,
+                                        void* stream) {
+  return tqc_run(d, b, grads, phase, stream, "pnp_tqc_update_phase");
 }

@@ -10,7 +10,7 @@ from .model import PnpIKParams, PnpModelDesc
 # PNP_LIB: another build of the same sources (tools/asan_cpu_tests.sh: the host-sanitizer build)
 LIB_PATH = os.environ.get("PNP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpnp.so")
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 # every symbol include/pnp.h declares (tests check the library exports all of them)
 EXPORTS = [
@@ -21,7 +21,7 @@ EXPORTS = [
     "pnp_env_params_size", "pnp_env_init", "pnp_env_init_f64", "pnp_env_reset", "pnp_env_reset_f64",
     "pnp_env_step", "pnp_env_step_f64", "pnp_env_evaluate", "pnp_env_evaluate_f64",
     "pnp_slerp_track_f64", "pnp_env_queue_status", "pnp_tqc_workspace_floats", "pnp_tqc_param_counts",
-    "pnp_tqc_update", "pnp_tqc_sample", "pnp_tqc_sample_draw",
+    "pnp_tqc_update", "pnp_tqc_update_phase", "pnp_tqc_sample", "pnp_tqc_sample_draw",
 ]
 
 STATE_FIELDS = ("qpos", "qvel", "ctrl", "mocap_pos", "mocap_quat", "qacc_warmstart", "time", "warn")
@@ -94,8 +94,8 @@ class PnpTqcReplay(C.Structure):
 
 # debug record layout (include/pnp.h PNP_DBG_*)
 DBG = dict(QM=0, BIAS=1296, ACT=1332, QACC_SMOOTH=1368, QACC=1404, COUNTS=1440, CON=1444, CON_STRIDE=16,
-           EFC_FORCE=2212, EFC_POS=2420, EFC_D=2628, EFC_AREF=2836, EFC_TYPE=3044, EFC_J=3252,
-           QACC_NEWTON=10740, NOSLIP_ITER=10776, SIZE=10780)
+           EFC_FORCE=4516, EFC_POS=5300, EFC_D=6084, EFC_AREF=6868, EFC_TYPE=7652, EFC_J=8436,
+           QACC_NEWTON=36660, NOSLIP_ITER=36696, SIZE=36700, MAXCON=192, MAXEFC=784)
 
 _lib = None
 
@@ -179,6 +179,8 @@ def load():
     L.pnp_tqc_param_counts.restype = I32
     L.pnp_tqc_update.argtypes = [C.POINTER(PnpTqcDesc), C.POINTER(PnpTqcBatch), P, P]
     L.pnp_tqc_update.restype = I32
+    L.pnp_tqc_update_phase.argtypes = [C.POINTER(PnpTqcDesc), C.POINTER(PnpTqcBatch), P, I32, P]
+    L.pnp_tqc_update_phase.restype = I32
     L.pnp_tqc_sample.argtypes = [C.POINTER(PnpTqcReplay), P, I32, P, P, P, P, P, P]
     L.pnp_tqc_sample.restype = I32
     L.pnp_tqc_sample_draw.argtypes = [C.POINTER(PnpTqcReplay), C.c_uint64, P, I32, P, P, P, P, P, P, P, P, P]

@@ -69,9 +69,10 @@ class TQCConfig:
     # process only; the data-parallel learner all-reduces eagerly)
     graph: bool = True
     # the hand-written fused gradient step (csrc/tqc_fused.hip, pnp_tqc_update) when the shapes are
-    # train.py's (obs 25, action 7, [256, 256, 256], 2 x 25 quantiles, batch a multiple of 16), on
-    # one GPU; else (and for the first gradient step, which creates the optimisers' state) the
-    # PyTorch step
+    # train.py's (obs 25, action 7, [256, 256, 256], 2 x 25 quantiles, batch a multiple of 16);
+    # with several ranks its data-parallel split (pnp_tqc_update_phase: the gradients all-reduced
+    # between the phases); else (and for the first gradient step, which creates the optimisers'
+    # state) the PyTorch step
     fused: bool = True
     # the fused step's random numbers (replay indices, the actor's two Gaussian draws) drawn on the
     # device with the replay sample (pnp_tqc_sample_draw: Philox keyed by `seed`, a device draw
@@ -320,7 +321,9 @@ class TQC:
         self._graph_out = None
         self._fdesc = None          # pnp_tqc_desc of the fused step (TQC._fused_desc)
         self._frb = None            # pnp_tqc_replay of the fused sample (TQC._fused_replay)
-        self._fctr = None           # device draw counter of pnp_tqc_sample_draw (cfg.device_rng)
+        # device draw counter of pnp_tqc_sample_draw (cfg.device_rng), allocated here so that a
+        # checkpoint's `fused_rng_draws` restores it before the first fused step of a resumed run
+        self._fctr = torch.zeros(2, dtype=torch.int64, device=self.device) if cuda else None
         self._eager_updates = 0     # steps run eagerly before the capture (allocator / optimiser state)
         self.vecnorm = VecNormalize(dims, self.device, c.clip_obs, c.norm_eps)
         self.buffer = DictReplayBuffer(c.buffer_size, self.n_envs, self.obs_dim, self.act_dim, self.device)
@@ -471,7 +474,7 @@ class TQC:
     # ------------------------------------------------------------------ the fused gradient step
     def _fused_ok(self):
         c = self.cfg
-        return (c.fused and self.device.type == "cuda" and _world() == 1 and tuple(c.net_arch) == (256, 256, 256)
+        return (c.fused and self.device.type == "cuda" and tuple(c.net_arch) == (256, 256, 256)
                 and c.n_critics == 2 and c.n_quantiles == 25 and c.top_quantiles_to_drop_per_net == 2
                 and c.batch_size % 16 == 0 and self.obs_dim == 25 and self.act_dim == 7
                 and c.target_update_interval == 1)
@@ -555,7 +558,10 @@ class TQC:
         self._fu_dev, self._feps = z(2, B), (z(B, self.act_dim), z(B, self.act_dim))
         if self._fctr is None:
             self._fctr = torch.zeros(2, dtype=torch.int64, device=self.device)
-        self._fseed = (int(self.cfg.seed) * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019) & 0xFFFFFFFFFFFFFFFF
+        # per-rank key (each rank samples its own replay buffer with its own noise, as the
+        # generator's per-rank seed does for the PyTorch step)
+        self._fseed = ((int(self.cfg.seed) * 1000003 + self.rank) * 0x9E3779B97F4A7C15
+                       + 0x632BE59BD9B4E019) & 0xFFFFFFFFFFFFFFFF
         self._frb = r
         return r
 
@@ -596,13 +602,46 @@ class TQC:
             eps_next = torch.randn(B, self.act_dim, device=self.device, generator=self.gen)
         ts = [t.contiguous() for t in (obs, act, nobs, done, rew, eps_pi, eps_next)]
         b = _lib.PnpTqcBatch(*[t.data_ptr() for t in ts])
-        gp = None if grads_out is None else C.c_void_p(grads_out.data_ptr())
-        _lib.check(L.pnp_tqc_update(C.byref(d), C.byref(b), gp, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
-                   "pnp_tqc_update")
+        stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        if _world() > 1:
+            self._update_fused_dp(L, d, b, stream, grads_out)
+        else:
+            gp = None if grads_out is None else C.c_void_p(grads_out.data_ptr())
+            _lib.check(L.pnp_tqc_update(C.byref(d), C.byref(b), gp, stream), "pnp_tqc_update")
         self._fbatch = ts   # (alive until the launch has read them; in a capture, the graph's pool)
         self.n_updates += 1
         lg = self._flogs
+        if torch.cuda.is_current_stream_capturing():
+            return lg[0], lg[1], lg[2], lg[3]   # the graph's static outputs (train() clones them)
+        # eager: the next step overwrites _flogs in place, so a caller keeping these gets copies
+        lg = lg.clone()
         return lg[0], lg[1], lg[2], lg[3]
+
+    def _update_fused_dp(self, L, d, b, stream, grads_out=None):
+        """The fused step on several ranks (pnp_tqc_update_phase): critic gradients (and the
+        entropy coefficient's) -> all-reduce -> critics' Adam, the actor against the updated
+        critics -> actor gradients -> all-reduce -> actor's Adam.  Two flattened buckets per step
+        over RCCL (gloo in the CPU-side tests), averaged like _allreduce_grads; the ranks stay in
+        lockstep.  grads_out (tests): the averaged gradients, actor then critics."""
+        from . import _lib
+        if getattr(self, "_fgrads", None) is None:
+            na, nc = C.c_int32(), C.c_int32()
+            _lib.check(L.pnp_tqc_param_counts(C.byref(na), C.byref(nc)), "pnp_tqc_param_counts")
+            self._fna, self._fnc = na.value, nc.value
+            self._fgrads = torch.zeros(self._fna + self._fnc + 1, dtype=torch.float32, device=self.device)
+        g, na, w = self._fgrads, self._fna, dist.get_world_size()
+        gp = C.c_void_p(g.data_ptr())
+        _lib.check(L.pnp_tqc_update_phase(C.byref(d), C.byref(b), gp, 0, stream), "pnp_tqc_update_phase(0)")
+        crit = g[na:]
+        dist.all_reduce(crit)
+        crit.div_(w)
+        _lib.check(L.pnp_tqc_update_phase(C.byref(d), C.byref(b), gp, 1, stream), "pnp_tqc_update_phase(1)")
+        act = g[:na]
+        dist.all_reduce(act)
+        act.div_(w)
+        _lib.check(L.pnp_tqc_update_phase(C.byref(d), C.byref(b), gp, 2, stream), "pnp_tqc_update_phase(2)")
+        if grads_out is not None:
+            grads_out.copy_(g[:grads_out.numel()])
 
     def _graph_ok(self):
         return (self.cfg.graph and _world() == 1 and self.device.type == "cuda"

@@ -262,8 +262,14 @@ static int box_face_contacts(const double* pr, const double* Rr, const double* s
  *   A2. Separation on any axis beyond the margin: no contact (the pair's early exit).
  *   A3. The contact axis is the one of least penetration, with ties and near-ties resolved toward
  *       faces: box 2's face replaces box 1's only when deeper by more than BB_TOL, and an edge axis
- *       wins only when 1.05 x its separation still beats the best face's (ODE's dBoxBox uses the
- *       same 1.05 edge fudge factor; MuJoCo's exact bias is assumed, not known).
+ *       wins only when 1.05 x its separation still beats the best face's by more than BB_TOL (ODE's
+ *       dBoxBox uses the same 1.05 edge fudge factor; MuJoCo's exact bias is assumed, not known).
+ *       The absolute BB_TOL matters where the factor cannot: two parallel boxes touching face to
+ *       face at distance ~0 (the closed gripper's finger pads) have an edge axis A_i x B_j equal to
+ *       the face normal with the same separation, and 1.05 x 0 decides nothing -- rounding picked
+ *       the edge axis (one contact) in one arithmetic and the face (the clipped rectangle's four)
+ *       in another (round 5 had a 1e-12 margin: the fp32 kernel made 1 contact per pad pair where
+ *       the oracle made 4, tools/knife_edge_pairs.py).
  *   A4. Face axis: the incident face of the other box (the face most anti-parallel to the contact
  *       normal) is clipped against the reference face's rectangle (grown by BB_TOL); the contacts
  *       are the clipped polygon's vertices -- incident edge entry / exit points in edge order, then
@@ -318,8 +324,8 @@ static int box_box(const double* p1, const double* R1, const double* s1, const d
       double rb = s2[0] * fabs(dot3(B[0], L)) + s2[1] * fabs(dot3(B[1], L)) + s2[2] * fabs(dot3(B[2], L));
       double sep = fabs(tl) - ra - rb;
       if (sep > margin) return 0;
-      /* edge axes must beat face axes clearly (ODE-style 1.05 depth fudge) */
-      if (1.05 * sep > best + 1e-12) {
+      /* edge axes must beat face axes clearly (ODE-style 1.05 depth fudge, and by BB_TOL: A3) */
+      if (1.05 * sep > best + BB_TOL) {
         best = sep; btype = 2; bi = i; bj = j;
         for (int k = 0; k < 3; k++) bestn[k] = tl >= 0 ? L[k] : -L[k];
       }

@@ -7,7 +7,8 @@ floor, two cubes overlapping, a cube half over a board edge (it
   * fp64 kernel = oracle: contact list (order, geoms, positions, normals, depths) and every stage
     within 1e-9, one and ten sub-steps within 1e-9 / 1e-8, warning bits equal.
   * fp32 product kernel: warning bits equal, finite, and the per-tree bar of test_step_gpu.py
-    (1e-5 or three times the one-ulp conditioning floor) on one sub-step.
+    (1e-5 or three times the one-ulp conditioning floor, in its backward-error form) on one
+    sub-step of every configuration.
 """
 import numpy as np
 import pytest
@@ -29,16 +30,13 @@ def boxes(model):
 
 def test_box_contacts_f64_match_oracle(engine, model, boxes):
     """Contact for contact: the fp64 kernel's list equals the oracle's (same order and geom pairs;
-    position, normal and depth within 1e-9), then every forward stage within 1e-9.  (forward_debug
-    runs the full tier alone, 48 contacts: the pressed pads' 56 are compared by the step tests,
-    which run the wide tier.)"""
+    position, normal and depth within 1e-9), then every forward stage within 1e-9 -- every
+    configuration, the pressed pads' 56 contacts included (forward_debug runs the step's tiers
+    since ABI 14: the full tier holds 64 contacts, the fp64 wide tier 96)."""
     from pnp_amd import _lib
     D = _lib.DBG
     idx, st = boxes
-    idx = {c: b for c, b in idx.items() if c != "pads"}
-    sel = np.array(sorted(idx.values()))
-    st = {k: v[sel] for k, v in st.items()}
-    idx = {c: int(np.nonzero(sel == b)[0][0]) for c, b in idx.items()}
+    assert "pads" in idx
     dbg = engine.forward_debug(T._dev(st, torch.float64)).cpu().numpy()
     for case, b in idx.items():
         f = O.forward_fields({k: st[k][b] for k in O.STATE_KEYS}, ["ncon", "contact"], model=model)
@@ -51,6 +49,8 @@ def test_box_contacts_f64_match_oracle(engine, model, boxes):
         assert np.abs(kc[:, 0:3] - c[:, 0:3]).max() < 1e-9, case
         assert np.abs(kc[:, 3:6] - c[:, 3:6]).max() < 1e-9, case
         assert np.abs(kc[:, 12] - c[:, 12]).max() < 1e-9, case
+        if case == "pads":
+            print(f"pads: {kn} contacts, kernel = oracle contact for contact")
     w = T._forward_compare(engine, model, st, torch.float64)
     assert max(w.values()) < 1e-9, w
 
@@ -69,15 +69,13 @@ def test_box_fixtures_step_f64(engine, model, boxes, nsub):
 
 def test_box_fixtures_f32(engine, model, boxes):
     """fp32: warning bits equal the oracle's over 25 sub-steps (one mj_step(nstep=25) call of the
-    gym step) from every configuration, state finite; one sub-step within the per-tree bar for
-    every configuration but "pads".  The pads pressed 4 mm together (past the finger joints' lower
-    limit, 56 contacts, zero velocities) sit on a contact knife edge: one-ulp perturbations of the
-    state move the exact step's arm velocity change by 5.1e-5 in the batch's three draws and by
-    9.4 % in the three draws of the state alone (a pad contact at distance ~0 flips; printed below
-    with the oracle's contact counts), so no fp32 bar is defined on it.  Its error is reported
-    (1.40e-4, profiles/r05/box_fixtures_f32.log); the closed-gripper class is graded by
-    test_step_gpu.py's `pressed` fixture (12 states, 1-4 mm, noisy velocities: worst arm tree 0.90
-    of its bar)."""
+    gym step) from every configuration, state finite; one sub-step of EVERY configuration within
+    the per-tree bar of test_step_gpu.py in its backward-error form (_assert_per_tree: the bar of
+    at least one oracle candidate -- the state or a one-ulp perturbation of it -- on the kernel's
+    contact branch).  Round 5 carved "pads" out (4 mm pressed, 56 contacts, zero velocities: its
+    arm tree was 1.12x the bar against the unperturbed oracle while the oracle's own contact count
+    flips under one-ulp perturbations of the state); it is asserted again, and the candidate it
+    matches is printed."""
     idx, st = boxes
     s32 = T._round32(st)
     ref = PS.copy_state(s32)
@@ -85,11 +83,5 @@ def test_box_fixtures_f32(engine, model, boxes):
     g = T._host(engine.step(T._dev(s32, torch.float32), 25))
     assert np.array_equal(g["warn"], ref["warn"]), (g["warn"], ref["warn"])
     assert np.isfinite(g["qpos"]).all() and np.isfinite(g["qvel"]).all()
-    keep = np.array(sorted(b for c, b in idx.items() if c != "pads"))
-    T._assert_per_tree(engine, model, {k: v[keep] for k, v in st.items()}, 1, "box fixtures (pads: see test_step_gpu pressed)")
-    pads = {k: v[[idx["pads"]]] for k, v in st.items()}
-    ev, _ = T._f32_tree_errors(engine, model, pads, nsub=1, per_env=True)
-    fv, _ = T._conditioning_floor(model, T._round32(pads), nsub=1, per_env=True)
-    knife = T._knife_edge_envs(model, T._round32(pads))
-    print(f"pads (reported): dqvel M-norm per tree {ev[0]}; one-ulp floor of the state alone {fv[0]}; "
-          f"oracle contact count changes under a one-ulp qpos perturbation: {bool(knife[0])}")
+    print("box fixtures:", {c: b for c, b in idx.items()})
+    T._assert_per_tree(engine, model, st, 1, "box fixtures")

@@ -72,7 +72,7 @@ def test_library_loads_and_exports_header_symbols():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_lib.EXPORTS)
-    assert L.pnp_abi_version() == _lib.ABI_VERSION == 13
+    assert L.pnp_abi_version() == _lib.ABI_VERSION == 14
     from pnp_amd.model import PnpModelDesc
     assert L.pnp_model_desc_size() == C.sizeof(PnpModelDesc)
 

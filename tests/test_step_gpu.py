@@ -207,54 +207,140 @@ def _conditioning_floor(model, st, nsub=1, trials=3, per_env=False, world=False)
     return fv, fa
 
 
-def _knife_edge_envs(model, st, trials=3):
-    """Per env: the oracle's contact count is not the same on the state and on one-ulp fp32
-    perturbations of its qpos (the perturbations of _conditioning_floor)."""
-    rng = np.random.default_rng(2024)
-    cnt = lambda s, b: int(O.forward_fields({k: s[k][b] for k in O.STATE_KEYS}, ["ncon"], model=model)["ncon"][0])
-    B = st["qpos"].shape[0]
-    base = [cnt(st, b) for b in range(B)]
-    out = np.zeros(B, bool)
-    for _ in range(trials):
-        p = PS.copy_state(st)
-        x = p["qpos"].astype(np.float32)
-        up = rng.random(x.shape) < 0.5
-        p["qpos"] = np.where(up, np.nextafter(x, np.float32(np.inf)), np.nextafter(x, np.float32(-np.inf))).astype(np.float64)
-        out |= np.array([cnt(p, b) != base[b] for b in range(B)])
-    return out
-
-
 def _f32_tree_errors(engine, model, st, nsub=1, per_env=False):
     """Per tree: (dqvel M-norm relative error, M dqacc relative error) of the fp32 kernel against
-    the oracle on identical (fp32-rounded) inputs; see the module docstring."""
+    the oracle on identical (fp32-rounded) inputs, the unperturbed oracle only (tools, the ten
+    sub-step test; the per-tree bar of _assert_per_tree uses _backward_errors)."""
     st = _round32(st)
     ref = PS.copy_state(st)
     O.step(ref, nsub=nsub, nthreads=8, model=model)
     got = _host(engine.step(_dev(st, torch.float32), nsub))
     assert np.array_equal(got["warn"], ref["warn"])
+    qa_ref = qa_got = None
+    if nsub == 1:
+        from pnp_amd import _lib
+        D, nv = _lib.DBG, model.nv
+        dbg = engine.forward_debug(_dev(st, torch.float32)).cpu().numpy()
+        qa_ref = _oracle_qacc(model, st)
+        qa_got = [dbg[b, D["QACC"]:D["QACC"] + nv] for b in range(st["qpos"].shape[0])]
+    return _tree_metrics(model, st, ref, got, qa_ref, qa_got, nsub, per_env)
+
+
+def _perturbed_states(st, trials, seed=2024):
+    """st and `trials` copies of it with every qpos / qvel coordinate moved one fp32 ulp up or down
+    at random (fixed seed; the first three are _conditioning_floor's one-ulp trials)."""
+    rng = np.random.default_rng(seed)
+    out = [PS.copy_state(st)]
+    for _ in range(trials):
+        p = PS.copy_state(st)
+        for k in ("qpos", "qvel"):
+            x = p[k].astype(np.float32)
+            up = rng.random(x.shape) < 0.5
+            p[k] = np.where(up, np.nextafter(x, np.float32(np.inf)), np.nextafter(x, np.float32(-np.inf))).astype(np.float64)
+        out.append(p)
+    return out
+
+
+def _geom_tree(model):
+    """geom id -> index into TREES (-1: a world geom)."""
+    root_of_tree = {int(model.body_rootid[int(model.dof_bodyid[sl.start])]): t for t, sl in enumerate(TREES)}
+    return np.array([root_of_tree.get(int(model.body_rootid[int(b)]), -1) for b in model.geom_bodyid])
+
+
+def _tree_contact_counts(gtree, pairs):
+    """Contacts touching each tree (a contact between two trees counts for both)."""
+    k = np.zeros(len(TREES), int)
+    for g1, g2 in pairs:
+        for t in {int(gtree[int(g1)]), int(gtree[int(g2)])}:
+            if t >= 0:
+                k[t] += 1
+    return k
+
+
+def _backward_errors(engine, model, st, nsub=1, trials=8):
+    """Backward-error form of the per-tree fp32 bar.  The oracle steps
+    the fp32-rounded state and `trials` one-ulp perturbations of it (candidates j = 0..trials, 0 =
+    unperturbed).  A contact at distance ~0 flips in or out under one ulp (a knife edge: cubes
+    resting exactly on a board, closed finger pads face to face), so candidates are grouped per
+    kinematic tree into branches by the number of contacts touching that tree.  Against candidate
+    j the kernel's error per env and tree is measured as in _tree_metrics (dqvel from each side's
+    own start; M dqacc for nsub = 1), and j's bar for the tree is 1e-5 per sub-step or three times
+    j's branch floor -- the largest change any other candidate of the same branch shows against j
+    (the one-ulp conditioning of the exact step on that branch; a floor above 1e-3 is held to
+    1e-5).  With nsub = 1 only candidates whose count for the tree equals the kernel's own
+    (forward_debug, through the tiers) are eligible, so M dqacc compares the same contacts.  Each
+    tree takes its best candidate (trees couple only through their shared contacts, which the
+    branch key counts on both).  Returns per env and tree the chosen candidate and its error / bar,
+    candidate 0's error / bar (nan when ineligible), the kernel's and the candidates' total contact
+    counts, and the per-env, per-tree errors against the chosen candidates."""
     from pnp_amd import _lib
     D = _lib.DBG
-    nv = model.nv
-    qa_ref = _oracle_qacc(model, st) if nsub == 1 else None
-    qa_got = None
+    nv, h = model.nv, float(model.opt_timestep)
+    g = float(np.linalg.norm(model.opt_gravity))
+    gtree = _geom_tree(model)
+    nt = len(TREES)
+    st = _round32(st)
+    B = st["qpos"].shape[0]
+    got = _host(engine.step(_dev(st, torch.float32), nsub))
+    kkey = kn = None
     if nsub == 1:
         dbg = engine.forward_debug(_dev(st, torch.float32)).cpu().numpy()
-        ncon = [O.forward_fields({k: st[k][b] for k in O.STATE_KEYS}, ["ncon"], model=model)["ncon"][0]
-                for b in range(st["qpos"].shape[0])]
-        # forward_debug runs the full tier alone (64 contacts, truncating like MuJoCo at a full
-        # buffer): envs beyond that capacity are left out of M dqacc (their dqvel is checked), and
-        # so are envs at a contact knife edge (the oracle's own contact count changes under a one-ulp
-        # perturbation of the state: pads touching at distance ~0); any other count difference fails
-        qa_got, knife = [], None
-        for b in range(st["qpos"].shape[0]):
-            same = int(dbg[b, D["COUNTS"]]) == int(ncon[b])
-            if not same and int(ncon[b]) <= PS.FULL_MAXCON:
-                knife = _knife_edge_envs(model, st) if knife is None else knife
-                assert knife[b], f"env {b}: contact count {int(dbg[b, D['COUNTS']])} != oracle {int(ncon[b])}"
-                print(f"env {b}: contact knife edge (kernel {int(dbg[b, D['COUNTS']])}, oracle {int(ncon[b])}): "
-                      f"M dqacc not compared")
-            qa_got.append(dbg[b, D["QACC"]:D["QACC"] + nv] if same else None)
-    return _tree_metrics(model, st, ref, got, qa_ref, qa_got, nsub, per_env)
+        kn = dbg[:, D["COUNTS"]].astype(int)
+        kkey = [_tree_contact_counts(gtree, dbg[b, D["CON"]:D["CON"] + 16 * kn[b]].reshape(kn[b], 16)[:, 13:15])
+                for b in range(B)]
+        qa_got = dbg[:, D["QACC"]:D["QACC"] + nv]
+    cands = []
+    for p in _perturbed_states(st, trials):
+        q = PS.copy_state(p)
+        O.step(q, nsub=nsub, nthreads=8, model=model)
+        f = [O.forward_fields({k: p[k][b] for k in O.STATE_KEYS}, ["qacc", "ncon", "contact"], model=model)
+             for b in range(B)]
+        cands.append(dict(p=p, q=q, qacc=np.array([x["qacc"] for x in f]), ncon=np.array([int(x["ncon"][0]) for x in f]),
+                          key=[_tree_contact_counts(gtree, x["contact"].reshape(-1, 30)[:, 27:29]) for x in f]))
+    assert np.array_equal(got["warn"], cands[0]["q"]["warn"])
+    Ms = [O.forward_fields({k: st[k][b] for k in O.STATE_KEYS}, ["qM"], model=model)["qM"].reshape(nv, nv)
+          for b in range(B)]
+    mt = np.array([_tree_mass(model, sl) for sl in TREES])
+
+    def err(b, t, dv_a, dv_r, qa_a, qa_r):
+        M, sl = Ms[b], TREES[t]
+        Mt = M[sl, sl]
+        nrm = lambda v: float(np.sqrt(max(v @ Mt @ v, 0.0)))
+        ev = nrm(dv_a[sl] - dv_r[sl]) / max(nrm(dv_r[sl]), h * g * nsub * np.sqrt(mt[t]))
+        ea = 0.0
+        if qa_a is not None:
+            ea = np.abs((M @ (qa_a - qa_r))[sl]).max() / max(np.abs((M @ qa_r)[sl]).max(), mt[t] * g)
+        return ev, ea
+
+    dv = lambda c, b: c["q"]["qvel"][b] - c["p"]["qvel"][b]
+    res, EV, EA = [], np.zeros((B, nt)), np.zeros((B, nt))
+    for b in range(B):
+        dk = got["qvel"][b] - st["qvel"][b]
+        pick, ratio, r0 = np.zeros(nt, int), np.zeros(nt), np.full(nt, np.nan)
+        for t in range(nt):
+            best = None
+            for j, cj in enumerate(cands):
+                if kkey is not None and cj["key"][b][t] != kkey[b][t]:
+                    continue
+                fv = fa = 0.0
+                for i, ci in enumerate(cands):
+                    if i != j and ci["key"][b][t] == cj["key"][b][t]:
+                        v, a = err(b, t, dv(ci, b), dv(cj, b), ci["qacc"][b] if kn is not None else None, cj["qacc"][b])
+                        fv, fa = max(fv, v), max(fa, a)
+                fv, fa = (fv if fv < 1e-3 else 0.0), (fa if fa < 1e-3 else 0.0)
+                bv, ba = max(1e-5 * nsub, 3 * fv), max(1e-5 * nsub, 3 * fa)
+                ev, ea = err(b, t, dk, dv(cj, b), qa_got[b] if kn is not None else None, cj["qacc"][b])
+                r = max(ev / bv, ea / ba)
+                if j == 0:
+                    r0[t] = r
+                if best is None or r < best[1]:
+                    best = (j, r, ev, ea)
+            assert best is not None, (b, t, "no oracle candidate has the kernel's contacts on this tree",
+                                      kkey[b].tolist(), [c["key"][b].tolist() for c in cands])
+            pick[t], ratio[t], EV[b, t], EA[b, t] = best
+        res.append(dict(pick=pick, ratio=ratio, r0=r0, kn=None if kn is None else int(kn[b]),
+                        ncon=[int(c["ncon"][b]) for c in cands]))
+    return res, EV, EA
 
 
 def test_forward_f32_matches_oracle(engine, model, scene):
@@ -296,26 +382,23 @@ def test_step_f32_matches_oracle_per_tree(engine, model, fixture, request):
 
 
 def _assert_per_tree(engine, model, st, nsub, label):
-    """Every env and tree within 1e-5, or 3x its own one-ulp conditioning floor, over nsub fp32
-    sub-steps (M dqacc for nsub = 1).  No env is left out: MPR runs in fp64 in the fp32 kernels
-    (round 4; round 3 excluded the envs whose fp32 MPR took another path, 5 of the mesh
-    fixture's 15)."""
-    ev, ea = _f32_tree_errors(engine, model, st, nsub=nsub, per_env=True)
-    fv, fa = _conditioning_floor(model, _round32(st), nsub=nsub, per_env=True)
-    wv, wa = _conditioning_floor(model, _round32(st), nsub=nsub, per_env=True, world=True)
-    print(f"{label}: one-ulp floor per tree dqvel {fv.max(0)} M dqacc {fa.max(0)}; world-scale floor (not "
-          f"asserted) dqvel {wv.max(0)} M dqacc {wa.max(0)}")
-    # a tree that moves by more than 1e-3 under a one-ulp perturbation went over a knife edge (a
-    # contact at distance 0 flipping in or out: the fresh-reset cubes), not ill-conditioning:
-    # such trees are held to 1e-5 outright
-    fv, fa = np.where(fv < 1e-3, fv, 0.0), np.where(fa < 1e-3, fa, 0.0)
-    # the single-step bar (1e-5) once per sub-step: an fp32 run rounds at every sub-step, the floor
-    # perturbs the start only
-    bar_v, bar_a = np.maximum(1e-5 * nsub, 3 * fv), np.maximum(1e-5 * nsub, 3 * fa)
-    print(f"{label}: dqvel M-norm per tree {ev.max(0)} (worst error / bar {(ev / bar_v).max(0)}); "
-          f"M dqacc per tree {ea.max(0)} (worst error / bar {(ea / bar_a).max(0)})")
-    assert (ev <= bar_v).all(), (label, ev, bar_v)
-    assert (ea <= bar_a).all(), (label, ea, bar_a)
+    """Every env and tree within the bar of at least one oracle candidate (_backward_errors: the
+    exact step of the state or of a one-ulp perturbation of it, on the kernel's contact branch for
+    that tree).  No env is left out: knife-edge states (the oracle's own contact count flips under
+    one ulp) are graded against a candidate on the kernel's branch instead of being excluded (round
+    5 left such envs out of M dqacc, and the `pads` box fixture out of the bar altogether)."""
+    res, ev, ea = _backward_errors(engine, model, st, nsub)
+    ratio = np.array([r["ratio"] for r in res])
+    b0, t0 = np.unravel_index(int(ratio.argmax()), ratio.shape)
+    print(f"{label}: dqvel M-norm per tree {ev.max(0)}, M dqacc per tree {ea.max(0)} (against each env and tree's "
+          f"chosen candidate); worst error / bar per tree {ratio.max(0)} (env {b0}, tree {t0}: candidate "
+          f"{res[b0]['pick'][t0]}, unperturbed {res[b0]['r0'][t0]:.3f})")
+    for b, r in enumerate(res):
+        if (r["pick"] != 0).any() and (np.isnan(r["r0"]) | (r["r0"] > 1.0)).any():
+            print(f"  {label} env {b}: candidates per tree {r['pick'].tolist()} (error / bar {np.round(r['ratio'], 3).tolist()}; "
+                  f"unperturbed {np.round(r['r0'], 3).tolist()}), contacts kernel {r['kn']}, oracle candidates {r['ncon']}")
+    assert (ratio <= 1.0).all(), (label, [(b, r["pick"].tolist(), np.round(r["ratio"], 3).tolist())
+                                          for b, r in enumerate(res) if (r["ratio"] > 1.0).any()])
 
 
 def test_step_f32_ten_substeps(engine, model, scene):

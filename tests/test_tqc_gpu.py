@@ -140,10 +140,10 @@ def test_captured_learner_step_equals_eager():
     assert ms[1] < ms[0]
 
 
-def _fused_agent(B=64, **cfg):
+def _fused_agent(B=64, env_offset=0, **cfg):
     from pnp_amd.envs import BatchedFrankaShelfPNPEnv, EnvConfig
     from pnp_amd.tqc import TQC, TQCConfig
-    env = BatchedFrankaShelfPNPEnv(B, config=EnvConfig(**SHORT))
+    env = BatchedFrankaShelfPNPEnv(B, config=EnvConfig(**SHORT), env_offset=env_offset)
     a = TQC(env, TQCConfig(**cfg))
     a.total_timesteps = 10 ** 6
     a.reset()
@@ -171,16 +171,24 @@ def test_fused_sample_matches_pytorch():
         a.collect_step()
 
 
-def test_fused_learner_step_matches_pytorch():
+@pytest.mark.parametrize("batch", [512, 48, 80])
+def test_fused_learner_step_matches_pytorch(batch):
     """pnp_tqc_update (csrc/tqc_fused.hip: the whole TQC gradient step on the matrix cores) against
     the PyTorch step (pnp_amd/tqc.py _update_torch, autograd) from the same state, replay sample and
     Gaussian draws: every gradient tensor it applies within 1e-4 (critics) / 1e-3 (actor, computed
     against the Adam-updated critics) of the PyTorch gradient in norm, the logged losses within
     1e-4, and the parameters after Adam (actor, critics, Polyak targets, log entropy coefficient)
-    within a small fraction of the learning rate."""
+    within a small fraction of the learning rate.  train.py's batch (512) and two multiples of 16
+    whose 16 weight-gradient waves get row ranges that are not multiples of the 4-row load group
+    (48: 3 rows per wave, 80: 5; round 5 summed rows of the next wave twice there)."""
+    _check_fused_against_pytorch(_fused_agent(graph=False, batch_size=batch))
+
+
+def _check_fused_against_pytorch(a):
+    """One fused step of agent `a` (eager; several ranks: the data-parallel split) against its
+    PyTorch step from the same state and draws; returns the parameters after the fused step."""
     import copy
     from pnp_amd import _lib
-    a = _fused_agent(graph=False)
     for _ in range(3):
         a.train()                  # the first creates the Adam state (PyTorch), then fused steps
     assert a._fdesc is not None
@@ -220,6 +228,90 @@ def test_fused_learner_step_matches_pytorch():
     for x, y in zip(after_f, after_t):
         d = (x - y).abs()
         assert float(d.max()) <= 2.5 * lr and float(d.median()) <= 1e-3 * lr, (float(d.max()), float(d.median()), lr)
+    return after_f
+
+
+def test_fused_draw_counter_survives_checkpoint(tmp_path):
+    """A run resumed from a checkpoint continues the device draw stream (pnp_tqc_sample_draw's
+    counter, `fused_rng_draws`) instead of replaying it from index 0: a freshly built agent that
+    loads the checkpoint draws, at its first fused step, what the original agent draws at its next."""
+    a = _fused_agent(graph=False)
+    a.train(4)                     # one PyTorch step (Adam state), three fused: counter at 3
+    torch.cuda.synchronize()
+    assert int(a._fctr[0]) == 3
+    p = tmp_path / "tqc.pt"
+    a.save(p)
+    b = _fused_agent(graph=False)
+    b.load(p)
+    assert int(b._fctr[0]) == 3, int(b._fctr[0])
+    ua = [t.clone() for t in a._sample_fused()]
+    ub = [t.clone() for t in b._sample_fused()]
+    torch.cuda.synchronize()
+    assert torch.equal(a._fu_dev, b._fu_dev) and torch.equal(a._feps[0], b._feps[0])
+    logs = a.train()               # eager fused step: the returned logs are copies
+    kept = float(logs["critic_loss"])
+    a.train()
+    assert float(logs["critic_loss"]) == kept
+
+
+def _dp_fused_worker(rank, world, port, out):
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "mujoco-panda-pnp_amd"), os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import test_tqc_gpu as T
+        a = T._fused_agent(graph=False, env_offset=64 * rank)
+        a.train(3)                 # a PyTorch step (Adam state), then two data-parallel fused steps
+        assert a._fused_ok() and a._fdesc is not None and a._fgrads is not None
+        a.cfg.device_rng = False   # the compared step: draws from the per-rank generator
+        after = T._check_fused_against_pytorch(a)
+        a.train(2)
+        flat = torch.cat([p.detach().reshape(-1) for p in list(a.actor.parameters()) + list(a.critic.parameters())])
+        res = dict(params=flat.cpu().numpy(), batch=a._fsb[0].cpu().numpy(),
+                   after=torch.cat([t.reshape(-1) for t in after]).cpu().numpy())
+        got = [None] * world
+        dist.all_gather_object(got, res)
+        if rank == 0:
+            out.put(got)
+        dist.barrier()
+    except BaseException as e:   # report instead of hanging the other rank's collective
+        out.put(repr(e))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_fused_learner_data_parallel_two_ranks():
+    """the fused step on two ranks (one GPU, gloo: RCCL refuses two ranks on one
+    device) runs pnp_tqc_update_phase with the gradients all-reduced between the phases.  On each
+    rank the step matches the data-parallel PyTorch step (_update_torch, whose gradients are
+    all-reduced the same way) on the bars of test_fused_learner_step_matches_pytorch, the ranks'
+    batches differ, and after further steps both ranks hold the same parameters bit for bit."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    out = ctx.Queue()
+    procs = [ctx.Process(target=_dp_fused_worker, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = out.get(timeout=280)
+    for p in procs:
+        p.join(60)
+    assert not isinstance(got, str), got
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    r0, r1 = got
+    assert not np.array_equal(r0["batch"], r1["batch"])        # each rank its own replay sample
+    assert np.array_equal(r0["after"], r1["after"])            # the averaged step, identical
+    assert np.array_equal(r0["params"], r1["params"])          # lockstep after two more steps
 
 
 def test_fused_device_draws():

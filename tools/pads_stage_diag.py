@@ -1,0 +1,92 @@
+"""Closed-gripper fp32 error by stage (GPU): on the `pads` box fixture and
+the `pressed` envs, the fp32 kernel's forward (forward_debug, fp32-rounded state) against the
+oracle's on the same state -- the arm tree's M-relative error of the Newton result (before
+no-slip) and of the final qacc, the constraint Jacobian's arm-dof entries on the pad-pad rows
+(one kinematic tree: MuJoCo's J = J(b2, p) - J(b1, p) cancels the shared arm dofs exactly), and
+the rows' D / aref / force -- next to the one-ulp floor of the same quantities (oracle on
+perturbed states).  usage: python tools/pads_stage_diag.py"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mujoco-panda-pnp_amd"), os.path.join(ROOT, "tests")]
+from oracle import oracle as O  # noqa: E402
+from pnp_amd import _lib  # noqa: E402
+from pnp_amd.engine import get_engine  # noqa: E402
+from pnp_amd.model import load_model  # noqa: E402
+import box_states as BS  # noqa: E402
+import physics_states as PS  # noqa: E402
+import test_step_gpu as T  # noqa: E402
+
+D = _lib.DBG
+ARM = slice(0, 9)
+
+
+def states(m):
+    idx, bs = BS.box_states(m)
+    n = 12
+    st = PS.reset_states(n, seed=11, model=m)
+    st["qpos"][:, 7:9] = -np.linspace(0.001, 0.004, n)[:, None]
+    st["ctrl"][:, -2:] = 0.0
+    st["qvel"] += np.random.default_rng(5).normal(size=st["qvel"].shape) * 0.02
+    keep = [4, 5, 6, 9]
+    out = {k: np.concatenate([bs[k][[idx["pads"]]], st[k][keep]]) for k in st}
+    return ["pads"] + [f"pressed{k}" for k in keep], T._round32(out)
+
+
+def main():
+    m = load_model()
+    eng = get_engine()
+    nv = m.nv
+    names, st = states(m)
+    B = st["qpos"].shape[0]
+    for dt, tag in ((torch.float32, "fp32"), (torch.float64, "fp64")):
+        dbg = eng.forward_debug(T._dev(st, dt)).cpu().numpy()
+        cands = T._perturbed_states(st, 8)
+        for b in range(B):
+            row = lambda s: {k: s[k][b] for k in O.STATE_KEYS}
+            f = O.forward_fields(row(st), ["qM", "qacc", "qacc_newton", "qacc_smooth", "ncon", "nefc", "efc_J",
+                                           "efc_D", "efc_aref", "efc_force", "efc_type", "contact"], model=m)
+            M = f["qM"].reshape(nv, nv)
+            ne, nc = int(f["nefc"][0]), int(f["ncon"][0])
+            g = dbg[b]
+            kne, knc = int(g[D["COUNTS"] + 1]), int(g[D["COUNTS"]])
+            scale = max(np.abs((M @ f["qacc"])[ARM]).max(), 1.0)
+            rel = lambda a, r: np.abs((M @ (a - r))[ARM]).max() / scale
+            e_sm = rel(g[D["QACC_SMOOTH"]:D["QACC_SMOOTH"] + nv], f["qacc_smooth"])
+            e_nt = rel(g[D["QACC_NEWTON"]:D["QACC_NEWTON"] + nv], f["qacc_newton"])
+            e_qa = rel(g[D["QACC"]:D["QACC"] + nv], f["qacc"])
+            fl_nt = fl_qa = 0.0
+            for p in cands[1:]:
+                q = O.forward_fields(row(p), ["qacc", "qacc_newton", "ncon"], model=m)
+                if int(q["ncon"][0]) != nc:
+                    continue
+                fl_nt = max(fl_nt, rel(q["qacc_newton"], f["qacc_newton"]))
+                fl_qa = max(fl_qa, rel(q["qacc"], f["qacc"]))
+            print(f"[{tag}] {names[b]}: ncon {knc}/{nc} nefc {kne}/{ne}; arm M-rel error: smooth {e_sm:.2e}, newton "
+                  f"{e_nt:.2e} (floor {fl_nt:.2e}), final {e_qa:.2e} (floor {fl_qa:.2e})", flush=True)
+            if kne != ne:
+                continue
+            J = f["efc_J"].reshape(ne, nv)
+            KJ = g[D["EFC_J"]:D["EFC_J"] + ne * nv].reshape(ne, nv)
+            con = f["contact"].reshape(nc, 30)
+            # rows of finger-finger contacts (pads): only the finger slides move them in the oracle
+            armrows = [r for r in range(ne) if np.abs(J[r, 7:9]).max() > 0 and np.abs(J[r, :7]).max() < 1e-12
+                       and np.abs(J[r, 9:]).max() == 0]
+            if armrows:
+                ar = np.array(armrows)
+                jarm_o = np.abs(J[ar][:, :7]).max()
+                jarm_k = np.abs(KJ[ar][:, :7]).max()
+                dj = np.abs(KJ[ar] - J[ar]).max()
+                dD = np.abs(g[D["EFC_D"] + ar] - f["efc_D"][ar]) / np.abs(f["efc_D"][ar])
+                dA = np.abs(g[D["EFC_AREF"] + ar] - f["efc_aref"][ar]).max() / max(np.abs(f["efc_aref"][ar]).max(), 1e-12)
+                dF = np.abs(g[D["EFC_FORCE"] + ar] - f["efc_force"][ar]).max() / max(np.abs(f["efc_force"][ar]).max(), 1e-12)
+                print(f"    arm-tree rows {len(ar)}: |J| on the 7 arm joints oracle {jarm_o:.2e} kernel {jarm_k:.2e}; "
+                      f"max |dJ| {dj:.2e}; rel dD max {dD.max():.2e}; rel daref {dA:.2e}; rel dforce {dF:.2e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
