@@ -3797,20 +3797,33 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     }
   }
   clk.sub_lap(SC_NS_W);
-  // v = M^-1 J^T f over the dof's island rows
-  const bool jt = s.jt_ok;
-  if (jt) {
-    gather_rows(s, s.efc_force, s.rr_g);
+  if constexpr (sizeof(T) == 4) {
+    // fp32: the constraint acceleration v = qacc - qacc_smooth from Newton's own iterate, not
+    // M^-1 J^T f recomputed from the forces: where large contact forces cancel on a dof (the pads
+    // pressed together push both fingers with ~100x the net force) the fp32 sum J^T f carries
+    // their rounding (the fingers' generalized forces 1.4e-3 N off on the `pads` fixture,
+    // tools/pads_stage_diag.py), while Newton's iterate is accurate to ~2e-7.  The Newton forces
+    // are kept in efc_aref (dead after Newton) for st_finish_accel, which adds only the no-slip
+    // sweeps' force changes.  (fp64 keeps MuJoCo's recomputation, the oracle's to 1e-9.)
+    for (int r = l; r < s.nefc; r += NT) s.efc_aref[r] = s.efc_force[r];
+    if (l < m.nv) s.v2[l] = s.qacc[l] - s.qacc_smooth[l];
     wsync();
+  } else {
+    // v = M^-1 J^T f over the dof's island rows
+    const bool jt = s.jt_ok;
+    if (jt) {
+      gather_rows(s, s.efc_force, s.rr_g);
+      wsync();
+    }
+    if (l < m.nv) {
+      const int t = s.c_dof_tree[l], I = s.tree_island[t];
+      const T g = jt ? jt_dof_sum(s, I, s.dof_ipos[l], T(0), s.rr_g)
+                     : dof_row_sum(T(0), s, I, t, l - s.c_tree_dofadr[t], s.efc_force, (const T*)nullptr, false);
+      s.v2[l] = g;
+    }
+    wsync();
+    solve_M(m, s, s.v2, s.v2);
   }
-  if (l < m.nv) {
-    const int t = s.c_dof_tree[l], I = s.tree_island[t];
-    const T g = jt ? jt_dof_sum(s, I, s.dof_ipos[l], T(0), s.rr_g)
-                   : dof_row_sum(T(0), s, I, t, l - s.c_tree_dofadr[t], s.efc_force, (const T*)nullptr, false);
-    s.v2[l] = g;
-  }
-  wsync();
-  solve_M(m, s, s.v2, s.v2);
   const int glen = s.ns_len[grp];
   clk.sub_lap(SC_NS_LISTS);
   clk.count(SN_NS_SWEEP, maxlen);
@@ -4163,19 +4176,35 @@ __device__ void st_finish_accel(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& 
   const int l = lane_id();
   if (s.nefc == 0) return;
   const bool jt = s.jt_ok;
+  constexpr bool f32 = sizeof(T) == 4;
+  if (f32 && m.noslip_iterations > 0) {
+    // fp32 (st_noslip): qacc = Newton's qacc + M^-1 J^T (f - f_newton), f_newton in efc_aref --
+    // only the forces no-slip changed enter the sum
+    for (int r = l; r < s.nefc; r += NT) s.efc_aref[r] = s.efc_force[r] - s.efc_aref[r];
+    wsync();
+  }
+  const T* fsrc = f32 && m.noslip_iterations > 0 ? s.efc_aref : s.efc_force;
   if (jt) {
-    gather_rows(s, s.efc_force, s.rr_g);
+    gather_rows(s, fsrc, s.rr_g);
     wsync();
   }
   if (l < m.nv) {
     // J^T f over the dof's island rows (the other rows do not touch it)
     const int t = s.c_dof_tree[l], I = s.tree_island[t];
     const T g = jt ? jt_dof_sum(s, I, s.dof_ipos[l], T(0), s.rr_g)
-                   : dof_row_sum(T(0), s, I, t, l - s.c_tree_dofadr[t], s.efc_force, (const T*)nullptr, false);
-    s.v2[l] = s.qfrc_smooth[l] + g;
+                   : dof_row_sum(T(0), s, I, t, l - s.c_tree_dofadr[t], fsrc, (const T*)nullptr, false);
+    s.v2[l] = f32 ? g : s.qfrc_smooth[l] + g;
   }
   wsync();
-  if (m.noslip_iterations > 0) solve_M(m, s, s.qacc, s.v2);
+  if (m.noslip_iterations > 0) {
+    if constexpr (f32) {
+      solve_M(m, s, s.v2, s.v2);
+      if (l < m.nv) s.qacc[l] += s.v2[l];
+      wsync();
+    } else {
+      solve_M(m, s, s.qacc, s.v2);
+    }
+  }
 }
 
 // ============================================================================ reset / Euler
@@ -4300,6 +4329,7 @@ __device__ void dump_smooth(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>
     o[PNP_DBG_ACT + l] = s.qfrc_act[l];
     o[PNP_DBG_QACC_SMOOTH + l] = s.qacc_smooth[l];
   }
+  for (int r = l; r < s.nefc; r += NT) o[PNP_DBG_EFC_AREF + r] = s.efc_aref[r];   // (fp32 no-slip reuses it)
 }
 
 template <typename T, class CLK>
@@ -4512,7 +4542,6 @@ __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) forwa
     o[PNP_DBG_EFC_POS + r] = s.efc_pos[r];
 #endif
     o[PNP_DBG_EFC_D + r] = s.efc_D[r];
-    o[PNP_DBG_EFC_AREF + r] = s.efc_aref[r];
     o[PNP_DBG_EFC_TYPE + r] = s.efc_type[r];
     const int t0 = s.efc_t0[r], t1 = s.efc_t1[r], w = row_width(m, t0, t1);
     double* Jr = o + PNP_DBG_EFC_J + r * nv;

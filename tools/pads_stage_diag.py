@@ -68,8 +68,18 @@ def main():
                 fl_qa = max(fl_qa, rel(q["qacc"], f["qacc"]))
             print(f"[{tag}] {names[b]}: ncon {knc}/{nc} nefc {kne}/{ne}; arm M-rel error: smooth {e_sm:.2e}, newton "
                   f"{e_nt:.2e} (floor {fl_nt:.2e}), final {e_qa:.2e} (floor {fl_qa:.2e})", flush=True)
+            print(f"    M dqacc per arm dof: newton {np.array2string((M @ (g[D['QACC_NEWTON']:D['QACC_NEWTON'] + nv] - f['qacc_newton']))[ARM], precision=2)}; "
+                  f"final {np.array2string((M @ (g[D['QACC']:D['QACC'] + nv] - f['qacc']))[ARM], precision=2)}; noslip sweeps kernel "
+                  f"{int(g[D['NOSLIP_ITER']])} oracle {int(O.forward_fields(row(st), ['noslip_iter'], model=m)['noslip_iter'][0])}", flush=True)
             if kne != ne:
                 continue
+            ty = f["efc_type"].astype(int)
+            dfo = np.abs(g[D["EFC_FORCE"]:D["EFC_FORCE"] + ne] - f["efc_force"])
+            for tt in sorted(set(ty.tolist())):
+                sel = np.nonzero(ty == tt)[0]
+                i = sel[int(np.argmax(dfo[sel]))]
+                print(f"    efc type {tt}: {len(sel)} rows, worst |dforce| {dfo[i]:.2e} at row {i} (oracle force {f['efc_force'][i]:.3e})",
+                      flush=True)
             J = f["efc_J"].reshape(ne, nv)
             KJ = g[D["EFC_J"]:D["EFC_J"] + ne * nv].reshape(ne, nv)
             con = f["contact"].reshape(nc, 30)

@@ -63,7 +63,7 @@ def main():
                # quad-cycles (its PMC-units row), so a wave keeps the pipe busy 2 x SQ_INSTS_VALU of its
                # 4 x SQ_WAVE_CYCLES, times the resident waves per SIMD
                "valu_pipe_util": (min(1.0, wps * 2.0 * per["SQ_INSTS_VALU"] / (4.0 * wc)) if "SQ_INSTS_VALU" in per else None),
-               "source": "rocprofv3 --pmc SQ_* (two passes of 8 SQ counters), tools/gpu_sq.sh"}
+               "source": "rocprofv3 --pmc SQ_* (two passes of 8 SQ counters), tools/gpu.sh sq"}
         json.dump(rec, open(jpath, "w"), indent=1)
 
 
