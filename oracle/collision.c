@@ -287,6 +287,14 @@ static int box_face_contacts(const double* pr, const double* Rr, const double* s
  * must produce there) and by the reference's behavioural tests (grasp, lift, placement).  The
  * device colliders (collide_dev.h c_box_box / c_box_face) are this routine in box-relative
  * coordinates, equal to it at 1e-9 in fp64 (tests/test_boxbox_gpu.py). */
+/* Assumption probes (tools/badqacc_probe.py; default 0 = the restatement above): bits that change
+ * one assumption each, to test which of them, changed, could produce MUJOCO_LOG.TXT's BADQACC.
+ *   1  A1: near-parallel edge axes kept down to |A_i x B_j| > 1e-12 (not 1e-6)
+ *   2  A3: round 5's edge tie margin (1e-12 instead of BB_TOL)
+ *   4  A6: no parallel-line guard on the edge closest points (den > 0, not den > 1e-12)
+ *   8  A6: the edge contact at box 2's closest point (MuJoCo may place it on one edge) */
+static int g_bb_variant = 0;
+void orc_set_boxbox_variant(int v) { g_bb_variant = v; }
 static int box_box(const double* p1, const double* R1, const double* s1, const double* p2, const double* R2,
                    const double* s2, double margin, orc_contact* c) {
   double T[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
@@ -317,7 +325,7 @@ static int box_box(const double* p1, const double* R1, const double* s1, const d
       double L[3];
       cross3(L, A[i], B[j]);
       double len = sqrt(dot3(L, L));
-      if (len < 1e-6) continue;
+      if (len < ((g_bb_variant & 1) ? 1e-12 : 1e-6)) continue;
       for (int k = 0; k < 3; k++) L[k] /= len;
       double tl = dot3(T, L);
       double ra = s1[0] * fabs(dot3(A[0], L)) + s1[1] * fabs(dot3(A[1], L)) + s1[2] * fabs(dot3(A[2], L));
@@ -325,7 +333,7 @@ static int box_box(const double* p1, const double* R1, const double* s1, const d
       double sep = fabs(tl) - ra - rb;
       if (sep > margin) return 0;
       /* edge axes must beat face axes clearly (ODE-style 1.05 depth fudge, and by BB_TOL: A3) */
-      if (1.05 * sep > best + BB_TOL) {
+      if (1.05 * sep > best + ((g_bb_variant & 2) ? 1e-12 : BB_TOL)) {
         best = sep; btype = 2; bi = i; bj = j;
         for (int k = 0; k < 3; k++) bestn[k] = tl >= 0 ? L[k] : -L[k];
       }
@@ -352,11 +360,11 @@ static int box_box(const double* p1, const double* R1, const double* s1, const d
   double w[3] = {pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]};
   double a = dot3(ua, ub), dd = dot3(ua, w), e = dot3(ub, w), den = 1 - a * a;
   double ta = 0, tb = 0;
-  if (den > 1e-12) { ta = (a * e - dd) / den; tb = (e - a * dd) / den; }
+  if (den > ((g_bb_variant & 4) ? 0.0 : 1e-12)) { ta = (a * e - dd) / den; tb = (e - a * dd) / den; }
   for (int k = 0; k < 3; k++) { pa[k] += ta * ua[k]; pb[k] += tb * ub[k]; }
   c->dist = best;
   set_normal(c, bestn);
-  for (int k = 0; k < 3; k++) c->pos[k] = 0.5 * (pa[k] + pb[k]);
+  for (int k = 0; k < 3; k++) c->pos[k] = (g_bb_variant & 8) ? pb[k] : 0.5 * (pa[k] + pb[k]);
   return 1;
 }
 

@@ -149,6 +149,8 @@ def _phys_lib():
         L.orc_field.restype = C.c_int
         L.orc_convex_probe.argtypes = [P, P, C.c_int, C.c_int, P, P, P]
         L.orc_convex_probe.restype = C.c_int
+        L.orc_set_boxbox_variant.argtypes = [C.c_int]
+        L.orc_set_boxbox_variant.restype = None
         L._phys_ready = True
     return L
 
@@ -176,6 +178,12 @@ def step(state, nsub=1, nthreads=1, model=None):
     if rc:
         raise RuntimeError("orc_step_batch failed")
     return state
+
+
+def set_boxbox_variant(bits=0):
+    """Assumption probes of the box-box restatement (oracle/collision.c above box_box; 0 = the
+    restatement itself).  Test infrastructure only: tools/badqacc_probe.py, tests/test_badqacc_probe_cpu.py."""
+    _phys_lib().orc_set_boxbox_variant(int(bits))
 
 
 def forward_fields(state_row, fields, model=None, do_step=False):

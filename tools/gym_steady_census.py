@@ -1,8 +1,9 @@
 """Steady-state census of the fp32 gym workload (bench.py run_gym_steady's shape: 4096 envs, uniform
 random actions, auto-reset): per gym step the envs starting in each tier, the hand-over queue's
 counts and the wall time; every `every` steps the contact / row distribution (forward_debug through
-the tiers), the finger opening and where the cubes are.  usage:
-python tools/gym_steady_census.py [B] [steps] [every]"""
+the tiers), the finger opening and where the cubes are; optionally the state after the last step
+(npz: the physics state, each env's tier and contact count) for tools/steady_stage_prof.py.  usage:
+python tools/gym_steady_census.py [B] [steps] [every] [dump.npz]"""
 import os
 import sys
 import time
@@ -22,6 +23,7 @@ def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 60
     every = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+    dump = sys.argv[4] if len(sys.argv) > 4 else None
     g = BatchedFrankaShelfPNPEnv(B, autoreset=True)
     m = g.model
     g.reset()
@@ -62,6 +64,14 @@ def main():
                 top = sorted(pairs.items(), key=lambda x: -x[1])[:6]
                 print(f"    env {b}: {int(nc[b])} contacts, {int(ne[b])} rows, fingers {fw[b] * 1e3:.2f} mm; by body pair {top}",
                       flush=True)
+
+    if dump:
+        dbg = g.engine.forward_debug({kk: v for kk, v in g.state.items()}).cpu().numpy()
+        out = {k: v.cpu().numpy() for k, v in g.state.items()}
+        out.update(tier=(g.env["tier"].to(torch.int64) & 3).cpu().numpy(), ncon=dbg[:, D["COUNTS"]],
+                   nefc=dbg[:, D["COUNTS"] + 1])
+        np.savez(dump, **out)
+        print(f"state after step {n} -> {dump}", flush=True)
 
 
 if __name__ == "__main__":
