@@ -73,6 +73,15 @@
 // does the same arithmetic); the quaternion remainder (PNP_XQLO) where MPR runs (it does not fit
 // the compact tier's 20 KB).
 #define PNP_XLO (!PNP_WIDE64)
+// Round 6 fp32 precision fixes (on; A/B builds: -DPNP_F32_SNAP=0 -DPNP_F32_NS_NEWTON=0): unresolved
+// tangent rows snapped to zero (st_constraints), no-slip from Newton's iterate (st_noslip /
+// st_finish_accel)
+#ifndef PNP_F32_SNAP
+#define PNP_F32_SNAP 1
+#endif
+#ifndef PNP_F32_NS_NEWTON
+#define PNP_F32_NS_NEWTON 1
+#endif
 #define PNP_XQLO (!PNP_COMPACT && !PNP_WIDE64)
 #define PNP_LEAN (PNP_COMPACT || PNP_WIDE || PNP_WIDE64)
 // PNP_BIG_ISLANDS: the solver's whole-wave paths for islands with more rows than a wave (line
@@ -1865,7 +1874,7 @@ __device__ void st_constraints(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s
       const T jd[3] = {jp2[0] - jp1[0], jp2[1] - jp1[1], jp2[2] - jp1[2]};
       for (int a = 0; a < 3; a++) cj[a] = con.frame[3 * a] * jd[0] + con.frame[3 * a + 1] * jd[1] + con.frame[3 * a + 2] * jd[2];
     }
-    if constexpr (sizeof(T) == 4) {
+    if constexpr (sizeof(T) == 4 && PNP_F32_SNAP) {
       // A tangent row at the rounding level of its normal row is rounding: two bodies of one tree
       // whose relative motion has no tangential component (the closed gripper's finger pads, face
       // to face: only the finger slides move them apart, along the normal) have J_t = 0 exactly in
@@ -1875,10 +1884,16 @@ __device__ void st_constraints(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s
       // accelerations 1.4e-4 off in the tree's M-norm, tools/pads_stage_diag.py).  Such a row (its
       // largest entry within 16 fp32 ulps of the normal row's largest) is snapped to zero, so the
       // edges are equal as in fp64; a resolved tangent (J_t / J_n >~ 2e-6) is unchanged.
-      const T nmax = rowmax16(fabs(cj[0])) * T(16 * 1.1920929e-7);
-      const T t1m = rowmax16(fabs(cj[1])), t2m = rowmax16(fabs(cj[2]));
-      if (t1m <= nmax) cj[1] = T(0);
-      if (t2m <= nmax) cj[2] = T(0);
+      // Only a contact between two bodies of one tree can cancel so (a world-body contact's
+      // tangent rows are O(1)): the row reductions run only when the wave holds such a contact
+      // (none on the settled C3 scene: cubes on boards).
+      const bool same = act && r1 == r2 && r1 != 0;
+      if (__ballot(same)) {
+        const T nmax = rowmax16(fabs(cj[0])) * T(16 * 1.1920929e-7);
+        const T t1m = rowmax16(fabs(cj[1])), t2m = rowmax16(fabs(cj[2]));
+        if (same && t1m <= nmax) cj[1] = T(0);
+        if (same && t2m <= nmax) cj[2] = T(0);
+      }
     }
     if (act) {
       const Con<T>& con = s.con[c];
@@ -3797,7 +3812,7 @@ __device__ void st_noslip(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK
     }
   }
   clk.sub_lap(SC_NS_W);
-  if constexpr (sizeof(T) == 4) {
+  if constexpr (sizeof(T) == 4 && PNP_F32_NS_NEWTON) {
     // fp32: the constraint acceleration v = qacc - qacc_smooth from Newton's own iterate, not
     // M^-1 J^T f recomputed from the forces: where large contact forces cancel on a dof (the pads
     // pressed together push both fingers with ~100x the net force) the fp32 sum J^T f carries
@@ -4176,7 +4191,7 @@ __device__ void st_finish_accel(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& 
   const int l = lane_id();
   if (s.nefc == 0) return;
   const bool jt = s.jt_ok;
-  constexpr bool f32 = sizeof(T) == 4;
+  constexpr bool f32 = sizeof(T) == 4 && PNP_F32_NS_NEWTON;
   if (f32 && m.noslip_iterations > 0) {
     // fp32 (st_noslip): qacc = Newton's qacc + M^-1 J^T (f - f_newton), f_newton in efc_aref --
     // only the forces no-slip changed enter the sum
