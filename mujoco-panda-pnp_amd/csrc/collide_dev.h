@@ -355,20 +355,29 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
 //
 // Wave-cooperative: the whole wave runs MPR on ONE pair (every lane holds the same portal, so
 // all branches are uniform) and splits each mesh support map over its 64 lanes.  Lane l keeps
-// hull vertices l, l+64, l+128 in registers for the whole MPR run (C_WV per lane; larger hulls
+// hull vertices l, l+64, l+128 in registers for the whole MPR run (CGrp<64>::NW per lane; larger hulls
 // stream the rest from global memory), a support is three dot products, a DPP max and a ballot
 // for the first vertex inside the tie band -- instead of 2 x nvert dependent global loads on a
 // single lane.
-constexpr int C_WV = 3;
+// Lane groups (round 6): G lanes run one MPR -- G = 64, the whole wave (the serial pass, the fp64
+// builds), or G = 16, one DPP row: four independent MPR runs per wave (the fp32 full / wide
+// builds' convex pass, step.hip convex_part).  Every lane of a group holds the same portal (the
+// group's branches are uniform) and the support maps split over the group's lanes; a group keeps
+// CGrp<G>::NW hull vertices per lane in registers (G = 64: 192 vertices, G = 16: 64) and streams the
+// rest from global memory.  The arithmetic of each lane is the same for both widths: the same bits.
+template <int G> struct CGrp;
+template <> struct CGrp<64> { static constexpr int NW = 3; };
+template <> struct CGrp<16> { static constexpr int NW = 4; };
 #ifndef PNP_MPR_CT
 #define PNP_MPR_CT double   // (A/B builds only: PNP_DEFS=-DPNP_MPR_CT=float)
 #endif
 typedef PNP_MPR_CT CT;   // MPR arithmetic (every build)
-template <typename T>
+template <typename T, int G = 64>
 struct CShape {
+  static constexpr int NW = CGrp<G>::NW;
   int type, mesh, vadr, nvert;
   CT pos[3], R[9], size[3], margin;
-  T wv[C_WV][3];   // mesh: vertices lane + 64 j (local frame, the image's precision)
+  T wv[NW][3];   // mesh: vertices (lane in the group) + G j (local frame, the image's precision)
 };
 struct SVert {
   CT v[3], v1[3], v2[3];
@@ -404,54 +413,67 @@ __device__ __forceinline__ T c_wave_max(T v) {
   v = fmax(v, dpp_f<0x140>(v));
   return fmax(fmax(rdlane(v, 0), rdlane(v, 16)), fmax(rdlane(v, 32), rdlane(v, 48)));
 }
-template <typename T>
-__device__ void c_load_shape(const DevPhys<T>& /*image: phys<T>()*/, CShape<T>& sh) {
+// max over the lane group (all its lanes active), group-uniform result
+template <int G, typename T>
+__device__ __forceinline__ T c_grp_max(T v) {
+  if constexpr (G == 64) return c_wave_max(v);
+  else return rowmax16(v);
+}
+template <typename T, int G>
+__device__ void c_load_shape(const DevPhys<T>& /*image: phys<T>()*/, CShape<T, G>& sh) {
   const DevPhys<T>& m = phys<T>();
-  const int l = threadIdx.x & 63;
+  const int l = threadIdx.x & (G - 1);
   sh.vadr = sh.type == 7 ? m.mesh_vertadr[sh.mesh] : 0;
   sh.nvert = sh.type == 7 ? m.mesh_vertnum[sh.mesh] : 0;
 #pragma unroll
-  for (int j = 0; j < C_WV; j++) {
-    const int i = 64 * j + l;
+  for (int j = 0; j < CShape<T, G>::NW; j++) {
+    const int i = G * j + l;
     for (int k = 0; k < 3; k++) sh.wv[j][k] = i < sh.nvert ? m.mesh_vert[sh.vadr + i][k] : T(0);
   }
 }
-// first vertex within the tie band of the maximum (oracle/convex.c support), wave-cooperative
-template <typename T>
-__device__ int c_mesh_argmax(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& s, const CT* ld) {
+// the lane group's bits of a wave ballot (G = 64: all of them)
+template <int G>
+__device__ __forceinline__ uint64_t c_grp_bits(uint64_t b) {
+  if constexpr (G == 64) return b;
+  else return (b >> ((threadIdx.x & 63) & ~(G - 1))) & ((1ull << G) - 1ull);
+}
+// first vertex within the tie band of the maximum (oracle/convex.c support), group-cooperative
+template <typename T, int G>
+__device__ int c_mesh_argmax(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T, G>& s, const CT* ld) {
   const DevPhys<T>& m = phys<T>();
-  const int l = threadIdx.x & 63, n = s.nvert;
-  CT dv[C_WV], bd = CT(-1e30);
+  constexpr int NW = CShape<T, G>::NW;
+  const int l = threadIdx.x & (G - 1), n = s.nvert;
+  CT dv[NW], bd = CT(-1e30);
 #pragma unroll
-  for (int j = 0; j < C_WV; j++) {
-    dv[j] = 64 * j + l < n ? CT(s.wv[j][0]) * ld[0] + CT(s.wv[j][1]) * ld[1] + CT(s.wv[j][2]) * ld[2] : CT(-1e30);
+  for (int j = 0; j < NW; j++) {
+    dv[j] = G * j + l < n ? CT(s.wv[j][0]) * ld[0] + CT(s.wv[j][1]) * ld[1] + CT(s.wv[j][2]) * ld[2] : CT(-1e30);
     bd = fmax(bd, dv[j]);
   }
-  for (int i = 64 * C_WV + l; i < n; i += 64) {
+  for (int i = G * NW + l; i < n; i += G) {
     const T* V = m.mesh_vert[s.vadr + i];
     bd = fmax(bd, CT(V[0]) * ld[0] + CT(V[1]) * ld[1] + CT(V[2]) * ld[2]);
   }
-  bd = c_wave_max(bd);
+  bd = c_grp_max<G>(bd);
   const CT lo = bd - CT(1e-9);
 #pragma unroll
-  for (int j = 0; j < C_WV; j++) {
-    const uint64_t b = __ballot(64 * j + l < n && dv[j] >= lo);
-    if (b) return 64 * j + __ffsll((unsigned long long)b) - 1;
+  for (int j = 0; j < NW; j++) {
+    const uint64_t b = c_grp_bits<G>(__ballot(G * j + l < n && dv[j] >= lo));
+    if (b) return G * j + __ffsll((unsigned long long)b) - 1;
   }
-  for (int base = 64 * C_WV; base < n; base += 64) {
+  for (int base = G * NW; base < n; base += G) {
     const int i = base + l;
     bool ok = false;
     if (i < n) {
       const T* V = m.mesh_vert[s.vadr + i];
       ok = CT(V[0]) * ld[0] + CT(V[1]) * ld[1] + CT(V[2]) * ld[2] >= lo;
     }
-    const uint64_t b = __ballot(ok);
+    const uint64_t b = c_grp_bits<G>(__ballot(ok));
     if (b) return base + __ffsll((unsigned long long)b) - 1;
   }
   return 0;
 }
-template <typename T>
-__device__ void c_support(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& s, const CT* d, CT* out) {
+template <typename T, int G>
+__device__ void c_support(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T, G>& s, const CT* d, CT* out) {
   const DevPhys<T>& m = phys<T>();
   CT ld[3];
   for (int k = 0; k < 3; k++) ld[k] = s.R[k] * d[0] + s.R[3 + k] * d[1] + s.R[6 + k] * d[2];
@@ -467,8 +489,8 @@ __device__ void c_support(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T
   for (int k = 0; k < 3; k++)
     out[k] = s.pos[k] + s.R[3 * k] * lp[0] + s.R[3 * k + 1] * lp[1] + s.R[3 * k + 2] * lp[2] + CT(0.5) * s.margin * d[k];
 }
-template <typename T>
-__device__ __forceinline__ void c_mksupport(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& a, const CShape<T>& b, const CT* d, SVert& v) {
+template <typename T, int G>
+__device__ __forceinline__ void c_mksupport(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T, G>& a, const CShape<T, G>& b, const CT* d, SVert& v) {
   const DevPhys<T>& m = phys<T>();
   const CT nd[3] = {-d[0], -d[1], -d[2]};
   c_support(m, a, d, v.v1);
@@ -483,13 +505,13 @@ struct SVertL {
   CT v[3];
   int id;
 };
-template <typename T>
-__device__ __forceinline__ void c_mks(const DevPhys<T>& m, const CShape<T>& a, const CShape<T>& b, const CT* d, SVert& v,
+template <typename T, int G>
+__device__ __forceinline__ void c_mks(const DevPhys<T>& m, const CShape<T, G>& a, const CShape<T, G>& b, const CT* d, SVert& v,
                                       double (*)[6], int) {
   c_mksupport(m, a, b, d, v);
 }
-template <typename T>
-__device__ __forceinline__ void c_mks(const DevPhys<T>& m, const CShape<T>& a, const CShape<T>& b, const CT* d, SVertL& v,
+template <typename T, int G>
+__device__ __forceinline__ void c_mks(const DevPhys<T>& m, const CShape<T, G>& a, const CShape<T, G>& b, const CT* d, SVertL& v,
                                       double (*sv)[6], int id) {
   SVert t;
   c_mksupport(m, a, b, d, t);
@@ -585,8 +607,8 @@ __device__ T c_tri_dist2(const T* P, const T* x0, const T* B, const T* C, T* w) 
 }
 
 // ccdMPRPenetration: true and (depth, dir, pos) on intersection
-template <typename T, typename V = SVert>
-__device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>& A, const CShape<T>& Bs, CT& depth, CT* dir, CT* pos,
+template <typename T, typename V = SVert, int G = 64>
+__device__ bool c_mpr(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T, G>& A, const CShape<T, G>& Bs, CT& depth, CT* dir, CT* pos,
                       double (*sv)[6] = nullptr) {
   const DevPhys<T>& m = phys<T>();
   const CT tol = CT(1e-6);   // mjOption mpr_tolerance
@@ -905,13 +927,13 @@ __device__ void t_makeframe(T f[9]) {
 // (dist, pos, normal) by lane 0; returns their number.  Wave-uniform call: every lane passes the
 // same pair and gets the same result.
 constexpr int C_MULTI = 5;
-template <typename T>
-__device__ __forceinline__ bool c_mpr_contact(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T>* sh, T margin,
+template <typename T, int G>
+__device__ __forceinline__ bool c_mpr_contact(const DevPhys<T>& /*image: phys<T>()*/, const CShape<T, G>* sh, T margin,
                                               T* c, double (*sv)[6]) {
   const DevPhys<T>& m = phys<T>();
   CT depth, nrm[3], pos[3];
 #if PNP_MPR_SLOTS
-  if (!c_mpr<T, SVertL>(m, sh[0], sh[1], depth, nrm, pos, sv)) return false;
+  if (!c_mpr<T, SVertL, G>(m, sh[0], sh[1], depth, nrm, pos, sv)) return false;
 #else
   (void)sv;
   if (!c_mpr(m, sh[0], sh[1], depth, nrm, pos)) return false;
@@ -991,9 +1013,9 @@ __device__ __forceinline__ void c_rel_pos(const DevPhys<T>& /*image: phys<T>()*/
 }
 // the pair's two shapes, origin at geom 1's centre (oracle/convex.c): centimetre-scale support
 // points, so the fp32 Minkowski differences keep ~20x more bits than in world coordinates
-template <typename T>
+template <typename T, int G>
 __device__ __forceinline__ void c_convex_shapes(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& s, int g1, int g2,
-                                                T margin, CShape<T>* sh) {
+                                                T margin, CShape<T, G>* sh) {
   const DevPhys<T>& m = phys<T>();
   const int gs[2] = {g1, g2};
   CT o1[3], o2[3];
@@ -1015,8 +1037,8 @@ __device__ __forceinline__ void c_convex_shapes(const DevPhys<T>& /*image: phys<
 // normal): q = (cos(a/2), axis sin(a/2)) (oracle: sp_axisangle2quat), R(q^-1) = R(q)^T.  sh[].pos
 // and sh[].R hold the unperturbed frames on entry (c_convex_shapes).
 // (One function for the serial and the multi-wave convex passes: same bits.)
-template <typename T>
-__device__ __forceinline__ void c_fan_rotate(CShape<T>* sh, const CT* f, const CT* o, int t) {
+template <typename T, int G>
+__device__ __forceinline__ void c_fan_rotate(CShape<T, G>* sh, const CT* f, const CT* o, int t) {
   const bool second = (t >> 1) != 0;   // (selects, not an index: f stays in registers)
   const CT ax[3] = {second ? f[6] : f[3], second ? f[7] : f[4], second ? f[8] : f[5]};
   const CT sh_ = (t & 1) ? CT(0.0004999999791666669) : CT(-0.0004999999791666669), q0 = CT(0.9999998750000026);
@@ -1076,10 +1098,12 @@ __device__ __forceinline__ bool c_fan_close(const T* a, const T* b, T tol) {
 #else
 #define C_RUN_INLINE __forceinline__              // one call site (c_convex's loop)
 #endif
-template <typename T>
+// G = 16: every argument is the lane group's own (four runs per wave, step.hip convex_part); the
+// group's first lane stages the contact
+template <typename T, int G = 64>
 __device__ C_RUN_INLINE bool c_convex_run(const Env<T>& s, int g1, int g2, T margin, int t, T (*val)[7], int slot) {
   const DevPhys<T>& m = phys<T>();
-  CShape<T> sh[2];
+  CShape<T, G> sh[2];
   c_convex_shapes(m, s, g1, g2, margin, sh);
   if (t >= 0) {
     CT f[9];
@@ -1089,12 +1113,13 @@ __device__ C_RUN_INLINE bool c_convex_run(const Env<T>& s, int g1, int g2, T mar
   }
   T c[7];
 #if PNP_MPR_SLOTS
-  double (*sv)[6] = const_cast<Env<T>&>(s).mpr_sv[threadIdx.x >> 6];   // this wave's portal slots
+  // this group's portal slots
+  double (*sv)[6] = const_cast<Env<T>&>(s).mpr_sv[threadIdx.x >> 6][(threadIdx.x & 63) / G];
 #else
   double (*sv)[6] = nullptr;
 #endif
   const bool hit = c_mpr_contact(m, sh, margin, c, sv);
-  if (hit && (threadIdx.x & 63) == 0)
+  if (hit && (threadIdx.x & (G - 1)) == 0)
     for (int k = 0; k < 7; k++) val[slot][k] = c[k];
   return hit;
 }

@@ -64,6 +64,12 @@
 // MPR's portal support points in per-wave LDS slots (collide_dev.h SVertL): the full and wide
 // builds (the compact builds run no MPR; the fp64 wide build keeps registers)
 #define PNP_MPR_SLOTS (!PNP_COMPACT && !PNP_WIDE64)
+// PNP_MPR_G: lanes per MPR run in the fp32 full / wide builds' convex pass (collide_dev.h CGrp): 16 =
+// four runs per wave, and every fp32 full / wide kernel takes the multi-wave pass (one wave or
+// more); 64 (A/B builds) = one run per wave, single-wave kernels on the serial pass
+#ifndef PNP_MPR_G
+#define PNP_MPR_G 16
+#endif
 // PNP_XLO: the fp32 builds keep each body's world position and quaternion as fp32 pairs (xpos /
 // xquat + the remainders of the fp64 kinematic chain, Env::xlo / xqlo); MPR's geom frames and the
 // box-box collider's centre offset are formed from them in fp64 (collide_dev.h c_geom_frame64,
@@ -280,7 +286,7 @@ struct Env {
   unsigned char mw_fan[NT];    // the convex pass: round-local pairs whose multiccd trials run
 #endif
 #if PNP_MPR_SLOTS
-  double mpr_sv[PNP_WIDE ? 4 : 2][4][6];   // per wave: MPR's portal support points (collide_dev.h SVertL)
+  double mpr_sv[PNP_WIDE ? 4 : 2][64 / PNP_MPR_G][4][6];   // per wave and lane group: MPR's portal support points (collide_dev.h SVertL)
 #endif
 };
 static_assert(sizeof(((Env<float>*)0)->efc_Jv) >= 7 * 4 * NT + 2 * NT + 4 + 2 * PH_MAXLIVE,
@@ -1396,7 +1402,9 @@ enum { MW_EXIT = 0, MW_MPR = 1, MW_FAN = 2 };
 // Four waves, one per SIMD: the wide tier's Env (192 contacts) holds one env per CU, so the helpers
 // cost no residency, and multiccd makes up to five MPR runs per convex pair to spread.  (Round 2 /
 // early round 3, at two envs per CU: two waves, four were slower -- profiles/r03/ab_mpr_helper_waves.log.)
+// Each wave runs 64 / PNP_MPR_G items at a time, one per lane group (round 6).
 constexpr int MW_WAVES = PNP_WIDE ? 4 : 2;   // full build: 2 x 3 envs per CU
+constexpr int MW_GROUPS = 64 / PNP_MPR_G;
 // A round's convex pairs (up to RN, listed by wave 0 in cst_key in live-list order), each with
 // `per` staging slots (cst_val, mw_hit): slot per o holds pair o's first MPR contact, slots
 // per o + 1 + t its multiccd trial t (positions relative to geom 1's centre).  Items are taken one
@@ -1412,19 +1420,25 @@ __device__ void convex_part(Env<float>& s, int cmd) {
   // readfirstlane no longer reads the lane that took the slot.  At most n trips in any case.
   const int n = __builtin_amdgcn_readfirstlane(cmd >> 8);
   const int per = m.multiccd ? C_MULTI : 1;
+  // a wave takes MW_GROUPS consecutive items (o wave-uniform), lane group q item o + q: a pair's four
+  // multiccd trials (items 4 i .. 4 i + 3) run side by side in one wave
+  const int q = l / PNP_MPR_G;
   for (int it = 0; it < n; it++) {
     int o = 0;
-    if (l == 0) o = atomicAdd(&s.mw_next, 1);
+    if (l == 0) o = atomicAdd(&s.mw_next, MW_GROUPS);
     o = __builtin_amdgcn_readfirstlane(__shfl(o, 0));
     if (o >= n) return;
-    const int po = kind == MW_FAN ? s.mw_fan[o >> 2] : o;   // round-local pair
-    const int slot = per * po + (kind == MW_FAN ? 1 + (o & 3) : 0);
-    const int p = s.cst_key[po];
-    const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
-    const float margin = fmaxf(m.geom_margin[g1], m.geom_margin[g2]);
-    const bool hit = c_convex_run(s, g1, g2, margin, kind == MW_FAN ? (o & 3) : -1, s.cst_val + per * po,
-                                  slot - per * po);
-    if (l == 0) s.mw_hit[slot] = hit;
+    const int oi = o + q;   // this group's item
+    if (oi < n) {           // (group-uniform)
+      const int po = kind == MW_FAN ? s.mw_fan[oi >> 2] : oi;   // round-local pair
+      const int slot = per * po + (kind == MW_FAN ? 1 + (oi & 3) : 0);
+      const int p = s.cst_key[po];
+      const int g1 = m.pair_g1[p], g2 = m.pair_g2[p];
+      const float margin = fmaxf(m.geom_margin[g1], m.geom_margin[g2]);
+      const bool hit = c_convex_run<float, PNP_MPR_G>(s, g1, g2, margin, kind == MW_FAN ? (oi & 3) : -1,
+                                                      s.cst_val + per * po, slot - per * po);
+      if ((l & (PNP_MPR_G - 1)) == 0) s.mw_hit[slot] = hit;
+    }
   }
 }
 __device__ void mw_helper(Env<float>& s) {
@@ -4358,7 +4372,7 @@ __device__ void forward(const DevPhys<T>& /*image: phys<T>()*/, Env<T>& s, CLK& 
     clk.sub_start();
 #if PNP_MW
     if constexpr (sizeof(T) == 4) {
-      if (s.mw > 1) st_collision_convex_mw(s);
+      if (PNP_MPR_G < 64 || s.mw > 1) st_collision_convex_mw(s);
       else st_collision_convex(m, s);
     } else {
       st_collision_convex(m, s);
