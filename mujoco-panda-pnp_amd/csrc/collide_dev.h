@@ -368,6 +368,7 @@ __device__ void c_box_box(const T* p1, const T* R1, const T* s1, const T* p2, co
 template <int G> struct CGrp;
 template <> struct CGrp<64> { static constexpr int NW = 3; };
 template <> struct CGrp<16> { static constexpr int NW = 4; };
+template <> struct CGrp<8> { static constexpr int NW = 8; };
 #ifndef PNP_MPR_CT
 #define PNP_MPR_CT double   // (A/B builds only: PNP_DEFS=-DPNP_MPR_CT=float)
 #endif
@@ -400,9 +401,9 @@ __device__ __forceinline__ void cc3(T* r, const T* a, const T* b) {
 }
 template <typename T> __device__ __forceinline__ void cs3(T* r, const T* a, const T* b) { r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2]; }
 template <typename T>
-__device__ __forceinline__ void cnorm(T* v) {
-  const T n = PM<T>::sqrt_(cd3(v, v));
-  v[0] /= n; v[1] /= n; v[2] /= n;
+__device__ __forceinline__ void cnorm(T* v) {   // ccdVec3Normalize: by the reciprocal length
+  const T k = T(1) / PM<T>::sqrt_(cd3(v, v));
+  v[0] *= k; v[1] *= k; v[2] *= k;
 }
 // max over the wave (all 64 lanes active), wave-uniform result
 template <typename T>
@@ -416,8 +417,16 @@ __device__ __forceinline__ T c_wave_max(T v) {
 // max over the lane group (all its lanes active), group-uniform result
 template <int G, typename T>
 __device__ __forceinline__ T c_grp_max(T v) {
-  if constexpr (G == 64) return c_wave_max(v);
-  else return rowmax16(v);
+  if constexpr (G == 64) {
+    return c_wave_max(v);
+  } else if constexpr (G == 16) {
+    return rowmax16(v);
+  } else {   // G == 8: quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror
+    static_assert(G == 8, "lane group width");
+    v = fmax(v, dpp_f<0xB1>(v));
+    v = fmax(v, dpp_f<0x4E>(v));
+    return fmax(v, dpp_f<0x141>(v));
+  }
 }
 template <typename T, int G>
 __device__ void c_load_shape(const DevPhys<T>& /*image: phys<T>()*/, CShape<T, G>& sh) {

@@ -1049,7 +1049,7 @@ static bool gym_full_resume_enabled() {
 // while one workgroup per env lets the dispatcher balance the CUs; profiles/r03/ab_gym_full_mw.log)
 static bool gym_full_mw_enabled() {
   const char* e = getenv("PNP_GYM_FULL_MW");
-  return e && e[0] == '1';
+  return PNP_MPR_SV_WAVES >= PNP_NS::MW_WAVES && e && e[0] == '1';
 }
 // PNP_GYM_QUEUE: unset / 1 = routed fp32 gym steps hand the full tier's hand-overs to the wide
 // tier through the device queue (hq_publish / hq_take), consumed concurrently with the full passes

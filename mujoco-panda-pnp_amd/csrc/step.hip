@@ -70,6 +70,10 @@
 #ifndef PNP_MPR_G
 #define PNP_MPR_G 16
 #endif
+// waves with MPR portal slots: the wide build's four; the full build's two (its opt-in two-wave
+// gym kernel, PNP_GYM_FULL_MW), one with eight-lane groups (the slots of 8 groups per wave would
+// cost the full tier its third env per CU)
+#define PNP_MPR_SV_WAVES (PNP_WIDE ? 4 : (PNP_MPR_G < 16 ? 1 : 2))
 // PNP_XLO: the fp32 builds keep each body's world position and quaternion as fp32 pairs (xpos /
 // xquat + the remainders of the fp64 kinematic chain, Env::xlo / xqlo); MPR's geom frames and the
 // box-box collider's centre offset are formed from them in fp64 (collide_dev.h c_geom_frame64,
@@ -286,7 +290,7 @@ struct Env {
   unsigned char mw_fan[NT];    // the convex pass: round-local pairs whose multiccd trials run
 #endif
 #if PNP_MPR_SLOTS
-  double mpr_sv[PNP_WIDE ? 4 : 2][64 / PNP_MPR_G][4][6];   // per wave and lane group: MPR's portal support points (collide_dev.h SVertL)
+  double mpr_sv[PNP_MPR_SV_WAVES][64 / PNP_MPR_G][4][6];   // per wave and lane group: MPR's portal support points (collide_dev.h SVertL)
 #endif
 };
 static_assert(sizeof(((Env<float>*)0)->efc_Jv) >= 7 * 4 * NT + 2 * NT + 4 + 2 * PH_MAXLIVE,

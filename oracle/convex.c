@@ -54,6 +54,18 @@ typedef struct {
   double v[3], v1[3], v2[3];   /* Minkowski point v = v1 - v2 and the supports it came from */
 } svert;
 
+/* MPR work counters (diagnostics: tools/mpr_census.py, single-threaded use only): runs, support
+ * pairs (mk_support calls), discover / refine / penetration loop trips, runs that hit the
+ * penetration loop's cap, and the largest support count of one run */
+static _Thread_local long long g_mpr[8];   /* per thread: the pthread baseline never reads them */
+void orc_mpr_stats(long long* out, int reset) {
+  for (int i = 0; i < 8; i++) {
+    out[i] = g_mpr[i];
+    if (reset) g_mpr[i] = 0;
+  }
+}
+static _Thread_local long long g_mpr_run_supports;
+
 static int is_zero(double x) { return fabs(x) < CCD_EPS; }
 static int ccd_eq(double a, double b) {
   double ab = fabs(a - b);
@@ -68,9 +80,10 @@ static void c3(double* r, const double* a, const double* b) {
   r[0] = t0; r[1] = t1; r[2] = t2;
 }
 static void sub3(double* r, const double* a, const double* b) { r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2]; }
+/* ccdVec3Normalize: scale by the reciprocal of the length (one division, as libccd does) */
 static void normalize(double* v) {
-  double n = sqrt(d3(v, v));
-  v[0] /= n; v[1] /= n; v[2] /= n;
+  const double k = 1.0 / sqrt(d3(v, v));
+  v[0] *= k; v[1] *= k; v[2] *= k;
 }
 
 /* mjccd_support: support point of one geom along world direction d (unit) */
@@ -106,6 +119,8 @@ static void support(const shape* s, const double* d, double* out) {
 /* __ccdSupport: v1 = supp1(d), v2 = supp2(-d), v = v1 - v2 */
 static void mk_support(const shape* a, const shape* b, const double* d, svert* v) {
   double nd[3] = {-d[0], -d[1], -d[2]};
+  g_mpr[1]++;
+  g_mpr_run_supports++;
   support(a, d, v->v1);
   support(b, nd, v->v2);
   sub3(v->v, v->v1, v->v2);
@@ -177,6 +192,7 @@ static int discover_portal(const shape* a, const shape* b, svert* p) {
     dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2];
   }
   for (int guard = 0; guard < 1000; guard++) {
+    g_mpr[2]++;
     mk_support(a, b, dir, &p[3]);
     dot = d3(p[3].v, dir);
     if (is_zero(dot) || dot < 0) return -1;
@@ -208,6 +224,7 @@ static int refine_portal(const shape* a, const shape* b, svert* p) {
   double dir[3];
   svert v4;
   for (int guard = 0; guard < 1000; guard++) {
+    g_mpr[3]++;
     portal_dir(p, dir);
     if (encapsules_origin(p, dir)) return 0;
     mk_support(a, b, dir, &v4);
@@ -298,7 +315,15 @@ static void find_pos(const svert* p, double* pos) {
 }
 
 /* ccdMPRPenetration: 0 and (depth, dir, pos) on intersection, -1 otherwise */
+static int mpr_penetration_(const shape* a, const shape* b, double* depth, double* dir, double* pos);
 static int mpr_penetration(const shape* a, const shape* b, double* depth, double* dir, double* pos) {
+  g_mpr[0]++;
+  g_mpr_run_supports = 0;
+  const int r = mpr_penetration_(a, b, depth, dir, pos);
+  if (g_mpr_run_supports > g_mpr[6]) g_mpr[6] = g_mpr_run_supports;
+  return r;
+}
+static int mpr_penetration_(const shape* a, const shape* b, double* depth, double* dir, double* pos) {
   svert p[4];
   int res = discover_portal(a, b, p);
   if (res < 0) return -1;
@@ -319,8 +344,10 @@ static int mpr_penetration(const shape* a, const shape* b, double* depth, double
   svert v4;
   double d[3];
   for (int it = 0;; it++) {
+    g_mpr[4]++;
     portal_dir(p, d);
     mk_support(a, b, d, &v4);
+    if (it > MPR_ITERS) g_mpr[5]++;
     if (reach_tolerance(p, &v4, d) || it > MPR_ITERS) {
       static const double O[3] = {0, 0, 0};
       *depth = sqrt(point_tri_dist2(O, p[1].v, p[2].v, p[3].v, dir));

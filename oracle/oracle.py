@@ -151,6 +151,8 @@ def _phys_lib():
         L.orc_convex_probe.restype = C.c_int
         L.orc_set_boxbox_variant.argtypes = [C.c_int]
         L.orc_set_boxbox_variant.restype = None
+        L.orc_mpr_stats.argtypes = [C.POINTER(C.c_longlong), C.c_int]
+        L.orc_mpr_stats.restype = None
         L._phys_ready = True
     return L
 
@@ -184,6 +186,16 @@ def set_boxbox_variant(bits=0):
     """Assumption probes of the box-box restatement (oracle/collision.c above box_box; 0 = the
     restatement itself).  Test infrastructure only: tools/badqacc_probe.py, tests/test_badqacc_probe_cpu.py."""
     _phys_lib().orc_set_boxbox_variant(int(bits))
+
+
+def mpr_stats(reset=False):
+    """MPR work counters since the last reset (oracle/convex.c g_mpr; diagnostics, single-threaded
+    oracle calls only): runs, supports, discover / refine / penetration trips, capped runs, the
+    largest support count of one run."""
+    out = (C.c_longlong * 8)()
+    _phys_lib().orc_mpr_stats(out, int(bool(reset)))
+    keys = ("runs", "supports", "discover", "refine", "penetration", "capped", "max_supports_run")
+    return dict(zip(keys, list(out)[:7]))
 
 
 def forward_fields(state_row, fields, model=None, do_step=False):

@@ -7,6 +7,7 @@
 #   smoke                 __graft_entry__.smoke()
 #   bench [bench args]    the default bench (CPU baseline included unless --no-cpu-baseline)
 #   trace                 rocprofv3 kernel trace + stats of the bench's step and gym legs
+#   steadytrace           the same for the gym leg's steady state (50 burn-in steps, 5 timed)
 #   pmc                   PMC HBM traffic of the step kernel (FETCH_SIZE, WRITE_SIZE: separate passes)
 #   sq                    SQ counters of the step kernel (two passes of 8) + tools/sq_summary.py
 #   stage                 per-stage shader-clock profile on the bench's inputs (tools/step_parity.py)
@@ -51,6 +52,9 @@ do_step() {
     trace)
       prof trace 600 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof" -o run -- \
         python3 "$ROOT/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --no-tqc --no-ik --steady-burn 0 ;;
+    steadytrace)
+      prof steadytrace 600 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_sprof" -o run -- \
+        python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-tqc --no-ik --steady-burn 50 ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         prof pmc_$c 300 --pmc $c --output-format csv -d "$OUT/${TAG}_pmc_$c" -o run -- python3 "$ROOT/bench.py" $BENCH_STEP
