@@ -653,7 +653,7 @@ __global__ void __launch_bounds__(1024) wide_select_kernel(const uint8_t* __rest
 // hq (resume passes of the gym step): consume the hand-over queue instead of the list -- claim
 // entries one at a time until hq_take reports the producers done (hq_target workgroups) and
 // the queue drained; B bounds the entries
-__global__ void __launch_bounds__(NT * MW_WAVES, PNP_WIDE ? 1 : 4) env_step_wide_kernel(pnp_state_t<float> st, pnp_env_params prm,
+__global__ void __launch_bounds__(NT * MW_WAVES, PNP_WIDE ? 1 : PNP_FULL_MW_EU) env_step_wide_kernel(pnp_state_t<float> st, pnp_env_params prm,
                                                                           EnvSoA<float> es, const float* __restrict__ action,
                                                                           EnvOutT<float> out, const int* __restrict__ list,
                                                                           int resume, int hand, int* __restrict__ hq,

@@ -4492,6 +4492,12 @@ __device__ void store_env(const DevPhys<T>& /*image: phys<T>()*/, const Env<T>& 
 #ifndef PNP_STEP_WAVES
 #define PNP_STEP_WAVES 1
 #endif
+// the full build's two-wave gym kernel (PNP_GYM_FULL_MW): waves per SIMD its registers are budgeted
+// for -- 2 lets three envs' six waves share a CU, but only when every fp32 kernel of the build is
+// budgeted alike (PNP_STEP_WAVES=2: the stages are shared functions)
+#ifndef PNP_FULL_MW_EU
+#define PNP_FULL_MW_EU 2
+#endif
 template <typename T, bool TIMED>
 __global__ void __launch_bounds__(NT, sizeof(T) == 4 ? PNP_STEP_WAVES : 1) step_kernel(const DevPhys<T>* __restrict__ mp, pnp_state_t<T> st, int B, int nsub,
                                                  unsigned long long* __restrict__ prof, int resume, int hand) {

@@ -76,6 +76,9 @@ constexpr int NSUM = 8;            // per slab: critic loss (c = 0, 1), sum(log_
 static_assert(S_TQ + NALL <= S_DQ && S_DQ + NALL <= S_DA && S_DLS + 8 <= HID, "per-row layout");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+#ifndef PNP_TQC_STAMPS
+#define PNP_TQC_STAMPS 0
+#endif
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -93,8 +96,103 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // MFMAs (and of B in the CR layout); the sum is the same, the fp32 accumulation order differs.
 // Reduction rows past GK read zeros from the staged chunk and are masked in A; columns past GN
 // compute garbage in output columns nobody keeps.  Every thread of the workgroup must call it.
+// PNP_TQC_DIRECT (default 1, round 6): every wave streams its own B operands straight from global
+// memory (L2) into registers, PF reduction blocks ahead -- no LDS staging of the weight and no
+// workgroup barrier inside the product.  Each wave owns whole output tiles, so the weight is still
+// read once per workgroup; the MFMA sequence and operands are the staged version's (the same bits).
+// 0: round 5's staged version below.
+#ifndef PNP_TQC_DIRECT
+#define PNP_TQC_DIRECT 1
+#endif
+// The stage functions are out of line and take generic pointers; loads through them would be flat
+// loads, which count against both the vector-memory and the LDS counters and are waited for with
+// vmcnt(0) lgkmcnt(0) -- every prefetched weight load drained at each reduction block.  The products
+// name the address spaces: the weights and workspace are global, the slab operands LDS.
+typedef const __attribute__((address_space(1))) float* gptr;
+typedef const __attribute__((address_space(3))) float* lptr;
+typedef __attribute__((address_space(3))) float* lmut;
 template <bool CR, int GK, int GN>
-__device__ void slab_gemm(const float* X, const float* __restrict__ W, float* Ws, f32x4 acc[2]) {
+__device__ __forceinline__ f32x4 gemm_bload(gptr W, int kb, int kq, int c) {
+  // B(k0 + s, c), s = 0..3, k0 = 16 kb + 4 kq: CR W[c * GK + k] (contiguous in k), RC W[k * GN + c]
+  const int k0 = 16 * kb + 4 * kq;
+  f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (c >= GN) return b;
+  if (CR && GK % 16 == 0) {
+    b = *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(W + (size_t)c * GK + k0);
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+      if (k0 + s < GK) b[s] = CR ? W[(size_t)c * GK + k0 + s] : W[(size_t)(k0 + s) * GN + c];
+  }
+  return b;
+}
+// CR with whole 16-blocks (nn.Linear rows, contiguous in k): the MFMA wants lane (kq, i) to hold
+// W[c_i][k0 .. k0 + 3], which puts consecutive lanes 1 KB apart.  The block is loaded with four
+// consecutive lanes on one row's 64 contiguous bytes instead (lane l: row l / 4, k 4 (l % 4)) and
+// moved to its MFMA lane through the LDS crossbar (ds_bpermute, no LDS storage) when it is used.
+#ifndef PNP_TQC_CR_PERM
+#define PNP_TQC_CR_PERM 1
+#endif
+template <int GK>
+__device__ __forceinline__ f32x4 gemm_bload_rows(gptr W, int kb, int tile) {
+  const int lane = threadIdx.x & 63;
+  return *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>(
+      W + (size_t)(tile * 16 + (lane >> 2)) * GK + 16 * kb + 4 * (lane & 3));
+}
+__device__ __forceinline__ f32x4 gemm_bperm(f32x4 v) {
+  const int lane = threadIdx.x & 63;
+  const int src = 4 * ((4 * (lane & 15)) + (lane >> 4));   // byte address of lane 4 i + kq
+  f32x4 r;
+#pragma unroll
+  for (int s = 0; s < 4; s++) r[s] = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(v[s])));
+  return r;
+}
+template <bool CR, int GK, int GN>
+__device__ void slab_gemm_direct(const float* Xg, const float* __restrict__ Wg, f32x4 acc[2]) {
+  const lptr X = (lptr)Xg;
+  const gptr W = (gptr)Wg;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 15, kq = lane >> 4;
+  constexpr int NTILE = (GN + 15) / 16, NKB = (GK + 15) / 16, PF = NKB < 8 ? NKB : 8;
+  static_assert(NTILE <= 2 * NW, "slab_gemm shape");
+  acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const int tile = wv + q * NW;
+    if (tile >= NTILE) continue;   // (wave-uniform)
+    const int c = tile * 16 + i;
+    constexpr bool ROWS = PNP_TQC_CR_PERM && CR && GK % 16 == 0 && GN % 16 == 0;
+    auto bload = [&](int kb) { return ROWS ? gemm_bload_rows<GK>(W, kb, tile) : gemm_bload<CR, GK, GN>(W, kb, kq, c); };
+    f32x4 pb[PF];
+#pragma unroll
+    for (int p = 0; p < PF; p++) pb[p] = bload(p);
+    // (the scheduling barriers keep each load PF blocks ahead of its use: left alone, the
+    // scheduler sank the loads next to their MFMAs, two blocks of cover for an L2 round trip)
+    // the A operand one block ahead as well (an LDS round trip under the previous block's MFMAs)
+    auto aload = [&](int kb) {
+      const int k = 16 * kb + 4 * kq;
+      f32x4 a = *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(X + i * LD + k);
+      if (GK % 16 != 0)
+#pragma unroll
+        for (int s = 0; s < 4; s++) a[s] = k + s < GK ? a[s] : 0.f;
+      return a;
+    };
+    f32x4 pa = aload(0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kb = 0; kb < NKB; kb++) {
+      const f32x4 b = ROWS ? gemm_bperm(pb[kb % PF]) : pb[kb % PF];
+      const f32x4 a = pa;
+      if (kb + PF < NKB) pb[kb % PF] = bload(kb + PF);
+      if (kb + 1 < NKB) pa = aload(kb + 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < 4; s++) acc[q] = mfma4(a[s], b[s], acc[q]);
+    }
+  }
+}
+template <bool CR, int GK, int GN>
+__device__ void slab_gemm_staged(const float* X, const float* __restrict__ W, float* Ws, f32x4 acc[2]) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, i = lane & 15, kq = lane >> 4;
   // narrow products (N <= 32: the heads, the critics' quantile layer, the input gradient) stage
   // the whole reduction at once -- one chunk, one barrier -- instead of 8 chunks whose MFMA work
@@ -203,6 +301,15 @@ __device__ void slab_gemm(const float* X, const float* __restrict__ W, float* Ws
     __syncthreads();
   }
 }
+template <bool CR, int GK, int GN>
+__device__ __forceinline__ void slab_gemm(const float* X, const float* __restrict__ W, float* Ws, f32x4 acc[2]) {
+#if PNP_TQC_DIRECT
+  (void)Ws;
+  slab_gemm_direct<CR, GK, GN>(X, W, acc);
+#else
+  slab_gemm_staged<CR, GK, GN>(X, W, Ws, acc);
+#endif
+}
 // Y = act(X Wk + b) with Wk(k, n) from nn.Linear's [out][in] (TR: CR view) or the stacked critics'
 // [in][out] (RC view)
 template <bool TR, int K, int N>
@@ -213,7 +320,7 @@ __device__ __attribute__((noinline)) void lin_fwd(const float* X, const float* _
 #pragma unroll
   for (int q = 0; q < 2; q++) {
     const int n = (wv + q * NW) * 16 + i;
-    bq[q] = n < N ? bias[n] : 0.f;
+    bq[q] = n < N ? ((gptr)bias)[n] : 0.f;
   }
   f32x4 acc[2];
   slab_gemm<TR, K, N>(X, W, Ws, acc);
@@ -225,7 +332,7 @@ __device__ __attribute__((noinline)) void lin_fwd(const float* X, const float* _
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const float v = bn + acc[q][r];
-        Y[(4 * kq + r) * LD + n] = relu ? fmaxf(v, 0.f) : v;
+        ((lmut)Y)[(4 * kq + r) * LD + n] = relu ? fmaxf(v, 0.f) : v;
       }
     }
   }
@@ -247,9 +354,9 @@ __device__ __attribute__((noinline)) void lin_dgrad(const float* dY, const float
       for (int r = 0; r < 4; r++) {
         const int row = 4 * kq + r;
         float v = acc[q][r];
-        if (accumulate) v += dX[row * LD + k];
-        if (H && !(H[row * LD + k] > 0.f)) v = 0.f;
-        dX[row * LD + k] = v;
+        if (accumulate) v += ((lmut)dX)[row * LD + k];
+        if (H && !(((lptr)H)[row * LD + k] > 0.f)) v = 0.f;
+        ((lmut)dX)[row * LD + k] = v;
       }
   }
 }
@@ -258,7 +365,7 @@ template <int COLS>
 __device__ void load_rows(float* D, const float* __restrict__ src, int row0, int ld_src, int col0 = 0) {
   for (int e = threadIdx.x; e < R * COLS; e += NTH) {
     const int r = e / COLS, c = e - r * COLS;
-    D[r * LD + col0 + c] = src[(size_t)(row0 + r) * ld_src + c];
+    ((lmut)D)[r * LD + col0 + c] = ((gptr)src)[(size_t)(row0 + r) * ld_src + c];
   }
 }
 template <int COLS>
@@ -266,7 +373,8 @@ __device__ void save_slab(float* __restrict__ dst, const float* S) {
   static_assert(COLS % 4 == 0, "save_slab");
   for (int e = threadIdx.x; e < R * COLS / 4; e += NTH) {
     const int r = e / (COLS / 4), c = 4 * (e - r * (COLS / 4));
-    *reinterpret_cast<f32x4*>(dst + 4 * e) = *reinterpret_cast<const f32x4*>(S + r * LD + c);
+    *reinterpret_cast<__attribute__((address_space(1))) f32x4*>((__attribute__((address_space(1))) float*)dst + 4 * e) =
+        *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>((lptr)S + r * LD + c);
   }
 }
 template <int COLS>
@@ -274,7 +382,8 @@ __device__ void load_slab(float* D, const float* __restrict__ src) {
   static_assert(COLS % 4 == 0, "load_slab");
   for (int e = threadIdx.x; e < R * COLS / 4; e += NTH) {
     const int r = e / (COLS / 4), c = 4 * (e - r * (COLS / 4));
-    *reinterpret_cast<f32x4*>(D + r * LD + c) = *reinterpret_cast<const f32x4*>(src + 4 * e);
+    *reinterpret_cast<__attribute__((address_space(3))) f32x4*>((lmut)D + r * LD + c) =
+        *reinterpret_cast<const __attribute__((address_space(1))) f32x4*>((gptr)src + 4 * e);
   }
 }
 
@@ -319,7 +428,41 @@ struct alignas(16) Lds {   // 146 KB (a workgroup may hold all 160 KB of a CU's 
   float W[2 * WCH];
   float row[R][NALL + 14], q[R][NALL], tq[R][NALL];
   float red[NTH];
+#if PNP_TQC_STAMPS
+  float* stamp;        // diagnostic build: shader-clock stamps of one workgroup (tools/tqc_stamps.py)
+  long long t0, r0;
+  int ns;
+#endif
 };
+// Diagnostic build (PNP_TQC_STAMPS=1): thread 0 of the chosen workgroup writes the cycles since the
+// kernel started at each tqc_stamp (16 slots: columns 240..255 of one per-row record of the
+// workspace, which nothing reads; slot 15: the kernel's shader cycles per 10 ns of real time)
+__device__ __forceinline__ void tqc_stamp_begin(Lds& L, float* where) {
+#if PNP_TQC_STAMPS
+  if (threadIdx.x == 0) {
+    L.stamp = where;
+    L.ns = 0;
+    L.t0 = __builtin_amdgcn_s_memtime();
+    L.r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  __syncthreads();
+#else
+  (void)L; (void)where;
+#endif
+}
+__device__ __forceinline__ void tqc_stamp(Lds& L, bool last = false) {
+#if PNP_TQC_STAMPS
+  __syncthreads();
+  if (threadIdx.x == 0 && L.stamp) {
+    const long long c = __builtin_amdgcn_s_memtime() - L.t0;
+    if (L.ns < 15) L.stamp[L.ns++] = (float)c;
+    if (last) L.stamp[15] = (float)c / (float)(__builtin_amdgcn_s_memrealtime() - L.r0);
+  }
+  __syncthreads();
+#else
+  (void)L; (void)last;
+#endif
+}
 
 // block sum of v (all threads), result on every thread
 __device__ float block_sum(Lds& L, float v) {
@@ -343,17 +486,21 @@ __device__ void actor_fwd(Lds& L, const TqcArgs& g, const float* __restrict__ ep
   const size_t MS = (size_t)g.B * HID;
   lin_fwd<true, OBS, HID>(L.A, P[0], P[1], L.Bf, true, L.W);
   __syncthreads();
+  tqc_stamp(L);
   if (hs) save_slab<HID>(hs, L.Bf);
   lin_fwd<true, HID, HID>(L.Bf, P[2], P[3], L.C, true, L.W);
   __syncthreads();
+  tqc_stamp(L);
   if (hs) save_slab<HID>(hs + MS, L.C);
   lin_fwd<true, HID, HID>(L.C, P[4], P[5], L.Bf, true, L.W);
   __syncthreads();
+  tqc_stamp(L);
   if (hs) save_slab<HID>(hs + 2 * MS, L.Bf);
   // heads: mu and log_std into C's first 16 columns (N = 7 each)
   lin_fwd<true, HID, ACT>(L.Bf, P[6], P[7], L.C, false, L.W);
   lin_fwd<true, HID, ACT>(L.Bf, P[8], P[9], L.C + 8, false, L.W);
   __syncthreads();
+  tqc_stamp(L);
   const int t = threadIdx.x;
   if (t < R * ACT) {
     const int r = t / ACT, j = t - r * ACT;
@@ -392,15 +539,19 @@ __device__ void critic_fwd(Lds& L, const float* const* P, int c, float* hs, floa
   const float* w3 = P[6] + (size_t)c * HID * NQ;
   lin_fwd<false, NIN, HID>(L.A, w0, P[1] + c * HID, L.Bf, true, L.W);
   __syncthreads();
+  tqc_stamp(L);
   if (hs) save_slab<HID>(hs, L.Bf);
   lin_fwd<false, HID, HID>(L.Bf, w1, P[3] + c * HID, L.C, true, L.W);
   __syncthreads();
+  tqc_stamp(L);
   if (hs) save_slab<HID>(hs + MS, L.C);
   lin_fwd<false, HID, HID>(L.C, w2, P[5] + c * HID, L.Bf, true, L.W);
   __syncthreads();
+  tqc_stamp(L);
   if (hs) save_slab<HID>(hs + 2 * MS, L.Bf);
   lin_fwd<false, HID, NQ>(L.Bf, w3, P[7] + c * NQ, L.C, false, L.W);
   __syncthreads();
+  tqc_stamp(L);
   for (int e = threadIdx.x; e < R * NQ; e += NTH) {
     const int r = e / NQ, j = e - r * NQ;
     out[r * os + j] = L.C[r * LD + j];
@@ -418,20 +569,24 @@ __device__ void critic_dgrad(Lds& L, const float* const* P, int c, const float* 
   __syncthreads();
   lin_dgrad<false, NQ, HID>(L.C, w3, L.Bf, L.A, false, L.W);   // dH3 = dq w3^T, relu'(H3)
   __syncthreads();
+  tqc_stamp(L);
   if (ds) save_slab<HID>(ds + 2 * MS, L.Bf);
   load_slab<HID>(L.A, hs + MS);
   __syncthreads();
   lin_dgrad<false, HID, HID>(L.Bf, w2, L.C, L.A, false, L.W);  // dH2
   __syncthreads();
+  tqc_stamp(L);
   if (ds) save_slab<HID>(ds + MS, L.C);
   load_slab<HID>(L.A, hs);
   __syncthreads();
   lin_dgrad<false, HID, HID>(L.C, w1, L.Bf, L.A, false, L.W);  // dH1
   __syncthreads();
+  tqc_stamp(L);
   if (ds) save_slab<HID>(ds, L.Bf);
   if (want_dx) {
     lin_dgrad<false, HID, NIN>(L.Bf, P[0] + (size_t)c * NIN * HID, L.A, nullptr, false, L.W);
     __syncthreads();
+    tqc_stamp(L);
   }
 }
 
@@ -441,6 +596,7 @@ __global__ void __launch_bounds__(NTH) tqc_fwd_kernel(TqcArgs g) {
   const int slab = blockIdx.x, job = blockIdx.y, row0 = slab * R, t = threadIdx.x;
   const size_t MS = (size_t)g.B * HID;
   float* sm = wmat(g, M_SM, row0);
+  tqc_stamp_begin(L, slab == 0 && job == 1 + NC ? wmat(g, M_SM, 0) + 240 : nullptr);
   if (slab == 0 && job == 0 && t < 10) g.astep[t][0] += 1.f;
   if (slab == 0 && job == 0 && t == 10 && g.draw_counter) g.draw_counter[0] += 1ull;   // (the sample has read it)
   if (job == 0) {   // actor(obs): a_pi, log_prob, activations (the actor step's)
@@ -469,6 +625,7 @@ __global__ void __launch_bounds__(NTH) tqc_fwd_kernel(TqcArgs g) {
   for (int e = t; e < R * ACT; e += NTH) L.A[(e / ACT) * LD + OBS + e % ACT] = ap[e / ACT][e % ACT];
   __syncthreads();
   critic_fwd(L, g.target, c, nullptr, sm + S_TQ + c * NQ, HID, MS);
+  tqc_stamp(L, true);
 }
 
 __global__ void __launch_bounds__(NTH) tqc_critic_bwd_kernel(TqcArgs g) {
@@ -476,6 +633,7 @@ __global__ void __launch_bounds__(NTH) tqc_critic_bwd_kernel(TqcArgs g) {
   const int slab = blockIdx.x, c = blockIdx.y, row0 = slab * R, t = threadIdx.x;
   const size_t MS = (size_t)g.B * HID;
   float* sm = wmat(g, M_SM, row0);
+  tqc_stamp_begin(L, slab == 0 && c == 0 ? wmat(g, M_SM, 1) + 240 : nullptr);
   const float ent_coef = expf(g.log_ent_coef[0]);
   // sort the 50 target quantiles per row (rank by counting; ties broken by index), keep the
   // lowest 46, TD target
@@ -519,7 +677,9 @@ __global__ void __launch_bounds__(NTH) tqc_critic_bwd_kernel(TqcArgs g) {
   }
   lsum = block_sum(L, lsum);
   if (t == 0) g.sums[slab * NSUM + c] = lsum;
+  tqc_stamp(L);
   critic_dgrad(L, g.critic, c, wmat(g, M_CH + 3 * c, row0), wmat(g, M_CD + 3 * c, row0), false, MS);
+  tqc_stamp(L, true);
 }
 
 __global__ void __launch_bounds__(NTH) tqc_pi_critic_kernel(TqcArgs g) {
@@ -527,6 +687,7 @@ __global__ void __launch_bounds__(NTH) tqc_pi_critic_kernel(TqcArgs g) {
   const int slab = blockIdx.x, c = blockIdx.y, row0 = slab * R, t = threadIdx.x;
   const size_t MS = (size_t)g.B * HID;
   float* sm = wmat(g, M_SM, row0);
+  tqc_stamp_begin(L, slab == 0 && c == 0 ? wmat(g, M_SM, 2) + 240 : nullptr);
   if (slab == 0 && c == 0 && t < 9) g.cstep[t][0] += 1.f;
   // critic c (updated) on (obs, a_pi): q_pi, then d loss / d a_pi
   load_rows<OBS>(L.A, g.obs, row0, OBS);
@@ -544,12 +705,14 @@ __global__ void __launch_bounds__(NTH) tqc_pi_critic_kernel(TqcArgs g) {
   __syncthreads();
   critic_dgrad(L, g.critic, c, hs, nullptr, true, MS);
   for (int e = t; e < R * ACT; e += NTH) sm[(e / ACT) * HID + S_DA + c * 8 + e % ACT] = L.A[(e / ACT) * LD + OBS + e % ACT];
+  tqc_stamp(L, true);
 }
 
 __global__ void __launch_bounds__(NTH) tqc_actor_bwd_kernel(TqcArgs g) {
   __shared__ Lds L;
   const int slab = blockIdx.x, row0 = slab * R, t = threadIdx.x;
   float* sm = wmat(g, M_SM, row0);
+  tqc_stamp_begin(L, slab == 0 ? wmat(g, M_SM, 3) + 240 : nullptr);
   const float ent_coef = g.logs[0];   // sb3: the coefficient before this step's entropy update
   const float lpsum = block_sum(L, t < R ? sm[t * HID + S_LP] : 0.f);
   if (t == 0) {
@@ -591,6 +754,7 @@ __global__ void __launch_bounds__(NTH) tqc_actor_bwd_kernel(TqcArgs g) {
   lin_dgrad<true, HID, HID>(L.Bf, P[2], L.C, L.A, false, L.W);   // dH1
   __syncthreads();
   save_slab<HID>(wmat(g, M_AD, row0), L.C);
+  tqc_stamp(L, true);
 }
 
 // ---- weight gradients over the whole batch + Adam (torch.optim.Adam fused / capturable semantics)
@@ -672,8 +836,9 @@ __global__ void __launch_bounds__(WTH) tqc_wgrad_adam_kernel(WArgs a) {
       const bool live = r < b1;
 #pragma unroll
       for (int h = 0; h < 2; h++) {   // rows past b1: zeros (the sum is unchanged)
-        xa[u][h] = live ? (xl[h] ? xp[h][(size_t)r * xld[h]] : xc[h]) : 0.f;
-        yb[u][h] = live && yl[h] ? yp[h][(size_t)r * J.ldy] : 0.f;
+        // (global loads: the job's pointers sit in a struct argument, generic to the compiler)
+        xa[u][h] = live ? (xl[h] ? ((gptr)xp[h])[(size_t)r * xld[h]] : xc[h]) : 0.f;
+        yb[u][h] = live && yl[h] ? ((gptr)yp[h])[(size_t)r * J.ldy] : 0.f;
       }
     }
 #pragma unroll

@@ -14,7 +14,8 @@
 #   tqcprof               rocprofv3 kernel trace of the fused TQC learner step
 #   tool <script> [args]  a python diagnostic (tools/*.py) -- all remaining arguments are its own
 #   ab                    library A/B: state digests of the tree's libpnp.so and of each $ALTS .so
-#                         (PNP_LIB), then the C3 and gym legs interleaved twice
+#                         (PNP_LIB; an <alt>.so.env file beside it is sourced for that alternative's
+#                         runs), then the C3 and gym legs interleaved twice
 #   evidence              tests smoke bench trace pmc sq stage tqcprof
 # (Round 5's 43 one-off gpu_*.sh launchers were folded into this script; older profiles name them,
 # their text is in the git history.)
@@ -76,7 +77,8 @@ do_step() {
       run digest_tree 300 python3 -u tools/state_digest.py 512
       for a in ${ALTS:-}; do
         local n; n=$(basename "$a" .so)
-        PNP_LIB="$ROOT/$a" run digest_$n 300 python3 -u tools/state_digest.py 512
+        ( if [ -f "$ROOT/$a.env" ]; then . "$ROOT/$a.env"; fi
+          PNP_LIB="$ROOT/$a" run digest_$n 300 python3 -u tools/state_digest.py 512 ) || exit $?
         if diff <(grep -v amdgpu "$OUT/${TAG}_digest_tree.log") <(grep -v amdgpu "$OUT/${TAG}_digest_$n.log") > /dev/null
         then echo "$n: digests identical"; else echo "$n: DIGESTS DIFFER"; fi
       done
@@ -84,6 +86,9 @@ do_step() {
         for a in tree ${ALTS:-}; do
           local n; n=$(basename "$a" .so)
           if [ "$a" = tree ]; then unset PNP_LIB; else export PNP_LIB="$ROOT/$a"; fi
+          # an alternative's own environment (runtime switches), from <alt>.env next to it
+          unset PNP_GYM_FULL_MW PNP_GYM_WIDE_PCT PNP_GYM_FULL_PCT
+          if [ "$a" != tree ] && [ -f "$ROOT/$a.env" ]; then . "$ROOT/$a.env"; fi
           run ab_${n}_$i 400 python -u bench.py --steps 20 --warmup 3 --no-tqc --no-ik --no-cpu-baseline ${AB_ARGS:-}
           echo "$n run $i: $(tail -1 "$OUT/${TAG}_ab_${n}_$i.log" | python3 -c 'import json,sys; r=json.loads(sys.stdin.read()); print(round(r["value"]/1e6,3), "M C3;", round(r["gym"]["gym_steps_per_s"]), "gym", ((r["gym"].get("steady") or {}).get("ms_per_gym_step")), "ms steady")' 2>/dev/null)"
         done

@@ -1,6 +1,6 @@
 """Learner-step timing (C5 at train.py's update ratio is ~all learner): the TQC gradient step on a
 64-env short-physics replay, fused HIP step (pnp_tqc_update) vs the PyTorch step, both captured in
-a HIP graph; for rocprofv3 --kernel-trace.  usage: python tools/tqc_learner_bench.py [fused|torch] [steps]"""
+a HIP graph; for rocprofv3 --kernel-trace; prints a digest of the trained parameters.  usage: python tools/tqc_learner_bench.py [fused|torch] [steps]"""
 import os
 import sys
 import time
@@ -29,6 +29,10 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / n * 1e3
     print(f"{mode}: {dt:.3f} ms per gradient step ({a.logs and {k: float(v) for k, v in a.logs.items()}})")
+    # parameter digest (A/B builds of the fused step must agree bit for bit)
+    import hashlib
+    flat = torch.cat([p.detach().reshape(-1) for p in list(a.actor.parameters()) + list(a.critic.parameters())])
+    print("param digest", hashlib.sha256(flat.cpu().numpy().tobytes()).hexdigest()[:16])
 
 
 if __name__ == "__main__":
