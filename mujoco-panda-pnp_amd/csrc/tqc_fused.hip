@@ -148,7 +148,7 @@ __device__ __forceinline__ f32x4 gemm_bperm(f32x4 v) {
   return r;
 }
 template <bool CR, int GK, int GN>
-__device__ void slab_gemm_direct(const float* Xg, const float* __restrict__ Wg, f32x4 acc[2]) {
+__device__ void slab_gemm_direct(const float* Xg, const float* __restrict__ Wg, float* Ws, f32x4 acc[2]) {
   const lptr X = (lptr)Xg;
   const gptr W = (gptr)Wg;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 15, kq = lane >> 4;
@@ -156,6 +156,41 @@ __device__ void slab_gemm_direct(const float* Xg, const float* __restrict__ Wg, 
   static_assert(NTILE <= 2 * NW, "slab_gemm shape");
   acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
   acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (NTILE <= 2 && NKB >= 8) {
+    // narrow products (the actor's heads, a critic's quantile layer, the gradient to a critic's
+    // input): one or two output tiles, so the reduction is split over the waves -- NW / NTILE waves
+    // per tile, each a strided share of the 16-deep blocks -- and the partial tiles are added in
+    // wave order through LDS (Ws), instead of one wave running the whole dependent MFMA chain
+    constexpr int WPT = NW / NTILE;
+    const int tile = wv / WPT, part = wv % WPT, c = tile * 16 + i;
+    f32x4 pt = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = part; kb < NKB; kb += WPT) {
+      const f32x4 b = gemm_bload<CR, GK, GN>(W, kb, kq, c);
+      const int k = 16 * kb + 4 * kq;
+      f32x4 a = *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(X + i * LD + k);
+      if (GK % 16 != 0)
+#pragma unroll
+        for (int s = 0; s < 4; s++) a[s] = k + s < GK ? a[s] : 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; s++) pt = mfma4(a[s], b[s], pt);
+    }
+    const lmut P = (lmut)Ws;
+    __syncthreads();   // (the previous product's readers of Ws are done)
+#pragma unroll
+    for (int q = 0; q < 4; q++) P[(wv * 16 + 4 * kq + q) * 16 + i] = pt[q];
+    __syncthreads();
+    if (wv < NTILE) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < WPT; w++) v += P[((wv * WPT + w) * 16 + 4 * kq + q) * 16 + i];
+        acc[0][q] = v;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < 2; q++) {
     const int tile = wv + q * NW;
@@ -304,8 +339,7 @@ __device__ void slab_gemm_staged(const float* X, const float* __restrict__ W, fl
 template <bool CR, int GK, int GN>
 __device__ __forceinline__ void slab_gemm(const float* X, const float* __restrict__ W, float* Ws, f32x4 acc[2]) {
 #if PNP_TQC_DIRECT
-  (void)Ws;
-  slab_gemm_direct<CR, GK, GN>(X, W, acc);
+  slab_gemm_direct<CR, GK, GN>(X, W, Ws, acc);
 #else
   slab_gemm_staged<CR, GK, GN>(X, W, Ws, acc);
 #endif
@@ -465,14 +499,16 @@ __device__ __forceinline__ void tqc_stamp(Lds& L, bool last = false) {
 }
 
 // block sum of v (all threads), result on every thread
+// (each wave sums its 64 values across lanes, then the 16 wave sums are added in wave order: two
+// workgroup barriers instead of a 1024-way tree's eleven)
 __device__ float block_sum(Lds& L, float v) {
-  L.red[threadIdx.x] = v;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
+  if ((threadIdx.x & 63) == 0) L.red[threadIdx.x >> 6] = v;
   __syncthreads();
-  for (int s = NTH / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) L.red[threadIdx.x] += L.red[threadIdx.x + s];
-    __syncthreads();
-  }
-  const float r = L.red[0];
+  float r = L.red[0];
+#pragma unroll
+  for (int w = 1; w < NW; w++) r += L.red[w];
   __syncthreads();
   return r;
 }
@@ -768,6 +804,12 @@ __global__ void __launch_bounds__(NTH) tqc_actor_bwd_kernel(TqcArgs g) {
 // Cache, each trip waits one round trip): four waves per SIMD hide that wait where one wave per
 // SIMD (WNW = 4, 128 rows each) left it exposed -- 22.2 -> 16.7 (8 waves) -> 15.9 µs per launch.
 constexpr int WT = 32, WNW = 16, WTH = 64 * WNW, MAXJ = 10, WRG = 8;
+// waves per SIMD the weight-gradient kernel's registers are budgeted for (A/B builds): 8 (<= 64
+// VGPRs, 32 B of spills) lets two 16-wave workgroups share a CU -- the critic pass's 338 tiles in one
+// round on 256 CUs -- and measured the same, 20.2 vs 19-20 us per launch (profiles/r06/ab_round6.log)
+#ifndef PNP_WGRAD_EU
+#define PNP_WGRAD_EU 1
+#endif
 struct WJob {
   const float* x0; const float* x1; const float* dy;
   float* p; float* m; float* v; float* tgt; const float* step;       // weight ([out][in] if tr, else [in][out])
@@ -793,15 +835,15 @@ struct WArgs {
   int ent_gi;
 };
 enum { WG_FUSED = 0, WG_GRAD = 1, WG_APPLY = 2 };
+// bc1 = 1 - b1^step, bc2 = 1 - b2^step: per parameter tensor, computed once by the caller
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float gr, float lr, float b1, float b2, float eps,
-                                          float step) {
-  const float bc1 = 1.f - powf(b1, step), bc2 = 1.f - powf(b2, step);
+                                          float bc1, float bc2) {
   m = b1 * m + (1.f - b1) * gr;
   v = b2 * v + (1.f - b2) * gr * gr;
   const float denom = sqrtf(v) / sqrtf(bc2) + eps;
   p -= (lr / bc1) * m / denom;
 }
-__global__ void __launch_bounds__(WTH) tqc_wgrad_adam_kernel(WArgs a) {
+__global__ void __launch_bounds__(WTH, PNP_WGRAD_EU) tqc_wgrad_adam_kernel(WArgs a) {
   __shared__ float red[WNW][WT][WT + 1];
   int ji = 0;
   while (ji + 1 < a.nj && (int)blockIdx.x >= a.j[ji + 1].tile0) ji++;
@@ -856,6 +898,10 @@ __global__ void __launch_bounds__(WTH) tqc_wgrad_adam_kernel(WArgs a) {
       for (int q = 0; q < 4; q++) red[w][16 * h + 4 * kq + q][16 * h2 + i] = acc[h][h2][q];
   __syncthreads();
   const float lr = a.lr[0];
+  // the bias corrections of the tile's weight and bias tensors (torch: per parameter's step)
+  const float sw = J.step[0] + a.step_add, sb = J.stepb[0] + a.step_add;
+  const float bc1w = 1.f - powf(a.beta1, sw), bc2w = 1.f - powf(a.beta2, sw);
+  const float bc1b = 1.f - powf(a.beta1, sb), bc2b = 1.f - powf(a.beta2, sb);
   for (int e = t; e < WT * WT; e += WTH) {
     // consecutive threads along the parameter's contiguous index
     const int kk = J.tr ? e % WT : e / WT, nn = J.tr ? e / WT : e % WT, k = k0 + kk, n = n0 + nn;
@@ -864,23 +910,23 @@ __global__ void __launch_bounds__(WTH) tqc_wgrad_adam_kernel(WArgs a) {
 #pragma unroll
     for (int q = 1; q < WNW; q++) gr += red[q][kk][nn];   // the waves' row blocks in order
     float *pp, *mp, *vp, *tp;
-    float step;
+    float bc1, bc2;
     int gi;
     if (k < J.K) {
       const int idx = J.tr ? n * J.K + k : k * J.N + n;
       pp = J.p + idx; mp = J.m + idx; vp = J.v + idx; tp = J.tgt ? J.tgt + idx : nullptr;
-      step = J.step[0] + a.step_add;
+      bc1 = bc1w; bc2 = bc2w;
       gi = J.goff + idx;
     } else {
       pp = J.pb + n; mp = J.mb + n; vp = J.vb + n; tp = J.tgtb ? J.tgtb + n : nullptr;
-      step = J.stepb[0] + a.step_add;
+      bc1 = bc1b; bc2 = bc2b;
       gi = J.goffb + n;
     }
     if (a.mode == WG_APPLY) gr = a.grad_in[gi];
     if (a.grad_out) a.grad_out[gi] = gr;
     if (a.mode == WG_GRAD) continue;
     float p = *pp, m = *mp, v = *vp;
-    adam_elem(p, m, v, gr, lr, a.beta1, a.beta2, a.eps, step);
+    adam_elem(p, m, v, gr, lr, a.beta1, a.beta2, a.eps, bc1, bc2);
     *pp = p; *mp = m; *vp = v;
     if (tp) *tp = *tp * (1.f - a.tau) + a.tau * p;   // Polyak (torch._foreach_mul_, then _foreach_add_ alpha = tau)
   }
@@ -904,7 +950,8 @@ __global__ void __launch_bounds__(WTH) tqc_wgrad_adam_kernel(WArgs a) {
       }
       if (a.mode != WG_GRAD) {
         float p = le, m = a.ent_m[0], v = a.ent_v[0];
-        adam_elem(p, m, v, ge, lr, a.beta1, a.beta2, a.eps, a.ent_step[0] + a.step_add);
+        const float se = a.ent_step[0] + a.step_add;
+        adam_elem(p, m, v, ge, lr, a.beta1, a.beta2, a.eps, 1.f - powf(a.beta1, se), 1.f - powf(a.beta2, se));
         a.ent[0] = p; a.ent_m[0] = m; a.ent_v[0] = v;
       }
     }
