@@ -803,7 +803,13 @@ __global__ void __launch_bounds__(NTH) tqc_actor_bwd_kernel(TqcArgs g) {
 // the wave's MFMAs, 32 loads in flight per lane; the tiles' operands come from L2 / the Infinity
 // Cache, each trip waits one round trip): four waves per SIMD hide that wait where one wave per
 // SIMD (WNW = 4, 128 rows each) left it exposed -- 22.2 -> 16.7 (8 waves) -> 15.9 µs per launch.
-constexpr int WT = 32, WNW = 16, WTH = 64 * WNW, MAXJ = 10, WRG = 8;
+// tile: WTK x WTN of (K + 1) x N (WTK = 16 HK), lane i holding HK columns of X and HN of dY
+// (below).  32 x 32 for both passes: 64 x 32 critic tiles (186 workgroups, one round on 256 CUs
+// instead of 338 in two) measured 23.7 against ~20 us per launch -- each workgroup's load phase grows
+// with its tile, and the CU's load rate (~10 B per cycle with every CU streaming) is the bound
+// (profiles/r06/ab_round6.log r6ak / r6al)
+constexpr int HK_CRITIC = 2, HK_ACTOR = 2, HN = 2, WTN = 16 * HN;
+constexpr int WNW = 16, WTH = 64 * WNW, MAXJ = 10, WRG = 8;
 // waves per SIMD the weight-gradient kernel's registers are budgeted for (A/B builds): 8 (<= 64
 // VGPRs, 32 B of spills) lets two 16-wave workgroups share a CU -- the critic pass's 338 tiles in one
 // round on 256 CUs -- and measured the same, 20.2 vs 19-20 us per launch (profiles/r06/ab_round6.log)
@@ -822,6 +828,8 @@ struct WArgs {
   const float* lr;
   float beta1, beta2, eps, tau;
   float* grad_out;           // optional: the gradients (tests), flat
+  float* stamps;             // diagnostic build (PNP_TQC_STAMPS): per-workgroup real-time stamps
+  int tiles, tiles_x;        // tiles of the pass; tiles per XCD run (ceil(tiles / 8))
   // the critic pass: the entropy coefficient's Adam and the losses; the actor pass: its loss
   float* ent; float* ent_m; float* ent_v; float* ent_step;
   const float* sums; int nslab;
@@ -843,68 +851,120 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float gr
   const float denom = sqrtf(v) / sqrtf(bc2) + eps;
   p -= (lr / bc1) * m / denom;
 }
+template <int HK>
 __global__ void __launch_bounds__(WTH, PNP_WGRAD_EU) tqc_wgrad_adam_kernel(WArgs a) {
-  __shared__ float red[WNW][WT][WT + 1];
+  constexpr int WTK = 16 * HK;
+  __shared__ float red[WNW][WTK][WTN + 1];
+#if PNP_TQC_STAMPS
+  const long long wst0 = __builtin_amdgcn_s_memrealtime();
+#endif
   int ji = 0;
-  while (ji + 1 < a.nj && (int)blockIdx.x >= a.j[ji + 1].tile0) ji++;
+  // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs (b and b + 8 share one), so
+  // block b takes tile (b % 8) * per + b / 8 -- each XCD a contiguous run of tiles, k-major within a
+  // tensor: the runs share X column blocks and dY in their XCD's L2 instead of every XCD fetching
+  // most of both from HBM (the grid is 8 x per; the blocks past the last tile end at once)
+  const int per = a.tiles_x;
+  const int lin = ((int)blockIdx.x % 8) * per + (int)blockIdx.x / 8;
+  if (lin >= a.tiles) return;
+  while (ji + 1 < a.nj && lin >= a.j[ji + 1].tile0) ji++;
   const WJob& J = a.j[ji];
-  const int tile = blockIdx.x - J.tile0, k0 = (tile / J.tiles_n) * WT, n0 = (tile % J.tiles_n) * WT;
+  const int tile = lin - J.tile0, k0 = (tile / J.tiles_n) * WTK, n0 = (tile % J.tiles_n) * WTN;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, i = lane & 15, kq = lane >> 4;
-  const float* xp[2]; int xld[2]; float xc[2]; bool xl[2];
-  const float* yp[2]; bool yl[2];
+  // lane i covers the tile's X columns HK i + h (h < HK) and dY columns HN i + h2 (h2 < HN): the
+  // MFMA tiles interleaved, so that a lane's columns are adjacent and, where they lie in one source
+  // with an aligned row stride, come in one 16- / 8-byte load (xv / yv) instead of HK / HN 4-byte
+  // ones.  A 64 x 32 tile (HK = 4) reads 192 KB of X and dY for 2048 outputs where two 32 x 32 tiles
+  // read 256 KB: the product's time is the CU's load bandwidth (~10 B per cycle with every CU
+  // streaming), and the critic pass's 186 tiles fit the 256 CUs in one round instead of two.
+  const float* xp[HK]; int xld[HK]; float xc[HK]; bool xl[HK];
+  const float* yp[HN]; bool yl[HN];
 #pragma unroll
-  for (int h = 0; h < 2; h++) {
-    const int k = k0 + 16 * h + i, n = n0 + 16 * h + i;
+  for (int h = 0; h < HK; h++) {
+    const int k = k0 + HK * i + h;
     xl[h] = k < J.K;
     xp[h] = k < J.kx ? J.x0 + k : J.x1 + (xl[h] ? k - J.kx : 0);
     xld[h] = k < J.kx ? J.ldx0 : J.ldx1;
     xc[h] = k == J.K ? 1.f : 0.f;
+  }
+#pragma unroll
+  for (int h = 0; h < HN; h++) {
+    const int n = n0 + HN * i + h;
     yl[h] = n < J.N;
     yp[h] = J.dy + (yl[h] ? n : 0);
   }
-  f32x4 acc[2][2];
+  const int kp = k0 + HK * i, np = n0 + HN * i;   // the lane's first columns
+  const bool xv = (kp + HK - 1 < J.kx && J.ldx0 % HK == 0) ||
+                  (kp >= J.kx && kp + HK - 1 < J.K && J.kx % HK == 0 && J.ldx1 % HK == 0);
+  const bool yv = np + HN - 1 < J.N && J.ldy % HN == 0;
+  typedef float fxk __attribute__((ext_vector_type(HK)));
+  typedef float fxn __attribute__((ext_vector_type(HN)));
+  f32x4 acc[HK][HN];
 #pragma unroll
-  for (int h = 0; h < 2; h++)
+  for (int h = 0; h < HK; h++)
 #pragma unroll
-    for (int h2 = 0; h2 < 2; h2++) acc[h][h2] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int h2 = 0; h2 < HN; h2++) acc[h][h2] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int rows = a.mode == WG_APPLY ? 0 : a.B / WNW, b0 = w * rows, b1 = b0 + rows;
   for (int b = b0; b < b1; b += 4 * WRG) {   // WRG row groups per trip, all their loads in flight
-    float xa[WRG][2], yb[WRG][2];
+    float xa[WRG][HK], yb[WRG][HN];
 #pragma unroll
     for (int u = 0; u < WRG; u++) {
       // each lane guards its own row: with B / WNW not a multiple of 4 a row group straddles the
-      // wave's range end (rows of the next wave, or past B for the last wave)
+      // wave's range end (rows of the next wave, or past B for the last wave); rows past b1: zeros
+      // (the sum is unchanged).  (Global loads: the job's pointers sit in a struct argument.)
       const int r = b + 4 * u + kq;
       const bool live = r < b1;
+      if (xv) {
+        fxk v = fxk{};
+        if (live) v = *(const __attribute__((address_space(1))) fxk*)((gptr)xp[0] + (size_t)r * xld[0]);
 #pragma unroll
-      for (int h = 0; h < 2; h++) {   // rows past b1: zeros (the sum is unchanged)
-        // (global loads: the job's pointers sit in a struct argument, generic to the compiler)
-        xa[u][h] = live ? (xl[h] ? ((gptr)xp[h])[(size_t)r * xld[h]] : xc[h]) : 0.f;
-        yb[u][h] = live && yl[h] ? ((gptr)yp[h])[(size_t)r * J.ldy] : 0.f;
+        for (int h = 0; h < HK; h++) xa[u][h] = v[h];
+      } else {
+#pragma unroll
+        for (int h = 0; h < HK; h++) xa[u][h] = live ? (xl[h] ? ((gptr)xp[h])[(size_t)r * xld[h]] : xc[h]) : 0.f;
+      }
+      if (yv) {
+        fxn v = fxn{};
+        if (live) v = *(const __attribute__((address_space(1))) fxn*)((gptr)yp[0] + (size_t)r * J.ldy);
+#pragma unroll
+        for (int h = 0; h < HN; h++) yb[u][h] = v[h];
+      } else {
+#pragma unroll
+        for (int h = 0; h < HN; h++) yb[u][h] = live && yl[h] ? ((gptr)yp[h])[(size_t)r * J.ldy] : 0.f;
       }
     }
+#if PNP_TQC_STAMPS
+    if (a.stamps && t == 0 && b == b0) {   // wave 0's loads landed (diagnostic: drains them)
+      float s0 = 0.f;
+#pragma unroll
+      for (int u = 0; u < WRG; u++) s0 += xa[u][0] + yb[u][0];
+      a.stamps[4 * lin + 3] = (float)(__builtin_amdgcn_s_memrealtime() & 0xFFFFFF) + 0.f * s0;
+    }
+#endif
 #pragma unroll
     for (int u = 0; u < WRG; u++)
 #pragma unroll
-      for (int h = 0; h < 2; h++)
+      for (int h = 0; h < HK; h++)
 #pragma unroll
-        for (int h2 = 0; h2 < 2; h2++) acc[h][h2] = mfma4(xa[u][h], yb[u][h2], acc[h][h2]);
+        for (int h2 = 0; h2 < HN; h2++) acc[h][h2] = mfma4(xa[u][h], yb[u][h2], acc[h][h2]);
   }
 #pragma unroll
-  for (int h = 0; h < 2; h++)
+  for (int h = 0; h < HK; h++)
 #pragma unroll
-    for (int h2 = 0; h2 < 2; h2++)
+    for (int h2 = 0; h2 < HN; h2++)
 #pragma unroll
-      for (int q = 0; q < 4; q++) red[w][16 * h + 4 * kq + q][16 * h2 + i] = acc[h][h2][q];
+      for (int q = 0; q < 4; q++) red[w][HK * (4 * kq + q) + h][HN * i + h2] = acc[h][h2][q];
   __syncthreads();
+#if PNP_TQC_STAMPS
+  if (a.stamps && t == 0) a.stamps[4 * lin + 1] = (float)(__builtin_amdgcn_s_memrealtime() & 0xFFFFFF);
+#endif
   const float lr = a.lr[0];
   // the bias corrections of the tile's weight and bias tensors (torch: per parameter's step)
   const float sw = J.step[0] + a.step_add, sb = J.stepb[0] + a.step_add;
   const float bc1w = 1.f - powf(a.beta1, sw), bc2w = 1.f - powf(a.beta2, sw);
   const float bc1b = 1.f - powf(a.beta1, sb), bc2b = 1.f - powf(a.beta2, sb);
-  for (int e = t; e < WT * WT; e += WTH) {
+  for (int e = t; e < WTK * WTN; e += WTH) {
     // consecutive threads along the parameter's contiguous index
-    const int kk = J.tr ? e % WT : e / WT, nn = J.tr ? e / WT : e % WT, k = k0 + kk, n = n0 + nn;
+    const int kk = J.tr ? e % WTK : e / WTN, nn = J.tr ? e / WTK : e % WTN, k = k0 + kk, n = n0 + nn;
     if (k > J.K || n >= J.N) continue;
     float gr = red[0][kk][nn];
 #pragma unroll
@@ -930,7 +990,13 @@ __global__ void __launch_bounds__(WTH, PNP_WGRAD_EU) tqc_wgrad_adam_kernel(WArgs
     *pp = p; *mp = m; *vp = v;
     if (tp) *tp = *tp * (1.f - a.tau) + a.tau * p;   // Polyak (torch._foreach_mul_, then _foreach_add_ alpha = tau)
   }
-  if (blockIdx.x == 0 && t == 0) {
+#if PNP_TQC_STAMPS
+  if (a.stamps && t == 0) {   // (start, product done, end, wave 0's loads landed), 100 MHz ticks, low 24 bits
+    a.stamps[4 * lin] = (float)(wst0 & 0xFFFFFF);
+    a.stamps[4 * lin + 2] = (float)(__builtin_amdgcn_s_memrealtime() & 0xFFFFFF);
+  }
+#endif
+  if (lin == 0 && t == 0) {
     if (a.ent) {   // entropy coefficient: loss = -(log_ent_coef * mean(log_prob + target)).mean()
       float s = 0.f, l = 0.f;
       for (int q = 0; q < a.nslab; q++) {
@@ -1062,7 +1128,8 @@ static bool tqc_desc_ok(const pnp_tqc_desc* d) {
     if (!d->critic[i] || !d->critic_m[i] || !d->critic_v[i] || !d->critic_step[i] || !d->target[i]) return false;
   return d->ent_m && d->ent_v && d->ent_step && d->workspace && d->logs;
 }
-static int64_t tqc_ws_floats(int64_t B) { return (int64_t)NMAT * B * HID + (B / R) * NSUM; }
+// (+ 4096 floats of stamps in the diagnostic build: 4 per weight-gradient workgroup of the critic pass)
+static int64_t tqc_ws_floats(int64_t B) { return (int64_t)NMAT * B * HID + (B / R) * NSUM + (PNP_TQC_STAMPS ? 4096 : 0); }
 
 extern "C" int64_t pnp_tqc_workspace_floats(const pnp_tqc_desc* d) {
   if (!tqc_shape_ok(d)) { pnp_set_error("pnp_tqc_workspace_floats: unsupported TQC shape"); return PNP_ERR_UNSUPPORTED; }
@@ -1122,7 +1189,7 @@ extern "C" int32_t pnp_tqc_sample_draw(const pnp_tqc_replay* rb, uint64_t seed, 
 }
 
 // one weight-gradient job: a layer's weight (and bias) tensors with their Adam state
-static int add_wjob(WArgs& a, int tile, const float* x0, int ldx0, int kx, const float* x1, int ldx1, const float* dy,
+static int add_wjob(WArgs& a, int hk, int tile, const float* x0, int ldx0, int kx, const float* x1, int ldx1, const float* dy,
                     int K, int N, int tr, float* p, float* m, float* v, float* tgt, const float* step, float* pb, float* mb,
                     float* vb, float* tgtb, const float* stepb, int goff, int goffb) {
   WJob& J = a.j[a.nj++];
@@ -1131,9 +1198,9 @@ static int add_wjob(WArgs& a, int tile, const float* x0, int ldx0, int kx, const
   J.p = p; J.m = m; J.v = v; J.tgt = tgt; J.step = step;
   J.pb = pb; J.mb = mb; J.vb = vb; J.tgtb = tgtb; J.stepb = stepb;
   J.goff = goff; J.goffb = goffb;
-  J.tiles_n = (N + WT - 1) / WT;
+  J.tiles_n = (N + WTN - 1) / WTN;
   J.tile0 = tile;
-  return tile + (K + 1 + WT - 1) / WT * J.tiles_n;
+  return tile + (K + 1 + 16 * hk - 1) / (16 * hk) * J.tiles_n;
 }
 
 // phase -1: the whole step (pnp_tqc_update); 0 / 1 / 2: pnp_tqc_update_phase's data-parallel split
@@ -1188,12 +1255,13 @@ static int32_t tqc_run(const pnp_tqc_desc* d, const pnp_tqc_batch* b, float* gra
       const size_t ow = (size_t)c * K * N, ob = (size_t)c * N;
       const float* x0 = l == 0 ? b->obs : M(M_CH + 3 * c + l - 1);
       const float* dy = l == 3 ? SM + S_DQ + c * NQ : M(M_CD + 3 * c + l);
-      ctiles = add_wjob(ac, ctiles, x0, l == 0 ? OBS : HID, l == 0 ? OBS : K, l == 0 ? b->act : x0, l == 0 ? ACT : HID, dy, K, N,
+      ctiles = add_wjob(ac, HK_CRITIC, ctiles, x0, l == 0 ? OBS : HID, l == 0 ? OBS : K, l == 0 ? b->act : x0, l == 0 ? ACT : HID, dy, K, N,
                         0, d->critic[tw] + ow, d->critic_m[tw] + ow, d->critic_v[tw] + ow, d->target[tw] + ow,
                         d->critic_step[tw], d->critic[tb] + ob, d->critic_m[tb] + ob, d->critic_v[tb] + ob,
                         d->target[tb] + ob, d->critic_step[tb], ACT_P + crit_off(tw) + (int)ow, ACT_P + crit_off(tb) + (int)ob);
     }
   ac.ent = d->log_ent_coef; ac.ent_m = d->ent_m; ac.ent_v = d->ent_v; ac.ent_step = d->ent_step;
+  if (PNP_TQC_STAMPS) ac.stamps = g.ws + (size_t)NMAT * B * HID + (size_t)(B / R) * NSUM;
   ac.sums = g.sums; ac.nslab = S; ac.logs = d->logs;
   ac.critic_scale = 1.f / ((float)B * NC * NQ * KEEP);
   int atiles = 0;
@@ -1201,7 +1269,7 @@ static int32_t tqc_run(const pnp_tqc_desc* d, const pnp_tqc_batch* b, float* gra
     const int K = l == 0 ? OBS : HID, N = l >= 3 ? ACT : HID, tw = 2 * l, tb = 2 * l + 1;
     const float* x0 = l == 0 ? b->obs : M(M_AH + (l < 3 ? l - 1 : 2));
     const float* dy = l == 3 ? SM + S_DMU : l == 4 ? SM + S_DLS : M(M_AD + l);
-    atiles = add_wjob(aa, atiles, x0, l == 0 ? OBS : HID, K, x0, HID, dy, K, N, 1, d->actor[tw], d->actor_m[tw],
+    atiles = add_wjob(aa, HK_ACTOR, atiles, x0, l == 0 ? OBS : HID, K, x0, HID, dy, K, N, 1, d->actor[tw], d->actor_m[tw],
                       d->actor_v[tw], nullptr, d->actor_step[tw], d->actor[tb], d->actor_m[tb], d->actor_v[tb], nullptr,
                       d->actor_step[tb], act_off(tw), act_off(tb));
   }
@@ -1210,7 +1278,10 @@ static int32_t tqc_run(const pnp_tqc_desc* d, const pnp_tqc_batch* b, float* gra
     a.mode = mode;
     if (mode == WG_APPLY) { a.grad_in = grads; a.grad_out = nullptr; }
     else a.grad_out = grads;
-    hipLaunchKernelGGL(tqc_wgrad_adam_kernel, dim3(tiles), dim3(WTH), 0, st, a);
+    a.tiles = tiles;
+    a.tiles_x = (tiles + 7) / 8;
+    if (a.actor) hipLaunchKernelGGL(tqc_wgrad_adam_kernel<HK_ACTOR>, dim3(8 * a.tiles_x), dim3(WTH), 0, st, a);
+    else hipLaunchKernelGGL(tqc_wgrad_adam_kernel<HK_CRITIC>, dim3(8 * a.tiles_x), dim3(WTH), 0, st, a);
     return pnp_check_launch(what);
   };
 

@@ -39,6 +39,24 @@ def main():
         print(f"{name}: {len(st)} stamps, total {st[-1]:.0f} cycles, clock {v[15] / 10:.2f} GHz")
         print("   at   " + " ".join(f"{x:7.0f}" for x in st))
         print("   step " + " ".join(f"{x:7.0f}" for x in steps))
+    wgrad_stamps(a)
+
+
+def wgrad_stamps(a):
+    """the critic pass's weight-gradient workgroups: (start, product done, end, loads landed), 100 MHz ticks"""
+    import numpy as np
+    B = a.cfg.batch_size
+    base = 25 * B * HID + (B // 16) * 8
+    v = a._fws[base:base + 4096].cpu().numpy().reshape(-1, 4)
+    v = v[v[:, 2] > 0]
+    t0 = v[:, 0].min()
+    st, pd, en = (v[:, 0] - t0) * 0.01, (v[:, 1] - v[:, 0]) * 0.01, (v[:, 2] - v[:, 0]) * 0.01   # us
+    ld = (v[:, 3] - v[:, 0]) * 0.01
+    print(f"wgrad loads landed (wave 0) p10/50/90/max {np.percentile(ld, [10, 50, 90, 100]).round(2).tolist()} us")
+    print(f"wgrad (critic pass): {len(v)} workgroups; span {(v[:, 2].max() - t0) * 0.01:.2f} us; start offsets "
+          f"p10/50/90/max {np.percentile(st, [10, 50, 90, 100]).round(2).tolist()} us; product "
+          f"{np.percentile(pd, [10, 50, 90, 100]).round(2).tolist()} us; whole workgroup "
+          f"{np.percentile(en, [10, 50, 90, 100]).round(2).tolist()} us")
 
 
 if __name__ == "__main__":
