@@ -847,6 +847,12 @@ static int32_t launch_env_step_mw(const pnp_state_t<float>* st, const pnp_env_pa
     if (grid > per_cu * ncu - 1) grid = per_cu * ncu - 1;
     if (grid < 1) { pnp_set_error("pnp_env_step: hand-over queue grid %d", grid); return PNP_ERR_ARG; }
   } else {
+    // PNP_GYM_WIDE_GRID (A/B): at most this many workgroups for a list pass (a wide workgroup holds
+    // a CU's LDS; fewer leave CUs to the concurrent full-tier pass)
+    if (const char* eg = getenv("PNP_GYM_WIDE_GRID")) {
+      const int cap = atoi(eg);
+      if (cap > 0 && grid > cap) grid = cap;
+    }
     hipLaunchKernelGGL(wide_select_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, e->tier, st->warn, B, resume,
                        only_tier, list, count_out);
     if (const int32_t rc = pnp_check_launch("wide_select_kernel")) return rc;
@@ -1047,6 +1053,10 @@ static bool gym_full_resume_enabled() {
 // 0 = one single-wave workgroup per env (default: the two-wave pass measured 5 % slower on the gym
 // step, 18.0 k vs 18.9 k gym-steps/s -- a persistent grid walks the selected envs in list order,
 // while one workgroup per env lets the dispatcher balance the CUs; profiles/r03/ab_gym_full_mw.log)
+static int gym_route_order() {
+  const char* e = getenv("PNP_GYM_ROUTE_ORDER");
+  return e ? atoi(e) : 0;
+}
 static bool gym_full_mw_enabled() {
   const char* e = getenv("PNP_GYM_FULL_MW");
   return PNP_MPR_SV_WAVES >= PNP_NS::MW_WAVES && e && e[0] == '1';
@@ -1238,7 +1248,9 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
     for (int i = 0; i < nside && he == hipSuccess; i++) he = hipStreamWaitEvent(rs->side[i], rs->fork, 0);
     if (he != hipSuccess) { pnp_set_error("pnp_env_step: fork: %s", hipGetErrorString(he)); return PNP_ERR_HIP; }
     forked = true;
-    if ((rc = launch_env_step_wide(model, st32, p, e, a32, o, B, rs->side[1], 0, 2))) return fail(rc);
+    // the routed passes' launch order (PNP_GYM_ROUTE_ORDER: 0 wide first, the default; 1 full first)
+    const bool full_first = gym_route_order() == 1;
+    if (!full_first && (rc = launch_env_step_wide(model, st32, p, e, a32, o, B, rs->side[1], 0, 2))) return fail(rc);
     if (full_mw) {
       rc = launch_env_step_mw(st32, p, e, a32, o, B, rs->side[0], 0, 1, hand_pct, "env_step_wide_kernel (full, routed)");
     } else {
@@ -1247,6 +1259,7 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
       rc = pnp_check_launch("env_step_kernel (full, routed)");
     }
     if (rc) return fail(rc);
+    if (full_first && (rc = launch_env_step_wide(model, st32, p, e, a32, o, B, rs->side[1], 0, 2))) return fail(rc);
   }
   if (compact && (rc = launch_env_step_compact(model, st32, p, e, a32, o, B, stream, route ? 0 : -1))) return fail(rc);
   if (compact && gym_compact_mode() == 2) {

@@ -87,7 +87,7 @@ do_step() {
           local n; n=$(basename "$a" .so)
           if [ "$a" = tree ]; then unset PNP_LIB; else export PNP_LIB="$ROOT/$a"; fi
           # an alternative's own environment (runtime switches), from <alt>.env next to it
-          unset PNP_GYM_FULL_MW PNP_GYM_WIDE_PCT PNP_GYM_FULL_PCT
+          unset PNP_GYM_FULL_MW PNP_GYM_WIDE_PCT PNP_GYM_FULL_PCT PNP_GYM_ROUTE_ORDER PNP_GYM_WIDE_GRID
           if [ "$a" != tree ] && [ -f "$ROOT/$a.env" ]; then . "$ROOT/$a.env"; fi
           run ab_${n}_$i 400 python -u bench.py --steps 20 --warmup 3 --no-tqc --no-ik --no-cpu-baseline ${AB_ARGS:-}
           echo "$n run $i: $(tail -1 "$OUT/${TAG}_ab_${n}_$i.log" | python3 -c 'import json,sys; r=json.loads(sys.stdin.read()); print(round(r["value"]/1e6,3), "M C3;", round(r["gym"]["gym_steps_per_s"]), "gym", ((r["gym"].get("steady") or {}).get("ms_per_gym_step")), "ms steady")' 2>/dev/null)"
