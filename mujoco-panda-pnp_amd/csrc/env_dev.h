@@ -1053,9 +1053,13 @@ static bool gym_full_resume_enabled() {
 // 0 = one single-wave workgroup per env (default: the two-wave pass measured 5 % slower on the gym
 // step, 18.0 k vs 18.9 k gym-steps/s -- a persistent grid walks the selected envs in list order,
 // while one workgroup per env lets the dispatcher balance the CUs; profiles/r03/ab_gym_full_mw.log)
+// PNP_GYM_ROUTE_ORDER: 1 (default) = the routed full pass is enqueued before the routed wide pass,
+// 0 = wide first (round 5).  A wide workgroup holds a CU's LDS (140 KB) for its env's whole step,
+// so the pass enqueued first takes the CUs: full first, the steady-state gym step 442.6 / 435.5 ->
+// 423.7 / 422.3 ms (profiles/r06/ab_round6.log r6am); from reset unchanged.
 static int gym_route_order() {
   const char* e = getenv("PNP_GYM_ROUTE_ORDER");
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : 1;
 }
 static bool gym_full_mw_enabled() {
   const char* e = getenv("PNP_GYM_FULL_MW");
@@ -1248,7 +1252,7 @@ static int32_t launch_env_step(pnp_model* model, const pnp_state_t<T>* st, const
     for (int i = 0; i < nside && he == hipSuccess; i++) he = hipStreamWaitEvent(rs->side[i], rs->fork, 0);
     if (he != hipSuccess) { pnp_set_error("pnp_env_step: fork: %s", hipGetErrorString(he)); return PNP_ERR_HIP; }
     forked = true;
-    // the routed passes' launch order (PNP_GYM_ROUTE_ORDER: 0 wide first, the default; 1 full first)
+    // the routed passes' launch order (PNP_GYM_ROUTE_ORDER: 1 full first, the default; 0 wide first)
     const bool full_first = gym_route_order() == 1;
     if (!full_first && (rc = launch_env_step_wide(model, st32, p, e, a32, o, B, rs->side[1], 0, 2))) return fail(rc);
     if (full_mw) {
